@@ -1,0 +1,249 @@
+/*
+ * pinotgpu.h — C ABI of libpinotgpu.so, the MI355X (gfx950) executor for Apache Pinot's server-side
+ * filter -> group-by -> aggregation path over dictionary-encoded immutable segments.
+ *
+ * Plain C: pointers, sizes and status codes; no C++ or torch types cross this boundary and no C++ exception
+ * escapes it.  Every call returns PGPU_OK (0) or a negative status; the message of the last failure on the
+ * calling thread is available from pgpu_last_error().
+ *
+ * Each entry point names the reference interface it stands in for.  Citations use SURVEY.md's abbreviations:
+ *   core/     = pinot-core/src/main/java/org/apache/pinot/core/
+ *   seglocal/ = pinot-segment-local/src/main/java/org/apache/pinot/segment/local/
+ *   segspi/   = pinot-segment-spi/src/main/java/org/apache/pinot/segment/spi/
+ * The Java-side bindings a maintainer adds (JNI, and the ctypes binding used by this repo's tests) are in
+ * INTEGRATION.md.
+ *
+ * Threading: every entry point is thread-safe.  Segments are immutable once pinned; queries on one table are
+ * serialised on that table's device work area (one in flight per table).
+ */
+#ifndef PINOTGPU_H
+#define PINOTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGPU_ABI_VERSION 1
+
+/* ---- status codes (BaseCombineOperator.java:101-107 maps failures to ProcessingException; the Java shim maps
+ * these codes the same way and keeps Pinot's CPU operator for PGPU_ERR_UNSUPPORTED). */
+#define PGPU_OK 0
+#define PGPU_ERR_INVALID_ARGUMENT (-1)
+#define PGPU_ERR_BAD_QUERY (-2)      /* literal does not convert to the column type: BadQueryRequestException
+                                        (core/operator/filter/predicate/PredicateEvaluatorProvider.java:85-88) */
+#define PGPU_ERR_UNSUPPORTED (-3)    /* query shape outside the GPU path (caller runs Pinot's own operator) */
+#define PGPU_ERR_DEVICE (-4)         /* HIP runtime / kernel failure */
+#define PGPU_ERR_OUT_OF_MEMORY (-5)
+#define PGPU_ERR_NOT_FOUND (-6)      /* unknown segment handle / column */
+
+/* FieldSpec.DataType subset of dictionary-encoded single-value columns. */
+enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE = 3, PGPU_STRING = 4 };
+
+/* Forward-index formats: FixedBitSVForwardIndexReaderV2 (seglocal/segment/index/readers/forward/
+ * FixedBitSVForwardIndexReaderV2.java:33-96: MSB-first big-endian bit packing, PinotDataBitSet layout) and
+ * SortedIndexReaderImpl (seglocal/segment/index/readers/sorted/SortedIndexReaderImpl.java:37-116: BIG_ENDIAN
+ * (startDocId, endDocId) int pairs per dictId). */
+enum pgpu_fwd_format { PGPU_FWD_FIXED_BIT = 0, PGPU_FWD_SORTED_PAIRS = 1 };
+
+int pgpu_abi_version(void);
+/* Copies the calling thread's last error message (NUL-terminated, truncated to len). Returns its full length. */
+int pgpu_last_error(char* buf, size_t len);
+int pgpu_device_count(int* count);
+
+/* ============================================================================ tables and pinned segments */
+
+typedef struct pgpu_table_s* pgpu_table;
+
+/* A table owns the per-column global dictionaries: the key space shared by all of its segments, replacing the
+ * by-value merge of GroupByCombineOperator (core/operator/combine/GroupByCombineOperator.java:132-151). */
+int pgpu_table_create(int device, int num_columns, const char* const* column_names, const int32_t* data_types,
+                      pgpu_table* out);
+int pgpu_table_destroy(pgpu_table table);
+
+/* One column of an ImmutableSegment as Pinot holds it in memory (PinotDataBuffer views; the JNI shim takes the
+ * addresses from PinotDataBuffer.toDirectByteBuffer, segspi/memory/PinotDataBuffer.java:382). */
+typedef struct {
+  int32_t cardinality;        /* Dictionary.length() (segspi/index/reader/Dictionary.java:49) */
+  int32_t bits_per_element;   /* column.X.bitsPerElement = PinotDataBitSet.getNumBitsPerValue(card - 1) */
+  int32_t entry_width;        /* bytes per dictionary entry (numBytesPerValue) */
+  int32_t padding_byte;       /* string dictionaries: segment.padding.character (0 for current segments) */
+  int32_t fwd_format;         /* enum pgpu_fwd_format */
+  int32_t reserved;
+  const uint8_t* dict;        /* BIG_ENDIAN fixed-width sorted values (BaseImmutableDictionary.java:45-60) */
+  int64_t dict_len;
+  const uint8_t* fwd;         /* forward index bytes */
+  int64_t fwd_len;
+} pgpu_column_buffers;
+
+typedef struct {
+  int32_t num_docs;
+  int32_t num_columns;        /* must equal the table's column count; entries follow the table's column order */
+  const pgpu_column_buffers* columns;
+} pgpu_segment_desc;
+
+/* Pins one ImmutableSegment into HBM (the H2D copy happens here, once; ImmutableSegmentLoader.load,
+ * seglocal/indexsegment/immutable/ImmutableSegmentLoader.java:67-201, is where the shim calls it). */
+int pgpu_pin_segment(pgpu_table table, const pgpu_segment_desc* desc, int64_t* segment_handle);
+/* Frees the device copy (ImmutableSegmentImpl.destroy, seglocal/indexsegment/immutable/ImmutableSegmentImpl.java:147). */
+int pgpu_unpin_segment(pgpu_table table, int64_t segment_handle);
+int pgpu_table_num_segments(pgpu_table table, int32_t* count);
+int64_t pgpu_table_device_bytes(pgpu_table table);
+
+/* Adds values to a column's global dictionary (multi-GPU: every rank merges the union of all ranks' values so
+ * per-GPU group tables share one key space before the RCCL reduce).  Numeric columns read `values_i64` (INT/LONG)
+ * or `values_f64` (FLOAT/DOUBLE); STRING columns read blob + offsets[n+1]. */
+int pgpu_table_add_dictionary_values(pgpu_table table, int column, int64_t n, const int64_t* values_i64,
+                                     const double* values_f64, const uint8_t* blob, const int64_t* offsets);
+/* Global dictionary of a column (sorted, ascending); gid = index. */
+int pgpu_table_dictionary_size(pgpu_table table, int column, int64_t* size);
+int pgpu_table_dictionary_i64(pgpu_table table, int column, int64_t* out);       /* INT / LONG */
+int pgpu_table_dictionary_f64(pgpu_table table, int column, double* out);        /* FLOAT / DOUBLE */
+/* STRING: writes all values as blob + offsets (offsets has size+1 entries); blob_cap in bytes. */
+int pgpu_table_dictionary_str(pgpu_table table, int column, uint8_t* blob, int64_t blob_cap, int64_t* offsets);
+
+/* ============================================================================ single-segment readers */
+
+/* ForwardIndexReader.readDictIds (segspi/index/reader/ForwardIndexReader.java:83; implemented by
+ * FixedBitSVForwardIndexReaderV2.readDictIds :62-96): host docIds in, host dictIds out, decoded on the GPU
+ * from the pinned copy by the unpack kernel (K1). */
+int pgpu_read_dict_ids(pgpu_table table, int64_t segment_handle, int column, const int32_t* doc_ids, int32_t n,
+                       int32_t* dict_ids_out);
+
+/* Device-level K1: unpack n values starting at `start` from a packed MSB-first buffer already in device memory
+ * into int32 (all pointers are device pointers; stream may be NULL). */
+int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bits, int64_t start, int64_t n,
+                                 int32_t* d_out, void* stream);
+
+/* ============================================================================ queries */
+
+/* Predicate types (segspi Predicate.Type subset on dictionary columns). RANGE literal pair uses "*" for
+ * unbounded (RangePredicate.UNBOUNDED). Literals are strings, converted per column type exactly as
+ * PredicateUtils.getStoredValue + Dictionary.insertionIndexOf do. */
+enum pgpu_predicate_type { PGPU_PRED_EQ = 0, PGPU_PRED_NOT_EQ = 1, PGPU_PRED_IN = 2, PGPU_PRED_NOT_IN = 3,
+                           PGPU_PRED_RANGE = 4 };
+typedef struct {
+  int32_t type;
+  int32_t column;
+  int32_t num_values;         /* EQ/NOT_EQ 1, IN/NOT_IN k, RANGE 2 (lower, upper) */
+  int32_t lower_inclusive;
+  const char* const* values;
+  int32_t upper_inclusive;
+  int32_t reserved;
+} pgpu_predicate;
+
+/* Filter tree (FilterContext AND / OR / PREDICATE, plus NOT) as a postfix program. */
+enum pgpu_filter_opcode { PGPU_OP_PRED = 0, PGPU_OP_AND = 1, PGPU_OP_OR = 2, PGPU_OP_NOT = 3 };
+typedef struct {
+  int32_t op;   /* PRED: arg = predicate index; AND / OR: arg = number of operands popped; NOT: unused */
+  int32_t arg;
+} pgpu_filter_op;
+
+/* AggregationFunctionType subset (core/query/aggregation/function/{Count,Sum,Min,Max,Avg}AggregationFunction). */
+enum pgpu_agg_fn { PGPU_AGG_COUNT = 0, PGPU_AGG_SUM = 1, PGPU_AGG_MIN = 2, PGPU_AGG_MAX = 3, PGPU_AGG_AVG = 4 };
+typedef struct {
+  int32_t fn;
+  int32_t column;   /* -1 for COUNT(*) */
+} pgpu_agg;
+
+typedef struct {
+  int32_t num_predicates;
+  int32_t num_filter_ops;     /* 0 = no filter (MatchAllFilterOperator) */
+  const pgpu_predicate* predicates;
+  const pgpu_filter_op* filter;
+  int32_t num_group_by;       /* >= 1 (the group-by path) */
+  int32_t num_aggs;
+  const int32_t* group_by;    /* table column indices */
+  const pgpu_agg* aggs;
+  int32_t num_groups_limit;   /* InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000 (:70); <= 0 = unlimited */
+  int32_t reserved;
+} pgpu_query;
+
+/* A query compiled against a list of pinned segments (InstancePlanMakerImplV2.makeInstancePlan +
+ * per-segment AggregationGroupByPlanNode: predicate evaluators per segment, group-key layout, accumulators). */
+typedef struct pgpu_plan_s* pgpu_plan;
+typedef struct pgpu_result_s* pgpu_result;
+
+int pgpu_plan_create(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,
+                     pgpu_plan* out);
+int pgpu_plan_destroy(pgpu_plan plan);
+
+/* Dense group table layout of a plan: num_slots rows of num_keys 8-byte words (row s holds accumulator s of
+ * every group key; row 0 is the COUNT row).  slot_kinds[s] (enum pgpu_slot_kind) gives the element type and the
+ * RCCL reduce op that merges two ranks' tables: COUNT/SUM_I64 -> int64 sum, SUM_F64 -> float64 sum,
+ * MIN_KEY -> int64 min, MAX_KEY -> int64 max.  num_keys = 0 when the plan uses the hash table (high cardinality). */
+enum pgpu_slot_kind { PGPU_SLOT_COUNT = 0, PGPU_SLOT_SUM_I64 = 1, PGPU_SLOT_SUM_F64 = 2, PGPU_SLOT_MIN_KEY = 3,
+                      PGPU_SLOT_MAX_KEY = 4 };
+int pgpu_plan_layout(pgpu_plan plan, int32_t* num_slots, int64_t* num_keys, int32_t* slot_kinds /* >= 32 */);
+
+/* Runs the plan on `stream` (hipStream_t; NULL = the table's stream): predicate translation results are
+ * uploaded, the fused filter/group/aggregate kernel runs over every segment, and the dense group table is
+ * written to d_table (device pointer, num_slots * num_keys * 8 bytes, caller-owned; may be NULL to use an
+ * internal buffer).  Asynchronous: nothing is copied back.  Replaces the per-segment operator loop
+ * (AggregationGroupByOperator.getNextBlock, core/operator/query/AggregationGroupByOperator.java:62-79) and the
+ * combine (GroupByCombineOperator.processSegments, :113-160) for the segments of the plan. */
+int pgpu_plan_execute(pgpu_plan plan, void* stream, void* d_table);
+
+/* Compacts the (possibly RCCL-reduced) dense group table into a result: groups with COUNT > 0, their global
+ * dictionary ids and finished aggregation values.  Synchronises `stream`. */
+int pgpu_plan_finalize(pgpu_plan plan, void* stream, const void* d_table, pgpu_result* out);
+
+/* One-call form: plan + execute + finalize (the whole per-server query path). */
+int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,
+                         void* stream, pgpu_result* out);
+
+/* Timing of the last pgpu_plan_execute of this plan (HIP events on the execution stream), microseconds:
+ * [0] whole execute, [1] the fused scan kernel, [2] number of fused-kernel launches. */
+int pgpu_plan_timing(pgpu_plan plan, double* out3);
+
+/* ---- results: AggregationGroupByResult (core/query/aggregation/groupby/AggregationGroupByResult.java:31-81) */
+int pgpu_result_num_groups(pgpu_result r, int64_t* n);
+/* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */
+int pgpu_result_group_ids(pgpu_result r, int32_t* out);
+/* Per aggregation i (query order): value per group as Pinot's intermediate result holds it (double) — COUNT,
+ * SUM, MIN, MAX, and AVG's AvgPair.sum; AVG's AvgPair.count via pgpu_result_avg_counts. */
+int pgpu_result_values(pgpu_result r, int agg, double* out);
+int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out);
+/* Exact integer accumulators where the aggregation is integer-valued (COUNT, AVG count, SUM over INT/LONG):
+ * returns PGPU_ERR_INVALID_ARGUMENT for floating-point sums. */
+int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out);
+/* ExecutionStatistics (core/operator/ExecutionStatistics.java:42): numDocsScanned, numEntriesScannedInFilter,
+ * numEntriesScannedPostFilter, numTotalDocs, plus [4] numSegmentsProcessed, [5] numSegmentsMatched. */
+int pgpu_result_stats(pgpu_result r, int64_t* out6);
+int pgpu_result_destroy(pgpu_result r);
+
+/* Docid match bitmap of one segment's filter (the FilterOperator's doc set, K2): bit d of 64-bit word d/64.
+ * out_words must hold ceil(num_docs / 64) words. */
+int pgpu_filter_bitmap(pgpu_table table, int64_t segment_handle, const pgpu_query* q, uint64_t* out_words);
+
+/* ============================================================================ synthetic segments (bench) */
+
+/* Column generators of BASELINE.md §3: value = f(splitmix64(seed_c ^ global_row)),
+ * seed_c = (0x5EED0000 + column_index) << 32.  UNIFORM: lo + h % (hi - lo); ZIPF: ids[first k with cdf[k] > u];
+ * TABLE: table[h % n].  The segment (dictionary = sorted distinct values present, fixed-bit forward index) is
+ * built on the device and pinned directly; bytes are identical to Pinot's segment creator on the same values. */
+enum pgpu_gen_kind { PGPU_GEN_UNIFORM = 0, PGPU_GEN_ZIPF = 1, PGPU_GEN_TABLE = 2 };
+typedef struct {
+  int32_t kind;
+  int32_t column_index;
+  int64_t lo, hi;             /* UNIFORM */
+  int32_t n;                  /* ZIPF ranks / TABLE size */
+  int32_t reserved;
+  const double* cdf;          /* ZIPF cumulative distribution (host) */
+  const int64_t* ids;         /* ZIPF rank -> value (host), ascending-id order not required */
+  const double* table;        /* TABLE values (host) */
+} pgpu_gen_column;
+int pgpu_generate_segment(pgpu_table table, const pgpu_gen_column* columns, int32_t num_columns, int64_t row0,
+                          int32_t num_docs, int64_t* segment_handle);
+/* Copies a pinned segment column's bytes back to the host (parity checks of the generator). */
+int pgpu_segment_column_info(pgpu_table table, int64_t segment_handle, int column, int32_t* cardinality,
+                             int32_t* bits, int64_t* dict_len, int64_t* fwd_len);
+int pgpu_segment_column_bytes(pgpu_table table, int64_t segment_handle, int column, uint8_t* dict_out,
+                              uint8_t* fwd_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1354 @@
+/*
+ * oracle.c — CPU restatement of Pinot's server filter -> group-by -> aggregation path.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h): the checker and the CPU baseline, never the product.
+ *
+ * Path abbreviations: seglocal/ = pinot-segment-local/src/main/java/org/apache/pinot/segment/local/,
+ * core/ = pinot-core/src/main/java/org/apache/pinot/core/.
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EOF_DOC INT32_MIN /* segspi Constants.EOF = Integer.MIN_VALUE */
+#define MAX_DOC_PER_CALL 10000 /* core/plan/DocIdSetPlanNode.java:29 */
+#define INVALID_ID (-1)        /* GroupKeyGenerator.INVALID_ID */
+
+/* ======================================================================================= codec */
+
+/* PinotDataBitSet.getNumBitsPerValue (seglocal/io/util/PinotDataBitSet.java:59-70). */
+int or_num_bits_per_value(int max_value) {
+  if (max_value <= 1) return 1;
+  int nbits = 8;
+  unsigned v = (unsigned)max_value;
+  while (v > 0xFF) {
+    v >>= 8;
+    nbits += 8;
+  }
+  int first_bit_set = 0; /* FIRST_BIT_SET[v]: index of the highest set bit counted from the MSB of the byte */
+  while (!(v & (0x80u >> first_bit_set))) first_bit_set++;
+  return nbits - first_bit_set;
+}
+
+/* PinotDataBitSet.readInt(index, numBitsPerValue) (:78-100). */
+int32_t or_bitset_read_int(const uint8_t* buf, int64_t index, int nbits) {
+  int64_t bit_offset = index * nbits;
+  int64_t byte_offset = bit_offset / 8;
+  int bit_in_first = (int)(bit_offset % 8);
+  uint32_t cur = buf[byte_offset] & (0xFFu >> bit_in_first);
+  int left = nbits - (8 - bit_in_first);
+  if (left <= 0) return (int32_t)(cur >> -left);
+  while (left > 8) {
+    byte_offset++;
+    cur = (cur << 8) | buf[byte_offset];
+    left -= 8;
+  }
+  return (int32_t)((cur << left) | ((uint32_t)buf[byte_offset + 1] >> (8 - left)));
+}
+
+/* PinotDataBitSet.readInt(startIndex, numBitsPerValue, length, buffer) (:102-136). */
+void or_bitset_read_ints(const uint8_t* buf, int64_t start, int nbits, int len, int32_t* out) {
+  int64_t bit_offset = start * nbits;
+  int64_t byte_offset = bit_offset / 8;
+  int bit_in_first = (int)(bit_offset % 8);
+  uint32_t cur = buf[byte_offset] & (0xFFu >> bit_in_first);
+  for (int i = 0; i < len; i++) {
+    if (bit_in_first == 8) {
+      bit_in_first = 0;
+      byte_offset++;
+      cur = buf[byte_offset];
+    }
+    int left = nbits - (8 - bit_in_first);
+    if (left <= 0) {
+      out[i] = (int32_t)(cur >> -left);
+      bit_in_first = 8 + left;
+      cur = cur & (0xFFu >> bit_in_first);
+    } else {
+      while (left > 8) {
+        byte_offset++;
+        cur = (cur << 8) | buf[byte_offset];
+        left -= 8;
+      }
+      byte_offset++;
+      uint32_t next = buf[byte_offset];
+      out[i] = (int32_t)((cur << left) | (next >> (8 - left)));
+      bit_in_first = left;
+      cur = next & (0xFFu >> bit_in_first);
+    }
+  }
+}
+
+/* PinotDataBitSet.writeInt(index, numBitsPerValue, value) (:138-165). */
+void or_bitset_write_int(uint8_t* buf, int64_t index, int nbits, int32_t value) {
+  int64_t bit_offset = index * nbits;
+  int64_t byte_offset = bit_offset / 8;
+  int bit_in_first = (int)(bit_offset % 8);
+  uint32_t v = (uint32_t)value;
+  uint32_t first = buf[byte_offset];
+  uint32_t first_mask = 0xFFu >> bit_in_first;
+  int left = nbits - (8 - bit_in_first);
+  if (left <= 0) {
+    first_mask &= 0xFFu << -left;
+    buf[byte_offset] = (uint8_t)((first & ~first_mask) | (v << -left));
+  } else {
+    buf[byte_offset] = (uint8_t)((first & ~first_mask) | ((v >> left) & first_mask));
+    while (left > 8) {
+      left -= 8;
+      byte_offset++;
+      buf[byte_offset] = (uint8_t)(v >> left);
+    }
+    byte_offset++;
+    uint32_t last = buf[byte_offset];
+    buf[byte_offset] = (uint8_t)((last & (0xFFu >> left)) | (v << (8 - left)));
+  }
+}
+
+/* PinotDataBitSet.writeInt(startIndex, numBitsPerValue, length, values) (:167-205); per-value form is equivalent. */
+void or_bitset_write_ints(uint8_t* buf, int64_t start, int nbits, int len, const int32_t* values) {
+  for (int i = 0; i < len; i++) or_bitset_write_int(buf, start + i, nbits, values[i]);
+}
+
+int64_t or_fwd_num_bytes(int64_t num_values, int nbits) { return (num_values * nbits + 7) / 8; }
+
+/* FixedBitIntReader.read/readUnchecked for every width (seglocal/io/reader/impl/FixedBitIntReader.java:37-119,
+ * e.g. Bit9Reader :656-725) return the same value as PinotDataBitSet.readInt; read32 decodes 32 values from
+ * 4*b bytes at byte offset (index/8)*b.  Restated as one generic BE/MSB-first extraction. */
+static inline int32_t fixedbit_read(const uint8_t* fwd, int64_t index, int nbits) {
+  return or_bitset_read_int(fwd, index, nbits);
+}
+
+/* FixedBitSVForwardIndexReaderV2.readDictIds (:62-96): bulk read32 when docIds are contiguous and >= 64 long,
+ * per-doc reads otherwise.  The bulk and per-doc paths decode identical values, so the restatement keeps the
+ * control flow (which docs go through which path) and one decoder. */
+void or_read_dict_ids(const uint8_t* fwd, int nbits, int num_docs, const int32_t* doc_ids, int len, int32_t* out) {
+  (void)num_docs;
+  if (len <= 0) return;
+  int first = doc_ids[0], last = doc_ids[len - 1];
+  int index = 0;
+  if (last - first + 1 == len && len >= 64) {
+    int bulk_start = (first + 31) & ~31;
+    int bulk_end = last & ~31;
+    for (int i = first; i < bulk_start; i++) out[index++] = fixedbit_read(fwd, i, nbits);
+    for (int i = bulk_start; i < bulk_end; i += 32) {
+      or_bitset_read_ints(fwd, i, nbits, 32, out + index); /* read32 */
+      index += 32;
+    }
+  }
+  for (int i = index; i < len; i++) out[i] = fixedbit_read(fwd, doc_ids[i], nbits);
+}
+
+/* ======================================================================================= dictionaries */
+
+static inline uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+static inline uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+static inline void put_be32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+static inline void put_be64(uint8_t* p, uint64_t v) { put_be32(p, (uint32_t)(v >> 32)); put_be32(p + 4, (uint32_t)v); }
+
+static inline int32_t dict_int(const or_column* c, int id) { return (int32_t)be32(c->dict + (int64_t)id * 4); }
+static inline int64_t dict_long(const or_column* c, int id) { return (int64_t)be64(c->dict + (int64_t)id * 8); }
+static inline float dict_float(const or_column* c, int id) {
+  uint32_t u = be32(c->dict + (int64_t)id * 4); float f; memcpy(&f, &u, 4); return f;
+}
+static inline double dict_double(const or_column* c, int id) {
+  uint64_t u = be64(c->dict + (int64_t)id * 8); double d; memcpy(&d, &u, 8); return d;
+}
+/* FixedByteValueReaderWriter.getUnpaddedString (seglocal/io/util/FixedByteValueReaderWriter.java:57-95):
+ * bytes up to the first padding byte. */
+static inline int dict_str(const or_column* c, int id, const uint8_t** p) {
+  const uint8_t* s = c->dict + (int64_t)id * c->entry_width;
+  int n = 0;
+  while (n < c->entry_width && s[n] != (uint8_t)c->padding_byte) n++;
+  *p = s;
+  return n;
+}
+
+/* Dictionary.readDoubleValues -> getDoubleValue per type (IntDictionary.java:62-64 etc.). */
+double or_dict_get_double(const or_column* c, int id) {
+  switch (c->data_type) {
+    case OR_INT: return (double)dict_int(c, id);
+    case OR_LONG: return (double)dict_long(c, id);
+    case OR_FLOAT: return (double)dict_float(c, id);
+    case OR_DOUBLE: return dict_double(c, id);
+    default: {
+      const uint8_t* p; int n = dict_str(c, id, &p);
+      char tmp[256]; if (n > 255) n = 255; memcpy(tmp, p, n); tmp[n] = 0;
+      return strtod(tmp, NULL); /* StringDictionary.getDoubleValue: Double.parseDouble */
+    }
+  }
+}
+
+/* Java Integer.parseInt / Long.parseLong: optional sign, decimal digits only, range-checked. */
+static int parse_java_long(const char* s, int64_t lo, int64_t hi, int64_t* out) {
+  const char* p = s;
+  int neg = 0;
+  if (*p == '-' || *p == '+') { neg = (*p == '-'); p++; }
+  if (!*p) return -1;
+  __int128 v = 0;
+  for (; *p; p++) {
+    if (*p < '0' || *p > '9') return -1;
+    v = v * 10 + (*p - '0');
+    if (v > (__int128)hi + 1) return -1;
+  }
+  if (neg) v = -v;
+  if (v < lo || v > hi) return -1;
+  *out = (int64_t)v;
+  return 0;
+}
+static int parse_java_double(const char* s, double* out) {
+  char* end; errno = 0;
+  double d = strtod(s, &end);
+  while (*end == ' ' || *end == 'd' || *end == 'D' || *end == 'f' || *end == 'F') end++;
+  if (end == s || *end) return -1;
+  *out = d;
+  return 0;
+}
+
+static int cmp_bytes(const uint8_t* a, int na, const uint8_t* b, int nb) {
+  int n = na < nb ? na : nb;
+  int c = memcmp(a, b, (size_t)n);
+  if (c) return c;
+  return na - nb;
+}
+
+/* BaseImmutableDictionary.binarySearch(int/long/float/double/String) (:97-230) behind
+ * {Int,Long,Float,Double,String}Dictionary.insertionIndexOf(String) (IntDictionary.java:32-34 etc.).
+ * *err = 1 when the literal does not parse for the column type (PredicateEvaluatorProvider.java:85-88 turns
+ * that into BadQueryRequestException). */
+int or_dict_insertion_index_of(const or_column* c, const char* lit, int* err) {
+  int low = 0, high = c->cardinality - 1;
+  *err = 0;
+  switch (c->data_type) {
+    case OR_INT: case OR_LONG: {
+      int64_t v;
+      if (parse_java_long(lit, c->data_type == OR_INT ? INT32_MIN : INT64_MIN,
+                          c->data_type == OR_INT ? INT32_MAX : INT64_MAX, &v)) { *err = 1; return 0; }
+      while (low <= high) {
+        int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+        int64_t m = c->data_type == OR_INT ? dict_int(c, mid) : dict_long(c, mid);
+        if (m < v) low = mid + 1; else if (m > v) high = mid - 1; else return mid;
+      }
+      return -(low + 1);
+    }
+    case OR_FLOAT: case OR_DOUBLE: {
+      double v;
+      if (parse_java_double(lit, &v)) { *err = 1; return 0; }
+      if (c->data_type == OR_FLOAT) v = (double)(float)v; /* Float.parseFloat */
+      while (low <= high) {
+        int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+        double m = c->data_type == OR_FLOAT ? (double)dict_float(c, mid) : dict_double(c, mid);
+        if (m < v) low = mid + 1; else if (m > v) high = mid - 1; else return mid;
+      }
+      return -(low + 1);
+    }
+    default: {
+      const uint8_t* lv = (const uint8_t*)lit;
+      int ln = (int)strlen(lit);
+      if (c->padding_byte == 0) {
+        while (low <= high) {
+          int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+          const uint8_t* p; int n = dict_str(c, mid, &p);
+          int r = cmp_bytes(p, n, lv, ln);
+          if (r < 0) low = mid + 1; else if (r > 0) high = mid - 1; else return mid;
+        }
+      } else { /* legacy non-zero padding: compare padded strings (BaseImmutableDictionary.java:215-228) */
+        uint8_t padded[4096];
+        int pn = ln;
+        if (ln < c->entry_width && c->entry_width <= (int)sizeof padded) {
+          memcpy(padded, lv, ln);
+          memset(padded + ln, c->padding_byte, c->entry_width - ln);
+          pn = c->entry_width;
+          lv = padded;
+        }
+        while (low <= high) {
+          int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
+          const uint8_t* p = c->dict + (int64_t)mid * c->entry_width;
+          int r = cmp_bytes(p, c->entry_width, lv, pn);
+          if (r < 0) low = mid + 1; else if (r > 0) high = mid - 1; else return mid;
+        }
+      }
+      return -(low + 1);
+    }
+  }
+}
+
+/* ---- dictionary creation (SegmentDictionaryCreator: sorted distinct values; dictId = rank) */
+
+/* Java Double.compare total order (used by Arrays.sort for the dictionary). */
+static int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  uint64_t ua, ub;
+  if (a != a) a = NAN; if (b != b) b = NAN; /* canonical NaN */
+  memcpy(&ua, &a, 8); memcpy(&ub, &b, 8);
+  int64_t sa = (int64_t)ua, sb = (int64_t)ub;
+  return sa == sb ? 0 : (sa < sb ? -1 : 1);
+}
+
+typedef struct { int64_t iv; double dv; int64_t row; } sort_rec;
+static int cmp_i64_rec(const void* a, const void* b) {
+  const sort_rec* x = a; const sort_rec* y = b;
+  if (x->iv != y->iv) return x->iv < y->iv ? -1 : 1;
+  return x->row < y->row ? -1 : (x->row > y->row);
+}
+static int cmp_f64_rec(const void* a, const void* b) {
+  const sort_rec* x = a; const sort_rec* y = b;
+  int c = java_double_compare(x->dv, y->dv);
+  if (c) return c;
+  return x->row < y->row ? -1 : (x->row > y->row);
+}
+
+static void pack_ids(const int32_t* ids, int64_t n, int bits, uint8_t* fwd) {
+  for (int64_t i = 0; i < n; i++) or_bitset_write_int(fwd, i, bits, ids[i]);
+}
+
+int or_build_column_i64(int data_type, const int64_t* values, int64_t n, uint8_t* dict_out, uint8_t* fwd_out,
+                        int* bits_out, int* width_out) {
+  sort_rec* r = malloc(sizeof(sort_rec) * (size_t)(n ? n : 1));
+  int32_t* ids = malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  for (int64_t i = 0; i < n; i++) { r[i].iv = values[i]; r[i].row = i; }
+  qsort(r, (size_t)n, sizeof(sort_rec), cmp_i64_rec);
+  int width = data_type == OR_INT ? 4 : 8;
+  int card = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (i == 0 || r[i].iv != r[i - 1].iv) {
+      if (width == 4) put_be32(dict_out + (int64_t)card * 4, (uint32_t)(int32_t)r[i].iv);
+      else put_be64(dict_out + (int64_t)card * 8, (uint64_t)r[i].iv);
+      card++;
+    }
+    ids[r[i].row] = card - 1;
+  }
+  int bits = or_num_bits_per_value(card - 1);
+  pack_ids(ids, n, bits, fwd_out);
+  *bits_out = bits; *width_out = width;
+  free(r); free(ids);
+  return card;
+}
+
+int or_build_column_f64(int data_type, const double* values, int64_t n, uint8_t* dict_out, uint8_t* fwd_out,
+                        int* bits_out, int* width_out) {
+  sort_rec* r = malloc(sizeof(sort_rec) * (size_t)(n ? n : 1));
+  int32_t* ids = malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  for (int64_t i = 0; i < n; i++) {
+    r[i].dv = data_type == OR_FLOAT ? (double)(float)values[i] : values[i];
+    r[i].row = i;
+  }
+  qsort(r, (size_t)n, sizeof(sort_rec), cmp_f64_rec);
+  int width = data_type == OR_FLOAT ? 4 : 8;
+  int card = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (i == 0 || java_double_compare(r[i].dv, r[i - 1].dv) != 0) {
+      if (width == 4) { float f = (float)r[i].dv; uint32_t u; memcpy(&u, &f, 4); put_be32(dict_out + (int64_t)card * 4, u); }
+      else { uint64_t u; memcpy(&u, &r[i].dv, 8); put_be64(dict_out + (int64_t)card * 8, u); }
+      card++;
+    }
+    ids[r[i].row] = card - 1;
+  }
+  int bits = or_num_bits_per_value(card - 1);
+  pack_ids(ids, n, bits, fwd_out);
+  *bits_out = bits; *width_out = width;
+  free(r); free(ids);
+  return card;
+}
+
+typedef struct { const uint8_t* p; int n; int64_t row; } str_rec;
+static int cmp_str_rec(const void* a, const void* b) {
+  const str_rec* x = a; const str_rec* y = b;
+  int c = cmp_bytes(x->p, x->n, y->p, y->n);
+  if (c) return c;
+  return x->row < y->row ? -1 : (x->row > y->row);
+}
+
+int or_build_column_str(const uint8_t* blob, const int64_t* offsets, int64_t n, uint8_t* dict_out,
+                        uint8_t* fwd_out, int* bits_out, int* width_out) {
+  str_rec* r = malloc(sizeof(str_rec) * (size_t)(n ? n : 1));
+  int32_t* ids = malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  int width = 0;
+  for (int64_t i = 0; i < n; i++) {
+    r[i].p = blob + offsets[i]; r[i].n = (int)(offsets[i + 1] - offsets[i]); r[i].row = i;
+    if (r[i].n > width) width = r[i].n;
+  }
+  if (width == 0) width = 1;
+  qsort(r, (size_t)n, sizeof(str_rec), cmp_str_rec);
+  int card = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (i == 0 || cmp_bytes(r[i].p, r[i].n, r[i - 1].p, r[i - 1].n) != 0) {
+      uint8_t* d = dict_out + (int64_t)card * width;
+      memset(d, 0, (size_t)width);
+      memcpy(d, r[i].p, (size_t)r[i].n);
+      card++;
+    }
+    ids[r[i].row] = card - 1;
+  }
+  int bits = or_num_bits_per_value(card - 1);
+  pack_ids(ids, n, bits, fwd_out);
+  *bits_out = bits; *width_out = width;
+  free(r); free(ids);
+  return card;
+}
+
+/* ======================================================================================= predicates */
+
+/* One dictionary-based PredicateEvaluator for one segment (core/operator/filter/predicate/). */
+typedef struct {
+  int always_true, always_false;
+  int kind;         /* 0 = range [start,end), 1 = dictId set, 2 = single id, 3 = not single id, 4 = not in set */
+  int start, end;
+  int id;
+  uint8_t* set;     /* card flags for kinds 1 / 4 */
+  int num_matching;
+} pred_eval;
+
+static int dict_index_of(const or_column* c, const char* lit, int* err) {
+  int idx = or_dict_insertion_index_of(c, lit, err);
+  return idx >= 0 ? idx : -1; /* BaseImmutableDictionary.indexOf :81-84 */
+}
+
+static int build_pred_eval(const or_segment* seg, const or_predicate* p, pred_eval* e, char* msg, int ml) {
+  memset(e, 0, sizeof *e);
+  if (p->column < 0 || p->column >= seg->num_columns) { snprintf(msg, ml, "bad predicate column"); return -1; }
+  const or_column* c = &seg->columns[p->column];
+  int err = 0;
+  switch (p->type) {
+    case OR_PRED_EQ: { /* EqualsPredicateEvaluatorFactory.java:86-99 */
+      int id = dict_index_of(c, p->values[0], &err);
+      if (err) goto bad;
+      e->kind = 2; e->id = id;
+      if (id >= 0) { if (c->cardinality == 1) e->always_true = 1; }
+      else e->always_false = 1;
+      return 0;
+    }
+    case OR_PRED_NOT_EQ: { /* NotEqualsPredicateEvaluatorFactory.java:88-102 */
+      int id = dict_index_of(c, p->values[0], &err);
+      if (err) goto bad;
+      e->kind = 3; e->id = id;
+      if (id >= 0) { if (c->cardinality == 1) e->always_false = 1; }
+      else e->always_true = 1;
+      return 0;
+    }
+    case OR_PRED_IN: case OR_PRED_NOT_IN: { /* InPredicateEvaluatorFactory.java:138-154, NotIn...:140-160 */
+      e->kind = p->type == OR_PRED_IN ? 1 : 4;
+      e->set = calloc((size_t)(c->cardinality ? c->cardinality : 1), 1);
+      int n = 0;
+      for (int i = 0; i < p->num_values; i++) {
+        int id = dict_index_of(c, p->values[i], &err);
+        if (err) goto bad;
+        if (id >= 0 && !e->set[id]) { e->set[id] = 1; n++; }
+      }
+      e->num_matching = n;
+      if (p->type == OR_PRED_IN) {
+        if (n == 0) e->always_false = 1; else if (n == c->cardinality) e->always_true = 1;
+      } else {
+        if (n == 0) e->always_true = 1; else if (n == c->cardinality) e->always_false = 1;
+      }
+      return 0;
+    }
+    case OR_PRED_RANGE: { /* SortedDictionaryBasedRangePredicateEvaluator (RangePredicateEvaluatorFactory.java:115-159) */
+      const char* lo = p->values[0];
+      const char* hi = p->values[1];
+      int start, end;
+      if (strcmp(lo, "*") == 0) start = 0;
+      else {
+        int ins = or_dict_insertion_index_of(c, lo, &err);
+        if (err) goto bad;
+        if (ins < 0) start = -(ins + 1); else start = p->lower_inclusive ? ins : ins + 1;
+      }
+      if (strcmp(hi, "*") == 0) end = c->cardinality;
+      else {
+        int ins = or_dict_insertion_index_of(c, hi, &err);
+        if (err) goto bad;
+        if (ins < 0) end = -(ins + 1); else end = p->upper_inclusive ? ins + 1 : ins;
+      }
+      e->kind = 0; e->start = start; e->end = end;
+      int nm = end - start;
+      if (nm <= 0) e->always_false = 1; else if (c->cardinality == nm) e->always_true = 1;
+      return 0;
+    }
+    default:
+      snprintf(msg, ml, "unsupported predicate type %d", p->type);
+      return -1;
+  }
+bad:
+  snprintf(msg, ml, "BadQueryRequestException: cannot convert literal for column %d", p->column);
+  free(e->set); e->set = NULL;
+  return -2;
+}
+
+static inline int pred_apply(const pred_eval* e, int id) {
+  switch (e->kind) {
+    case 0: return e->start <= id && e->end > id;
+    case 1: return e->set[id];
+    case 2: return e->id == id;
+    case 3: return e->id != id;
+    default: return !e->set[id];
+  }
+}
+
+/* ======================================================================================= filter operators */
+
+/* Operator tree after FilterPlanNode.constructPhysicalOperator (core/plan/FilterPlanNode.java:146-247) and
+ * FilterOperatorUtils.getAnd/OrFilterOperator (:87-135): EMPTY, MATCH_ALL, SCAN leaf, AND, OR, NOT. */
+enum { FN_EMPTY = 0, FN_ALL = 1, FN_SCAN = 2, FN_AND = 3, FN_OR = 4, FN_NOT = 5 };
+typedef struct fnode {
+  int type;
+  int pred;              /* SCAN: predicate index */
+  int nchild;
+  struct fnode** child;
+} fnode;
+
+static fnode* fn_new(int type) { fnode* n = calloc(1, sizeof(fnode)); n->type = type; return n; }
+static void fn_free(fnode* n) {
+  if (!n) return;
+  for (int i = 0; i < n->nchild; i++) fn_free(n->child[i]);
+  free(n->child); free(n);
+}
+
+/* Build from the postfix program, simplifying always-true/false leaves exactly as FilterPlanNode does. */
+static fnode* build_filter_tree(const or_query* q, const pred_eval* evals, char* msg, int ml) {
+  if (q->num_filter_ops == 0) return fn_new(FN_ALL);
+  fnode** stack = calloc((size_t)q->num_filter_ops + 1, sizeof(fnode*));
+  int sp = 0;
+  for (int i = 0; i < q->num_filter_ops; i++) {
+    const or_filter_op* op = &q->filter[i];
+    if (op->op == OR_OP_PRED) {
+      const pred_eval* e = &evals[op->arg];
+      fnode* n;
+      if (e->always_false) n = fn_new(FN_EMPTY);          /* FilterOperatorUtils.java:44-46 */
+      else if (e->always_true) n = fn_new(FN_ALL);        /* :47-48 */
+      else { n = fn_new(FN_SCAN); n->pred = op->arg; }
+      stack[sp++] = n;
+    } else if (op->op == OR_OP_NOT) {
+      if (sp < 1) goto bad;
+      fnode* c = stack[--sp];
+      fnode* n;
+      if (c->type == FN_EMPTY) { fn_free(c); n = fn_new(FN_ALL); }
+      else if (c->type == FN_ALL) { fn_free(c); n = fn_new(FN_EMPTY); }
+      else { n = fn_new(FN_NOT); n->nchild = 1; n->child = malloc(sizeof(fnode*)); n->child[0] = c; }
+      stack[sp++] = n;
+    } else {
+      int k = op->arg;
+      if (k < 1 || sp < k) goto bad;
+      fnode** kids = stack + sp - k;
+      int is_and = op->op == OR_OP_AND;
+      fnode* result = NULL;
+      fnode** keep = malloc(sizeof(fnode*) * (size_t)k);
+      int nk = 0;
+      for (int j = 0; j < k; j++) {
+        fnode* c = kids[j];
+        if (result) { fn_free(c); continue; }
+        if (is_and) {
+          if (c->type == FN_EMPTY) { result = c; continue; }      /* FilterPlanNode.java:152-155 */
+          if (c->type == FN_ALL) { fn_free(c); continue; }
+        } else {
+          if (c->type == FN_ALL) { result = c; continue; }        /* :167-170 */
+          if (c->type == FN_EMPTY) { fn_free(c); continue; }
+        }
+        keep[nk++] = c;
+      }
+      if (result) { for (int j = 0; j < nk; j++) fn_free(keep[j]); free(keep); }
+      else if (nk == 0) { free(keep); result = fn_new(is_and ? FN_ALL : FN_EMPTY); }
+      else if (nk == 1) { result = keep[0]; free(keep); }
+      else {
+        result = fn_new(is_and ? FN_AND : FN_OR);
+        if (is_and) {
+          /* reorderAndFilterChildOperators (FilterOperatorUtils.java:143-178): stable sort by priority
+           * AND=3, OR=4, scan=5 (no indexes in this model). */
+          fnode** sorted = malloc(sizeof(fnode*) * (size_t)nk);
+          int ns = 0;
+          for (int pr = 3; pr <= 5; pr++)
+            for (int j = 0; j < nk; j++) {
+              int p = keep[j]->type == FN_AND ? 3 : keep[j]->type == FN_OR ? 4 : 5;
+              if (p == pr) sorted[ns++] = keep[j];
+            }
+          free(keep);
+          keep = sorted;
+        }
+        result->nchild = nk; result->child = keep;
+      }
+      sp -= k;
+      stack[sp++] = result;
+    }
+  }
+  if (sp != 1) goto bad;
+  fnode* root = stack[0];
+  free(stack);
+  return root;
+bad:
+  for (int i = 0; i < sp; i++) fn_free(stack[i]);
+  free(stack);
+  snprintf(msg, ml, "malformed filter program");
+  return NULL;
+}
+
+/* ---- DocId iterators: SVScanDocIdIterator (:56-66), AndDocIdIterator (:40-67), OrDocIdIterator (:25-130),
+ * MatchAllDocIdIterator.  NOT is evaluated as a scan over its child (not part of the 0.10 FilterContext). */
+typedef struct iter {
+  int type;
+  int next_doc;            /* scan / and / all */
+  int64_t scanned;         /* scan: _numEntriesScanned */
+  const pred_eval* eval;
+  const or_column* col;
+  int num_docs;
+  int n;                   /* children */
+  struct iter** kids;
+  int* next_ids;           /* or: _nextDocIds */
+  int num_not_exhausted;   /* or */
+  int prev_doc;            /* or */
+  const fnode* node;       /* not */
+  const or_segment* seg;
+  const pred_eval* evals;
+  const or_query* q;
+} iter;
+
+static int it_next(iter* it);
+static int it_advance(iter* it, int target);
+
+static inline int scan_match(iter* it, int doc) {
+  return pred_apply(it->eval, fixedbit_read(it->col->fwd, doc, it->col->bits));
+}
+
+static int node_match(const fnode* n, const or_segment* seg, const pred_eval* evals, const or_query* q, int doc) {
+  switch (n->type) {
+    case FN_EMPTY: return 0;
+    case FN_ALL: return 1;
+    case FN_SCAN: {
+      const or_column* c = &seg->columns[q->predicates[n->pred].column];
+      return pred_apply(&evals[n->pred], fixedbit_read(c->fwd, doc, c->bits));
+    }
+    case FN_AND: for (int i = 0; i < n->nchild; i++) if (!node_match(n->child[i], seg, evals, q, doc)) return 0; return 1;
+    case FN_OR: for (int i = 0; i < n->nchild; i++) if (node_match(n->child[i], seg, evals, q, doc)) return 1; return 0;
+    default: return !node_match(n->child[0], seg, evals, q, doc);
+  }
+}
+
+static int it_next(iter* it) {
+  switch (it->type) {
+    case FN_EMPTY: return EOF_DOC;
+    case FN_ALL: return it->next_doc < it->num_docs ? it->next_doc++ : EOF_DOC;
+    case FN_SCAN: /* SVScanDocIdIterator.next :56-66 */
+      while (it->next_doc < it->num_docs) {
+        int d = it->next_doc++;
+        it->scanned++;
+        if (scan_match(it, d)) return d;
+      }
+      return EOF_DOC;
+    case FN_NOT:
+      while (it->next_doc < it->num_docs) {
+        int d = it->next_doc++;
+        it->scanned++;
+        if (!node_match(it->node->child[0], it->seg, it->evals, it->q, d)) return d;
+      }
+      return EOF_DOC;
+    case FN_AND: { /* AndDocIdIterator.next :40-67 */
+      int max_doc = it->next_doc, max_idx = -1, index = 0;
+      while (index < it->n) {
+        if (index == max_idx) { index++; continue; }
+        int d = it_advance(it->kids[index], max_doc);
+        if (d != EOF_DOC) {
+          if (d == max_doc) index++;
+          else { max_doc = d; max_idx = index; index = 0; }
+        } else return EOF_DOC;
+      }
+      it->next_doc = max_doc;
+      return it->next_doc++;
+    }
+    default: { /* FN_OR: OrDocIdIterator.next */
+      int next = INT32_MAX;
+      int exhausted = 0;
+      for (int i = 0; i < it->num_not_exhausted; i++) {
+        int d = it->next_ids[i];
+        if (d == it->prev_doc) {
+          d = it_next(it->kids[i]);
+          it->next_ids[i] = d;
+          if (d == EOF_DOC) { exhausted = 1; continue; }
+        }
+        if (d < next) next = d;
+      }
+      if (exhausted) { /* removeExhaustedIterators */
+        int w = 0;
+        for (int i = 0; i < it->num_not_exhausted; i++)
+          if (it->next_ids[i] != EOF_DOC) { it->kids[w] = it->kids[i]; it->next_ids[w] = it->next_ids[i]; w++; }
+        it->num_not_exhausted = w;
+      }
+      if (next != INT32_MAX) { it->prev_doc = next; return next; }
+      return EOF_DOC;
+    }
+  }
+}
+
+static int it_advance(iter* it, int target) {
+  switch (it->type) {
+    case FN_EMPTY: return EOF_DOC;
+    case FN_ALL: it->next_doc = target; return it_next(it);
+    case FN_SCAN: case FN_NOT: it->next_doc = target; return it_next(it); /* SVScanDocIdIterator.advance :69-72 */
+    case FN_AND: it->next_doc = target; return it_next(it);
+    default: { /* OrDocIdIterator.advance */
+      int next = INT32_MAX;
+      int exhausted = 0;
+      for (int i = 0; i < it->num_not_exhausted; i++) {
+        int d = it->next_ids[i];
+        if (d < target) {
+          d = it_advance(it->kids[i], target);
+          it->next_ids[i] = d;
+          if (d == EOF_DOC) { exhausted = 1; continue; }
+        }
+        if (d < next) next = d;
+      }
+      if (exhausted) {
+        int w = 0;
+        for (int i = 0; i < it->num_not_exhausted; i++)
+          if (it->next_ids[i] != EOF_DOC) { it->kids[w] = it->kids[i]; it->next_ids[w] = it->next_ids[i]; w++; }
+        it->num_not_exhausted = w;
+      }
+      if (next != INT32_MAX) { it->prev_doc = next; return next; }
+      return EOF_DOC;
+    }
+  }
+}
+
+typedef struct { iter** all; int n, cap; } iter_pool;
+static iter* it_build(const fnode* n, const or_segment* seg, const pred_eval* evals, const or_query* q,
+                      iter_pool* pool) {
+  iter* it = calloc(1, sizeof(iter));
+  if (pool->n == pool->cap) { pool->cap = pool->cap ? pool->cap * 2 : 16; pool->all = realloc(pool->all, sizeof(iter*) * pool->cap); }
+  pool->all[pool->n++] = it;
+  it->type = n->type;
+  it->num_docs = seg->num_docs;
+  it->seg = seg;
+  it->evals = evals;
+  it->q = q;
+  if (n->type == FN_SCAN) {
+    it->eval = &evals[n->pred];
+    it->col = &seg->columns[q->predicates[n->pred].column];
+  } else if (n->type == FN_NOT) {
+    it->node = n;
+  } else if (n->type == FN_AND || n->type == FN_OR) {
+    it->n = n->nchild;
+    it->kids = calloc((size_t)n->nchild, sizeof(iter*));
+    for (int i = 0; i < n->nchild; i++) it->kids[i] = it_build(n->child[i], seg, evals, q, pool);
+    if (n->type == FN_OR) {
+      it->next_ids = malloc(sizeof(int) * (size_t)n->nchild);
+      for (int i = 0; i < n->nchild; i++) it->next_ids[i] = -1;
+      it->num_not_exhausted = n->nchild;
+      it->prev_doc = -1;
+    }
+  }
+  return it;
+}
+static int64_t pool_scanned(iter_pool* p) {
+  int64_t s = 0;
+  for (int i = 0; i < p->n; i++) if (p->all[i]->type == FN_SCAN || p->all[i]->type == FN_NOT) s += p->all[i]->scanned;
+  return s;
+}
+static void pool_free(iter_pool* p) {
+  for (int i = 0; i < p->n; i++) { free(p->all[i]->kids); free(p->all[i]->next_ids); free(p->all[i]); }
+  free(p->all);
+}
+
+/* ======================================================================================= group-by */
+
+/* fastutil 8.2.3 it.unimi.dsi.fastutil.HashCommon.mix(int) — published: h = x * 0x9E3779B9; h ^ (h >>> 16). */
+static inline int32_t or_mix32(int32_t x) {
+  uint32_t h = (uint32_t)x * 0x9E3779B9u;
+  return (int32_t)(h ^ (h >> 16));
+}
+
+/* IntGroupIdMap (DictionaryBasedGroupKeyGenerator.java:1061-1152). */
+typedef struct { int32_t* kv; int capacity, mask, max_entries, size; } int_gid_map;
+static void igm_init(int_gid_map* m) {
+  m->capacity = 1 << 9;
+  int holder = m->capacity << 1;
+  m->kv = calloc((size_t)holder, sizeof(int32_t));
+  m->mask = holder - 1;
+  m->max_entries = (int)(m->capacity * 0.75f);
+  m->size = 0;
+}
+static void igm_expand(int_gid_map* m) {
+  m->capacity <<= 1;
+  int holder = m->capacity << 1;
+  int32_t* old = m->kv;
+  m->kv = calloc((size_t)holder, sizeof(int32_t));
+  m->mask = holder - 1;
+  m->max_entries <<= 1;
+  int oi = 0;
+  for (int i = 0; i < m->size; i++) {
+    while (old[oi] == 0) oi += 2;
+    int32_t key = old[oi], val = old[oi + 1];
+    int ni = (or_mix32(key) << 1) & m->mask;
+    while (m->kv[ni] != 0) ni = (ni + 2) & m->mask;
+    m->kv[ni] = key; m->kv[ni + 1] = val;
+    oi += 2;
+  }
+  free(old);
+}
+static int igm_get_group_id(int_gid_map* m, int32_t raw_key, int upper_bound) {
+  int32_t ik = raw_key + 1;
+  int idx = (or_mix32(ik) << 1) & m->mask;
+  for (;;) {
+    int32_t k = m->kv[idx];
+    if (k == ik) return m->kv[idx + 1];
+    if (k == 0) {
+      if (m->size >= upper_bound) return INVALID_ID;
+      int gid = m->size++;
+      m->kv[idx] = ik; m->kv[idx + 1] = gid;
+      if (m->size > m->max_entries) igm_expand(m);
+      return gid;
+    }
+    idx = (idx + 2) & m->mask;
+  }
+}
+
+/* Generic first-seen id map for LONG_MAP (fastutil Long2IntOpenHashMap.putIfAbsent, :675-683) and ARRAY_MAP
+ * (Object2IntOpenHashMap<IntArray>.computeIntIfAbsent, :886-893).  Only first-seen id assignment and the
+ * upper-bound cut are observable; slot order is not. */
+typedef struct { uint64_t* keys; int32_t* keylen_or_ids; int32_t* ids; int nkeyw; int64_t cap; int64_t size; } gen_map;
+static uint64_t hash_words(const uint64_t* w, int n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < n; i++) { h ^= w[i]; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 31; }
+  return h;
+}
+static void gm_init(gen_map* m, int nkeyw) {
+  m->nkeyw = nkeyw; m->cap = 1024; m->size = 0;
+  m->keys = malloc(sizeof(uint64_t) * (size_t)m->cap * nkeyw);
+  m->ids = malloc(sizeof(int32_t) * (size_t)m->cap);
+  for (int64_t i = 0; i < m->cap; i++) m->ids[i] = -1;
+  m->keylen_or_ids = NULL;
+}
+static void gm_grow(gen_map* m) {
+  int64_t oc = m->cap;
+  uint64_t* ok = m->keys; int32_t* oid = m->ids;
+  m->cap *= 2;
+  m->keys = malloc(sizeof(uint64_t) * (size_t)m->cap * m->nkeyw);
+  m->ids = malloc(sizeof(int32_t) * (size_t)m->cap);
+  for (int64_t i = 0; i < m->cap; i++) m->ids[i] = -1;
+  for (int64_t i = 0; i < oc; i++) {
+    if (oid[i] < 0) continue;
+    int64_t s = (int64_t)(hash_words(ok + i * m->nkeyw, m->nkeyw) & (uint64_t)(m->cap - 1));
+    while (m->ids[s] >= 0) s = (s + 1) & (m->cap - 1);
+    memcpy(m->keys + s * m->nkeyw, ok + i * m->nkeyw, sizeof(uint64_t) * m->nkeyw);
+    m->ids[s] = oid[i];
+  }
+  free(ok); free(oid);
+}
+static int gm_get_group_id(gen_map* m, const uint64_t* key, int upper_bound) {
+  int64_t s = (int64_t)(hash_words(key, m->nkeyw) & (uint64_t)(m->cap - 1));
+  for (;;) {
+    if (m->ids[s] < 0) {
+      if (m->size >= upper_bound) return INVALID_ID;
+      memcpy(m->keys + s * m->nkeyw, key, sizeof(uint64_t) * m->nkeyw);
+      int id = (int)m->size++;
+      m->ids[s] = id;
+      if (m->size * 2 > m->cap) gm_grow(m);
+      return id;
+    }
+    if (memcmp(m->keys + s * m->nkeyw, key, sizeof(uint64_t) * m->nkeyw) == 0) return m->ids[s];
+    s = (s + 1) & (m->cap - 1);
+  }
+}
+static void gm_free(gen_map* m) { free(m->keys); free(m->ids); }
+
+/* Per-segment group-by state: DictionaryBasedGroupKeyGenerator + DoubleGroupByResultHolder per function. */
+typedef struct {
+  int holder;
+  int nk;                    /* group-by columns */
+  int card[16];
+  int64_t upper_bound;       /* _globalGroupIdUpperBound */
+  uint8_t* flags;            /* ARRAY */
+  int64_t num_keys;          /* ARRAY */
+  int_gid_map imap;
+  gen_map gmap;              /* LONG_MAP (1 word) and ARRAY_MAP (nk words) */
+  int64_t* raw_of_gid;       /* gid -> raw key (INT/LONG map) */
+  int32_t* dictids_of_gid;   /* gid -> dictIds (ARRAY_MAP) */
+  int64_t ngid_cap;
+  double** vals;             /* per agg */
+  int64_t** avg_cnt;
+  int64_t vcap;
+} seg_groupby;
+
+static void sg_ensure(seg_groupby* g, const or_query* q, int64_t need) {
+  if (need <= g->vcap) return;
+  int64_t nc = g->vcap ? g->vcap : 1024;
+  while (nc < need) nc *= 2;
+  for (int a = 0; a < q->num_aggs; a++) {
+    g->vals[a] = realloc(g->vals[a], sizeof(double) * (size_t)nc);
+    g->avg_cnt[a] = realloc(g->avg_cnt[a], sizeof(int64_t) * (size_t)nc);
+    double dv = q->aggs[a].fn == OR_AGG_MIN ? INFINITY : q->aggs[a].fn == OR_AGG_MAX ? -INFINITY : 0.0;
+    for (int64_t i = g->vcap; i < nc; i++) { g->vals[a][i] = dv; g->avg_cnt[a][i] = 0; }
+  }
+  if (g->holder == OR_HOLDER_INT_MAP || g->holder == OR_HOLDER_LONG_MAP) {
+    g->raw_of_gid = realloc(g->raw_of_gid, sizeof(int64_t) * (size_t)nc);
+  } else if (g->holder == OR_HOLDER_ARRAY_MAP) {
+    g->dictids_of_gid = realloc(g->dictids_of_gid, sizeof(int32_t) * (size_t)nc * g->nk);
+  }
+  g->vcap = nc;
+}
+
+/* ---- result blobs */
+typedef struct { uint8_t* b; int64_t n, cap; } bbuf;
+static void bb_put(bbuf* b, const void* p, int64_t n) {
+  if (b->n + n > b->cap) { b->cap = (b->cap + n) * 2; b->b = realloc(b->b, (size_t)b->cap); }
+  memcpy(b->b + b->n, p, (size_t)n); b->n += n;
+}
+static void key_append_value(bbuf* b, const or_column* c, int id) {
+  if (c->data_type == OR_INT || c->data_type == OR_LONG) {
+    int64_t v = c->data_type == OR_INT ? dict_int(c, id) : dict_long(c, id);
+    bb_put(b, &v, 8);
+  } else if (c->data_type == OR_FLOAT || c->data_type == OR_DOUBLE) {
+    double v = c->data_type == OR_FLOAT ? (double)dict_float(c, id) : dict_double(c, id);
+    bb_put(b, &v, 8);
+  } else {
+    const uint8_t* p; int n = dict_str(c, id, &p);
+    uint32_t len = (uint32_t)n;
+    bb_put(b, &len, 4); bb_put(b, p, n);
+  }
+}
+
+typedef struct {
+  int64_t ngroups;
+  bbuf keys;
+  int64_t* koff; int64_t kcap;
+  double* vals;      /* [ngroups][naggs] */
+  int64_t* cnts;
+  int64_t vcap;
+  int64_t docs_scanned, in_filter, post_filter, total_docs;
+  int holder;
+  int limit_reached;
+  int status;
+  char msg[256];
+} seg_result;
+
+static void sr_add_group(seg_result* r, int naggs) {
+  if (r->ngroups + 2 > r->kcap) { r->kcap = (r->kcap + 2) * 2; r->koff = realloc(r->koff, sizeof(int64_t) * (size_t)r->kcap); }
+  if (r->ngroups + 1 > r->vcap) {
+    r->vcap = (r->vcap + 1) * 2;
+    r->vals = realloc(r->vals, sizeof(double) * (size_t)r->vcap * (naggs ? naggs : 1));
+    r->cnts = realloc(r->cnts, sizeof(int64_t) * (size_t)r->vcap * (naggs ? naggs : 1));
+  }
+}
+
+/* Columns projected by the operator (TransformOperator.getNumColumnsProjected): distinct columns referenced by
+ * group-by expressions and aggregation arguments. */
+static int num_projected(const or_query* q) {
+  int seen[256] = {0};
+  int n = 0;
+  for (int i = 0; i < q->num_group_by; i++) if (!seen[q->group_by[i]]) { seen[q->group_by[i]] = 1; n++; }
+  for (int i = 0; i < q->num_aggs; i++)
+    if (q->aggs[i].column >= 0 && !seen[q->aggs[i].column]) { seen[q->aggs[i].column] = 1; n++; }
+  return n;
+}
+
+/* AggregationGroupByOperator.getNextBlock (core/operator/query/AggregationGroupByOperator.java:62-79) on one
+ * segment: DocIdSetOperator blocks of <= 10000 docIds, DefaultGroupByExecutor.process (:117-147). */
+static void run_segment(const or_segment* seg, const or_query* q, seg_result* r) {
+  memset(r, 0, sizeof *r);
+  r->total_docs = seg->num_docs;
+  int np = q->num_predicates;
+  pred_eval* evals = calloc((size_t)(np ? np : 1), sizeof(pred_eval));
+  for (int i = 0; i < np; i++) {
+    int st = build_pred_eval(seg, &q->predicates[i], &evals[i], r->msg, sizeof r->msg);
+    if (st) { r->status = st; for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return; }
+  }
+  fnode* root = build_filter_tree(q, evals, r->msg, sizeof r->msg);
+  if (!root) { r->status = -1; for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return; }
+  iter_pool pool = {0};
+  iter* it = it_build(root, seg, evals, q, &pool);
+
+  /* DictionaryBasedGroupKeyGenerator ctor (:97-161): holder choice. */
+  seg_groupby g;
+  memset(&g, 0, sizeof g);
+  g.nk = q->num_group_by;
+  g.vals = calloc((size_t)q->num_aggs + 1, sizeof(double*));
+  g.avg_cnt = calloc((size_t)q->num_aggs + 1, sizeof(int64_t*));
+  long long card_product = 1;
+  int long_overflow = 0;
+  for (int i = 0; i < g.nk; i++) {
+    int card = seg->columns[q->group_by[i]].cardinality;
+    g.card[i] = card;
+    if (!long_overflow) {
+      if (card_product > INT64_MAX / card) long_overflow = 1;
+      else card_product *= card;
+    }
+  }
+  if (long_overflow) {
+    g.holder = OR_HOLDER_ARRAY_MAP; g.upper_bound = q->num_groups_limit;
+    gm_init(&g.gmap, g.nk);
+  } else if (card_product > INT32_MAX) {
+    g.holder = OR_HOLDER_LONG_MAP; g.upper_bound = q->num_groups_limit;
+    gm_init(&g.gmap, 1);
+  } else {
+    g.upper_bound = card_product < q->num_groups_limit ? card_product : q->num_groups_limit;
+    if (card_product > q->max_initial_result_holder_capacity) { g.holder = OR_HOLDER_INT_MAP; igm_init(&g.imap); }
+    else { g.holder = OR_HOLDER_ARRAY; g.flags = calloc((size_t)g.upper_bound + 1, 1); }
+  }
+  r->holder = g.holder;
+  if (g.holder == OR_HOLDER_ARRAY) sg_ensure(&g, q, g.upper_bound);
+
+  int32_t* docs = malloc(sizeof(int32_t) * MAX_DOC_PER_CALL);
+  int32_t* gids = malloc(sizeof(int32_t) * MAX_DOC_PER_CALL);
+  int32_t* dids[16];
+  for (int i = 0; i < g.nk; i++) dids[i] = malloc(sizeof(int32_t) * MAX_DOC_PER_CALL);
+  int32_t* mids = malloc(sizeof(int32_t) * MAX_DOC_PER_CALL);
+  double* dvals = malloc(sizeof(double) * MAX_DOC_PER_CALL);
+  int nproj = num_projected(q);
+
+  int eof = 0;
+  while (!eof) {
+    /* DocIdSetOperator.getNextBlock (core/operator/DocIdSetOperator.java:59-84) */
+    int pos = 0;
+    for (int i = 0; i < MAX_DOC_PER_CALL; i++) {
+      int d = it_next(it);
+      if (d == EOF_DOC) { eof = 1; break; }
+      docs[pos++] = d;
+    }
+    if (pos == 0) break;
+    r->docs_scanned += pos;
+    /* generateKeysForBlock: DataFetcher.readDictIds -> FixedBitSVForwardIndexReaderV2.readDictIds */
+    for (int i = 0; i < g.nk; i++) {
+      const or_column* c = &seg->columns[q->group_by[i]];
+      or_read_dict_ids(c->fwd, c->bits, seg->num_docs, docs, pos, dids[i]);
+    }
+    switch (g.holder) {
+      case OR_HOLDER_ARRAY: /* ArrayBasedHolder.processSingleValue (:259-323) */
+        for (int d = 0; d < pos; d++) {
+          int gid = 0;
+          for (int j = g.nk - 1; j >= 0; j--) gid = gid * g.card[j] + dids[j][d];
+          gids[d] = gid;
+        }
+        if (g.num_keys < g.upper_bound) /* markGroups (:296-308) */
+          for (int d = 0; d < pos; d++)
+            if (!g.flags[gids[d]]) { g.num_keys++; g.flags[gids[d]] = 1; if (g.num_keys == g.upper_bound) break; }
+        break;
+      case OR_HOLDER_INT_MAP: /* IntMapBasedHolder (:420-450) */
+        for (int d = 0; d < pos; d++) {
+          int raw = 0;
+          for (int j = g.nk - 1; j >= 0; j--) raw = raw * g.card[j] + dids[j][d];
+          int gid = igm_get_group_id(&g.imap, raw, (int)g.upper_bound);
+          if (gid >= 0) { sg_ensure(&g, q, gid + 1); g.raw_of_gid[gid] = raw; }
+          gids[d] = gid;
+        }
+        break;
+      case OR_HOLDER_LONG_MAP: /* LongMapBasedHolder (:644-683) */
+        for (int d = 0; d < pos; d++) {
+          uint64_t raw = 0;
+          for (int j = g.nk - 1; j >= 0; j--) raw = raw * (uint64_t)g.card[j] + (uint64_t)dids[j][d];
+          int gid = gm_get_group_id(&g.gmap, &raw, (int)g.upper_bound);
+          if (gid >= 0) { sg_ensure(&g, q, gid + 1); g.raw_of_gid[gid] = (int64_t)raw; }
+          gids[d] = gid;
+        }
+        break;
+      default: /* ArrayMapBasedHolder (:850-893) */
+        for (int d = 0; d < pos; d++) {
+          uint64_t key[16];
+          for (int j = 0; j < g.nk; j++) key[j] = (uint64_t)dids[j][d];
+          int gid = gm_get_group_id(&g.gmap, key, (int)g.upper_bound);
+          if (gid >= 0) {
+            sg_ensure(&g, q, gid + 1);
+            for (int j = 0; j < g.nk; j++) g.dictids_of_gid[(int64_t)gid * g.nk + j] = dids[j][d];
+          }
+          gids[d] = gid;
+        }
+        break;
+    }
+    /* aggregateGroupBySV per function, in query order, docs in block order. */
+    for (int a = 0; a < q->num_aggs; a++) {
+      const or_agg* ag = &q->aggs[a];
+      double* h = g.vals[a];
+      if (ag->fn == OR_AGG_COUNT) { /* CountAggregationFunction.java:90-96 */
+        for (int d = 0; d < pos; d++) if (gids[d] != INVALID_ID) h[gids[d]] = h[gids[d]] + 1;
+        continue;
+      }
+      const or_column* c = &seg->columns[ag->column];
+      or_read_dict_ids(c->fwd, c->bits, seg->num_docs, docs, pos, mids);   /* DataFetcher.readDoubleValues */
+      for (int d = 0; d < pos; d++) dvals[d] = or_dict_get_double(c, mids[d]);
+      switch (ag->fn) {
+        case OR_AGG_SUM: /* SumAggregationFunction.java:66-73 */
+          for (int d = 0; d < pos; d++) if (gids[d] != INVALID_ID) h[gids[d]] = h[gids[d]] + dvals[d];
+          break;
+        case OR_AGG_MIN: /* MinAggregationFunction.java:69-79 */
+          for (int d = 0; d < pos; d++) if (gids[d] != INVALID_ID && dvals[d] < h[gids[d]]) h[gids[d]] = dvals[d];
+          break;
+        case OR_AGG_MAX:
+          for (int d = 0; d < pos; d++) if (gids[d] != INVALID_ID && dvals[d] > h[gids[d]]) h[gids[d]] = dvals[d];
+          break;
+        default: /* AVG: AvgPair(sum, count) (AvgAggregationFunction.java:93-146) */
+          for (int d = 0; d < pos; d++)
+            if (gids[d] != INVALID_ID) { h[gids[d]] += dvals[d]; g.avg_cnt[a][gids[d]] += 1; }
+          break;
+      }
+    }
+  }
+  r->in_filter = pool_scanned(&pool);
+  r->post_filter = r->docs_scanned * nproj; /* AggregationGroupByOperator.java:94 */
+
+  /* Emit groups through getStringGroupKeys order: ARRAY ascending raw key; maps in id order (iteration order of
+   * hash maps is not observable after the combine). */
+  bbuf* kb = &r->keys;
+  int64_t ngid = 0;
+  if (g.holder == OR_HOLDER_ARRAY) ngid = g.upper_bound;
+  else if (g.holder == OR_HOLDER_INT_MAP) ngid = g.imap.size;
+  else ngid = g.gmap.size;
+  if (g.holder != OR_HOLDER_ARRAY && (ngid >= g.upper_bound)) r->limit_reached = 1;
+  for (int64_t gid = 0; gid < ngid; gid++) {
+    if (g.holder == OR_HOLDER_ARRAY && !g.flags[gid]) continue;
+    sr_add_group(r, q->num_aggs);
+    r->koff[r->ngroups] = kb->n;
+    int64_t raw = 0;
+    if (g.holder == OR_HOLDER_ARRAY) raw = gid;
+    else if (g.holder != OR_HOLDER_ARRAY_MAP) raw = g.raw_of_gid[gid];
+    for (int j = 0; j < g.nk; j++) {
+      int id;
+      if (g.holder == OR_HOLDER_ARRAY_MAP) id = g.dictids_of_gid[gid * g.nk + j];
+      else { id = (int)(raw % g.card[j]); raw /= g.card[j]; } /* getKeys (:608-624) */
+      key_append_value(kb, &seg->columns[q->group_by[j]], id);
+    }
+    for (int a = 0; a < q->num_aggs; a++) {
+      r->vals[r->ngroups * q->num_aggs + a] = g.vals[a][gid];
+      r->cnts[r->ngroups * q->num_aggs + a] = g.avg_cnt[a][gid];
+    }
+    r->ngroups++;
+  }
+  if (r->koff) r->koff[r->ngroups] = kb->n;
+
+  for (int a = 0; a < q->num_aggs; a++) { free(g.vals[a]); free(g.avg_cnt[a]); }
+  free(g.vals); free(g.avg_cnt); free(g.flags); free(g.raw_of_gid); free(g.dictids_of_gid);
+  if (g.holder == OR_HOLDER_INT_MAP) free(g.imap.kv);
+  if (g.holder == OR_HOLDER_LONG_MAP || g.holder == OR_HOLDER_ARRAY_MAP) gm_free(&g.gmap);
+  free(docs); free(gids); free(mids); free(dvals);
+  for (int i = 0; i < g.nk; i++) free(dids[i]);
+  pool_free(&pool);
+  fn_free(root);
+  for (int j = 0; j < np; j++) free(evals[j].set);
+  free(evals);
+}
+
+/* ======================================================================================= combine */
+
+typedef struct { const or_segment* segs; int nsegs; const or_query* q; seg_result* res; atomic_int next; } task_ctx;
+static void* worker(void* arg) {
+  task_ctx* t = arg;
+  for (;;) {
+    int i = atomic_fetch_add(&t->next, 1);
+    if (i >= t->nsegs) break;
+    run_segment(&t->segs[i], t->q, &t->res[i]);
+  }
+  return NULL;
+}
+
+/* blob-keyed map for GroupByCombineOperator._resultsMap */
+typedef struct { int64_t* slot; int64_t cap; } blob_map;
+static uint64_t hash_bytes(const uint8_t* p, int64_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (int64_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+  return h;
+}
+
+int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int nthreads, or_result* out,
+                       char* msg, int msg_len) {
+  memset(out, 0, sizeof *out);
+  if (q->num_group_by < 1 || q->num_group_by > 16) { snprintf(msg, msg_len, "need 1..16 group-by columns"); return -1; }
+  /* DictionaryBasedGroupKeyGenerator ctor: assert numGroupsLimit >= arrayBasedThreshold (:99) */
+  if (q->num_groups_limit < q->max_initial_result_holder_capacity) {
+    snprintf(msg, msg_len, "numGroupsLimit must be >= maxInitialResultHolderCapacity");
+    return -1;
+  }
+  seg_result* res = calloc((size_t)(nsegs ? nsegs : 1), sizeof(seg_result));
+  task_ctx t = {segs, nsegs, q, res, 0};
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > nsegs) nthreads = nsegs > 0 ? nsegs : 1;
+  pthread_t* th = malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, worker, &t);
+  for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+  free(th);
+  for (int i = 0; i < nsegs; i++)
+    if (res[i].status) {
+      snprintf(msg, msg_len, "%s", res[i].msg);
+      int st = res[i].status;
+      for (int j = 0; j < nsegs; j++) { free(res[j].keys.b); free(res[j].koff); free(res[j].vals); free(res[j].cnts); }
+      free(res);
+      return st;
+    }
+
+  /* GroupByCombineOperator.processSegments merge (:113-160), segments in order. */
+  int na = q->num_aggs;
+  int64_t limit = q->combine ? (int64_t)q->num_groups_limit * 2 : INT64_MAX; /* INTER_SEGMENT_NUM_GROUPS_LIMIT_FACTOR */
+  if (limit > INT32_MAX) limit = INT32_MAX;
+  int64_t counter = 0;
+  blob_map bm; bm.cap = 1024; bm.slot = malloc(sizeof(int64_t) * (size_t)bm.cap);
+  for (int64_t i = 0; i < bm.cap; i++) bm.slot[i] = -1;
+  bbuf kb = {0};
+  int64_t* koff = malloc(sizeof(int64_t) * 2); int64_t kcap = 2;
+  double* vals = NULL; int64_t* cnts = NULL; int64_t ng = 0, vcap = 0;
+  koff[0] = 0;
+  for (int s = 0; s < nsegs; s++) {
+    seg_result* r = &res[s];
+    out->num_docs_scanned += r->docs_scanned;
+    out->num_entries_scanned_in_filter += r->in_filter;
+    out->num_entries_scanned_post_filter += r->post_filter;
+    out->num_total_docs += r->total_docs;
+    out->holder_kind = r->holder;
+    out->num_groups_limit_reached |= r->limit_reached;
+    for (int64_t gi = 0; gi < r->ngroups; gi++) {
+      const uint8_t* k = r->keys.b + r->koff[gi];
+      int64_t kn = r->koff[gi + 1] - r->koff[gi];
+      uint64_t h = hash_bytes(k, kn);
+      int64_t sidx = (int64_t)(h & (uint64_t)(bm.cap - 1));
+      int64_t found = -1;
+      while (bm.slot[sidx] >= 0) {
+        int64_t cand = bm.slot[sidx];
+        if (koff[cand + 1] - koff[cand] == kn && memcmp(kb.b + koff[cand], k, (size_t)kn) == 0) { found = cand; break; }
+        sidx = (sidx + 1) & (bm.cap - 1);
+      }
+      const double* v = r->vals + gi * na;
+      const int64_t* c = r->cnts + gi * na;
+      if (found < 0) {
+        if (counter++ >= limit) continue; /* _numGroups.getAndIncrement() < _interSegmentNumGroupsLimit */
+        if (ng + 2 > kcap) { kcap *= 2; koff = realloc(koff, sizeof(int64_t) * (size_t)kcap); }
+        if (ng + 1 > vcap) { vcap = vcap ? vcap * 2 : 64; vals = realloc(vals, sizeof(double) * vcap * (na ? na : 1)); cnts = realloc(cnts, sizeof(int64_t) * vcap * (na ? na : 1)); }
+        bb_put(&kb, k, kn);
+        koff[ng + 1] = kb.n;
+        for (int a = 0; a < na; a++) { vals[ng * na + a] = v[a]; cnts[ng * na + a] = c[a]; }
+        bm.slot[sidx] = ng;
+        ng++;
+        if (ng * 2 > bm.cap) {
+          int64_t nc = bm.cap * 2;
+          int64_t* ns = malloc(sizeof(int64_t) * (size_t)nc);
+          for (int64_t i = 0; i < nc; i++) ns[i] = -1;
+          for (int64_t e = 0; e < ng; e++) {
+            uint64_t hh = hash_bytes(kb.b + koff[e], koff[e + 1] - koff[e]);
+            int64_t p = (int64_t)(hh & (uint64_t)(nc - 1));
+            while (ns[p] >= 0) p = (p + 1) & (nc - 1);
+            ns[p] = e;
+          }
+          free(bm.slot); bm.slot = ns; bm.cap = nc;
+        }
+      } else {
+        for (int a = 0; a < na; a++) { /* AggregationFunction.merge */
+          double* dst = &vals[found * na + a];
+          switch (q->aggs[a].fn) {
+            case OR_AGG_MIN: if (!(*dst < v[a])) *dst = v[a]; break; /* MinAggregationFunction.merge */
+            case OR_AGG_MAX: if (!(*dst > v[a])) *dst = v[a]; break;
+            case OR_AGG_COUNT: *dst = (double)((int64_t)*dst + (int64_t)v[a]); break; /* Long merge */
+            default: *dst += v[a]; cnts[found * na + a] += c[a]; break;        /* SUM / AvgPair.apply */
+          }
+        }
+      }
+    }
+  }
+  out->num_groups = ng;
+  out->key_blob = kb.b;
+  out->key_offsets = koff;
+  out->values = malloc(sizeof(double) * (size_t)(ng * na + 1));
+  out->avg_counts = malloc(sizeof(int64_t) * (size_t)(ng * na + 1));
+  for (int64_t gi = 0; gi < ng; gi++)
+    for (int a = 0; a < na; a++) {
+      out->values[a * ng + gi] = vals[gi * na + a];
+      out->avg_counts[a * ng + gi] = cnts[gi * na + a];
+    }
+  free(vals); free(cnts); free(bm.slot);
+  for (int j = 0; j < nsegs; j++) { free(res[j].keys.b); free(res[j].koff); free(res[j].vals); free(res[j].cnts); }
+  free(res);
+  return 0;
+}
+
+void or_free_result(or_result* r) {
+  free(r->key_blob); free(r->key_offsets); free(r->values); free(r->avg_counts);
+  memset(r, 0, sizeof *r);
+}
+
+int or_filter_bitmap(const or_segment* seg, const or_query* q, uint64_t* bits, char* msg, int ml) {
+  int np = q->num_predicates;
+  pred_eval* evals = calloc((size_t)(np ? np : 1), sizeof(pred_eval));
+  for (int i = 0; i < np; i++) {
+    int st = build_pred_eval(seg, &q->predicates[i], &evals[i], msg, ml);
+    if (st) { for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return st; }
+  }
+  fnode* root = build_filter_tree(q, evals, msg, ml);
+  if (!root) { for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return -1; }
+  memset(bits, 0, sizeof(uint64_t) * (size_t)((seg->num_docs + 63) / 64));
+  for (int d = 0; d < seg->num_docs; d++)
+    if (node_match(root, seg, evals, q, d)) bits[d >> 6] |= 1ull << (d & 63);
+  fn_free(root);
+  for (int j = 0; j < np; j++) free(evals[j].set);
+  free(evals);
+  return 0;
+}
+
+int64_t or_bytes_alg(const or_segment* seg, const or_query* q, const uint64_t* match) {
+  int is_filter[256] = {0}, is_other[256] = {0};
+  for (int i = 0; i < q->num_predicates; i++) is_filter[q->predicates[i].column] = 1;
+  for (int i = 0; i < q->num_group_by; i++) is_other[q->group_by[i]] = 1;
+  for (int i = 0; i < q->num_aggs; i++) if (q->aggs[i].column >= 0) is_other[q->aggs[i].column] = 1;
+  int64_t bytes = 0;
+  for (int c = 0; c < seg->num_columns && c < 256; c++) {
+    const or_column* col = &seg->columns[c];
+    if (!is_filter[c] && !is_other[c]) continue;
+    bytes += (int64_t)col->cardinality * col->entry_width; /* dictionary once per segment */
+    if (is_filter[c]) { bytes += or_fwd_num_bytes(seg->num_docs, col->bits); continue; }
+    int64_t nbytes = or_fwd_num_bytes(seg->num_docs, col->bits);
+    int64_t nlines = (nbytes + 127) / 128;
+    int64_t last_line = -1, lines = 0;
+    for (int64_t w = 0; w < (seg->num_docs + 63) / 64; w++) {
+      uint64_t m = match[w];
+      while (m) {
+        int b = __builtin_ctzll(m); m &= m - 1;
+        int64_t d = w * 64 + b;
+        int64_t bit0 = d * col->bits, bit1 = bit0 + col->bits - 1;
+        for (int64_t l = (bit0 >> 3) / 128; l <= (bit1 >> 3) / 128; l++)
+          if (l > last_line) { last_line = l; lines++; }
+      }
+    }
+    (void)nlines;
+    bytes += lines * 128;
+  }
+  return bytes;
+}
+
+/* ======================================================================================= synthetic data */
+
+uint64_t or_splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t or_seed(int column_index) { return (uint64_t)(0x5EED0000u + (uint32_t)column_index) << 32; }
+
+void or_zipf_cdf(int n, double s, double* cdf) {
+  double acc = 0.0;
+  for (int k = 0; k < n; k++) { acc += 1.0 / pow((double)(k + 1), s); cdf[k] = acc; }
+  for (int k = 0; k < n; k++) cdf[k] /= acc;
+  cdf[n - 1] = 1.0;
+}
+static inline double unit_double(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+void or_double_table(int n, int column_index, double lo, double hi, double* out) {
+  for (int i = 0; i < n; i++) out[i] = lo + (hi - lo) * unit_double(or_splitmix64(or_seed(column_index) ^ (uint64_t)(0xDB1E000000ull + i)));
+}
+static inline int zipf_rank(const double* cdf, int n, double u) {
+  int lo = 0, hi = n - 1; /* first k with cdf[k] > u */
+  while (lo < hi) { int mid = (lo + hi) >> 1; if (cdf[mid] > u) hi = mid; else lo = mid + 1; }
+  return lo;
+}
+void or_gen_i64(const or_gen_spec* sp, int64_t row0, int64_t n, int64_t* out) {
+  uint64_t seed = or_seed(sp->column_index);
+  for (int64_t i = 0; i < n; i++) {
+    uint64_t h = or_splitmix64(seed ^ (uint64_t)(row0 + i));
+    if (sp->kind == OR_GEN_UNIFORM) out[i] = sp->lo + (int64_t)(h % (uint64_t)(sp->hi - sp->lo));
+    else out[i] = sp->ids[zipf_rank(sp->cdf, sp->n, unit_double(h))];
+  }
+}
+void or_gen_f64(const or_gen_spec* sp, int64_t row0, int64_t n, double* out) {
+  uint64_t seed = or_seed(sp->column_index);
+  for (int64_t i = 0; i < n; i++) {
+    uint64_t h = or_splitmix64(seed ^ (uint64_t)(row0 + i));
+    out[i] = sp->table[h % (uint64_t)sp->n];
+  }
+}

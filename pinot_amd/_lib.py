@@ -1,0 +1,177 @@
+"""ctypes binding of libpinotgpu.so (the C ABI in include/pinotgpu.h).
+
+This is the same binding a Java maintainer writes with JNI/Panama; here it serves the
+Python host layer, the tests and bench.py.  The product path has no CPU fallback: if the HIP library is
+missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+from .build import LIB_PATH
+
+c_int = ctypes.c_int
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_f64p = ctypes.POINTER(ctypes.c_double)
+c_voidp = ctypes.c_void_p
+c_char_pp = ctypes.POINTER(ctypes.c_char_p)
+
+PGPU_OK = 0
+PGPU_ERR_INVALID_ARGUMENT = -1
+PGPU_ERR_BAD_QUERY = -2
+PGPU_ERR_UNSUPPORTED = -3
+PGPU_ERR_DEVICE = -4
+PGPU_ERR_OUT_OF_MEMORY = -5
+PGPU_ERR_NOT_FOUND = -6
+
+INT, LONG, FLOAT, DOUBLE, STRING = 0, 1, 2, 3, 4
+TYPE_NAMES = {"INT": INT, "LONG": LONG, "FLOAT": FLOAT, "DOUBLE": DOUBLE, "STRING": STRING}
+FWD_FIXED_BIT, FWD_SORTED_PAIRS = 0, 1
+PRED_EQ, PRED_NOT_EQ, PRED_IN, PRED_NOT_IN, PRED_RANGE = 0, 1, 2, 3, 4
+OP_PRED, OP_AND, OP_OR, OP_NOT = 0, 1, 2, 3
+AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
+SLOT_COUNT, SLOT_SUM_I64, SLOT_SUM_F64, SLOT_MIN_KEY, SLOT_MAX_KEY = 0, 1, 2, 3, 4
+GEN_UNIFORM, GEN_ZIPF, GEN_TABLE = 0, 1, 2
+
+
+class ColumnBuffers(ctypes.Structure):
+    _fields_ = [("cardinality", c_i32), ("bits_per_element", c_i32), ("entry_width", c_i32),
+                ("padding_byte", c_i32), ("fwd_format", c_i32), ("reserved", c_i32),
+                ("dict", c_voidp), ("dict_len", c_i64), ("fwd", c_voidp), ("fwd_len", c_i64)]
+
+
+class SegmentDesc(ctypes.Structure):
+    _fields_ = [("num_docs", c_i32), ("num_columns", c_i32), ("columns", ctypes.POINTER(ColumnBuffers))]
+
+
+class PredicateC(ctypes.Structure):
+    _fields_ = [("type", c_i32), ("column", c_i32), ("num_values", c_i32), ("lower_inclusive", c_i32),
+                ("values", c_char_pp), ("upper_inclusive", c_i32), ("reserved", c_i32)]
+
+
+class FilterOpC(ctypes.Structure):
+    _fields_ = [("op", c_i32), ("arg", c_i32)]
+
+
+class AggC(ctypes.Structure):
+    _fields_ = [("fn", c_i32), ("column", c_i32)]
+
+
+class QueryC(ctypes.Structure):
+    _fields_ = [("num_predicates", c_i32), ("num_filter_ops", c_i32), ("predicates", ctypes.POINTER(PredicateC)),
+                ("filter", ctypes.POINTER(FilterOpC)), ("num_group_by", c_i32), ("num_aggs", c_i32),
+                ("group_by", c_i32p), ("aggs", ctypes.POINTER(AggC)), ("num_groups_limit", c_i32),
+                ("reserved", c_i32)]
+
+
+class GenColumnC(ctypes.Structure):
+    _fields_ = [("kind", c_i32), ("column_index", c_i32), ("lo", c_i64), ("hi", c_i64), ("n", c_i32),
+                ("reserved", c_i32), ("cdf", c_f64p), ("ids", c_i64p), ("table", c_f64p)]
+
+
+class PinotGpuError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("pgpu error %d: %s" % (code, message))
+        self.code = code
+        self.message = message
+
+
+class BadQueryRequestException(PinotGpuError):
+    """PGPU_ERR_BAD_QUERY: mirrors org.apache.pinot.spi.exception.BadQueryRequestException."""
+
+
+class UnsupportedQueryError(PinotGpuError):
+    """PGPU_ERR_UNSUPPORTED: the query shape is outside the GPU path."""
+
+
+_PROTOS = {
+    "pgpu_abi_version": (c_int, []),
+    "pgpu_last_error": (c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "pgpu_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "pgpu_table_create": (c_int, [c_int, c_int, c_char_pp, c_i32p, ctypes.POINTER(c_voidp)]),
+    "pgpu_table_destroy": (c_int, [c_voidp]),
+    "pgpu_pin_segment": (c_int, [c_voidp, ctypes.POINTER(SegmentDesc), c_i64p]),
+    "pgpu_unpin_segment": (c_int, [c_voidp, c_i64]),
+    "pgpu_table_num_segments": (c_int, [c_voidp, c_i32p]),
+    "pgpu_table_device_bytes": (c_i64, [c_voidp]),
+    "pgpu_table_add_dictionary_values": (c_int, [c_voidp, c_int, c_i64, c_i64p, c_f64p, c_u8p, c_i64p]),
+    "pgpu_table_dictionary_size": (c_int, [c_voidp, c_int, c_i64p]),
+    "pgpu_table_dictionary_i64": (c_int, [c_voidp, c_int, c_i64p]),
+    "pgpu_table_dictionary_f64": (c_int, [c_voidp, c_int, c_f64p]),
+    "pgpu_table_dictionary_str": (c_int, [c_voidp, c_int, c_u8p, c_i64, c_i64p]),
+    "pgpu_read_dict_ids": (c_int, [c_voidp, c_i64, c_int, c_i32p, c_i32, c_i32p]),
+    "pgpu_unpack_fixed_bit_device": (c_int, [c_voidp, c_i64, c_i32, c_i64, c_i64, c_voidp, c_voidp]),
+    "pgpu_plan_create": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), ctypes.POINTER(c_voidp)]),
+    "pgpu_plan_destroy": (c_int, [c_voidp]),
+    "pgpu_plan_layout": (c_int, [c_voidp, c_i32p, c_i64p, c_i32p]),
+    "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
+    "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
+    "pgpu_execute_groupby": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp,
+                                     ctypes.POINTER(c_voidp)]),
+    "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),
+    "pgpu_result_num_groups": (c_int, [c_voidp, c_i64p]),
+    "pgpu_result_group_ids": (c_int, [c_voidp, c_i32p]),
+    "pgpu_result_values": (c_int, [c_voidp, c_int, c_f64p]),
+    "pgpu_result_avg_counts": (c_int, [c_voidp, c_int, c_i64p]),
+    "pgpu_result_values_i64": (c_int, [c_voidp, c_int, c_i64p]),
+    "pgpu_result_stats": (c_int, [c_voidp, c_i64p]),
+    "pgpu_result_destroy": (c_int, [c_voidp]),
+    "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
+    "pgpu_generate_segment": (c_int, [c_voidp, ctypes.POINTER(GenColumnC), c_i32, c_i64, c_i32, c_i64p]),
+    "pgpu_segment_column_info": (c_int, [c_voidp, c_i64, c_int, c_i32p, c_i32p, c_i64p, c_i64p]),
+    "pgpu_segment_column_bytes": (c_int, [c_voidp, c_i64, c_int, c_u8p, c_u8p]),
+}
+
+_lib = None
+
+
+def exported_symbols():
+    return sorted(_PROTOS)
+
+
+def load(path=None):
+    """Loads libpinotgpu.so (dlopen only: no GPU call is made)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError("libpinotgpu.so is not built (%s); run `python -m pinot_amd.build` "
+                          "or __graft_entry__.build()" % p)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pgpu_abi_version() != 1:
+        raise ImportError("libpinotgpu.so ABI mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error():
+    lib = load()
+    buf = ctypes.create_string_buffer(2048)
+    lib.pgpu_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(code):
+    if code == PGPU_OK:
+        return
+    msg = last_error()
+    if code == PGPU_ERR_BAD_QUERY:
+        raise BadQueryRequestException(code, msg)
+    if code == PGPU_ERR_UNSUPPORTED:
+        raise UnsupportedQueryError(code, msg)
+    raise PinotGpuError(code, msg)
+
+
+def ptr(arr, ctype):
+    """Pointer to a numpy array's data (keeps no reference: the caller holds the array)."""
+    return arr.ctypes.data_as(ctypes.POINTER(ctype))

@@ -1,0 +1,107 @@
+// internal.h — device-side data layout shared by the gfx950 kernels (kernels.hip) and the host runtime
+// (runtime.cpp).  Not part of the ABI.
+//
+// HBM layout of a pinned segment column (one hipMalloc per segment, columns packed back to back):
+//   fwd   : Pinot's forward-index bytes verbatim (MSB-first, big-endian bit packing of
+//           FixedBitSVForwardIndexReaderV2), read as big-endian u32 words, zero-padded to
+//           ceil(numDocs/32) * bits words + 4 spare words so that a 32-doc group load and a two-word gather
+//           never leave the allocation;
+//   lut   : int32 local dictId -> table-global dictId (group-by columns; built lazily, rebuilt when the
+//           table's global dictionary grows);
+//   dkey  : int64 per dictId: the value (INT/LONG) or an order-preserving key of the IEEE double
+//           (FLOAT/DOUBLE) — the operand of SUM over integers and of MIN/MAX;
+//   dval  : double per dictId — the operand of SUM/AVG over FLOAT/DOUBLE.
+#pragma once
+#include <stdint.h>
+
+namespace pgpu {
+
+constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
+constexpr int kDocsPerLane = 32;            // one lane owns a 32-doc group = `bits` u32 words
+constexpr int kTileDocs = kBlock * kDocsPerLane;  // 8192 docs per tile
+constexpr int kMaxQueryCols = 16;           // distinct columns referenced by one query
+constexpr int kMaxLeaves = 16;              // predicate leaves
+constexpr int kMaxOps = 48;                 // postfix filter program length
+constexpr int kMaxKeys = 8;                 // group-by columns handled on the GPU
+constexpr int kMaxSlots = 24;               // accumulator rows of the group table
+constexpr int kMaxStack = 8;                // filter evaluation stack depth
+constexpr int kFwdPadWords = 4;
+
+enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3 };
+enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
+enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
+enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };
+
+// One predicate leaf evaluated against one segment: dictId in [lo, lo + span) (RANGE), bit set in `set`
+// (SET), constant (ALL / NONE); `negate` flips the result (NOT_EQ / NOT_IN).
+struct KLeaf {
+  int32_t kind;
+  int32_t negate;
+  uint32_t lo;
+  uint32_t span;
+  const uint32_t* set;
+};
+
+// One query column of one segment.
+struct KCol {
+  const uint32_t* fwd;
+  const int32_t* lut;
+  const int64_t* dkey;
+  const double* dval;
+  int32_t bits;
+  int32_t pad;
+};
+
+// Per-plan, per-segment record (uploaded once per plan): a KSegHdr followed by num_cols KCol and num_leaves
+// KLeaf; records are seg_stride bytes apart.
+struct KSegHdr {
+  int32_t num_docs;
+  int32_t tile_base;  // first tile of this segment in the plan's tile space
+  int32_t num_tiles;
+  int32_t pad;
+};
+
+struct KParams {
+  const uint8_t* segs;     // num_segs records of seg_stride bytes
+  int32_t seg_stride;
+  int32_t num_cols;
+  int32_t num_segs;
+  int32_t num_tiles;
+  int32_t num_ops;         // 0 = match all
+  int32_t pure_and;        // program is LEAF... AND(n): evaluate leaves with early exit, no stack
+  int32_t ops[kMaxOps];    // (opcode << 16) | arg
+  int32_t num_leaves;
+  int32_t leaf_col[kMaxLeaves];
+  int32_t num_keys;
+  int32_t key_col[kMaxKeys];
+  int64_t key_stride[kMaxKeys];
+  int64_t num_keys_total;  // dense table width G, or hash capacity
+  int32_t num_slots;
+  int32_t slot_kind[kMaxSlots];
+  int32_t slot_col[kMaxSlots];
+  uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
+  uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
+  unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
+  unsigned long long* stats;      // [0] docs matched
+};
+
+// Host-callable launchers (kernels.hip).
+int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
+int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
+int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
+                      unsigned long long* hash_keys, void* stream);
+int launch_filter_groupby(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
+int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int32_t num_slots, int64_t num_keys,
+                        int32_t num_blocks, uint64_t* out, void* stream);
+int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
+                   unsigned long long* counter, uint64_t* out_keys, uint64_t* out_slots, int64_t out_cap,
+                   void* stream);
+int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
+// Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.
+int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,
+                         const int32_t* code_to_pos, int32_t n_codes, int64_t row0, int32_t num_docs,
+                         int32_t* pos_out, uint32_t* presence, void* stream);
+int launch_gen_pack(const int32_t* pos, const int32_t* pos_to_id, int32_t num_docs, int32_t bits, uint32_t* fwd_out,
+                    void* stream);
+
+}  // namespace pgpu

@@ -1,0 +1,1631 @@
+// runtime.cpp — host runtime of libpinotgpu.so: tables, pinned segments, global dictionaries, query plans and
+// results behind the C ABI of include/pinotgpu.h.
+//
+// What runs where:
+//   host  : per-segment predicate translation into dictId space (the PredicateEvaluators of
+//           core/operator/filter/predicate/, once per segment per query, O(log card) each), filter constant
+//           folding (FilterPlanNode.java:146-247), group-key layout (DictionaryBasedGroupKeyGenerator key math
+//           over the table-global dictionaries), result decoding;
+//   device: everything per document (kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pinotgpu.h"
+#include "internal.h"
+
+using namespace pgpu;
+
+// ================================================================================================ errors
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                               \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      return fail(_e == hipErrorOutOfMemory ? PGPU_ERR_OUT_OF_MEMORY : PGPU_ERR_DEVICE, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(_e), __FILE__, __LINE__);                                \
+  } while (0)
+
+#define TRY(expr)          \
+  do {                     \
+    int _rc = (expr);      \
+    if (_rc) return _rc;   \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+// Device buffer that only grows (hipFree synchronises the device; growth is rare after warm-up).
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    size_t c = std::max<size_t>(n + n / 4, 4096);
+    HIP_TRY(hipMalloc(&p, c));
+    cap = c;
+    return 0;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct HostPinned {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    size_t c = std::max<size_t>(n + n / 4, 4096);
+    HIP_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
+    cap = c;
+    return 0;
+  }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// ================================================================================================ values
+inline uint32_t rd_be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+inline uint64_t rd_be64(const uint8_t* p) { return ((uint64_t)rd_be32(p) << 32) | rd_be32(p + 4); }
+inline void wr_be32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+inline void wr_be64(uint8_t* p, uint64_t v) { wr_be32(p, (uint32_t)(v >> 32)); wr_be32(p + 4, (uint32_t)v); }
+
+// Order-preserving int64 key of a double (MIN/MAX operand on the device).
+inline int64_t double_key(double d) {
+  int64_t b;
+  memcpy(&b, &d, 8);
+  return b >= 0 ? b : (b ^ INT64_MAX);
+}
+inline double key_double(int64_t k) {
+  int64_t b = k >= 0 ? k : (k ^ INT64_MAX);
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}
+
+bool is_int_type(int t) { return t == PGPU_INT || t == PGPU_LONG; }
+bool is_fp_type(int t) { return t == PGPU_FLOAT || t == PGPU_DOUBLE; }
+
+// PinotDataBitSet.getNumBitsPerValue (seglocal/io/util/PinotDataBitSet.java:59-70): bit length, at least 1.
+int num_bits_per_value(int max_value) {
+  if (max_value <= 1) return 1;
+  int n = 0;
+  while (max_value) { n++; max_value >>= 1; }
+  return n;
+}
+
+// Strict decimal conversion of Integer.parseInt / Long.parseLong.
+bool parse_long(const char* s, int64_t lo, int64_t hi, int64_t* out) {
+  const char* p = s;
+  bool neg = false;
+  if (*p == '+' || *p == '-') { neg = *p == '-'; ++p; }
+  if (!*p) return false;
+  unsigned __int128 v = 0;
+  for (; *p; ++p) {
+    if (*p < '0' || *p > '9') return false;
+    v = v * 10 + (unsigned)(*p - '0');
+    if (v > ((unsigned __int128)1 << 64)) return false;
+  }
+  __int128 sv = neg ? -(__int128)v : (__int128)v;
+  if (sv < lo || sv > hi) return false;
+  *out = (int64_t)sv;
+  return true;
+}
+// Double.parseDouble / Float.parseFloat (decimal and the Java 'd'/'f' suffixes).
+bool parse_double(const char* s, double* out) {
+  char* end = nullptr;
+  errno = 0;
+  double d = strtod(s, &end);
+  if (end == s) return false;
+  while (*end == 'd' || *end == 'D' || *end == 'f' || *end == 'F' || *end == ' ') ++end;
+  if (*end) return false;
+  *out = d;
+  return true;
+}
+
+int cmp_bytes(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
+  int c = memcmp(a, b, std::min(na, nb));
+  if (c) return c;
+  return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+// ================================================================================================ model
+// Host copy of one dictionary (segment-local or table-global), sorted ascending.
+struct Dict {
+  int type = PGPU_INT;
+  std::vector<int64_t> iv;       // INT / LONG
+  std::vector<double> dv;        // FLOAT / DOUBLE
+  std::vector<std::string> sv;   // STRING (unpadded)
+  size_t size() const { return is_int_type(type) ? iv.size() : is_fp_type(type) ? dv.size() : sv.size(); }
+};
+
+struct Column {
+  int32_t card = 0, bits = 0, entry_width = 0, padding = 0;
+  int64_t fwd_bytes = 0;            // Pinot byte length of the forward index
+  uint32_t* d_fwd = nullptr;        // inside the segment's allocation
+  int64_t fwd_words = 0;            // padded words
+  Dict dict;                        // parsed local dictionary
+  std::vector<uint8_t> raw_dict;    // BIG_ENDIAN bytes as pinned (string padding semantics, column_bytes)
+  // lazily built device arrays
+  int32_t* d_lut = nullptr;
+  uint64_t lut_version = ~0ull;
+  int64_t* d_key = nullptr;
+  double* d_val = nullptr;
+};
+
+struct Segment {
+  int64_t handle = 0;
+  int32_t num_docs = 0;
+  void* d_block = nullptr;
+  std::vector<Column> cols;
+};
+
+struct Scratch {
+  DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap;
+  HostPinned stage;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  void release() {
+    segrec.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
+    ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release();
+    for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
+  }
+};
+
+struct GenScratch {
+  DevBuf pos, presence, code_to_pos, cdf, pos_to_id;
+};
+
+}  // namespace
+
+struct pgpu_table_s {
+  int device = 0;
+  std::vector<std::string> names;
+  std::vector<int32_t> types;
+  std::mutex mu;
+  std::map<int64_t, std::unique_ptr<Segment>> segments;
+  int64_t next_handle = 1;
+  std::vector<Dict> global;
+  std::vector<uint64_t> global_version;
+  hipStream_t stream = nullptr;
+  std::vector<std::unique_ptr<Scratch>> scratch_pool;
+  GenScratch gen;
+  int64_t device_bytes = 0;
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------ dictionaries
+int parse_dictionary(int type, const pgpu_column_buffers& cb, Dict* d) {
+  d->type = type;
+  const int64_t card = cb.cardinality;
+  if (card < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "negative cardinality");
+  const int w = cb.entry_width;
+  if (card > 0 && (!cb.dict || cb.dict_len < card * (int64_t)w))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "dictionary buffer too small (%lld < %lld x %d)", (long long)cb.dict_len,
+                (long long)card, w);
+  switch (type) {
+    case PGPU_INT:
+      if (w != 4) return fail(PGPU_ERR_INVALID_ARGUMENT, "INT dictionary entry width %d", w);
+      d->iv.resize(card);
+      for (int64_t i = 0; i < card; ++i) d->iv[i] = (int32_t)rd_be32(cb.dict + i * 4);
+      break;
+    case PGPU_LONG:
+      if (w != 8) return fail(PGPU_ERR_INVALID_ARGUMENT, "LONG dictionary entry width %d", w);
+      d->iv.resize(card);
+      for (int64_t i = 0; i < card; ++i) d->iv[i] = (int64_t)rd_be64(cb.dict + i * 8);
+      break;
+    case PGPU_FLOAT:
+      if (w != 4) return fail(PGPU_ERR_INVALID_ARGUMENT, "FLOAT dictionary entry width %d", w);
+      d->dv.resize(card);
+      for (int64_t i = 0; i < card; ++i) {
+        uint32_t u = rd_be32(cb.dict + i * 4);
+        float f;
+        memcpy(&f, &u, 4);
+        d->dv[i] = f;
+      }
+      break;
+    case PGPU_DOUBLE:
+      if (w != 8) return fail(PGPU_ERR_INVALID_ARGUMENT, "DOUBLE dictionary entry width %d", w);
+      d->dv.resize(card);
+      for (int64_t i = 0; i < card; ++i) {
+        uint64_t u = rd_be64(cb.dict + i * 8);
+        memcpy(&d->dv[i], &u, 8);
+      }
+      break;
+    case PGPU_STRING:
+      d->sv.resize(card);
+      for (int64_t i = 0; i < card; ++i) {  // FixedByteValueReaderWriter.getUnpaddedString (:57-95)
+        const uint8_t* s = cb.dict + i * w;
+        int n = 0;
+        while (n < w && s[n] != (uint8_t)cb.padding_byte) ++n;
+        d->sv[i].assign(reinterpret_cast<const char*>(s), n);
+      }
+      break;
+    default:
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "unsupported data type %d", type);
+  }
+  return 0;
+}
+
+bool dbl_less(double a, double b) {  // Double.compare order for the sorted global dictionary
+  if (a < b) return true;
+  if (a > b) return false;
+  int64_t x, y;
+  memcpy(&x, &a, 8);
+  memcpy(&y, &b, 8);
+  return x < y;
+}
+
+// Merges sorted `src` into the global dictionary `dst`; returns true if it grew.
+bool merge_dict(Dict& dst, const Dict& src) {
+  const size_t before = dst.size();
+  if (is_int_type(dst.type)) {
+    std::vector<int64_t> out;
+    out.reserve(dst.iv.size() + src.iv.size());
+    std::set_union(dst.iv.begin(), dst.iv.end(), src.iv.begin(), src.iv.end(), std::back_inserter(out));
+    dst.iv.swap(out);
+  } else if (is_fp_type(dst.type)) {
+    std::vector<double> s = src.dv;
+    std::sort(s.begin(), s.end(), dbl_less);
+    std::vector<double> out;
+    out.reserve(dst.dv.size() + s.size());
+    std::set_union(dst.dv.begin(), dst.dv.end(), s.begin(), s.end(), std::back_inserter(out), dbl_less);
+    dst.dv.swap(out);
+  } else {
+    std::vector<std::string> s = src.sv;
+    std::sort(s.begin(), s.end());
+    std::vector<std::string> out;
+    out.reserve(dst.sv.size() + s.size());
+    std::set_union(dst.sv.begin(), dst.sv.end(), s.begin(), s.end(), std::back_inserter(out));
+    dst.sv.swap(out);
+  }
+  return dst.size() != before;
+}
+
+// BaseImmutableDictionary.insertionIndexOf behind PredicateUtils.getStoredValue (Dictionary.java:49-100,
+// BaseImmutableDictionary.java:97-230).  Returns false when the literal does not convert (BadQueryRequest).
+bool insertion_index_of(const Column& c, const char* lit, int* out) {
+  const Dict& d = c.dict;
+  int lo = 0, hi = (int)d.size() - 1;
+  switch (d.type) {
+    case PGPU_INT: case PGPU_LONG: {
+      int64_t v;
+      if (!parse_long(lit, d.type == PGPU_INT ? INT32_MIN : INT64_MIN, d.type == PGPU_INT ? INT32_MAX : INT64_MAX, &v))
+        return false;
+      while (lo <= hi) {
+        int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+        if (d.iv[mid] < v) lo = mid + 1;
+        else if (d.iv[mid] > v) hi = mid - 1;
+        else { *out = mid; return true; }
+      }
+      *out = -(lo + 1);
+      return true;
+    }
+    case PGPU_FLOAT: case PGPU_DOUBLE: {
+      double v;
+      if (!parse_double(lit, &v)) return false;
+      if (d.type == PGPU_FLOAT) v = (double)(float)v;
+      while (lo <= hi) {
+        int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+        if (d.dv[mid] < v) lo = mid + 1;
+        else if (d.dv[mid] > v) hi = mid - 1;
+        else { *out = mid; return true; }
+      }
+      *out = -(lo + 1);
+      return true;
+    }
+    default: {
+      const uint8_t* lv = reinterpret_cast<const uint8_t*>(lit);
+      size_t ln = strlen(lit);
+      if (c.padding == 0) {
+        while (lo <= hi) {
+          int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+          const std::string& m = d.sv[mid];
+          int r = cmp_bytes(reinterpret_cast<const uint8_t*>(m.data()), m.size(), lv, ln);
+          if (r < 0) lo = mid + 1;
+          else if (r > 0) hi = mid - 1;
+          else { *out = mid; return true; }
+        }
+      } else {  // legacy non-zero padding: padded comparison (BaseImmutableDictionary.java:215-228)
+        std::string padded(lit);
+        if ((int)padded.size() < c.entry_width) padded.append(c.entry_width - padded.size(), (char)c.padding);
+        while (lo <= hi) {
+          int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+          const uint8_t* m = c.raw_dict.data() + (int64_t)mid * c.entry_width;
+          int r = cmp_bytes(m, c.entry_width, reinterpret_cast<const uint8_t*>(padded.data()), padded.size());
+          if (r < 0) lo = mid + 1;
+          else if (r > 0) hi = mid - 1;
+          else { *out = mid; return true; }
+        }
+      }
+      *out = -(lo + 1);
+      return true;
+    }
+  }
+}
+
+int64_t global_index_of(const Dict& g, const Dict& local, size_t i) {
+  if (is_int_type(g.type)) {
+    auto it = std::lower_bound(g.iv.begin(), g.iv.end(), local.iv[i]);
+    return (it != g.iv.end() && *it == local.iv[i]) ? it - g.iv.begin() : -1;
+  }
+  if (is_fp_type(g.type)) {
+    auto it = std::lower_bound(g.dv.begin(), g.dv.end(), local.dv[i], dbl_less);
+    return (it != g.dv.end() && !dbl_less(local.dv[i], *it)) ? it - g.dv.begin() : -1;
+  }
+  auto it = std::lower_bound(g.sv.begin(), g.sv.end(), local.sv[i]);
+  return (it != g.sv.end() && *it == local.sv[i]) ? it - g.sv.begin() : -1;
+}
+
+// Makes the local->global LUT of (seg, col) current.
+int ensure_lut(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
+  Column& c = s.cols[col];
+  if (c.lut_version == t->global_version[col] && c.d_lut) return 0;
+  std::vector<int32_t> lut(std::max<int32_t>(c.card, 1));
+  for (int32_t i = 0; i < c.card; ++i) {
+    int64_t g = global_index_of(t->global[col], c.dict, i);
+    if (g < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "value missing from the global dictionary (column %d)", col);
+    lut[i] = (int32_t)g;
+  }
+  if (!c.d_lut) {
+    HIP_TRY(hipMalloc(&c.d_lut, sizeof(int32_t) * lut.size()));
+    t->device_bytes += sizeof(int32_t) * lut.size();
+  }
+  HIP_TRY(hipMemcpyAsync(c.d_lut, lut.data(), sizeof(int32_t) * lut.size(), hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  c.lut_version = t->global_version[col];
+  return 0;
+}
+
+// Dictionary values for aggregation (Dictionary.readDoubleValues, DataFetcher.java:469-478).
+int ensure_values(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
+  Column& c = s.cols[col];
+  if (c.d_key) return 0;
+  const size_t n = std::max<int32_t>(c.card, 1);
+  std::vector<int64_t> key(n, 0);
+  std::vector<double> val(n, 0.0);
+  for (int32_t i = 0; i < c.card; ++i) {
+    if (is_int_type(c.dict.type)) {
+      key[i] = c.dict.iv[i];
+      val[i] = (double)c.dict.iv[i];
+    } else {
+      key[i] = double_key(c.dict.dv[i]);
+      val[i] = c.dict.dv[i];
+    }
+  }
+  HIP_TRY(hipMalloc(&c.d_key, sizeof(int64_t) * n));
+  HIP_TRY(hipMalloc(&c.d_val, sizeof(double) * n));
+  t->device_bytes += 16 * n;
+  HIP_TRY(hipMemcpyAsync(c.d_key, key.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(c.d_val, val.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  return 0;
+}
+
+void free_segment(pgpu_table_s* t, Segment* s) {
+  for (auto& c : s->cols) {
+    if (c.d_lut) hipFree(c.d_lut);
+    if (c.d_key) hipFree(c.d_key);
+    if (c.d_val) hipFree(c.d_val);
+    t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) + (c.d_key ? 16 * std::max(c.card, 1) : 0);
+  }
+  if (s->d_block) hipFree(s->d_block);
+}
+
+int64_t padded_fwd_words(int64_t num_docs, int bits) { return ((num_docs + 31) / 32) * bits + kFwdPadWords; }
+
+// Registers a segment whose columns have parsed dictionaries and device forward indexes.
+int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
+  for (size_t c = 0; c < seg->cols.size(); ++c)
+    if (merge_dict(t->global[c], seg->cols[c].dict)) t->global_version[c]++;
+  int64_t h = t->next_handle++;
+  seg->handle = h;
+  t->segments[h] = std::move(seg);
+  return h;
+}
+
+// ------------------------------------------------------------------------------------------------ plans
+struct LeafHost {
+  int32_t kind = LEAF_NONE, negate = 0;
+  uint32_t lo = 0, span = 0;
+  std::vector<uint32_t> set;  // bitset words for LEAF_SET
+};
+
+enum Tri { T_NONE = 0, T_ALL = 1, T_VAR = 2 };
+
+}  // namespace
+
+struct pgpu_plan_s {
+  pgpu_table_s* table = nullptr;
+  std::vector<Segment*> segs;
+  std::vector<int32_t> query_cols;        // table column of each query column slot
+  int num_leaves = 0;
+  std::vector<int32_t> leaf_slot;         // query column slot of each leaf
+  std::vector<int32_t> ops;               // encoded postfix program
+  bool pure_and = false;
+  int max_depth = 0;
+  std::vector<int32_t> key_cols;          // table columns of group-by expressions
+  std::vector<int64_t> key_card;          // global cardinalities
+  std::vector<int64_t> key_stride;
+  int64_t num_keys = 0;                   // dense G or hash capacity
+  int mode = MODE_LDS;
+  std::vector<int32_t> slot_kind, slot_col, slot_tcol;
+  std::vector<int32_t> agg_fn, agg_slot, agg_col;   // per aggregation: fn, value slot (or -1), table column
+  int num_projected = 0;
+  // per-segment compiled data
+  std::vector<uint8_t> segrec;            // host image of the KSeg records
+  int seg_stride = 0;
+  std::vector<uint32_t> set_words;        // all SET bitsets back to back
+  std::vector<std::pair<int64_t, int64_t>> set_fix;  // (offset of KLeaf.set field in segrec, word offset)
+  int64_t num_tiles = 0;
+  int64_t total_docs = 0;
+  int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
+  int segments_matched_filter = 0;
+  int grid = 0;
+  size_t lds_bytes = 0;
+  Scratch* scratch = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool executed = false;
+  const void* d_table_used = nullptr;
+  bool hash = false;
+};
+
+struct pgpu_result_s {
+  int64_t n = 0;
+  int num_keys = 0;
+  int num_aggs = 0;
+  std::vector<int32_t> gids;              // [n][num_keys]
+  std::vector<double> values;             // [num_aggs][n]
+  std::vector<int64_t> avg_counts;        // [num_aggs][n]
+  std::vector<int64_t> exact;             // [num_aggs][n]
+  std::vector<uint8_t> has_exact;         // per agg
+  int64_t stats[6] = {0, 0, 0, 0, 0, 0};
+};
+
+namespace {
+
+Scratch* acquire_scratch(pgpu_table_s* t) {
+  std::lock_guard<std::mutex> g(t->mu);
+  for (auto& s : t->scratch_pool)
+    if (s) {
+      Scratch* r = s.release();
+      s.reset();
+      return r;
+    }
+  return new Scratch();
+}
+void release_scratch(pgpu_table_s* t, Scratch* s) {
+  if (!s) return;
+  std::lock_guard<std::mutex> g(t->mu);
+  for (auto& p : t->scratch_pool)
+    if (!p) { p.reset(s); return; }
+  t->scratch_pool.emplace_back(s);
+}
+
+// Translates predicate `p` against one segment's column dictionary (dictionary-based PredicateEvaluators).
+int translate_predicate(const Column& c, const pgpu_predicate& p, LeafHost* L) {
+  const int32_t card = c.card;
+  auto index_of = [&](const char* lit, int* id) -> bool {
+    int ins;
+    if (!insertion_index_of(c, lit, &ins)) return false;
+    *id = ins >= 0 ? ins : -1;  // BaseImmutableDictionary.indexOf (:81-84)
+    return true;
+  };
+  auto bad = [&](const char* lit) {
+    return fail(PGPU_ERR_BAD_QUERY, "BadQueryRequestException: cannot convert '%s' to the type of column %d", lit,
+                p.column);
+  };
+  switch (p.type) {
+    case PGPU_PRED_EQ: {  // EqualsPredicateEvaluatorFactory.java:86-99
+      if (p.num_values < 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "EQ needs a value");
+      int id;
+      if (!index_of(p.values[0], &id)) return bad(p.values[0]);
+      if (id < 0) L->kind = LEAF_NONE;
+      else if (card == 1) L->kind = LEAF_ALL;
+      else { L->kind = LEAF_RANGE; L->lo = id; L->span = 1; }
+      return 0;
+    }
+    case PGPU_PRED_NOT_EQ: {  // NotEqualsPredicateEvaluatorFactory.java:88-102
+      if (p.num_values < 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "NOT_EQ needs a value");
+      int id;
+      if (!index_of(p.values[0], &id)) return bad(p.values[0]);
+      if (id < 0) L->kind = LEAF_ALL;
+      else if (card == 1) L->kind = LEAF_NONE;
+      else { L->kind = LEAF_RANGE; L->lo = id; L->span = 1; L->negate = 1; }
+      return 0;
+    }
+    case PGPU_PRED_IN: case PGPU_PRED_NOT_IN: {  // InPredicateEvaluatorFactory.java:138-154, NotIn...:140-160
+      std::vector<int> ids;
+      for (int i = 0; i < p.num_values; ++i) {
+        int id;
+        if (!index_of(p.values[i], &id)) return bad(p.values[i]);
+        if (id >= 0) ids.push_back(id);
+      }
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      const int n = (int)ids.size();
+      const bool in = p.type == PGPU_PRED_IN;
+      if (n == 0) { L->kind = in ? LEAF_NONE : LEAF_ALL; return 0; }
+      if (n == card) { L->kind = in ? LEAF_ALL : LEAF_NONE; return 0; }
+      L->negate = in ? 0 : 1;
+      if (ids.back() - ids.front() + 1 == n) {  // contiguous dictIds: a range test
+        L->kind = LEAF_RANGE;
+        L->lo = ids.front();
+        L->span = n;
+      } else {
+        L->kind = LEAF_SET;
+        L->set.assign(((size_t)card + 31) / 32, 0u);
+        for (int id : ids) L->set[id >> 5] |= 1u << (id & 31);
+      }
+      return 0;
+    }
+    case PGPU_PRED_RANGE: {  // SortedDictionaryBasedRangePredicateEvaluator (RangePredicateEvaluatorFactory.java:115-159)
+      if (p.num_values < 2) return fail(PGPU_ERR_INVALID_ARGUMENT, "RANGE needs (lower, upper)");
+      int start, end;
+      if (strcmp(p.values[0], "*") == 0) start = 0;
+      else {
+        int ins;
+        if (!insertion_index_of(c, p.values[0], &ins)) return bad(p.values[0]);
+        start = ins < 0 ? -(ins + 1) : (p.lower_inclusive ? ins : ins + 1);
+      }
+      if (strcmp(p.values[1], "*") == 0) end = card;
+      else {
+        int ins;
+        if (!insertion_index_of(c, p.values[1], &ins)) return bad(p.values[1]);
+        end = ins < 0 ? -(ins + 1) : (p.upper_inclusive ? ins + 1 : ins);
+      }
+      const int nm = end - start;
+      if (nm <= 0) L->kind = LEAF_NONE;
+      else if (nm == card) L->kind = LEAF_ALL;
+      else { L->kind = LEAF_RANGE; L->lo = start; L->span = nm; }
+      return 0;
+    }
+    default:
+      return fail(PGPU_ERR_UNSUPPORTED, "predicate type %d is not on the GPU path", p.type);
+  }
+}
+
+// Constant folding of the program against the leaves' constants (FilterPlanNode.java:146-176).
+Tri fold_program(const std::vector<int32_t>& ops, const std::vector<Tri>& leaf) {
+  std::vector<Tri> st;
+  for (int32_t e : ops) {
+    const int op = e >> 16, arg = e & 0xFFFF;
+    if (op == OP_LEAF) st.push_back(leaf[arg]);
+    else if (op == OP_NOT) {
+      Tri& x = st.back();
+      x = x == T_ALL ? T_NONE : x == T_NONE ? T_ALL : T_VAR;
+    } else {
+      bool any_none = false, any_all = false, all_all = true, all_none = true;
+      for (int j = (int)st.size() - arg; j < (int)st.size(); ++j) {
+        any_none |= st[j] == T_NONE;
+        any_all |= st[j] == T_ALL;
+        all_all &= st[j] == T_ALL;
+        all_none &= st[j] == T_NONE;
+      }
+      st.resize(st.size() - arg);
+      if (op == OP_AND) st.push_back(any_none ? T_NONE : all_all ? T_ALL : T_VAR);
+      else st.push_back(any_all ? T_ALL : all_none ? T_NONE : T_VAR);
+    }
+  }
+  return st.empty() ? T_ALL : st.back();
+}
+
+int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P) {
+  if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
+  const int ncols = (int)t->names.size();
+  if (q->num_group_by < 1) return fail(PGPU_ERR_UNSUPPORTED, "aggregation without GROUP BY is not on this path");
+  if (q->num_group_by > kMaxKeys) return fail(PGPU_ERR_UNSUPPORTED, "more than %d group-by columns", kMaxKeys);
+  if (q->num_predicates > kMaxLeaves) return fail(PGPU_ERR_UNSUPPORTED, "more than %d predicates", kMaxLeaves);
+  if (q->num_filter_ops > kMaxOps) return fail(PGPU_ERR_UNSUPPORTED, "filter program longer than %d", kMaxOps);
+  P->table = t;
+  {
+    std::lock_guard<std::mutex> g(t->mu);
+    for (int i = 0; i < nsegs; ++i) {
+      auto it = t->segments.find(handles[i]);
+      if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)handles[i]);
+      P->segs.push_back(it->second.get());
+    }
+  }
+  // query columns
+  auto slot_of = [&](int col) -> int {
+    for (size_t i = 0; i < P->query_cols.size(); ++i)
+      if (P->query_cols[i] == col) return (int)i;
+    P->query_cols.push_back(col);
+    return (int)P->query_cols.size() - 1;
+  };
+  for (int i = 0; i < q->num_predicates; ++i) {
+    const int c = q->predicates[i].column;
+    if (c < 0 || c >= ncols) return fail(PGPU_ERR_INVALID_ARGUMENT, "predicate %d: bad column %d", i, c);
+    P->leaf_slot.push_back(slot_of(c));
+  }
+  P->num_leaves = q->num_predicates;
+  for (int i = 0; i < q->num_group_by; ++i) {
+    const int c = q->group_by[i];
+    if (c < 0 || c >= ncols) return fail(PGPU_ERR_INVALID_ARGUMENT, "group-by %d: bad column %d", i, c);
+    P->key_cols.push_back(c);
+    slot_of(c);
+  }
+  // program
+  int depth = 0, max_depth = 0;
+  bool pure_and = q->num_filter_ops > 0;
+  int leaves_seen = 0;
+  for (int i = 0; i < q->num_filter_ops; ++i) {
+    const pgpu_filter_op& o = q->filter[i];
+    if (o.op == PGPU_OP_PRED) {
+      if (o.arg < 0 || o.arg >= q->num_predicates) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad predicate index");
+      if (o.arg != leaves_seen) pure_and = false;
+      ++leaves_seen;
+      ++depth;
+      P->ops.push_back((OP_LEAF << 16) | o.arg);
+    } else if (o.op == PGPU_OP_NOT) {
+      if (depth < 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed filter program");
+      pure_and = false;
+      P->ops.push_back(OP_NOT << 16);
+    } else if (o.op == PGPU_OP_AND || o.op == PGPU_OP_OR) {
+      if (o.arg < 1 || o.arg > depth) return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed filter program");
+      if (o.op == PGPU_OP_OR || i != q->num_filter_ops - 1) pure_and = false;
+      depth -= o.arg - 1;
+      P->ops.push_back(((o.op == PGPU_OP_AND ? OP_AND : OP_OR) << 16) | o.arg);
+    } else {
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "bad filter opcode %d", o.op);
+    }
+    max_depth = std::max(max_depth, depth);
+  }
+  if (q->num_filter_ops > 0 && depth != 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed filter program");
+  if (max_depth > kMaxStack) return fail(PGPU_ERR_UNSUPPORTED, "filter nesting deeper than %d", kMaxStack);
+  if (q->num_filter_ops == 1) pure_and = true;  // a single leaf
+  if (pure_and && leaves_seen != q->num_predicates) pure_and = false;
+  P->pure_and = pure_and;
+  P->max_depth = max_depth;
+
+  // aggregations -> accumulator slots (slot 0 = COUNT)
+  P->slot_kind.push_back(SLOT_COUNT);
+  P->slot_col.push_back(0);
+  P->slot_tcol.push_back(-1);
+  auto add_slot = [&](int kind, int tcol) -> int {
+    for (size_t s = 1; s < P->slot_kind.size(); ++s)
+      if (P->slot_kind[s] == kind && P->slot_tcol[s] == tcol) return (int)s;
+    P->slot_kind.push_back(kind);
+    P->slot_tcol.push_back(tcol);
+    P->slot_col.push_back(slot_of(tcol));
+    return (int)P->slot_kind.size() - 1;
+  };
+  for (int i = 0; i < q->num_aggs; ++i) {
+    const pgpu_agg& a = q->aggs[i];
+    P->agg_fn.push_back(a.fn);
+    P->agg_col.push_back(a.column);
+    if (a.fn == PGPU_AGG_COUNT) { P->agg_slot.push_back(0); continue; }
+    if (a.column < 0 || a.column >= ncols) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d: bad column", i);
+    const int type = t->types[a.column];
+    if (type == PGPU_STRING) return fail(PGPU_ERR_UNSUPPORTED, "numeric aggregation over a STRING column");
+    int kind;
+    switch (a.fn) {
+      case PGPU_AGG_SUM: case PGPU_AGG_AVG: kind = is_int_type(type) ? SLOT_SUM_I64 : SLOT_SUM_F64; break;
+      case PGPU_AGG_MIN: kind = SLOT_MIN_KEY; break;
+      case PGPU_AGG_MAX: kind = SLOT_MAX_KEY; break;
+      default: return fail(PGPU_ERR_UNSUPPORTED, "aggregation function %d", a.fn);
+    }
+    P->agg_slot.push_back(add_slot(kind, a.column));
+  }
+  if ((int)P->slot_kind.size() > kMaxSlots) return fail(PGPU_ERR_UNSUPPORTED, "too many accumulators");
+  if ((int)P->query_cols.size() > kMaxQueryCols) return fail(PGPU_ERR_UNSUPPORTED, "too many columns");
+  {  // TransformOperator.getNumColumnsProjected: distinct group-by and aggregation columns
+    std::vector<int> proj(P->key_cols.begin(), P->key_cols.end());
+    for (int i = 0; i < q->num_aggs; ++i) if (q->aggs[i].column >= 0) proj.push_back(q->aggs[i].column);
+    std::sort(proj.begin(), proj.end());
+    P->num_projected = (int)(std::unique(proj.begin(), proj.end()) - proj.begin());
+  }
+
+  // group-key layout over the table-global dictionaries (mixed radix, first column fastest: ArrayBasedHolder)
+  bool overflow = false;
+  int64_t G = 1;
+  for (int c : P->key_cols) {
+    const int64_t card = std::max<int64_t>((int64_t)t->global[c].size(), 1);
+    P->key_card.push_back(card);
+    P->key_stride.push_back(G);
+    if (!overflow && G > INT64_MAX / card) overflow = true;
+    else if (!overflow) G *= card;
+  }
+  if (overflow) return fail(PGPU_ERR_UNSUPPORTED, "group key space exceeds 64 bits (ARRAY_MAP holder)");
+  const int nslots = (int)P->slot_kind.size();
+  constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
+  constexpr int64_t kLdsBudget = 48 * 1024;
+  const size_t stack_bytes = pure_and ? 0 : (size_t)std::max(max_depth, 1) * kBlock * 4;
+  for (Segment* s : P->segs) P->total_docs += s->num_docs;
+  if ((int64_t)nslots * G * 8 <= kLdsBudget) {
+    P->mode = MODE_LDS;
+    P->num_keys = G;
+    P->lds_bytes = (size_t)nslots * G * 8 + stack_bytes;
+  } else if (G <= kDenseGlobalMax) {
+    P->mode = MODE_GLOBAL;
+    P->num_keys = G;
+    P->lds_bytes = stack_bytes;
+  } else {
+    P->mode = MODE_HASH;
+    P->hash = true;
+    int64_t want = std::max<int64_t>(2 * std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)), 1024);
+    int64_t cap = 1;
+    while (cap < want) cap <<= 1;
+    P->num_keys = cap;
+    P->lds_bytes = stack_bytes;
+  }
+
+  // per-segment records
+  const int nqc = (int)P->query_cols.size();
+  P->seg_stride = (int)(sizeof(KSegHdr) + sizeof(KCol) * nqc + sizeof(KLeaf) * std::max(P->num_leaves, 0));
+  P->seg_stride = (P->seg_stride + 15) & ~15;
+  hipStream_t stream = t->stream;
+  std::vector<uint8_t> rec(P->seg_stride);
+  std::vector<LeafHost> leaves(P->num_leaves);
+  std::vector<Tri> tri(P->num_leaves);
+  int64_t tile_base = 0;
+  std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
+  for (Segment* s : P->segs) {
+    for (int l = 0; l < P->num_leaves; ++l) {
+      leaves[l] = LeafHost();
+      TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], &leaves[l]));
+      tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
+    }
+    const Tri whole = P->num_leaves ? fold_program(P->ops, tri) : T_ALL;
+    if (whole == T_NONE || s->num_docs == 0) continue;  // EmptyFilterOperator: the segment is not scanned
+    P->segments_matched_filter++;
+    for (int l = 0; l < P->num_leaves; ++l)
+      if (tri[l] == T_VAR) P->scanned_entries_model += s->num_docs;
+    for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
+    for (size_t k = 1; k < P->slot_kind.size(); ++k) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
+    std::fill(rec.begin(), rec.end(), 0);
+    KSegHdr* h = reinterpret_cast<KSegHdr*>(rec.data());
+    h->num_docs = s->num_docs;
+    h->tile_base = (int32_t)tile_base;
+    h->num_tiles = (int32_t)((s->num_docs + kTileDocs - 1) / kTileDocs);
+    KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
+    for (int j = 0; j < nqc; ++j) {
+      const Column& c = s->cols[P->query_cols[j]];
+      kc[j].fwd = c.d_fwd;
+      kc[j].lut = c.d_lut;
+      kc[j].dkey = c.d_key;
+      kc[j].dval = c.d_val;
+      kc[j].bits = c.bits;
+    }
+    KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
+    const int64_t rec_off = (int64_t)P->segrec.size();
+    for (int l = 0; l < P->num_leaves; ++l) {
+      kl[l].kind = leaves[l].kind;
+      kl[l].negate = leaves[l].negate;
+      kl[l].lo = leaves[l].lo;
+      kl[l].span = leaves[l].span;
+      kl[l].set = nullptr;
+      if (leaves[l].kind == LEAF_SET) {
+        const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[l].set - rec.data());
+        P->set_fix.emplace_back(field, (int64_t)P->set_words.size());
+        P->set_words.insert(P->set_words.end(), leaves[l].set.begin(), leaves[l].set.end());
+      }
+    }
+    P->segrec.insert(P->segrec.end(), rec.begin(), rec.end());
+    tile_base += h->num_tiles;
+  }
+  P->num_tiles = tile_base;
+  if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
+  P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));
+  return 0;
+}
+
+int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
+  pgpu_table_s* t = P->table;
+  Scratch* sc = P->scratch;
+  const int nslots = (int)P->slot_kind.size();
+  const int64_t words = (int64_t)nslots * P->num_keys;
+  for (auto& e : sc->ev)
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventRecord(sc->ev[0], stream));
+  // uploads: segment records (with SET pointers patched) and SET bitsets
+  TRY(sc->sets.ensure(std::max<size_t>(P->set_words.size() * 4, 16)));
+  std::vector<uint8_t>& rec = P->segrec;
+  for (auto& f : P->set_fix) {
+    const uint32_t* p = sc->sets.as<uint32_t>() + f.second;
+    memcpy(rec.data() + f.first, &p, sizeof p);
+  }
+  const size_t up = rec.size() + P->set_words.size() * 4;
+  TRY(sc->stage.ensure(std::max<size_t>(up, 16)));
+  memcpy(sc->stage.p, rec.data(), rec.size());
+  if (!P->set_words.empty()) memcpy((uint8_t*)sc->stage.p + rec.size(), P->set_words.data(), P->set_words.size() * 4);
+  TRY(sc->segrec.ensure(std::max<size_t>(rec.size(), 16)));
+  if (!rec.empty()) HIP_TRY(hipMemcpyAsync(sc->segrec.p, sc->stage.p, rec.size(), hipMemcpyHostToDevice, stream));
+  if (!P->set_words.empty())
+    HIP_TRY(hipMemcpyAsync(sc->sets.p, (uint8_t*)sc->stage.p + rec.size(), P->set_words.size() * 4,
+                           hipMemcpyHostToDevice, stream));
+  TRY(sc->stats.ensure(64));
+  HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
+  uint64_t* table = reinterpret_cast<uint64_t*>(d_table);
+  if (!table) {
+    TRY(sc->table.ensure((size_t)words * 8));
+    table = sc->table.as<uint64_t>();
+  }
+  P->d_table_used = table;
+  KParams kp;
+  memset(&kp, 0, sizeof kp);
+  kp.segs = sc->segrec.as<uint8_t>();
+  kp.seg_stride = P->seg_stride;
+  kp.num_cols = (int)P->query_cols.size();
+  kp.num_segs = (int)(P->segrec.size() / std::max(P->seg_stride, 1));
+  kp.num_tiles = (int32_t)P->num_tiles;
+  kp.num_ops = (int)P->ops.size();
+  kp.pure_and = P->pure_and ? 1 : 0;
+  for (size_t i = 0; i < P->ops.size(); ++i) kp.ops[i] = P->ops[i];
+  kp.num_leaves = P->num_leaves;
+  for (int i = 0; i < P->num_leaves; ++i) kp.leaf_col[i] = P->leaf_slot[i];
+  kp.num_keys = (int)P->key_cols.size();
+  for (size_t j = 0; j < P->key_cols.size(); ++j) {
+    int slot = 0;
+    for (size_t i = 0; i < P->query_cols.size(); ++i) if (P->query_cols[i] == P->key_cols[j]) slot = (int)i;
+    kp.key_col[j] = slot;
+    kp.key_stride[j] = P->key_stride[j];
+  }
+  kp.num_keys_total = P->num_keys;
+  kp.num_slots = nslots;
+  for (int s = 0; s < nslots; ++s) { kp.slot_kind[s] = P->slot_kind[s]; kp.slot_col[s] = P->slot_col[s]; }
+  kp.stats = sc->stats.as<unsigned long long>();
+  if (P->mode == MODE_LDS) {
+    TRY(sc->slab.ensure((size_t)P->grid * words * 8));
+    kp.slab = sc->slab.as<uint64_t>();
+  } else {
+    if (P->mode == MODE_HASH) {
+      TRY(sc->hash_keys.ensure((size_t)P->num_keys * 8));
+      kp.hash_keys = sc->hash_keys.as<unsigned long long>();
+    }
+    if (launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, kp.hash_keys, stream))
+      return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
+    kp.table = table;
+  }
+  HIP_TRY(hipEventRecord(sc->ev[1], stream));
+  if (P->num_tiles > 0) {
+    if (launch_filter_groupby(kp, P->mode, P->grid, P->lds_bytes, stream))
+      return fail(PGPU_ERR_DEVICE, "filter_groupby launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
+  HIP_TRY(hipEventRecord(sc->ev[2], stream));
+  if (P->mode == MODE_LDS) {
+    const int nb = P->num_tiles > 0 ? P->grid : 0;
+    if (nb == 0) {
+      if (launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
+        return fail(PGPU_ERR_DEVICE, "table init launch failed");
+    } else if (launch_reduce_slabs(kp.slab, P->slot_kind.data(), nslots, P->num_keys, nb, table, stream)) {
+      return fail(PGPU_ERR_DEVICE, "reduce launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+  }
+  HIP_TRY(hipEventRecord(sc->ev[3], stream));
+  P->last_stream = stream;
+  P->executed = true;
+  return 0;
+}
+
+int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, pgpu_result_s* R) {
+  Scratch* sc = P->scratch;
+  if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  const uint64_t* table = reinterpret_cast<const uint64_t*>(d_table ? d_table : P->d_table_used);
+  const int nslots = (int)P->slot_kind.size();
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
+  TRY(sc->counter.ensure(64));
+  TRY(sc->ckeys.ensure((size_t)cap * 8));
+  TRY(sc->cslots.ensure((size_t)cap * 8 * nslots));
+  HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
+  if (launch_compact(table, P->hash ? sc->hash_keys.as<unsigned long long>() : nullptr, nslots, P->num_keys,
+                     sc->counter.as<unsigned long long>(), sc->ckeys.as<uint64_t>(), sc->cslots.as<uint64_t>(), cap,
+                     stream))
+    return fail(PGPU_ERR_DEVICE, "compact launch failed");
+  uint64_t hdr[2] = {0, 0};
+  TRY(sc->stage.ensure(64));
+  HIP_TRY(hipMemcpyAsync(sc->stage.p, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync((uint8_t*)sc->stage.p + 8, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  memcpy(hdr, sc->stage.p, 16);
+  const int64_t n = (int64_t)std::min<uint64_t>(hdr[0], (uint64_t)cap);
+  std::vector<uint64_t> keys(n), slots((size_t)n * nslots);
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(keys.data(), sc->ckeys.p, n * 8, hipMemcpyDeviceToHost, stream));
+    for (int s = 0; s < nslots; ++s)
+      HIP_TRY(hipMemcpyAsync(slots.data() + (size_t)s * n, sc->cslots.as<uint64_t>() + (size_t)s * cap, n * 8,
+                             hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+  // order groups by composite key
+  std::vector<int64_t> order(n);
+  for (int64_t i = 0; i < n; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return keys[a] < keys[b]; });
+  const int nk = (int)P->key_cols.size();
+  const int na = (int)P->agg_fn.size();
+  R->n = n;
+  R->num_keys = nk;
+  R->num_aggs = na;
+  R->gids.resize((size_t)n * nk);
+  R->values.assign((size_t)na * n, 0.0);
+  R->avg_counts.assign((size_t)na * n, 0);
+  R->exact.assign((size_t)na * n, 0);
+  R->has_exact.assign(na, 0);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t i = order[r];
+    uint64_t key = keys[i];
+    for (int j = 0; j < nk; ++j) R->gids[(size_t)r * nk + j] = (int32_t)((key / P->key_stride[j]) % P->key_card[j]);
+    const int64_t count = (int64_t)slots[i];
+    for (int a = 0; a < na; ++a) {
+      const int fn = P->agg_fn[a];
+      const int s = P->agg_slot[a];
+      const uint64_t w = slots[(size_t)s * n + i];
+      double v = 0.0;
+      int64_t ex = 0;
+      bool exact = false;
+      switch (fn) {
+        case PGPU_AGG_COUNT: v = (double)count; ex = count; exact = true; break;  // CountAggregationFunction: double count
+        case PGPU_AGG_SUM: case PGPU_AGG_AVG:
+          if (P->slot_kind[s] == SLOT_SUM_I64) { ex = (int64_t)w; v = (double)ex; exact = true; }
+          else memcpy(&v, &w, 8);
+          if (fn == PGPU_AGG_AVG) R->avg_counts[(size_t)a * n + r] = count;
+          break;
+        default: {  // MIN / MAX: ordered key -> value
+          const int type = P->table->types[P->agg_col[a]];
+          if (is_int_type(type)) { ex = (int64_t)w; v = (double)ex; exact = true; }
+          else v = key_double((int64_t)w);
+          break;
+        }
+      }
+      R->values[(size_t)a * n + r] = v;
+      R->exact[(size_t)a * n + r] = ex;
+      if (r == 0) R->has_exact[a] = exact;
+    }
+  }
+  if (n == 0)
+    for (int a = 0; a < na; ++a) {
+      const int fn = P->agg_fn[a];
+      R->has_exact[a] = fn == PGPU_AGG_COUNT || (P->slot_kind[P->agg_slot[a]] == SLOT_SUM_I64) ||
+                        ((fn == PGPU_AGG_MIN || fn == PGPU_AGG_MAX) && is_int_type(P->table->types[P->agg_col[a]]));
+    }
+  R->stats[0] = (int64_t)hdr[1];
+  R->stats[1] = P->scanned_entries_model;
+  R->stats[2] = (int64_t)hdr[1] * P->num_projected;
+  R->stats[3] = P->total_docs;
+  R->stats[4] = (int64_t)P->segs.size();
+  R->stats[5] = P->segments_matched_filter;
+  return 0;
+}
+
+}  // namespace
+
+// ================================================================================================ C ABI
+extern "C" {
+
+int pgpu_abi_version(void) { return PGPU_ABI_VERSION; }
+
+int pgpu_last_error(char* buf, size_t len) {
+  if (buf && len) {
+    size_t n = std::min(len - 1, g_err.size());
+    memcpy(buf, g_err.data(), n);
+    buf[n] = 0;
+  }
+  return (int)g_err.size();
+}
+
+int pgpu_device_count(int* count) {
+  if (!count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) { *count = 0; return fail(PGPU_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
+  *count = n;
+  return 0;
+}
+
+int pgpu_table_create(int device, int num_columns, const char* const* names, const int32_t* types, pgpu_table* out) {
+  if (!out || num_columns <= 0 || !types) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad table arguments");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PGPU_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(PGPU_ERR_INVALID_ARGUMENT, "device %d out of range", device);
+  for (int i = 0; i < num_columns; ++i)
+    if (types[i] < PGPU_INT || types[i] > PGPU_STRING) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad type", i);
+  auto t = std::make_unique<pgpu_table_s>();
+  t->device = device;
+  for (int i = 0; i < num_columns; ++i) {
+    t->names.push_back(names && names[i] ? names[i] : ("col" + std::to_string(i)));
+    t->types.push_back(types[i]);
+    Dict d;
+    d.type = types[i];
+    t->global.push_back(d);
+    t->global_version.push_back(0);
+  }
+  DeviceGuard g(device);
+  HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+  *out = t.release();
+  return 0;
+}
+
+int pgpu_table_destroy(pgpu_table t) {
+  if (!t) return 0;
+  DeviceGuard g(t->device);
+  hipStreamSynchronize(t->stream);
+  for (auto& kv : t->segments) free_segment(t, kv.second.get());
+  t->segments.clear();
+  for (auto& s : t->scratch_pool) if (s) s->release();
+  t->gen.pos.release(); t->gen.presence.release(); t->gen.code_to_pos.release(); t->gen.cdf.release();
+  t->gen.pos_to_id.release();
+  hipStreamDestroy(t->stream);
+  delete t;
+  return 0;
+}
+
+int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) {
+  if (!t || !d || !handle) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  if (d->num_columns != (int)t->names.size())
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "segment has %d columns, table has %zu", d->num_columns, t->names.size());
+  if (d->num_docs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "negative numDocs");
+  DeviceGuard g(t->device);
+  auto seg = std::make_unique<Segment>();
+  seg->num_docs = d->num_docs;
+  seg->cols.resize(d->num_columns);
+  int64_t total_words = 0;
+  std::vector<std::vector<uint32_t>> sorted_expansion(d->num_columns);
+  for (int c = 0; c < d->num_columns; ++c) {
+    const pgpu_column_buffers& cb = d->columns[c];
+    Column& col = seg->cols[c];
+    col.card = cb.cardinality;
+    col.entry_width = cb.entry_width;
+    col.padding = cb.padding_byte;
+    TRY(parse_dictionary(t->types[c], cb, &col.dict));
+    if (cb.dict && cb.cardinality > 0) col.raw_dict.assign(cb.dict, cb.dict + (int64_t)cb.cardinality * cb.entry_width);
+    if (cb.fwd_format == PGPU_FWD_FIXED_BIT) {
+      col.bits = cb.bits_per_element;
+      if (col.bits < 1 || col.bits > 31) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bitsPerElement %d", c, col.bits);
+      const int64_t need = ((int64_t)d->num_docs * col.bits + 7) / 8;
+      if (d->num_docs > 0 && (!cb.fwd || cb.fwd_len < need))
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: forward index has %lld bytes, needs %lld", c,
+                    (long long)cb.fwd_len, (long long)need);
+      col.fwd_bytes = need;
+    } else if (cb.fwd_format == PGPU_FWD_SORTED_PAIRS) {
+      // SortedIndexReaderImpl (start, end) pairs -> the fixed-bit layout the kernels read.
+      if (cb.fwd_len < (int64_t)cb.cardinality * 8) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: sorted index too small", c);
+      col.bits = num_bits_per_value(cb.cardinality - 1);
+      col.fwd_bytes = ((int64_t)d->num_docs * col.bits + 7) / 8;
+      std::vector<uint32_t>& w = sorted_expansion[c];
+      w.assign(padded_fwd_words(d->num_docs, col.bits), 0u);
+      for (int32_t id = 0; id < cb.cardinality; ++id) {
+        const int32_t s = (int32_t)rd_be32(cb.fwd + (int64_t)id * 8), e = (int32_t)rd_be32(cb.fwd + (int64_t)id * 8 + 4);
+        if (s < 0 || e >= d->num_docs || (e < s && e != s - 1)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad sorted pair");
+        for (int32_t doc = s; doc <= e; ++doc) {  // PinotDataBitSet.writeInt into BE words
+          const uint64_t bit = (uint64_t)doc * col.bits;
+          for (int b = 0; b < col.bits; ++b)
+            if ((id >> (col.bits - 1 - b)) & 1) {
+              const uint64_t pos = bit + b;
+              w[pos >> 5] |= 1u << (31 - (pos & 31));
+            }
+        }
+      }
+    } else {
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad forward-index format", c);
+    }
+    col.fwd_words = padded_fwd_words(d->num_docs, col.bits);
+    total_words += (col.fwd_words + 63) & ~int64_t(63);  // 256-byte aligned columns
+  }
+  HIP_TRY(hipMalloc(&seg->d_block, (size_t)std::max<int64_t>(total_words, 64) * 4));
+  t->device_bytes += std::max<int64_t>(total_words, 64) * 4;
+  int64_t off = 0;
+  for (int c = 0; c < d->num_columns; ++c) {
+    Column& col = seg->cols[c];
+    col.d_fwd = reinterpret_cast<uint32_t*>(seg->d_block) + off;
+    const pgpu_column_buffers& cb = d->columns[c];
+    HIP_TRY(hipMemsetAsync(col.d_fwd, 0, (size_t)col.fwd_words * 4, t->stream));
+    if (cb.fwd_format == PGPU_FWD_SORTED_PAIRS) {
+      HIP_TRY(hipMemcpyAsync(col.d_fwd, sorted_expansion[c].data(), (size_t)col.fwd_words * 4, hipMemcpyHostToDevice,
+                             t->stream));
+    } else if (col.fwd_bytes > 0) {
+      HIP_TRY(hipMemcpyAsync(col.d_fwd, cb.fwd, (size_t)col.fwd_bytes, hipMemcpyHostToDevice, t->stream));
+    }
+    off += (col.fwd_words + 63) & ~int64_t(63);
+  }
+  HIP_TRY(hipStreamSynchronize(t->stream));
+  std::lock_guard<std::mutex> lk(t->mu);
+  *handle = register_segment(t, std::move(seg));
+  return 0;
+}
+
+int pgpu_unpin_segment(pgpu_table t, int64_t h) {
+  if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
+  DeviceGuard g(t->device);
+  std::lock_guard<std::mutex> lk(t->mu);
+  auto it = t->segments.find(h);
+  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+  hipStreamSynchronize(t->stream);
+  free_segment(t, it->second.get());
+  t->segments.erase(it);
+  return 0;
+}
+
+int pgpu_table_num_segments(pgpu_table t, int32_t* count) {
+  if (!t || !count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(t->mu);
+  *count = (int32_t)t->segments.size();
+  return 0;
+}
+
+int64_t pgpu_table_device_bytes(pgpu_table t) { return t ? t->device_bytes : 0; }
+
+int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int64_t* vi, const double* vd,
+                                     const uint8_t* blob, const int64_t* offsets) {
+  if (!t || col < 0 || col >= (int)t->names.size() || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  Dict d;
+  d.type = t->types[col];
+  if (is_int_type(d.type)) {
+    if (n && !vi) return fail(PGPU_ERR_INVALID_ARGUMENT, "values_i64 required");
+    d.iv.assign(vi, vi + n);
+    std::sort(d.iv.begin(), d.iv.end());
+    d.iv.erase(std::unique(d.iv.begin(), d.iv.end()), d.iv.end());
+  } else if (is_fp_type(d.type)) {
+    if (n && !vd) return fail(PGPU_ERR_INVALID_ARGUMENT, "values_f64 required");
+    d.dv.assign(vd, vd + n);
+  } else {
+    if (n && (!blob || !offsets)) return fail(PGPU_ERR_INVALID_ARGUMENT, "blob/offsets required");
+    for (int64_t i = 0; i < n; ++i) d.sv.emplace_back(reinterpret_cast<const char*>(blob + offsets[i]), offsets[i + 1] - offsets[i]);
+    std::sort(d.sv.begin(), d.sv.end());
+    d.sv.erase(std::unique(d.sv.begin(), d.sv.end()), d.sv.end());
+  }
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (merge_dict(t->global[col], d)) t->global_version[col]++;
+  return 0;
+}
+
+int pgpu_table_dictionary_size(pgpu_table t, int col, int64_t* size) {
+  if (!t || !size || col < 0 || col >= (int)t->names.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::lock_guard<std::mutex> lk(t->mu);
+  *size = (int64_t)t->global[col].size();
+  return 0;
+}
+
+int pgpu_table_dictionary_i64(pgpu_table t, int col, int64_t* out) {
+  if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_int_type(t->types[col]))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::lock_guard<std::mutex> lk(t->mu);
+  std::copy(t->global[col].iv.begin(), t->global[col].iv.end(), out);
+  return 0;
+}
+
+int pgpu_table_dictionary_f64(pgpu_table t, int col, double* out) {
+  if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_fp_type(t->types[col]))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::lock_guard<std::mutex> lk(t->mu);
+  std::copy(t->global[col].dv.begin(), t->global[col].dv.end(), out);
+  return 0;
+}
+
+int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap, int64_t* offsets) {
+  if (!t || !offsets || col < 0 || col >= (int)t->names.size() || t->types[col] != PGPU_STRING)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::lock_guard<std::mutex> lk(t->mu);
+  int64_t off = 0;
+  offsets[0] = 0;
+  const auto& sv = t->global[col].sv;
+  for (size_t i = 0; i < sv.size(); ++i) {
+    if (blob) {
+      if (off + (int64_t)sv[i].size() > cap) return fail(PGPU_ERR_INVALID_ARGUMENT, "blob too small");
+      memcpy(blob + off, sv[i].data(), sv[i].size());
+    }
+    off += (int64_t)sv[i].size();
+    offsets[i + 1] = off;
+  }
+  return 0;
+}
+
+int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, int32_t n, int32_t* out) {
+  if (!t || (n > 0 && (!docs || !out))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(t->device);
+  Segment* s;
+  {
+    std::lock_guard<std::mutex> lk(t->mu);
+    auto it = t->segments.find(h);
+    if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle");
+    s = it->second.get();
+  }
+  if (col < 0 || col >= (int)s->cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column");
+  if (n <= 0) return 0;
+  for (int32_t i = 0; i < n; ++i)
+    if (docs[i] < 0 || docs[i] >= s->num_docs) return fail(PGPU_ERR_INVALID_ARGUMENT, "docId %d out of range", docs[i]);
+  int32_t *d_docs = nullptr, *d_out = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&d_docs, (size_t)n * 4, t->stream));
+  HIP_TRY(hipMallocAsync((void**)&d_out, (size_t)n * 4, t->stream));
+  HIP_TRY(hipMemcpyAsync(d_docs, docs, (size_t)n * 4, hipMemcpyHostToDevice, t->stream));
+  if (launch_gather_ids(s->cols[col].d_fwd, s->cols[col].bits, d_docs, n, d_out, t->stream))
+    return fail(PGPU_ERR_DEVICE, "gather launch failed");
+  HIP_TRY(hipMemcpyAsync(out, d_out, (size_t)n * 4, hipMemcpyDeviceToHost, t->stream));
+  HIP_TRY(hipFreeAsync(d_docs, t->stream));
+  HIP_TRY(hipFreeAsync(d_out, t->stream));
+  HIP_TRY(hipStreamSynchronize(t->stream));
+  return 0;
+}
+
+int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bits, int64_t start, int64_t n,
+                                 int32_t* d_out, void* stream) {
+  if (bits < 1 || bits > 31 || start < 0 || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  // the two-word gather reads up to word ((start+n-1)*bits >> 5) + 1
+  const int64_t last_word = n > 0 ? (((start + n - 1) * bits) >> 5) + 1 : 0;
+  if (n > 0 && (last_word + 1) * 4 > fwd_len)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "device buffer must hold %lld bytes (2 words past the last value)",
+                (long long)((last_word + 1) * 4));
+  if (launch_unpack(reinterpret_cast<const uint32_t*>(d_fwd), bits, start, n, d_out, stream))
+    return fail(PGPU_ERR_DEVICE, "unpack launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan* out) {
+  if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(t->device);
+  auto P = std::make_unique<pgpu_plan_s>();
+  TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
+  P->scratch = acquire_scratch(t);
+  *out = P.release();
+  return 0;
+}
+
+int pgpu_plan_destroy(pgpu_plan P) {
+  if (!P) return 0;
+  release_scratch(P->table, P->scratch);
+  delete P;
+  return 0;
+}
+
+int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
+  if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  if (num_slots) *num_slots = (int32_t)P->slot_kind.size();
+  if (num_keys) *num_keys = P->hash ? 0 : P->num_keys;
+  if (kinds) for (size_t i = 0; i < P->slot_kind.size(); ++i) kinds[i] = P->slot_kind[i];
+  return 0;
+}
+
+int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
+  if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  if (P->hash && d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  return plan_execute_impl(P, s, d_table);
+}
+
+int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_result* out) {
+  if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  auto R = std::make_unique<pgpu_result_s>();
+  TRY(plan_finalize_impl(P, s, d_table, R.get()));
+  *out = R.release();
+  return 0;
+}
+
+int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
+                         pgpu_result* out) {
+  pgpu_plan P = nullptr;
+  TRY(pgpu_plan_create(t, handles, nsegs, q, &P));
+  int rc = pgpu_plan_execute(P, stream, nullptr);
+  if (!rc) rc = pgpu_plan_finalize(P, stream, nullptr, out);
+  std::string keep = g_err;
+  pgpu_plan_destroy(P);
+  g_err = keep;
+  return rc;
+}
+
+int pgpu_plan_timing(pgpu_plan P, double* out3) {
+  if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  Scratch* sc = P->scratch;
+  HIP_TRY(hipEventSynchronize(sc->ev[3]));
+  float a = 0, b = 0;
+  HIP_TRY(hipEventElapsedTime(&a, sc->ev[0], sc->ev[3]));
+  HIP_TRY(hipEventElapsedTime(&b, sc->ev[1], sc->ev[2]));
+  out3[0] = a * 1000.0;
+  out3[1] = b * 1000.0;
+  out3[2] = P->num_tiles > 0 ? 1.0 : 0.0;
+  return 0;
+}
+
+int pgpu_result_num_groups(pgpu_result r, int64_t* n) {
+  if (!r || !n) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *n = r->n;
+  return 0;
+}
+int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
+  if (!r || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::copy(r->gids.begin(), r->gids.end(), out);
+  return 0;
+}
+int pgpu_result_values(pgpu_result r, int agg, double* out) {
+  if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::copy(r->values.begin() + (size_t)agg * r->n, r->values.begin() + (size_t)(agg + 1) * r->n, out);
+  return 0;
+}
+int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) {
+  if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::copy(r->avg_counts.begin() + (size_t)agg * r->n, r->avg_counts.begin() + (size_t)(agg + 1) * r->n, out);
+  return 0;
+}
+int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
+  if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (!r->has_exact[agg]) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
+  std::copy(r->exact.begin() + (size_t)agg * r->n, r->exact.begin() + (size_t)(agg + 1) * r->n, out);
+  return 0;
+}
+int pgpu_result_stats(pgpu_result r, int64_t* out6) {
+  if (!r || !out6) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  memcpy(out6, r->stats, sizeof r->stats);
+  return 0;
+}
+int pgpu_result_destroy(pgpu_result r) {
+  delete r;
+  return 0;
+}
+
+int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* out_words) {
+  if (!t || !q || !out_words) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(t->device);
+  // A plan over the one segment with a COUNT-by-first-column shape; only its filter part is used.
+  pgpu_query fq = *q;
+  int32_t gb = q->num_group_by > 0 ? q->group_by[0] : 0;
+  fq.num_group_by = 1;
+  fq.group_by = &gb;
+  fq.num_aggs = 0;
+  fq.aggs = nullptr;
+  auto P = std::make_unique<pgpu_plan_s>();
+  TRY(plan_create_impl(t, &h, 1, &fq, P.get()));
+  Segment* s = P->segs[0];
+  const int64_t ngroups = ((int64_t)s->num_docs + 31) / 32;
+  const int64_t nwords = ((int64_t)s->num_docs + 63) / 64;
+  if (P->segrec.empty()) {  // filter folded to EmptyFilterOperator
+    memset(out_words, 0, (size_t)nwords * 8);
+    return 0;
+  }
+  Scratch* sc = acquire_scratch(t);
+  int rc = 0;
+  do {
+    if ((rc = sc->segrec.ensure(P->segrec.size()))) break;
+    if ((rc = sc->sets.ensure(std::max<size_t>(P->set_words.size() * 4, 16)))) break;
+    for (auto& f : P->set_fix) {
+      const uint32_t* p = sc->sets.as<uint32_t>() + f.second;
+      memcpy(P->segrec.data() + f.first, &p, sizeof p);
+    }
+    if ((rc = sc->bitmap.ensure((size_t)nwords * 8))) break;
+    hipMemsetAsync(sc->bitmap.p, 0, (size_t)nwords * 8, t->stream);
+    hipMemcpyAsync(sc->segrec.p, P->segrec.data(), P->segrec.size(), hipMemcpyHostToDevice, t->stream);
+    if (!P->set_words.empty())
+      hipMemcpyAsync(sc->sets.p, P->set_words.data(), P->set_words.size() * 4, hipMemcpyHostToDevice, t->stream);
+    KParams kp;
+    memset(&kp, 0, sizeof kp);
+    kp.segs = sc->segrec.as<uint8_t>();
+    kp.seg_stride = P->seg_stride;
+    kp.num_cols = (int)P->query_cols.size();
+    kp.num_segs = 1;
+    kp.num_tiles = (int32_t)((ngroups + kBlock - 1) / kBlock);
+    kp.num_ops = (int)P->ops.size();
+    kp.pure_and = P->pure_and;
+    for (size_t i = 0; i < P->ops.size(); ++i) kp.ops[i] = P->ops[i];
+    kp.num_leaves = P->num_leaves;
+    for (int i = 0; i < P->num_leaves; ++i) kp.leaf_col[i] = P->leaf_slot[i];
+    if (launch_filter_bitmap(kp, sc->bitmap.as<uint32_t>(), t->stream)) {
+      rc = fail(PGPU_ERR_DEVICE, "filter bitmap launch failed");
+      break;
+    }
+    hipError_t e = hipMemcpyAsync(out_words, sc->bitmap.p, (size_t)nwords * 8, hipMemcpyDeviceToHost, t->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+    if (e != hipSuccess) rc = fail(PGPU_ERR_DEVICE, "filter bitmap: %s", hipGetErrorString(e));
+  } while (0);
+  release_scratch(t, sc);
+  return rc;
+}
+
+int pgpu_generate_segment(pgpu_table t, const pgpu_gen_column* gc, int32_t ncols, int64_t row0, int32_t num_docs,
+                          int64_t* handle) {
+  if (!t || !gc || !handle || ncols != (int)t->names.size() || num_docs < 0)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(t->device);
+  hipStream_t st = t->stream;
+  auto seg = std::make_unique<Segment>();
+  seg->num_docs = num_docs;
+  seg->cols.resize(ncols);
+  // Domain of each column in value order: positions; the dictionary is the set of positions present.
+  struct Domain {
+    std::vector<int32_t> code_to_pos;
+    std::vector<int64_t> pos_i64;
+    std::vector<double> pos_f64;
+    int64_t npos = 0;
+  };
+  std::vector<Domain> dom(ncols);
+  int64_t total_words = 0;
+  for (int c = 0; c < ncols; ++c) {
+    const pgpu_gen_column& g0 = gc[c];
+    const int type = t->types[c];
+    Domain& D = dom[c];
+    if (g0.kind == PGPU_GEN_UNIFORM) {
+      if (!is_int_type(type) || g0.hi <= g0.lo || g0.hi - g0.lo > (int64_t(1) << 28))
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad UNIFORM spec", c);
+      D.npos = g0.hi - g0.lo;
+    } else if (g0.kind == PGPU_GEN_ZIPF) {
+      if (!is_int_type(type) || g0.n <= 0 || !g0.cdf || !g0.ids) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad ZIPF spec");
+      std::vector<int32_t> order(g0.n);
+      for (int i = 0; i < g0.n; ++i) order[i] = i;
+      std::sort(order.begin(), order.end(), [&](int a, int b) { return g0.ids[a] < g0.ids[b]; });
+      D.code_to_pos.assign(g0.n, 0);
+      for (int i = 0; i < g0.n; ++i) {
+        if (i > 0 && g0.ids[order[i]] == g0.ids[order[i - 1]]) return fail(PGPU_ERR_INVALID_ARGUMENT, "duplicate ZIPF ids");
+        D.code_to_pos[order[i]] = i;
+        D.pos_i64.push_back(g0.ids[order[i]]);
+      }
+      D.npos = g0.n;
+    } else if (g0.kind == PGPU_GEN_TABLE) {
+      if (!is_fp_type(type) || g0.n <= 0 || !g0.table) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad TABLE spec");
+      std::vector<double> vals(g0.table, g0.table + g0.n);
+      if (type == PGPU_FLOAT) for (double& v : vals) v = (double)(float)v;
+      std::vector<double> sorted = vals;
+      std::sort(sorted.begin(), sorted.end(), dbl_less);
+      sorted.erase(std::unique(sorted.begin(), sorted.end(),
+                               [](double a, double b) { return !dbl_less(a, b) && !dbl_less(b, a); }),
+                   sorted.end());
+      D.code_to_pos.resize(g0.n);
+      for (int i = 0; i < g0.n; ++i)
+        D.code_to_pos[i] = (int32_t)(std::lower_bound(sorted.begin(), sorted.end(), vals[i], dbl_less) - sorted.begin());
+      D.pos_f64 = sorted;
+      D.npos = (int64_t)sorted.size();
+    } else {
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad generator kind", c);
+    }
+  }
+  // pass 1 per column: positions + presence bitmap
+  GenScratch& G = t->gen;
+  std::vector<std::vector<int32_t>> pos_to_id(ncols);
+  TRY(G.pos.ensure((size_t)std::max(num_docs, 1) * 4 * ncols));
+  for (int c = 0; c < ncols; ++c) {
+    const pgpu_gen_column& g0 = gc[c];
+    Domain& D = dom[c];
+    const int64_t pres_words = (D.npos + 31) / 32;
+    TRY(G.presence.ensure((size_t)pres_words * 4));
+    HIP_TRY(hipMemsetAsync(G.presence.p, 0, (size_t)pres_words * 4, st));
+    if (!D.code_to_pos.empty()) {
+      TRY(G.code_to_pos.ensure(D.code_to_pos.size() * 4));
+      HIP_TRY(hipMemcpyAsync(G.code_to_pos.p, D.code_to_pos.data(), D.code_to_pos.size() * 4, hipMemcpyHostToDevice, st));
+    }
+    if (g0.kind == PGPU_GEN_ZIPF) {
+      TRY(G.cdf.ensure((size_t)g0.n * 8));
+      HIP_TRY(hipMemcpyAsync(G.cdf.p, g0.cdf, (size_t)g0.n * 8, hipMemcpyHostToDevice, st));
+    }
+    const uint64_t seed = (uint64_t)(0x5EED0000u + (uint32_t)g0.column_index) << 32;
+    const int32_t ncodes = g0.kind == PGPU_GEN_UNIFORM ? 0 : g0.n;
+    if (launch_gen_positions(g0.kind, seed, g0.lo, g0.hi - g0.lo, G.cdf.as<double>(), G.code_to_pos.as<int32_t>(),
+                             ncodes, row0, num_docs, G.pos.as<int32_t>() + (size_t)c * std::max(num_docs, 1),
+                             G.presence.as<uint32_t>(), st))
+      return fail(PGPU_ERR_DEVICE, "gen positions launch failed");
+    std::vector<uint32_t> pres(pres_words);
+    HIP_TRY(hipMemcpyAsync(pres.data(), G.presence.p, (size_t)pres_words * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // dictionary = present positions in value order (SegmentDictionaryCreator: sorted distinct values)
+    Column& col = seg->cols[c];
+    col.dict.type = t->types[c];
+    std::vector<int32_t>& p2i = pos_to_id[c];
+    p2i.assign(std::max<int64_t>(D.npos, 1), 0);
+    int32_t card = 0;
+    for (int64_t p = 0; p < D.npos; ++p)
+      if ((pres[p >> 5] >> (p & 31)) & 1u) {
+        p2i[p] = card++;
+        if (g0.kind == PGPU_GEN_UNIFORM) col.dict.iv.push_back(g0.lo + p);
+        else if (g0.kind == PGPU_GEN_ZIPF) col.dict.iv.push_back(D.pos_i64[p]);
+        else col.dict.dv.push_back(D.pos_f64[p]);
+      }
+    col.card = card;
+    col.bits = num_bits_per_value(card - 1);
+    const int type = t->types[c];
+    col.entry_width = (type == PGPU_INT || type == PGPU_FLOAT) ? 4 : 8;
+    col.raw_dict.assign((size_t)card * col.entry_width, 0);
+    for (int32_t i = 0; i < card; ++i) {
+      uint8_t* o = col.raw_dict.data() + (size_t)i * col.entry_width;
+      if (type == PGPU_INT) wr_be32(o, (uint32_t)(int32_t)col.dict.iv[i]);
+      else if (type == PGPU_LONG) wr_be64(o, (uint64_t)col.dict.iv[i]);
+      else if (type == PGPU_FLOAT) { float f = (float)col.dict.dv[i]; uint32_t u; memcpy(&u, &f, 4); wr_be32(o, u); }
+      else { uint64_t u; memcpy(&u, &col.dict.dv[i], 8); wr_be64(o, u); }
+    }
+    col.fwd_bytes = ((int64_t)num_docs * col.bits + 7) / 8;
+    col.fwd_words = padded_fwd_words(num_docs, col.bits);
+    total_words += (col.fwd_words + 63) & ~int64_t(63);
+  }
+  HIP_TRY(hipMalloc(&seg->d_block, (size_t)std::max<int64_t>(total_words, 64) * 4));
+  t->device_bytes += std::max<int64_t>(total_words, 64) * 4;
+  HIP_TRY(hipMemsetAsync(seg->d_block, 0, (size_t)std::max<int64_t>(total_words, 64) * 4, st));
+  int64_t off = 0;
+  for (int c = 0; c < ncols; ++c) {
+    Column& col = seg->cols[c];
+    col.d_fwd = reinterpret_cast<uint32_t*>(seg->d_block) + off;
+    off += (col.fwd_words + 63) & ~int64_t(63);
+    TRY(G.pos_to_id.ensure(pos_to_id[c].size() * 4));
+    HIP_TRY(hipMemcpyAsync(G.pos_to_id.p, pos_to_id[c].data(), pos_to_id[c].size() * 4, hipMemcpyHostToDevice, st));
+    if (launch_gen_pack(G.pos.as<int32_t>() + (size_t)c * std::max(num_docs, 1), G.pos_to_id.as<int32_t>(), num_docs,
+                        col.bits, col.d_fwd, st))
+      return fail(PGPU_ERR_DEVICE, "gen pack launch failed");
+    HIP_TRY(hipStreamSynchronize(st));  // pos_to_id is reused by the next column
+  }
+  std::lock_guard<std::mutex> lk(t->mu);
+  *handle = register_segment(t, std::move(seg));
+  return 0;
+}
+
+int pgpu_segment_column_info(pgpu_table t, int64_t h, int col, int32_t* card, int32_t* bits, int64_t* dict_len,
+                             int64_t* fwd_len) {
+  if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
+  std::lock_guard<std::mutex> lk(t->mu);
+  auto it = t->segments.find(h);
+  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle");
+  if (col < 0 || col >= (int)it->second->cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column");
+  const Column& c = it->second->cols[col];
+  if (card) *card = c.card;
+  if (bits) *bits = c.bits;
+  if (dict_len) *dict_len = (int64_t)c.raw_dict.size();
+  if (fwd_len) *fwd_len = c.fwd_bytes;
+  return 0;
+}
+
+int pgpu_segment_column_bytes(pgpu_table t, int64_t h, int col, uint8_t* dict_out, uint8_t* fwd_out) {
+  if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
+  DeviceGuard g(t->device);
+  Segment* s;
+  {
+    std::lock_guard<std::mutex> lk(t->mu);
+    auto it = t->segments.find(h);
+    if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle");
+    s = it->second.get();
+  }
+  if (col < 0 || col >= (int)s->cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column");
+  const Column& c = s->cols[col];
+  if (dict_out && !c.raw_dict.empty()) memcpy(dict_out, c.raw_dict.data(), c.raw_dict.size());
+  if (fwd_out && c.fwd_bytes > 0) {
+    HIP_TRY(hipMemcpyAsync(fwd_out, c.d_fwd, (size_t)c.fwd_bytes, hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+  }
+  return 0;
+}
+
+}  // extern "C"

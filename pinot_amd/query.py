@@ -1,0 +1,330 @@
+"""Query model of the path: the subset of Pinot's QueryContext that reaches the per-segment group-by operator.
+
+Mirrors (names and meaning):
+  Predicate / FilterContext   pinot-core .../query/request/context/predicate/*, FilterContext (AND / OR /
+                              PREDICATE; NOT is accepted too)
+  QueryContext                core/query/request/context/QueryContext.java:164-317 (filter, group-by
+                              expressions, aggregation functions, numGroupsLimit)
+A small parser for the SQL/PQL subset the reference tests use (comparisons, BETWEEN, IN / NOT IN, AND / OR /
+NOT, GROUP BY, TOP / LIMIT / ORDER BY accepted and ignored: trimming and ordering are broker-side) turns
+strings such as the README AdAnalytics query into a QueryContext.  Literals stay strings: they are converted
+per column type by the dictionary lookup, exactly as PredicateUtils.getStoredValue does.
+"""
+import ctypes
+import re
+
+from . import _lib as L
+
+EQ, NOT_EQ, IN, NOT_IN, RANGE = "EQ", "NOT_EQ", "IN", "NOT_IN", "RANGE"
+UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
+_PRED_CODE = {EQ: L.PRED_EQ, NOT_EQ: L.PRED_NOT_EQ, IN: L.PRED_IN, NOT_IN: L.PRED_NOT_IN, RANGE: L.PRED_RANGE}
+AGG_FUNCTIONS = {"COUNT": L.AGG_COUNT, "SUM": L.AGG_SUM, "MIN": L.AGG_MIN, "MAX": L.AGG_MAX, "AVG": L.AGG_AVG}
+DEFAULT_NUM_GROUPS_LIMIT = 100000  # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT (:70)
+
+
+class Predicate:
+    def __init__(self, ptype, column, values, lower_inclusive=True, upper_inclusive=True):
+        self.type = ptype
+        self.column = column
+        self.values = [str(v) for v in values]
+        self.lower_inclusive = bool(lower_inclusive)
+        self.upper_inclusive = bool(upper_inclusive)
+
+    @staticmethod
+    def eq(col, v):
+        return Predicate(EQ, col, [v])
+
+    @staticmethod
+    def not_eq(col, v):
+        return Predicate(NOT_EQ, col, [v])
+
+    @staticmethod
+    def in_(col, vals):
+        return Predicate(IN, col, list(vals))
+
+    @staticmethod
+    def not_in(col, vals):
+        return Predicate(NOT_IN, col, list(vals))
+
+    @staticmethod
+    def range(col, lower=UNBOUNDED, upper=UNBOUNDED, lower_inclusive=True, upper_inclusive=True):
+        return Predicate(RANGE, col, [lower, upper], lower_inclusive, upper_inclusive)
+
+    def __repr__(self):
+        return "Predicate(%s %s %r)" % (self.column, self.type, self.values)
+
+
+class FilterContext:
+    AND, OR, NOT, PREDICATE = "AND", "OR", "NOT", "PREDICATE"
+
+    def __init__(self, ftype, children=None, predicate=None):
+        self.type = ftype
+        self.children = children or []
+        self.predicate = predicate
+
+    @staticmethod
+    def and_(*children):
+        return FilterContext(FilterContext.AND, list(children))
+
+    @staticmethod
+    def or_(*children):
+        return FilterContext(FilterContext.OR, list(children))
+
+    @staticmethod
+    def not_(child):
+        return FilterContext(FilterContext.NOT, [child])
+
+    @staticmethod
+    def pred(p):
+        return FilterContext(FilterContext.PREDICATE, predicate=p)
+
+    def postfix(self, preds, ops):
+        """Flattens to a postfix program (predicates numbered in left-to-right order)."""
+        if self.type == FilterContext.PREDICATE:
+            preds.append(self.predicate)
+            ops.append((L.OP_PRED, len(preds) - 1))
+        elif self.type == FilterContext.NOT:
+            self.children[0].postfix(preds, ops)
+            ops.append((L.OP_NOT, 0))
+        else:
+            for c in self.children:
+                c.postfix(preds, ops)
+            ops.append((L.OP_AND if self.type == FilterContext.AND else L.OP_OR, len(self.children)))
+
+
+class QueryContext:
+    def __init__(self, group_by, aggregations, filter=None, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
+        self.filter = filter
+        self.group_by = list(group_by)
+        self.aggregations = [(fn.upper(), col) for fn, col in aggregations]
+        self.num_groups_limit = num_groups_limit
+
+    def columns(self):
+        cols = []
+        if self.filter is not None:
+            preds = []
+            self.filter.postfix(preds, [])
+            cols += [p.column for p in preds]
+        cols += self.group_by
+        cols += [c for _, c in self.aggregations if c != "*"]
+        out = []
+        for c in cols:
+            if c not in out:
+                out.append(c)
+        return out
+
+    # ---- JSON form used by tests/golden/kat_sv.json
+    @staticmethod
+    def filter_from_json(j):
+        if j is None:
+            return None
+        if "and" in j:
+            return FilterContext.and_(*[QueryContext.filter_from_json(c) for c in j["and"]])
+        if "or" in j:
+            return FilterContext.or_(*[QueryContext.filter_from_json(c) for c in j["or"]])
+        if "not" in j:
+            return FilterContext.not_(QueryContext.filter_from_json(j["not"]))
+        t = j["pred"]
+        if t in (EQ, NOT_EQ):
+            return FilterContext.pred(Predicate(t, j["col"], [j["value"]]))
+        if t in (IN, NOT_IN):
+            return FilterContext.pred(Predicate(t, j["col"], j["values"]))
+        return FilterContext.pred(Predicate.range(j["col"], j["lower"], j["upper"], j.get("li", True), j.get("ui", True)))
+
+    # ---- C ABI form
+    def to_c(self, column_index):
+        """Returns (QueryC, keepalive) for a table whose column name -> index map is `column_index`."""
+        keep = []
+        preds, ops = [], []
+        if self.filter is not None:
+            self.filter.postfix(preds, ops)
+        pc = (L.PredicateC * max(len(preds), 1))()
+        for i, p in enumerate(preds):
+            if p.column not in column_index:
+                raise KeyError("unknown column %r" % p.column)
+            vals = (ctypes.c_char_p * max(len(p.values), 1))(*[v.encode() for v in p.values])
+            keep.append(vals)
+            pc[i].type = _PRED_CODE[p.type]
+            pc[i].column = column_index[p.column]
+            pc[i].num_values = len(p.values)
+            pc[i].values = ctypes.cast(vals, L.c_char_pp)
+            pc[i].lower_inclusive = int(p.lower_inclusive)
+            pc[i].upper_inclusive = int(p.upper_inclusive)
+        oc = (L.FilterOpC * max(len(ops), 1))()
+        for i, (o, a) in enumerate(ops):
+            oc[i].op, oc[i].arg = o, a
+        gb = (ctypes.c_int32 * max(len(self.group_by), 1))(*[column_index[c] for c in self.group_by])
+        ac = (L.AggC * max(len(self.aggregations), 1))()
+        for i, (fn, col) in enumerate(self.aggregations):
+            if fn not in AGG_FUNCTIONS:
+                raise L.UnsupportedQueryError(L.PGPU_ERR_UNSUPPORTED, "aggregation %s" % fn)
+            ac[i].fn = AGG_FUNCTIONS[fn]
+            ac[i].column = -1 if col == "*" else column_index[col]
+        q = L.QueryC()
+        q.num_predicates = len(preds)
+        q.num_filter_ops = len(ops)
+        q.predicates = pc
+        q.filter = oc
+        q.num_group_by = len(self.group_by)
+        q.group_by = gb
+        q.num_aggs = len(self.aggregations)
+        q.aggs = ac
+        q.num_groups_limit = self.num_groups_limit
+        keep += [pc, oc, gb, ac]
+        return q, keep
+
+
+# ================================================================================ SQL / PQL subset parser
+_TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][+-]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
+                    r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*|\"[^\"]+\")|(?P<op><=|>=|<>|!=|=|<|>|\(|\)|,|\*))")
+
+
+def _tokenize(s):
+    pos, out = 0, []
+    s = s.strip().rstrip(";")
+    while pos < len(s):
+        m = _TOKEN.match(s, pos)
+        if not m or m.end() == pos:
+            if s[pos:].strip() == "":
+                break
+            raise ValueError("cannot parse near %r" % s[pos:pos + 20])
+        pos = m.end()
+        if m.group("num") is not None:
+            out.append(("lit", m.group("num")))
+        elif m.group("str") is not None:
+            out.append(("lit", m.group("str")[1:-1].replace("''", "'")))
+        elif m.group("id") is not None:
+            out.append(("id", m.group("id").strip('"')))
+        else:
+            out.append(("op", m.group("op")))
+    return out
+
+
+class _Parser:
+    def __init__(self, sql):
+        self.t = _tokenize(sql)
+        self.i = 0
+
+    def peek(self, k=0):
+        return self.t[self.i + k] if self.i + k < len(self.t) else (None, None)
+
+    def kw(self, *words):
+        tok = self.peek()
+        return tok[0] == "id" and tok[1].upper() in words
+
+    def take(self, kind=None, value=None):
+        tok = self.peek()
+        if tok[0] is None or (kind and tok[0] != kind) or (value and str(tok[1]).upper() != value):
+            raise ValueError("expected %s %s, got %r" % (kind, value, tok))
+        self.i += 1
+        return tok[1]
+
+    def select_list(self):
+        items = []
+        while True:
+            tok = self.peek()
+            if tok[0] == "id" and self.peek(1) == ("op", "("):
+                fn = self.take("id").upper()
+                self.take("op", "(")
+                col = "*" if self.peek() == ("op", "*") else None
+                if col:
+                    self.take("op", "*")
+                else:
+                    col = self.take("id")
+                self.take("op", ")")
+                items.append(("agg", fn, col))
+            else:
+                items.append(("col", self.take("id")))
+            if self.peek() == ("op", ","):
+                self.take("op", ",")
+                continue
+            return items
+
+    def literal(self):
+        tok = self.peek()
+        if tok[0] not in ("lit", "id"):
+            raise ValueError("literal expected, got %r" % (tok,))
+        self.i += 1
+        return tok[1]
+
+    def expr_or(self):
+        kids = [self.expr_and()]
+        while self.kw("OR"):
+            self.take("id")
+            kids.append(self.expr_and())
+        return kids[0] if len(kids) == 1 else FilterContext.or_(*kids)
+
+    def expr_and(self):
+        kids = [self.expr_not()]
+        while self.kw("AND"):
+            self.take("id")
+            kids.append(self.expr_not())
+        return kids[0] if len(kids) == 1 else FilterContext.and_(*kids)
+
+    def expr_not(self):
+        if self.kw("NOT"):
+            self.take("id")
+            return FilterContext.not_(self.expr_not())
+        if self.peek() == ("op", "("):
+            self.take("op", "(")
+            e = self.expr_or()
+            self.take("op", ")")
+            return e
+        col = self.take("id")
+        if self.kw("BETWEEN"):
+            self.take("id")
+            lo = self.literal()
+            self.take("id", "AND")
+            hi = self.literal()
+            return FilterContext.pred(Predicate.range(col, lo, hi, True, True))
+        negate = False
+        if self.kw("NOT"):
+            self.take("id")
+            negate = True
+        if self.kw("IN"):
+            self.take("id")
+            self.take("op", "(")
+            vals = [self.literal()]
+            while self.peek() == ("op", ","):
+                self.take("op", ",")
+                vals.append(self.literal())
+            self.take("op", ")")
+            return FilterContext.pred(Predicate.not_in(col, vals) if negate else Predicate.in_(col, vals))
+        op = self.take("op")
+        v = self.literal()
+        if op == "=":
+            return FilterContext.pred(Predicate.eq(col, v))
+        if op in ("!=", "<>"):
+            return FilterContext.pred(Predicate.not_eq(col, v))
+        if op == ">":
+            return FilterContext.pred(Predicate.range(col, v, UNBOUNDED, False, False))
+        if op == ">=":
+            return FilterContext.pred(Predicate.range(col, v, UNBOUNDED, True, False))
+        if op == "<":
+            return FilterContext.pred(Predicate.range(col, UNBOUNDED, v, False, False))
+        if op == "<=":
+            return FilterContext.pred(Predicate.range(col, UNBOUNDED, v, False, True))
+        raise ValueError("unsupported operator %s" % op)
+
+
+def parse_query(sql, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
+    """Parses `SELECT aggs FROM t [WHERE ...] GROUP BY cols [TOP n | ORDER BY ... | LIMIT n]`."""
+    p = _Parser(sql)
+    p.take("id", "SELECT")
+    items = p.select_list()
+    p.take("id", "FROM")
+    p.take("id")
+    flt = None
+    if p.kw("WHERE"):
+        p.take("id")
+        flt = p.expr_or()
+    group_by = []
+    if p.kw("GROUP"):
+        p.take("id")
+        p.take("id", "BY")
+        group_by.append(p.take("id"))
+        while p.peek() == ("op", ","):
+            p.take("op", ",")
+            group_by.append(p.take("id"))
+    aggs = [(fn, col) for kind, *rest in items if kind == "agg" for fn, col in [rest]]
+    return QueryContext(group_by, aggs, flt, num_groups_limit)

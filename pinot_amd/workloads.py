@@ -1,0 +1,94 @@
+"""Synthetic workloads of BASELINE.json / BASELINE.md §3 (C1, C2, C3, C5): schemas, column generators and
+queries.  Values follow f(splitmix64(seed_c ^ global_row)), seed_c = (0x5EED0000 + column index) << 32, so the
+device generator (pgpu_generate_segment) and the CPU oracle produce identical segments.
+"""
+import numpy as np
+
+SEGMENT_DOCS = 1_000_000
+
+
+def zipf_cdf(n, s=1.0):
+    """P(rank k) ~ 1 / (k + 1)^s, cumulative, last entry forced to 1 (same arithmetic as oracle or_zipf_cdf)."""
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+    c = np.cumsum(w)
+    out = c / c[-1]
+    out[-1] = 1.0
+    return out
+
+
+def account_ids(n):
+    """Rank -> accountId: rank 0 is 123456789 (the README query's account), the rest 1000000 + 37 * rank."""
+    ids = 1_000_000 + 37 * np.arange(n, dtype=np.int64)
+    ids[0] = 123456789
+    return ids
+
+
+def double_table(n, column_index, lo, hi):
+    """Fixed table of n doubles U[lo, hi) (C2's `md` dictionary values)."""
+    from ._splitmix import splitmix64_np
+    seed = np.uint64((0x5EED0000 + column_index) << 32)
+    h = splitmix64_np(seed ^ (np.uint64(0xDB1E000000) + np.arange(n, dtype=np.uint64)))
+    u = (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    return lo + (hi - lo) * u
+
+
+class Workload:
+    def __init__(self, name, schema, gen, sql, description):
+        self.name = name
+        self.schema = schema          # [(column, type)]
+        self.gen = gen                # generator spec per column (table column order)
+        self.sql = sql
+        self.description = description
+
+
+def adanalytics():
+    """C3: the README AdAnalytics query (README.md:82-87) over daysSinceEpoch / accountId / clicks / impressions."""
+    n = 100_000
+    schema = [("daysSinceEpoch", "INT"), ("accountId", "INT"), ("clicks", "INT"), ("impressions", "INT")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 17532, "hi": 17897},
+        {"kind": "ZIPF", "column_index": 1, "cdf": zipf_cdf(n), "ids": account_ids(n)},
+        {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 1000},
+        {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 100_000},
+    ]
+    sql = ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN 17849 AND 17856 "
+           "AND accountId IN (123456789) GROUP BY daysSinceEpoch TOP 100")
+    return Workload("adanalytics", schema, gen, sql, "C3 AdAnalytics filtered GROUP BY day")
+
+
+def c1():
+    schema = [("dim", "INT"), ("filt", "INT"), ("metric", "INT")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 16},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 1000},
+        {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 10_000},
+    ]
+    sql = "SELECT SUM(metric) FROM t WHERE filt BETWEEN 250 AND 749 GROUP BY dim"
+    return Workload("c1", schema, gen, sql, "C1 pinot-perf style range filter, SUM GROUP BY low-card dim")
+
+
+def c2():
+    schema = [("f", "INT"), ("d", "INT"), ("mi", "INT"), ("md", "DOUBLE")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 1000},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 100},
+        {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 65536},
+        {"kind": "TABLE", "column_index": 3, "table": double_table(100_000, 3, -1e6, 1e6)},
+    ]
+    sql = "SELECT COUNT(*), SUM(mi), MIN(mi), MAX(mi), SUM(md) FROM t WHERE f < 500 GROUP BY d"
+    return Workload("c2", schema, gen, sql, "C2 filtered SUM/COUNT/MIN/MAX GROUP BY")
+
+
+def c5():
+    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 1000},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 100},
+        {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 100},
+        {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 1000},
+    ]
+    sql = "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3"
+    return Workload("c5", schema, gen, sql, "C5 high-cardinality 3-column GROUP BY")
+
+
+WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c5": c5}

@@ -1,0 +1,323 @@
+"""ctypes bridge to oracle/liboracle.so — the CPU restatement of the reference path (test infrastructure only).
+
+Builds segments in Pinot's byte format (dictionary + fixed-bit forward index) from raw column values, and runs
+queries through the restated per-segment operator + combine.  Results come back keyed by python value tuples.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from pinot_amd import _lib as L
+from pinot_amd.executor import AvgPair
+from pinot_amd.segment import ColumnData, SegmentBuffers
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+
+def build_oracle():
+    src = [os.path.join(ORACLE_DIR, f) for f in ("oracle.c", "oracle.h", "Makefile")]
+    if not os.path.exists(ORACLE_LIB) or any(os.path.getmtime(s) > os.path.getmtime(ORACLE_LIB) for s in src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    return ORACLE_LIB
+
+
+class OrColumn(ctypes.Structure):
+    _fields_ = [("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32), ("bits", ctypes.c_int32),
+                ("entry_width", ctypes.c_int32), ("padding_byte", ctypes.c_int32), ("is_sorted", ctypes.c_int32),
+                ("dict", ctypes.c_void_p), ("fwd", ctypes.c_void_p)]
+
+
+class OrSegment(ctypes.Structure):
+    _fields_ = [("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32), ("columns", ctypes.POINTER(OrColumn))]
+
+
+class OrPredicate(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("column", ctypes.c_int32), ("num_values", ctypes.c_int32),
+                ("values", ctypes.POINTER(ctypes.c_char_p)), ("lower_inclusive", ctypes.c_int32),
+                ("upper_inclusive", ctypes.c_int32)]
+
+
+class OrFilterOp(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("arg", ctypes.c_int32)]
+
+
+class OrAgg(ctypes.Structure):
+    _fields_ = [("fn", ctypes.c_int32), ("column", ctypes.c_int32)]
+
+
+class OrQuery(ctypes.Structure):
+    _fields_ = [("num_predicates", ctypes.c_int32), ("predicates", ctypes.POINTER(OrPredicate)),
+                ("num_filter_ops", ctypes.c_int32), ("filter", ctypes.POINTER(OrFilterOp)),
+                ("num_group_by", ctypes.c_int32), ("group_by", ctypes.POINTER(ctypes.c_int32)),
+                ("num_aggs", ctypes.c_int32), ("aggs", ctypes.POINTER(OrAgg)),
+                ("num_groups_limit", ctypes.c_int32), ("max_initial_result_holder_capacity", ctypes.c_int32),
+                ("combine", ctypes.c_int32)]
+
+
+class OrResult(ctypes.Structure):
+    _fields_ = [("num_groups", ctypes.c_int64), ("key_blob", ctypes.POINTER(ctypes.c_uint8)),
+                ("key_offsets", ctypes.POINTER(ctypes.c_int64)), ("values", ctypes.POINTER(ctypes.c_double)),
+                ("avg_counts", ctypes.POINTER(ctypes.c_int64)), ("num_docs_scanned", ctypes.c_int64),
+                ("num_entries_scanned_in_filter", ctypes.c_int64), ("num_entries_scanned_post_filter", ctypes.c_int64),
+                ("num_total_docs", ctypes.c_int64), ("holder_kind", ctypes.c_int32),
+                ("num_groups_limit_reached", ctypes.c_int32)]
+
+
+class OrGenSpec(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("column_index", ctypes.c_int32), ("lo", ctypes.c_int64),
+                ("hi", ctypes.c_int64), ("n", ctypes.c_int32), ("cdf", ctypes.POINTER(ctypes.c_double)),
+                ("ids", ctypes.POINTER(ctypes.c_int64)), ("table", ctypes.POINTER(ctypes.c_double))]
+
+
+HOLDERS = {0: "ARRAY", 1: "INT_MAP", 2: "LONG_MAP", 3: "ARRAY_MAP"}
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build_oracle()
+        o = ctypes.CDLL(ORACLE_LIB)
+        o.or_num_bits_per_value.restype = ctypes.c_int
+        o.or_bitset_read_int.restype = ctypes.c_int32
+        o.or_bitset_read_int.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
+        o.or_bitset_read_ints.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        o.or_bitset_write_int.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int32]
+        o.or_bitset_write_ints.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        o.or_fwd_num_bytes.restype = ctypes.c_int64
+        o.or_fwd_num_bytes.argtypes = [ctypes.c_int64, ctypes.c_int]
+        o.or_read_dict_ids.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_void_p]
+        for f in ("or_build_column_i64", "or_build_column_f64"):
+            getattr(o, f).restype = ctypes.c_int
+            getattr(o, f).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        o.or_build_column_str.restype = ctypes.c_int
+        o.or_build_column_str.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        o.or_execute_groupby.restype = ctypes.c_int
+        o.or_execute_groupby.argtypes = [ctypes.POINTER(OrSegment), ctypes.c_int, ctypes.POINTER(OrQuery), ctypes.c_int,
+                                         ctypes.POINTER(OrResult), ctypes.c_char_p, ctypes.c_int]
+        o.or_free_result.argtypes = [ctypes.POINTER(OrResult)]
+        o.or_filter_bitmap.restype = ctypes.c_int
+        o.or_filter_bitmap.argtypes = [ctypes.POINTER(OrSegment), ctypes.POINTER(OrQuery), ctypes.c_void_p,
+                                       ctypes.c_char_p, ctypes.c_int]
+        o.or_bytes_alg.restype = ctypes.c_int64
+        o.or_bytes_alg.argtypes = [ctypes.POINTER(OrSegment), ctypes.POINTER(OrQuery), ctypes.c_void_p]
+        o.or_splitmix64.restype = ctypes.c_uint64
+        o.or_splitmix64.argtypes = [ctypes.c_uint64]
+        o.or_zipf_cdf.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
+        o.or_double_table.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+        o.or_gen_i64.argtypes = [ctypes.POINTER(OrGenSpec), ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        o.or_gen_f64.argtypes = [ctypes.POINTER(OrGenSpec), ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        _lib = o
+    return _lib
+
+
+# ----------------------------------------------------------------------------------------------- builders
+def build_column(dtype, values):
+    """Pinot segment creation for one column: (sorted distinct) dictionary + fixed-bit forward index."""
+    o = lib()
+    bits, width = ctypes.c_int(), ctypes.c_int()
+    if dtype == L.STRING:
+        enc = [v.encode("utf-8") if isinstance(v, str) else bytes(v) for v in values]
+        n = len(enc)
+        blob = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
+        off = np.zeros(n + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(e) for e in enc])
+        maxw = max([len(e) for e in enc] + [1])
+        d = np.zeros(max(n, 1) * maxw, dtype=np.uint8)
+        f = np.zeros(o.or_fwd_num_bytes(n, 31) + 16, dtype=np.uint8)
+        card = o.or_build_column_str(blob.ctypes.data, off.ctypes.data, n, d.ctypes.data, f.ctypes.data,
+                                     ctypes.byref(bits), ctypes.byref(width))
+    else:
+        n = len(values)
+        f = np.zeros(o.or_fwd_num_bytes(n, 31) + 16, dtype=np.uint8)
+        if dtype in (L.INT, L.LONG):
+            a = np.ascontiguousarray(values, dtype=np.int64)
+            d = np.zeros(max(n, 1) * 8, dtype=np.uint8)
+            card = o.or_build_column_i64(dtype, a.ctypes.data, n, d.ctypes.data, f.ctypes.data,
+                                         ctypes.byref(bits), ctypes.byref(width))
+        else:
+            a = np.ascontiguousarray(values, dtype=np.float64)
+            d = np.zeros(max(n, 1) * 8, dtype=np.uint8)
+            card = o.or_build_column_f64(dtype, a.ctypes.data, n, d.ctypes.data, f.ctypes.data,
+                                         ctypes.byref(bits), ctypes.byref(width))
+    nfwd = o.or_fwd_num_bytes(n, bits.value)
+    return ColumnData(dtype, card, bits.value, width.value, d[:card * width.value].tobytes(), f[:nfwd].tobytes())
+
+
+def make_segment(schema, columns):
+    """schema: [(name, type)], columns: name -> values.  Returns SegmentBuffers."""
+    n = None
+    cols = {}
+    for name, t in schema:
+        tt = L.TYPE_NAMES[t] if isinstance(t, str) else t
+        vals = columns[name]
+        n = len(vals) if n is None else n
+        assert len(vals) == n
+        cols[name] = build_column(tt, vals)
+    return SegmentBuffers(n or 0, cols)
+
+
+# ----------------------------------------------------------------------------------------------- queries
+class _OrSeg:
+    def __init__(self, schema, seg):
+        self.keep = []
+        cols = (OrColumn * len(schema))()
+        for i, (name, t) in enumerate(schema):
+            c = seg.columns[name]
+            d = ctypes.create_string_buffer(bytes(c.dict_bytes), max(len(c.dict_bytes), 1))
+            f = ctypes.create_string_buffer(bytes(c.fwd_bytes) + b"\0" * 16, len(c.fwd_bytes) + 16)
+            self.keep += [d, f]
+            cols[i] = OrColumn(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.padding_byte,
+                               int(c.is_sorted), ctypes.cast(d, ctypes.c_void_p), ctypes.cast(f, ctypes.c_void_p))
+        self.keep.append(cols)
+        self.seg = OrSegment(seg.num_docs, len(schema), cols)
+
+
+def _or_query(schema, q, combine=True, max_initial_capacity=10000):
+    idx = {n: i for i, (n, _) in enumerate(schema)}
+    keep = []
+    preds, ops = [], []
+    if q.filter is not None:
+        q.filter.postfix(preds, ops)
+    pc = (OrPredicate * max(len(preds), 1))()
+    codes = {"EQ": 0, "NOT_EQ": 1, "IN": 2, "NOT_IN": 3, "RANGE": 4}
+    for i, p in enumerate(preds):
+        vals = (ctypes.c_char_p * max(len(p.values), 1))(*[v.encode() for v in p.values])
+        keep.append(vals)
+        pc[i] = OrPredicate(codes[p.type], idx[p.column], len(p.values), vals, int(p.lower_inclusive),
+                            int(p.upper_inclusive))
+    oc = (OrFilterOp * max(len(ops), 1))(*[OrFilterOp(o, a) for o, a in ops])
+    gb = (ctypes.c_int32 * max(len(q.group_by), 1))(*[idx[c] for c in q.group_by])
+    fns = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4}
+    ac = (OrAgg * max(len(q.aggregations), 1))(*[OrAgg(fns[f], -1 if c == "*" else idx[c]) for f, c in q.aggregations])
+    keep += [pc, oc, gb, ac]
+    oq = OrQuery(len(preds), pc, len(ops), oc, len(q.group_by), gb, len(q.aggregations), ac, q.num_groups_limit,
+                 max_initial_capacity, int(combine))
+    return oq, keep
+
+
+class OracleResult:
+    def __init__(self, groups, stats, holder, limit_reached):
+        self.groups = groups   # key tuple -> [values] (AVG -> AvgPair, COUNT -> int)
+        self.stats = stats     # (docsScanned, inFilter, postFilter, totalDocs)
+        self.holder = holder
+        self.limit_reached = limit_reached
+
+
+def _decode_key(blob, types):
+    out, p = [], 0
+    for t in types:
+        if t in (L.INT, L.LONG):
+            out.append(int(np.frombuffer(blob[p:p + 8], dtype=np.int64)[0]))
+            p += 8
+        elif t in (L.FLOAT, L.DOUBLE):
+            out.append(float(np.frombuffer(blob[p:p + 8], dtype=np.float64)[0]))
+            p += 8
+        else:
+            n = int(np.frombuffer(blob[p:p + 4], dtype=np.uint32)[0])
+            out.append(blob[p + 4:p + 4 + n].decode("utf-8", errors="surrogateescape"))
+            p += 4 + n
+    return tuple(out)
+
+
+def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000):
+    o = lib()
+    segs = [_OrSeg(schema, s) for s in segments]
+    arr = (OrSegment * max(len(segs), 1))(*[s.seg for s in segs])
+    oq, keep = _or_query(schema, q, combine, max_initial_capacity)
+    res = OrResult()
+    msg = ctypes.create_string_buffer(512)
+    rc = o.or_execute_groupby(arr, len(segs), ctypes.byref(oq), nthreads, ctypes.byref(res), msg, 512)
+    if rc != 0:
+        raise RuntimeError("oracle error %d: %s" % (rc, msg.value.decode()))
+    try:
+        types = {n: (L.TYPE_NAMES[t] if isinstance(t, str) else t) for n, t in schema}
+        ktypes = [types[c] for c in q.group_by]
+        n = res.num_groups
+        na = len(q.aggregations)
+        blob = ctypes.string_at(res.key_blob, res.key_offsets[n]) if n else b""
+        groups = {}
+        for gi in range(n):
+            k = _decode_key(blob[res.key_offsets[gi]:res.key_offsets[gi + 1]], ktypes)
+            vals = []
+            for a, (fn, _) in enumerate(q.aggregations):
+                v = res.values[a * n + gi]
+                if fn == "AVG":
+                    vals.append(AvgPair(v, res.avg_counts[a * n + gi]))
+                elif fn == "COUNT":
+                    vals.append(int(v))
+                else:
+                    vals.append(float(v))
+            groups[k] = vals
+        stats = (res.num_docs_scanned, res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter,
+                 res.num_total_docs)
+        return OracleResult(groups, stats, HOLDERS[res.holder_kind], bool(res.num_groups_limit_reached))
+    finally:
+        o.or_free_result(ctypes.byref(res))
+
+
+def filter_bitmap(schema, seg, q):
+    o = lib()
+    s = _OrSeg(schema, seg)
+    oq, keep = _or_query(schema, q)
+    out = np.zeros(max((seg.num_docs + 63) // 64, 1), dtype=np.uint64)
+    msg = ctypes.create_string_buffer(512)
+    rc = o.or_filter_bitmap(ctypes.byref(s.seg), ctypes.byref(oq), out.ctypes.data, msg, 512)
+    if rc != 0:
+        raise RuntimeError("oracle error %d: %s" % (rc, msg.value.decode()))
+    return out
+
+
+def bytes_alg(schema, seg, q, bitmap):
+    s = _OrSeg(schema, seg)
+    oq, keep = _or_query(schema, q)
+    return int(lib().or_bytes_alg(ctypes.byref(s.seg), ctypes.byref(oq), bitmap.ctypes.data))
+
+
+# ----------------------------------------------------------------------------------------------- data
+def zipf_cdf(n, s=1.0):
+    out = np.zeros(n, dtype=np.float64)
+    lib().or_zipf_cdf(n, s, out.ctypes.data)
+    return out
+
+
+def double_table(n, column_index, lo, hi):
+    out = np.zeros(n, dtype=np.float64)
+    lib().or_double_table(n, column_index, lo, hi, out.ctypes.data)
+    return out
+
+
+def gen_values(spec, row0, n):
+    """spec: dict as for GpuTable.generate_segment."""
+    kinds = {"UNIFORM": 0, "ZIPF": 1, "TABLE": 2}
+    keep = []
+    g = OrGenSpec()
+    g.kind = kinds[spec["kind"]]
+    g.column_index = spec["column_index"]
+    g.lo = int(spec.get("lo", 0))
+    g.hi = int(spec.get("hi", 0))
+    if spec["kind"] == "ZIPF":
+        cdf = np.ascontiguousarray(spec["cdf"], dtype=np.float64)
+        ids = np.ascontiguousarray(spec["ids"], dtype=np.int64)
+        keep += [cdf, ids]
+        g.n = len(cdf)
+        g.cdf = cdf.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        g.ids = ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    if spec["kind"] == "TABLE":
+        tab = np.ascontiguousarray(spec["table"], dtype=np.float64)
+        keep.append(tab)
+        g.n = len(tab)
+        g.table = tab.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        out = np.zeros(n, dtype=np.float64)
+        lib().or_gen_f64(ctypes.byref(g), row0, n, out.ctypes.data)
+        return out
+    out = np.zeros(n, dtype=np.int64)
+    lib().or_gen_i64(ctypes.byref(g), row0, n, out.ctypes.data)
+    return out

@@ -1,0 +1,251 @@
+"""Benchmark: the README AdAnalytics filtered GROUP BY (BASELINE.json configs[2], C3) on synthetic segments
+pinned in HBM, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|c1|c2|c5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A step is one whole query on every rank: plan (per-segment predicate translation), the fused scan kernel over
+all local segments, the dense group-table merge across ranks (RCCL all-reduce over xGMI) and the compacted
+result copied back to the host.  Each rank holds --segments-per-gpu segments of 1M docs (weak scaling: the
+default 1000 segments = 1B rows per GPU).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="adanalytics")
+    p.add_argument("--segments-per-gpu", type=int, default=1000)
+    p.add_argument("--docs-per-segment", type=int, default=1_000_000)
+    p.add_argument("--cpu-sample-segments", type=int, default=64)
+    p.add_argument("--cpu-target-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
+    p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
+    return p.parse_args()
+
+
+def compulsory_bytes(table, handles, query, docs_per_segment):
+    """bytes_alg (compulsory-traffic form): full forward-index bytes of every filter column, plus
+    the 128-B lines of every other referenced column's forward index that hold >= 1 matched doc, plus the 128-B
+    lines of the group-by / aggregated columns' dictionaries that hold >= 1 matched dictId."""
+    from pinot_amd.query import FilterContext  # noqa: F401
+    preds = []
+    if query.filter is not None:
+        query.filter.postfix(preds, [])
+    filter_cols = sorted({p.column for p in preds})
+    other_cols = [c for c in query.columns() if c not in filter_cols]
+    dict_cols = [c for c in query.group_by] + [c for _, c in query.aggregations if c != "*"]
+    dict_cols = sorted(set(dict_cols))
+    width = {n: (4 if t in ("INT", "FLOAT") else 8) for n, t in zip(table.names, [None] * len(table.names))}
+    for i, n in enumerate(table.names):
+        width[n] = 4 if table.types[i] in (0, 2) else 8
+    total = 0
+    matched_total = 0
+    for h in handles:
+        bm = table.filter_bitmap(h, query, docs_per_segment)
+        bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:docs_per_segment]
+        docs = np.nonzero(bits)[0].astype(np.int64)
+        matched_total += len(docs)
+        info = {}
+        for c in set(filter_cols) | set(other_cols):
+            card, b, dlen, flen = _col_info(table, h, c)
+            info[c] = (card, b, flen)
+        for c in filter_cols:
+            total += info[c][2]
+        for c in other_cols:
+            b = info[c][1]
+            if len(docs):
+                first = (docs * b) >> 10          # 1024 bits = one 128-B line
+                last = (docs * b + b - 1) >> 10
+                total += len(np.union1d(first, last)) * 128
+        for c in dict_cols:
+            if len(docs):
+                ids = table.read_dict_ids(h, c, docs.astype(np.int32)).astype(np.int64)
+                total += len(np.unique((ids * width[c]) >> 7)) * 128
+    return total, matched_total
+
+
+def _col_info(table, h, c):
+    import ctypes
+    from pinot_amd import _lib as L
+    card, bits = ctypes.c_int32(), ctypes.c_int32()
+    dl, fl = ctypes.c_int64(), ctypes.c_int64()
+    L.check(table.lib.pgpu_segment_column_info(table.handle, h, table.index[c], ctypes.byref(card),
+                                               ctypes.byref(bits), ctypes.byref(dl), ctypes.byref(fl)))
+    return card.value, bits.value, dl.value, fl.value
+
+
+def cpu_baseline(table, handles, query, workload, docs, args):
+    """The oracle (C restatement of Pinot's per-segment operator + combine, one task per segment) timed on the
+    host cores over a bounded sample of the same segments (bytes pulled back from HBM)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    types = dict(workload.schema)
+    sample = handles[:max(1, min(args.cpu_sample_segments, len(handles)))]
+    segs = []
+    from pinot_amd import _lib as L
+    for h in sample:
+        cols = {}
+        for name, typ in workload.schema:
+            card, bits, d, f = table.segment_column_bytes(h, name)
+            tcode = L.TYPE_NAMES[typ]
+            cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
+        segs.append(SegmentBuffers(docs, cols))
+    threads = max(1, min(16, os.cpu_count() or 1))
+    _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads)  # warm-up
+    reps, elapsed = 0, 0.0
+    t0 = time.perf_counter()
+    while True:
+        _oracle.run_groupby(workload.schema, segs, query, nthreads=threads)
+        reps += 1
+        elapsed = time.perf_counter() - t0
+        if elapsed >= args.cpu_target_seconds or reps >= 50:
+            break
+    rows = reps * len(segs) * docs
+    _ = types
+    return {"value": rows / elapsed, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "%d segments x %d rows, %d repetitions, %.1f s, %d worker threads (oracle/oracle.c)" % (
+                len(segs), docs, reps, elapsed, threads)}
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    device = local_rank if world > 1 else 0
+
+    from pinot_amd import _lib as L
+    from pinot_amd.build import build
+    from pinot_amd.combine import allreduce_group_table, union_dictionaries
+    from pinot_amd.executor import GpuTable
+    from pinot_amd.query import parse_query
+    from pinot_amd.workloads import WORKLOADS
+
+    if rank == 0:
+        build()
+    if world > 1:
+        dist.barrier()
+    L.load()
+    w = WORKLOADS[args.workload]()
+    q = parse_query(w.sql)
+    docs = args.docs_per_segment
+    nseg = args.segments_per_gpu
+    table = GpuTable(w.schema, device=device)
+    t_gen = time.perf_counter()
+    handles = []
+    for i in range(nseg):
+        global_seg = rank * nseg + i
+        handles.append(table.generate_segment(w.gen, row0=global_seg * docs, num_docs=docs))
+    t_gen = time.perf_counter() - t_gen
+    if world > 1:
+        union_dictionaries(table, q.group_by)
+
+    stream = torch.cuda.current_stream().cuda_stream
+    probe = table.plan(handles, q)
+    nslots, nkeys, kinds = probe.layout()
+    probe.close()
+    d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
+
+    def step():
+        plan = table.plan(handles, q)
+        plan.execute(stream, d_table.data_ptr() if nkeys > 0 else None)
+        if world > 1:
+            allreduce_group_table(d_table, kinds)
+        res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
+        k_us = plan.timing_us()[1]
+        plan.close()
+        return res, k_us
+
+    first = None
+    for _ in range(args.warmup):
+        first, _ = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_us = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, k_us = step()
+        kernel_us.append(k_us)
+        if args.verify and first is not None:
+            assert res.as_dict() == first.as_dict()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    total_rows = float(nseg) * docs * world
+    value = total_rows * args.steps / elapsed
+    kernel_avg_us = float(np.mean(kernel_us)) if kernel_us else 0.0
+
+    roofline = None
+    if not args.no_bytes:
+        bytes_alg, matched = compulsory_bytes(table, handles, q, docs)
+        achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                    "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
+                    "matched_docs_per_gpu": int(matched)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(table, handles, q, w, docs, args)
+
+    if rank == 0:
+        line = {
+            "metric": "rows/sec scanned+aggregated (node) & % HBM peak, AdAnalytics GROUP BY query",
+            "value": round(value, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (BASELINE.md §3 generators, built on the device)",
+            "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
+                       "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
+                       "groups": len(first) if first is not None else None, "setup_s": round(t_gen, 1)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    table.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

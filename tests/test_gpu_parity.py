@@ -1,0 +1,316 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the reference KATs.
+
+Bar: bit-exact for COUNT, integer SUM/MIN/MAX, AVG counts, dictIds and filter bitmaps; 1e-9 relative error
+for sums over FLOAT/DOUBLE columns (the reference sums doubles in a thread-order-dependent order).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import kat_common as K
+from pinot_amd import _lib as L
+from pinot_amd.executor import AvgPair, GpuTable
+from pinot_amd.query import FilterContext, Predicate, QueryContext, parse_query
+
+pytestmark = pytest.mark.gpu
+REL = 1e-9
+
+
+def assert_same(gpu, orc, q, schema):
+    types = dict(schema)
+    g = gpu.as_dict()
+    assert set(g) == set(orc.groups), (sorted(set(g) ^ set(orc.groups))[:5])
+    for k, ov in orc.groups.items():
+        gv = g[k]
+        for a, (fn, col) in enumerate(q.aggregations):
+            fp = col != "*" and types[col] in ("FLOAT", "DOUBLE")
+            x, y = gv[a], ov[a]
+            if isinstance(y, AvgPair):
+                assert x.count == y.count, (k, fn)
+                if fp:
+                    assert x.sum == pytest.approx(y.sum, rel=REL, abs=1e-6), (k, fn)
+                else:
+                    assert x.sum == y.sum, (k, fn)
+            elif fp and fn == "SUM":
+                assert x == pytest.approx(y, rel=REL, abs=1e-6), (k, fn)
+            else:
+                assert x == y, (k, fn, x, y)
+
+
+def gpu_table(schema, segments):
+    t = GpuTable(schema)
+    handles = [t.pin_segment(s) for s in segments]
+    return t, handles
+
+
+# ------------------------------------------------------------------------------------------------ KATs
+@pytest.fixture(scope="module")
+def sv(oracle, gpu_lib):
+    seg = oracle.make_segment(K.SCHEMA, K.sv_columns())
+    t, hs = gpu_table(K.SCHEMA, [seg])
+    yield seg, t, hs[0]
+    t.close()
+
+
+@pytest.mark.parametrize("case", K.KAT["inner_segment_group_by"][:3], ids=lambda c: c["holder"])
+@pytest.mark.parametrize("with_filter", [False, True], ids=["no_filter", "filter"])
+def test_kat_inner_segment(oracle, sv, case, with_filter):
+    seg, t, h = sv
+    q = K.inner_query(case["group_by"], with_filter)
+    r = t.execute_groupby([h], q)
+    exp = case["filter" if with_filter else "no_filter"]
+    docs, _, post, total = exp["stats"]
+    assert (r.stats.num_docs_scanned, r.stats.num_entries_scanned_post_filter, r.stats.num_total_docs) == \
+        (docs, post, total)
+    key = K.key_tuple(case["group_by"], exp["key"])
+    K.check_inner_values(r.as_dict()[key], exp["values"])
+    assert_same(r, oracle.run_groupby(K.SCHEMA, [seg], q, combine=False), q, K.SCHEMA)
+
+
+def test_kat_array_map_shape_is_unsupported(sv):
+    """VERY_LARGE_GROUP_BY overflows a 64-bit composite key (Pinot's ARRAY_MAP holder): the GPU path declines
+    and the caller keeps Pinot's operator."""
+    seg, t, h = sv
+    case = K.KAT["inner_segment_group_by"][3]
+    with pytest.raises(L.UnsupportedQueryError):
+        t.execute_groupby([h], K.inner_query(case["group_by"], False))
+
+
+@pytest.mark.parametrize("with_filter", [False, True])
+def test_kat_aggregation_totals(sv, with_filter):
+    seg, t, h = sv
+    r = t.execute_groupby([h], K.inner_query(["column5"], with_filter))
+    exp = K.KAT["inner_segment_aggregation_only"]["filter" if with_filter else "no_filter"]
+    K.check_inner_values(r.as_dict()[("gFuH",)], exp["values"])
+
+
+@pytest.mark.parametrize("case", K.KAT["inter_segment_group_by"], ids=lambda c: "_".join(c["group_by"]))
+def test_kat_inter_segment(oracle, sv, case):
+    seg, t, h = sv
+    handles = [h] * K.KAT["inter_segment_num_segments"]
+    q = QueryContext(case["group_by"], [tuple(a) for a in case["aggs"]])
+    r = t.execute_groupby(handles, q)
+    assert (r.stats.num_docs_scanned, r.stats.num_entries_scanned_post_filter, r.stats.num_total_docs) == \
+        (case["stats"][0], case["stats"][2], case["stats"][3])
+    got = r.as_dict()
+    rows = {K.key_tuple(case["group_by"], k): v for k, v in case["rows"]}
+    if case["complete"]:
+        assert set(got) == set(rows)
+    for k, v in rows.items():
+        assert [float(x) for x in got[k]] == [float(x) for x in v], k
+
+
+def test_kat_sql_string_filter(oracle, sv):
+    """The reference's filter string parsed by the PQL/SQL subset parser gives the same answer."""
+    seg, t, h = sv
+    sql = ("SELECT COUNT(*), SUM(column1), MAX(column3), MIN(column6), AVG(column7) FROM testTable "
+           "WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 1000000000 AND column5 = 'gFuH' "
+           "AND (column6 < 500000000 OR column11 NOT IN ('t', 'P')) AND daysSinceEpoch = 126164076 GROUP BY column9")
+    q = parse_query(sql)
+    r = t.execute_groupby([h], q)
+    exp = K.KAT["inner_segment_group_by"][0]["filter"]
+    K.check_inner_values(r.as_dict()[(242920,)], exp["values"])
+    assert r.stats.num_docs_scanned == 6129
+
+
+def test_bad_literal_is_bad_query(sv):
+    seg, t, h = sv
+    q = QueryContext(["column9"], [("COUNT", "*")], FilterContext.pred(Predicate.eq("column1", "abc")))
+    with pytest.raises(L.BadQueryRequestException):
+        t.execute_groupby([h], q)
+
+
+# ------------------------------------------------------------------------------------------------ randomized
+def _random_segment(oracle, rng, schema, n):
+    cols = {}
+    for name, typ in schema:
+        card = int(rng.integers(1, 3000))
+        if typ == "INT":
+            dom = rng.integers(-2 ** 31, 2 ** 31, size=card)
+        elif typ == "LONG":
+            dom = rng.integers(-2 ** 50, 2 ** 50, size=card)
+        elif typ == "DOUBLE":
+            dom = rng.uniform(-1e6, 1e6, size=card)
+        elif typ == "FLOAT":
+            dom = rng.uniform(-1e3, 1e3, size=card).astype(np.float32).astype(np.float64)
+        else:
+            dom = np.array(["s%05d" % i for i in rng.integers(0, 5000, size=card)])
+        pick = rng.integers(0, card, size=n)
+        cols[name] = [str(x) for x in dom[pick]] if typ == "STRING" else dom[pick]
+    return oracle.make_segment(schema, cols)
+
+
+SCHEMA_R = [("a", "INT"), ("b", "INT"), ("c", "LONG"), ("d", "DOUBLE"), ("e", "STRING"), ("f", "FLOAT")]
+
+
+def _some_value(seg, col, rng):
+    c = seg.columns[col]
+    i = int(rng.integers(0, c.cardinality))
+    w = c.entry_width
+    raw = c.dict_bytes[i * w:(i + 1) * w]
+    if c.data_type == L.INT:
+        return str(int.from_bytes(raw, "big", signed=True))
+    if c.data_type == L.LONG:
+        return str(int.from_bytes(raw, "big", signed=True))
+    if c.data_type == L.DOUBLE:
+        return repr(float(np.frombuffer(raw, dtype=">f8")[0]))
+    if c.data_type == L.FLOAT:
+        return repr(float(np.frombuffer(raw, dtype=">f4")[0]))
+    return raw.rstrip(b"\0").decode()
+
+
+def _random_filter(rng, seg, depth=0):
+    if depth < 2 and rng.random() < 0.4:
+        kids = [_random_filter(rng, seg, depth + 1) for _ in range(int(rng.integers(2, 4)))]
+        r = rng.random()
+        f = FilterContext.and_(*kids) if r < 0.5 else FilterContext.or_(*kids)
+        return FilterContext.not_(f) if rng.random() < 0.15 else f
+    col = ["a", "b", "c", "d", "e", "f"][int(rng.integers(0, 6))]
+    kind = int(rng.integers(0, 5))
+    v1, v2 = _some_value(seg, col, rng), _some_value(seg, col, rng)
+    if kind == 0:
+        return FilterContext.pred(Predicate.eq(col, v1))
+    if kind == 1:
+        return FilterContext.pred(Predicate.not_eq(col, v1))
+    if kind == 2:
+        return FilterContext.pred(Predicate.in_(col, [v1, v2, _some_value(seg, col, rng)]))
+    if kind == 3:
+        return FilterContext.pred(Predicate.not_in(col, [v1, v2]))
+    if col == "e":
+        lo, hi = sorted([v1, v2])
+    else:
+        lo, hi = sorted([v1, v2], key=float)
+    return FilterContext.pred(Predicate.range(col, lo if rng.random() < 0.8 else "*", hi if rng.random() < 0.8 else "*",
+                                              bool(rng.random() < 0.5), bool(rng.random() < 0.5)))
+
+
+@pytest.mark.parametrize("seed", list(range(12)))
+def test_random_queries_vs_oracle(oracle, gpu_lib, seed):
+    rng = np.random.default_rng(1000 + seed)
+    nseg = int(rng.integers(1, 5))
+    segs = [_random_segment(oracle, rng, SCHEMA_R, int(rng.integers(1, 40000))) for _ in range(nseg)]
+    t, hs = gpu_table(SCHEMA_R, segs)
+    try:
+        for qi in range(4):
+            gb = list(rng.choice(["a", "b", "e", "c"], size=int(rng.integers(1, 3)), replace=False))
+            aggs = [("COUNT", "*"), ("SUM", "a"), ("MIN", "d"), ("MAX", "c"), ("AVG", "f"), ("SUM", "d"),
+                    ("MAX", "f"), ("MIN", "b")]
+            flt = _random_filter(rng, segs[0]) if qi % 3 != 0 else None
+            q = QueryContext(gb, aggs, flt, num_groups_limit=10 ** 9)
+            r = t.execute_groupby(hs, q)
+            o = oracle.run_groupby(SCHEMA_R, segs, q, combine=False, max_initial_capacity=10000)
+            assert_same(r, o, q, SCHEMA_R)
+            assert r.stats.num_docs_scanned == o.stats[0]
+            assert r.stats.num_total_docs == o.stats[3]
+    finally:
+        t.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 8191, 8192, 8193, 70001])
+def test_ragged_segment_sizes(oracle, gpu_lib, n):
+    rng = np.random.default_rng(n)
+    schema = [("g", "INT"), ("v", "INT")]
+    seg = oracle.make_segment(schema, {"g": rng.integers(0, 7, size=n), "v": rng.integers(0, 1000, size=n)})
+    t, hs = gpu_table(schema, [seg, seg])
+    try:
+        q = parse_query("SELECT COUNT(*), SUM(v) FROM t WHERE v >= 100 GROUP BY g")
+        r = t.execute_groupby(hs, q)
+        o = oracle.run_groupby(schema, [seg, seg], q)
+        assert_same(r, o, q, schema)
+        if n > 0:
+            bm = t.filter_bitmap(hs[0], q, n)
+            ob = oracle.filter_bitmap(schema, seg, q)
+            np.testing.assert_array_equal(bm, ob)
+    finally:
+        t.close()
+
+
+@pytest.mark.parametrize("nbits_card", [2, 3, 17, 255, 256, 5000, 70000, 2 ** 20 + 7])
+def test_read_dict_ids_every_width(oracle, gpu_lib, nbits_card):
+    rng = np.random.default_rng(nbits_card)
+    n = 50000
+    vals = rng.integers(0, nbits_card, size=n)
+    vals[:nbits_card if nbits_card < n else 0] = np.arange(min(nbits_card, n))
+    seg = oracle.make_segment([("x", "INT")], {"x": vals})
+    t, hs = gpu_table([("x", "INT")], [seg])
+    try:
+        docs = np.sort(rng.choice(n, 5000, replace=False)).astype(np.int32)
+        got = t.read_dict_ids(hs[0], "x", docs)
+        o = oracle.lib()
+        c = seg.columns["x"]
+        buf = np.frombuffer(c.fwd_bytes + b"\0" * 16, dtype=np.uint8).copy()
+        exp = np.zeros(len(docs), dtype=np.int32)
+        o.or_read_dict_ids(buf.ctypes.data, c.bits_per_element, n, docs.ctypes.data, len(docs), exp.ctypes.data)
+        np.testing.assert_array_equal(got, exp)
+    finally:
+        t.close()
+
+
+def test_unpack_device_with_torch(oracle, gpu_lib):
+    import torch
+    rng = np.random.default_rng(5)
+    for bits in (1, 7, 9, 16, 17, 23, 31):
+        n = 100003
+        vals = rng.integers(0, 1 << bits, size=n).astype(np.int32)
+        buf = np.zeros(oracle.lib().or_fwd_num_bytes(n, bits) + 16, dtype=np.uint8)
+        oracle.lib().or_bitset_write_ints(buf.ctypes.data, 0, bits, n, vals.ctypes.data)
+        d_fwd = torch.from_numpy(buf).cuda()
+        d_out = torch.empty(n - 5, dtype=torch.int32, device="cuda")
+        L.check(gpu_lib.pgpu_unpack_fixed_bit_device(ctypes.c_void_p(d_fwd.data_ptr()), len(buf), bits, 5, n - 5,
+                                                     ctypes.c_void_p(d_out.data_ptr()), None))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_out.cpu().numpy(), vals[5:])
+
+
+def test_sorted_forward_index_format(oracle, gpu_lib):
+    """SortedIndexReaderImpl pairs (sorted columns, e.g. daysSinceEpoch in the KAT segment) pin correctly."""
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    vals = np.repeat(np.arange(5), [3, 0, 4, 1, 2])[:10]
+    seg = oracle.make_segment([("s", "INT"), ("v", "INT")], {"s": vals * 10, "v": np.arange(10)})
+    c = seg.columns["s"]
+    ids = np.unique(vals, return_inverse=True)[1]
+    pairs = b"".join(int(np.where(ids == i)[0][0]).to_bytes(4, "big") + int(np.where(ids == i)[0][-1]).to_bytes(4, "big")
+                     for i in range(c.cardinality))
+    sorted_seg = SegmentBuffers(10, {"s": ColumnData(c.data_type, c.cardinality, c.bits_per_element, 4, c.dict_bytes,
+                                                     pairs, fwd_format=L.FWD_SORTED_PAIRS),
+                                     "v": seg.columns["v"]})
+    t, hs = gpu_table([("s", "INT"), ("v", "INT")], [sorted_seg])
+    try:
+        r = t.execute_groupby(hs, parse_query("SELECT SUM(v), COUNT(*) FROM t GROUP BY s"))
+        o = oracle.run_groupby([("s", "INT"), ("v", "INT")], [seg],
+                               parse_query("SELECT SUM(v), COUNT(*) FROM t GROUP BY s"))
+        assert r.as_dict() == o.groups
+    finally:
+        t.close()
+
+
+def test_padding_segments_pin_and_query(gpu_lib, tmp_path):
+    """Real Pinot-written v1 segments (padding*.tar.gz) pin and answer like the oracle reading the same bytes."""
+    import json
+    import os
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    segs = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "padding_segments.json")))
+    for name, s in segs.items():
+        pad = 0 if "u0000" in s["paddingCharacter"] else ord(s["paddingCharacter"][0])
+        cols = {}
+        schema = []
+        for col, c in s["columns"].items():
+            typ = c["dataType"]
+            width = {"INT": 4, "FLOAT": 4, "LONG": 8, "DOUBLE": 8}.get(typ, c["lengthOfEachEntry"])
+            cols[col] = ColumnData(L.TYPE_NAMES[typ], c["cardinality"], c["bitsPerElement"], width,
+                                   bytes.fromhex(c["dict_hex"]), bytes.fromhex(c["fwd_hex"]),
+                                   pad if typ == "STRING" else 0)
+            schema.append((col, typ))
+        t, hs = gpu_table(schema, [SegmentBuffers(s["totalDocs"], cols)])
+        try:
+            r = t.execute_groupby(hs, parse_query("SELECT SUM(age), COUNT(*) FROM t GROUP BY name"))
+            got = {k[0]: v for k, v in r.as_dict().items()}
+            assert sum(v[1] for v in got.values()) == 5
+            assert got["lynda"][1] == 2 and got["lynda 2.0"][1] == 3
+            ages = {617, 824, 837, 1209, 1228}
+            assert sum(v[0] for v in got.values()) == float(sum(ages))
+            r2 = t.execute_groupby(hs, parse_query("SELECT COUNT(*) FROM t WHERE name = 'lynda' GROUP BY age"))
+            assert sum(v[0] for v in r2.as_dict().values()) == 2
+        finally:
+            t.close()

@@ -36,6 +36,7 @@ def parse_args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
     p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
+    p.add_argument("--host-profile", action="store_true", help="report host time per phase of a step")
     return p.parse_args()
 
 
@@ -172,19 +173,31 @@ def main():
     probe.close()
     d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
 
+    phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0}
+
     def step():
+        c0 = time.perf_counter()
         plan = table.plan(handles, q)
+        c1 = time.perf_counter()
         plan.execute(stream, d_table.data_ptr() if nkeys > 0 else None)
+        c2 = time.perf_counter()
         if world > 1:
             allreduce_group_table(d_table, kinds)
+        c3 = time.perf_counter()
         res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
+        c4 = time.perf_counter()
         k_us = plan.timing_us()[1]
         plan.close()
+        c5 = time.perf_counter()
+        for k, v in zip(phases, (c1 - c0, c2 - c1, c3 - c2, c4 - c3, c5 - c4)):
+            phases[k] += v
         return res, k_us
 
     first = None
     for _ in range(args.warmup):
         first, _ = step()
+    for k in phases:
+        phases[k] = 0.0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -239,6 +252,7 @@ def main():
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
                        "groups": len(first) if first is not None else None, "setup_s": round(t_gen, 1)},
             "roofline": roofline,
+            "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -972,6 +972,7 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   int long_overflow = 0;
   for (int i = 0; i < g.nk; i++) {
     int card = seg->columns[q->group_by[i]].cardinality;
+    if (card < 1) card = 1; /* empty segment: Pinot never builds one; keep the key math defined */
     g.card[i] = card;
     if (!long_overflow) {
       if (card_product > INT64_MAX / card) long_overflow = 1;

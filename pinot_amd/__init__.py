@@ -4,7 +4,7 @@ The compute path is libpinotgpu.so (HIP kernels for gfx950 behind the C ABI in i
 package is the host layer over it: query model, pinned tables, plans, results, and the Pinot-named operator
 mirror used by the tests and bench.py.
 """
-from .build import LIB_PATH, build  # noqa: F401
+from .build import LIB_PATH  # noqa: F401
 from .query import FilterContext, Predicate, QueryContext, parse_query  # noqa: F401
 from .segment import ColumnData, SegmentBuffers, load_v1_segment_dir  # noqa: F401
 

@@ -138,10 +138,16 @@ def load(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("PGPU_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise ImportError("libpinotgpu.so is not built (%s); run `python -m pinot_amd.build` "
                           "or __graft_entry__.build()" % p)
+    try:
+        # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7 must be the one the
+        # dynamic linker resolves for this library too (loading the system copy first breaks torch.cuda).
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(p)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

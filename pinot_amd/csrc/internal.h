@@ -3,9 +3,9 @@
 //
 // HBM layout of a pinned segment column (one hipMalloc per segment, columns packed back to back):
 //   fwd   : Pinot's forward-index bytes verbatim (MSB-first, big-endian bit packing of
-//           FixedBitSVForwardIndexReaderV2), read as big-endian u32 words, zero-padded to
-//           ceil(numDocs/32) * bits words + 4 spare words so that a 32-doc group load and a two-word gather
-//           never leave the allocation;
+//           FixedBitSVForwardIndexReaderV2), read as big-endian u32 words, zero-padded to a whole number of
+//           8192-doc tiles (ceil(numDocs/8192) * 256 * bits words) + 4 spare words, so that a tile's LDS-DMA and a
+//           two-word gather never leave the allocation;
 //   lut   : int32 local dictId -> table-global dictId (group-by columns; built lazily, rebuilt when the
 //           table's global dictionary grows);
 //   dkey  : int64 per dictId: the value (INT/LONG) or an order-preserving key of the IEEE double
@@ -26,6 +26,8 @@ constexpr int kMaxKeys = 8;                 // group-by columns handled on the G
 constexpr int kMaxSlots = 24;               // accumulator rows of the group table
 constexpr int kMaxStack = 8;                // filter evaluation stack depth
 constexpr int kFwdPadWords = 4;
+constexpr int kMaxStage = 4;                // distinct filter columns staged into LDS per tile
+constexpr int kQueueCap = 1024;             // matched-doc queue entries per workgroup (LDS)
 
 enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
@@ -63,6 +65,7 @@ struct KSegHdr {
 
 struct KParams {
   const uint8_t* segs;     // num_segs records of seg_stride bytes
+  const int32_t* tile_seg; // tile -> segment record (expand_tiles_kernel)
   int32_t seg_stride;
   int32_t num_cols;
   int32_t num_segs;
@@ -79,6 +82,11 @@ struct KParams {
   int32_t num_slots;
   int32_t slot_kind[kMaxSlots];
   int32_t slot_col[kMaxSlots];
+  int32_t num_stage;               // staged (filter) columns: query column slots, LDS-DMA'd per tile
+  int32_t stage_col[kMaxStage];
+  int32_t leaf_stage[kMaxLeaves];  // staged column of each leaf
+  int32_t stage_words;             // words of one stage buffer (max over the plan's segments)
+  int32_t lds_table_words;         // MODE_LDS group table words at the start of LDS
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
@@ -90,12 +98,13 @@ int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, i
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
 int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                       unsigned long long* hash_keys, void* stream);
+int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg, void* stream);
 int launch_filter_groupby(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
+int launch_scan(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
 int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int32_t num_slots, int64_t num_keys,
                         int32_t num_blocks, uint64_t* out, void* stream);
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
-                   unsigned long long* counter, uint64_t* out_keys, uint64_t* out_slots, int64_t out_cap,
-                   void* stream);
+                   unsigned long long* counter, uint64_t* out, int64_t out_cap, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.
 int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,

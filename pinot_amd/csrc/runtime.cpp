@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -32,6 +33,15 @@ using namespace pgpu;
 namespace {
 
 thread_local std::string g_err;
+
+// PGPU_TRACE=1: per-phase host timings on stderr (diagnostics only).
+bool trace_on() {
+  static const bool on = getenv("PGPU_TRACE") && getenv("PGPU_TRACE")[0] == '1';
+  return on;
+}
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 int fail(int code, const char* fmt, ...) {
   char buf[1024];
@@ -134,6 +144,10 @@ inline double key_double(int64_t k) {
   return d;
 }
 
+constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kMaxScanLds = 128 * 1024;          // larger staging falls back to the direct-load kernel
+
 bool is_int_type(int t) { return t == PGPU_INT || t == PGPU_LONG; }
 bool is_fp_type(int t) { return t == PGPU_FLOAT || t == PGPU_DOUBLE; }
 
@@ -212,11 +226,11 @@ struct Segment {
 };
 
 struct Scratch {
-  DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap;
+  DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg;
   HostPinned stage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   void release() {
-    segrec.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
+    segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
@@ -241,6 +255,7 @@ struct pgpu_table_s {
   std::vector<std::unique_ptr<Scratch>> scratch_pool;
   GenScratch gen;
   int64_t device_bytes = 0;
+  int num_cus = 256;
 };
 
 namespace {
@@ -463,7 +478,9 @@ void free_segment(pgpu_table_s* t, Segment* s) {
   if (s->d_block) hipFree(s->d_block);
 }
 
-int64_t padded_fwd_words(int64_t num_docs, int bits) { return ((num_docs + 31) / 32) * bits + kFwdPadWords; }
+int64_t padded_fwd_words(int64_t num_docs, int bits) {
+  return ((num_docs + kTileDocs - 1) / kTileDocs) * (int64_t)kBlock * bits + kFwdPadWords;
+}
 
 // Registers a segment whose columns have parsed dictionaries and device forward indexes.
 int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
@@ -514,6 +531,11 @@ struct pgpu_plan_s {
   int segments_matched_filter = 0;
   int grid = 0;
   size_t lds_bytes = 0;
+  bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
+  std::vector<int32_t> stage_slot;        // query column slot of each staged filter column
+  std::vector<int32_t> leaf_stage;        // staged column of each leaf
+  int64_t stage_words = 0;                // one stage buffer (max over segments)
+  int lds_table_words = 0;
   Scratch* scratch = nullptr;
   hipStream_t last_stream = nullptr;
   bool executed = false;
@@ -663,6 +685,7 @@ Tri fold_program(const std::vector<int32_t>& ops, const std::vector<Tri>& leaf) 
 
 int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P) {
   if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
+  const double t_start = trace_on() ? now_us() : 0;
   const int ncols = (int)t->names.size();
   if (q->num_group_by < 1) return fail(PGPU_ERR_UNSUPPORTED, "aggregation without GROUP BY is not on this path");
   if (q->num_group_by > kMaxKeys) return fail(PGPU_ERR_UNSUPPORTED, "more than %d group-by columns", kMaxKeys);
@@ -857,12 +880,43 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   }
   P->num_tiles = tile_base;
   if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
-  P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));
+  P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));  // 4 workgroups per CU
+  // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
+  for (int l = 0; l < P->num_leaves; ++l) {
+    int sidx = -1;
+    for (size_t k = 0; k < P->stage_slot.size(); ++k)
+      if (P->stage_slot[k] == P->leaf_slot[l]) sidx = (int)k;
+    if (sidx < 0) {
+      P->stage_slot.push_back(P->leaf_slot[l]);
+      sidx = (int)P->stage_slot.size() - 1;
+    }
+    P->leaf_stage.push_back(sidx);
+  }
+  static const bool scan_off = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '0';  // A/B switch for profiling
+  if ((int)P->stage_slot.size() <= kMaxStage && !scan_off) {
+    const bool pure_and = P->pure_and && P->num_leaves <= 4;  // the staged fast path holds at most 4 leaves in registers
+    for (Segment* s : P->segs) {
+      int64_t bits = 0;
+      for (int slot : P->stage_slot) bits += s->cols[P->query_cols[slot]].bits;
+      P->stage_words = std::max<int64_t>(P->stage_words, bits * kBlock);
+    }
+    P->lds_table_words = P->mode == MODE_LDS ? (int)((nslots * G + 1) & ~int64_t(1)) : 0;
+    const size_t lds = (size_t)P->lds_table_words * 8 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + 16 +
+                       (size_t)kQueueCap * 8 + (size_t)P->stage_words * 2 * 4;
+    if (lds <= kMaxScanLds) {
+      P->staged = true;
+      P->pure_and = pure_and;
+      P->lds_bytes = lds;
+      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, kLdsPerCu / lds));
+      P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+    }
+  }
+  if (trace_on()) fprintf(stderr, "[pgpu] plan_create: %.1f us (%zu segments)\n", now_us() - t_start, P->segs.size());
   return 0;
 }
 
 int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
-  pgpu_table_s* t = P->table;
+  const double t_start = trace_on() ? now_us() : 0;
   Scratch* sc = P->scratch;
   const int nslots = (int)P->slot_kind.size();
   const int64_t words = (int64_t)nslots * P->num_keys;
@@ -928,10 +982,20 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
       return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
     kp.table = table;
   }
+  TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(P->num_tiles, 1) * 4));
+  kp.tile_seg = sc->tile_seg.as<int32_t>();
+  if (launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>(), stream))
+    return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
+  kp.num_stage = (int)P->stage_slot.size();
+  for (size_t k = 0; k < P->stage_slot.size() && k < (size_t)kMaxStage; ++k) kp.stage_col[k] = P->stage_slot[k];
+  for (size_t l = 0; l < P->leaf_stage.size(); ++l) kp.leaf_stage[l] = P->leaf_stage[l];
+  kp.stage_words = (int32_t)P->stage_words;
+  kp.lds_table_words = P->lds_table_words;
   HIP_TRY(hipEventRecord(sc->ev[1], stream));
   if (P->num_tiles > 0) {
-    if (launch_filter_groupby(kp, P->mode, P->grid, P->lds_bytes, stream))
-      return fail(PGPU_ERR_DEVICE, "filter_groupby launch failed: %s", hipGetErrorString(hipGetLastError()));
+    const int rc = P->staged ? launch_scan(kp, P->mode, P->grid, P->lds_bytes, stream)
+                             : launch_filter_groupby(kp, P->mode, P->grid, P->lds_bytes, stream);
+    if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
   if (P->mode == MODE_LDS) {
@@ -946,38 +1010,72 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   HIP_TRY(hipEventRecord(sc->ev[3], stream));
   P->last_stream = stream;
   P->executed = true;
+  if (trace_on()) fprintf(stderr, "[pgpu] execute: %.1f us host\n", now_us() - t_start);
   return 0;
 }
 
 int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, pgpu_result_s* R) {
   Scratch* sc = P->scratch;
+  const double t_start = trace_on() ? now_us() : 0;
   if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   const uint64_t* table = reinterpret_cast<const uint64_t*>(d_table ? d_table : P->d_table_used);
   const int nslots = (int)P->slot_kind.size();
-  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
-  TRY(sc->counter.ensure(64));
-  TRY(sc->ckeys.ensure((size_t)cap * 8));
-  TRY(sc->cslots.ensure((size_t)cap * 8 * nslots));
-  HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
-  if (launch_compact(table, P->hash ? sc->hash_keys.as<unsigned long long>() : nullptr, nslots, P->num_keys,
-                     sc->counter.as<unsigned long long>(), sc->ckeys.as<uint64_t>(), sc->cslots.as<uint64_t>(), cap,
-                     stream))
-    return fail(PGPU_ERR_DEVICE, "compact launch failed");
-  uint64_t hdr[2] = {0, 0};
-  TRY(sc->stage.ensure(64));
-  HIP_TRY(hipMemcpyAsync(sc->stage.p, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync((uint8_t*)sc->stage.p + 8, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
-  memcpy(hdr, sc->stage.p, 16);
-  const int64_t n = (int64_t)std::min<uint64_t>(hdr[0], (uint64_t)cap);
-  std::vector<uint64_t> keys(n), slots((size_t)n * nslots);
-  if (n > 0) {
-    HIP_TRY(hipMemcpyAsync(keys.data(), sc->ckeys.p, n * 8, hipMemcpyDeviceToHost, stream));
-    for (int s = 0; s < nslots; ++s)
-      HIP_TRY(hipMemcpyAsync(slots.data() + (size_t)s * n, sc->cslots.as<uint64_t>() + (size_t)s * cap, n * 8,
-                             hipMemcpyDeviceToHost, stream));
+  const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
+  std::vector<uint64_t> keys, slots;  // keys[n], slots[s * n + i]
+  int64_t n = 0;
+  uint64_t matched = 0;
+  const int64_t words = (int64_t)nslots * P->num_keys;
+  double t_sync1 = 0;
+  if (!P->hash && words * 8 <= kHostCompactBytes) {
+    // small dense table: one copy (table + stats) and one sync, compacted on the host
+    TRY(sc->stage.ensure((size_t)words * 8 + 64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    t_sync1 = trace_on() ? now_us() : 0;
+    matched = st[words];
+    const int64_t G = P->num_keys;
+    for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
+    keys.resize(n);
+    slots.resize((size_t)n * nslots);
+    int64_t j = 0;
+    for (int64_t k = 0; k < G; ++k) {
+      if (!st[k]) continue;
+      keys[j] = (uint64_t)k;
+      for (int s = 0; s < nslots; ++s) slots[(size_t)s * n + j] = st[(int64_t)s * G + k];
+      ++j;
+    }
+  } else {
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
+    TRY(sc->counter.ensure(64));
+    TRY(sc->ckeys.ensure((size_t)cap * 8 * rec));
+    HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
+    if (launch_compact(table, P->hash ? sc->hash_keys.as<unsigned long long>() : nullptr, nslots, P->num_keys,
+                       sc->counter.as<unsigned long long>(), sc->ckeys.as<uint64_t>(), cap, stream))
+      return fail(PGPU_ERR_DEVICE, "compact launch failed");
+    TRY(sc->stage.ensure(64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    t_sync1 = trace_on() ? now_us() : 0;
+    n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
+    matched = st[1];
+    if (n > 0) {
+      TRY(sc->stage.ensure((size_t)n * rec * 8));
+      st = reinterpret_cast<uint64_t*>(sc->stage.p);
+      HIP_TRY(hipMemcpyAsync(st, sc->ckeys.p, (size_t)n * rec * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+    }
+    keys.resize(n);
+    slots.resize((size_t)n * nslots);
+    for (int64_t j = 0; j < n; ++j) {
+      keys[j] = st[j * rec];
+      for (int s = 0; s < nslots; ++s) slots[(size_t)s * n + j] = st[j * rec + 1 + s];
+    }
   }
+  const double t_sync2 = trace_on() ? now_us() : 0;
   // order groups by composite key
   std::vector<int64_t> order(n);
   for (int64_t i = 0; i < n; ++i) order[i] = i;
@@ -1029,12 +1127,15 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       R->has_exact[a] = fn == PGPU_AGG_COUNT || (P->slot_kind[P->agg_slot[a]] == SLOT_SUM_I64) ||
                         ((fn == PGPU_AGG_MIN || fn == PGPU_AGG_MAX) && is_int_type(P->table->types[P->agg_col[a]]));
     }
-  R->stats[0] = (int64_t)hdr[1];
+  R->stats[0] = (int64_t)matched;
   R->stats[1] = P->scanned_entries_model;
-  R->stats[2] = (int64_t)hdr[1] * P->num_projected;
+  R->stats[2] = (int64_t)matched * P->num_projected;
   R->stats[3] = P->total_docs;
   R->stats[4] = (int64_t)P->segs.size();
   R->stats[5] = P->segments_matched_filter;
+  if (trace_on())
+    fprintf(stderr, "[pgpu] finalize: launch+sync1 %.1f us, copy+sync2 %.1f us, decode %.1f us (n=%lld)\n",
+            t_sync1 - t_start, t_sync2 - t_sync1, now_us() - t_sync2, (long long)n);
   return 0;
 }
 
@@ -1082,6 +1183,9 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
   }
   DeviceGuard g(device);
   HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    t->num_cus = cus;
   *out = t.release();
   return 0;
 }
@@ -1146,6 +1250,7 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
             }
         }
       }
+      for (auto& x : w) x = __builtin_bswap32(x);  // the device reads the forward index as big-endian bytes
     } else {
       return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad forward-index format", c);
     }

@@ -231,7 +231,8 @@ def test_read_dict_ids_every_width(oracle, gpu_lib, nbits_card):
     rng = np.random.default_rng(nbits_card)
     n = 50000
     vals = rng.integers(0, nbits_card, size=n)
-    vals[:nbits_card if nbits_card < n else 0] = np.arange(min(nbits_card, n))
+    m = min(nbits_card, n)
+    vals[:m] = np.arange(m)
     seg = oracle.make_segment([("x", "INT")], {"x": vals})
     t, hs = gpu_table([("x", "INT")], [seg])
     try:

@@ -8,8 +8,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB_PATH = os.path.join(HERE, "libpinotgpu.so")
-SOURCES = ["kernels.hip", "runtime.cpp"]
-HEADERS = ["internal.h"]
+# (source, extra flags, object name): the scan kernels are compiled once per accumulator mode so the objects
+# build in parallel.
+SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime")] + \
+    [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
+    [("k_staged.hip", ["-DPGPU_MODE=%d" % m], "k_staged_%d" % m) for m in range(3)]
+HEADERS = ["internal.h", "device.h", "scan_direct.h", "scan_staged.h"]
 ARCH = os.environ.get("PGPU_OFFLOAD_ARCH", "gfx950")
 
 
@@ -21,7 +25,7 @@ def _hipcc():
 
 
 def _inputs():
-    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files = [os.path.join(CSRC, s[0]) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
     files.append(os.path.join(ROOT, "include", "pinotgpu.h"))
     return files
 
@@ -34,19 +38,36 @@ def is_stale():
 
 
 def build(force=False, verbose=False):
-    """Compiles the kernels and the host runtime into pinot_amd/libpinotgpu.so (cross-compiles without a GPU)."""
+    """Compiles the kernels and the host runtime into pinot_amd/libpinotgpu.so (cross-compiles without a GPU).
+    Each source is compiled to an object in parallel, then linked."""
     if not force and not is_stale():
         return LIB_PATH
-    cmd = [
-        _hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17", "-munsafe-fp-atomics",
-        "-Wall", "-Wno-unused-result", "-Wno-unused-value",
-        "-o", LIB_PATH + ".tmp",
-    ] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
+    hipcc = _hipcc()
+    flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
+             "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
+    objdir = os.path.join(ROOT, "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    procs = []
+    objs = []
+    for src, extra, name in SOURCES:
+        obj = os.path.join(objdir, name + ".o")
+        objs.append(obj)
+        cmd = [hipcc] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                            text=True)))
+    errors = []
+    for src, pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            errors.append("%s:\n%s" % (src, out[-8000:]))
+    if errors:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
     res = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if res.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + res.stdout[-8000:])
+        raise RuntimeError("hipcc link failed:\n" + res.stdout[-8000:])
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 

@@ -1,0 +1,336 @@
+// device.h — device-side building blocks shared by the gfx950 kernels: the MSB-first fixed-bit decoders
+// (PinotDataBitSet / FixedBitIntReader layout), predicate leaf masks, segment-record views, accumulators and
+// the batched group-by aggregation.  Included by every kernel translation unit (one object per kernel family and
+// accumulator mode, compiled in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "internal.h"
+
+namespace pgpu {
+
+#define PGPU_HIP_OK(x) ((x) == hipSuccess ? 0 : -1)
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Value of doc `doc` in a packed column (PinotDataBitSet.readInt semantics).  The two-word window never leaves
+// the allocation thanks to the padding words.
+__device__ __forceinline__ uint32_t gather_id(const uint32_t* __restrict__ fwd, int bits, int64_t doc) {
+  const uint64_t bit = (uint64_t)doc * (uint64_t)bits;
+  const uint64_t wi = bit >> 5;
+  const uint32_t sh = (uint32_t)(bit & 31);
+  const uint64_t two = ((uint64_t)bswap32(fwd[wi]) << 32) | (uint64_t)bswap32(fwd[wi + 1]);
+  return (uint32_t)(two >> (64 - sh - bits)) & ((1u << bits) - 1u);
+}
+
+// ---------------------------------------------------------------------------------------------- K2 leaf masks
+// A lane's 32-doc group is B big-endian u32 words; doc i occupies bits [i*B, i*B+B) counted from the MSB of word
+// 0 (FixedBitIntReader.read32 layout).  Each decoder walks the docs from 31 down to 0 and shifts the predicate
+// bit in with v_alignbit (mask = mask << 1 | sign(test)), so doc i lands on bit i without materialising 1 << i.
+template <int B, int I>
+__device__ __forceinline__ uint32_t extract(const uint32_t (&w)[B + 1]) {
+  constexpr int bit = I * B, wi = bit >> 5, sh = bit & 31;
+  if constexpr (sh + B <= 32) {
+    return __builtin_amdgcn_ubfe(w[wi], 32 - sh - B, B);
+  } else {
+    return __builtin_amdgcn_alignbit(w[wi], w[wi + 1], 64 - sh - B) & ((1u << B) - 1u);
+  }
+}
+
+template <int B>
+__device__ __forceinline__ void load_group(const uint32_t* __restrict__ words, uint32_t (&w)[B + 1]) {
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(words[k]);
+  w[B] = 0;
+}
+
+// value in [lo, hi): sign bit of (v - hi) & ~(v - lo)   (values, lo, hi < 2^31)
+template <int B, int I>
+__device__ __forceinline__ uint32_t range_step(const uint32_t (&w)[B + 1], uint32_t lo, uint32_t hi, uint32_t m) {
+  const uint32_t v = extract<B, I>(w);
+  const uint32_t t = (v - hi) & ~(v - lo);
+  return __builtin_amdgcn_alignbit(m, t, 31);
+}
+// value == eq: sign bit of (v ^ eq) - 1
+template <int B, int I>
+__device__ __forceinline__ uint32_t eq_step(const uint32_t (&w)[B + 1], uint32_t eq, uint32_t m) {
+  const uint32_t v = extract<B, I>(w);
+  return __builtin_amdgcn_alignbit(m, (v ^ eq) - 1u, 31);
+}
+
+template <int B, int... I>
+__device__ __forceinline__ uint32_t range_all(const uint32_t (&w)[B + 1], uint32_t lo, uint32_t hi,
+                                              std::integer_sequence<int, I...>) {
+  uint32_t m = 0;
+  ((m = range_step<B, 31 - I>(w, lo, hi, m)), ...);
+  return m;
+}
+template <int B, int... I>
+__device__ __forceinline__ uint32_t eq_all(const uint32_t (&w)[B + 1], uint32_t eq, std::integer_sequence<int, I...>) {
+  uint32_t m = 0;
+  ((m = eq_step<B, 31 - I>(w, eq, m)), ...);
+  return m;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t leaf_range_b(const uint32_t* __restrict__ words, uint32_t lo, uint32_t span) {
+  uint32_t w[B + 1];
+  load_group<B>(words, w);
+  if (span == 1) return eq_all<B>(w, lo, std::make_integer_sequence<int, 32>{});
+  return range_all<B>(w, lo, lo + span, std::make_integer_sequence<int, 32>{});
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t leaf_set_b(const uint32_t* __restrict__ words, const uint32_t* __restrict__ set) {
+  uint32_t w[B + 1];
+  load_group<B>(words, w);
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int bit = i * B, wi = bit >> 5, sh = bit & 31;
+    uint32_t v;
+    if (sh + B <= 32) v = (w[wi] >> (32 - sh - B)) & ((1u << B) - 1u);
+    else v = ((w[wi] << (sh + B - 32)) | (w[wi + 1] >> (64 - sh - B))) & ((1u << B) - 1u);
+    m |= ((set[v >> 5] >> (v & 31)) & 1u) << i;
+  }
+  return m;
+}
+
+// Wave-uniform dispatch on (kind, bits) to the decoder instance; `words` = this lane's 32-doc group (global
+// memory or an LDS stage buffer).
+__device__ __forceinline__ uint32_t leaf_eval_words(int kind, int negate, uint32_t lo, uint32_t span,
+                                                    const uint32_t* set, const uint32_t* words, int bits) {
+  if (kind == LEAF_ALL) return ~0u;
+  if (kind == LEAF_NONE) return 0u;
+  uint32_t m = 0;
+  if (kind == LEAF_RANGE) {
+    switch (bits) {
+#define PGPU_CASE(B) \
+  case B:            \
+    m = leaf_range_b<B>(words, lo, span); \
+    break;
+      PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
+      PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
+      PGPU_CASE(16) PGPU_CASE(17) PGPU_CASE(18) PGPU_CASE(19) PGPU_CASE(20) PGPU_CASE(21) PGPU_CASE(22)
+      PGPU_CASE(23) PGPU_CASE(24) PGPU_CASE(25) PGPU_CASE(26) PGPU_CASE(27) PGPU_CASE(28) PGPU_CASE(29)
+      PGPU_CASE(30) PGPU_CASE(31)
+#undef PGPU_CASE
+      default: break;
+    }
+  } else {
+    switch (bits) {
+#define PGPU_CASE(B) \
+  case B:            \
+    m = leaf_set_b<B>(words, set); \
+    break;
+      PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
+      PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
+      PGPU_CASE(16) PGPU_CASE(17) PGPU_CASE(18) PGPU_CASE(19) PGPU_CASE(20) PGPU_CASE(21) PGPU_CASE(22)
+      PGPU_CASE(23) PGPU_CASE(24) PGPU_CASE(25) PGPU_CASE(26) PGPU_CASE(27) PGPU_CASE(28) PGPU_CASE(29)
+      PGPU_CASE(30) PGPU_CASE(31)
+#undef PGPU_CASE
+      default: break;
+    }
+  }
+  return negate ? ~m : m;
+}
+
+__device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo, uint32_t span, const uint32_t* set,
+                                              const uint32_t* fwd, int bits, int64_t group) {
+  return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
+}
+
+__device__ __forceinline__ uint32_t leaf_mask(const KLeaf& L, const KCol& C, int64_t group) {
+  return leaf_eval(L.kind, L.negate, L.lo, L.span, L.set, C.fwd, C.bits, group);
+}
+
+// ---------------------------------------------------------------------------------------------- helpers
+struct SegView {
+  const KSegHdr* hdr;
+  const KCol* cols;
+  const KLeaf* leaves;
+};
+
+__device__ __forceinline__ SegView seg_view(const KParams& p, int seg) {
+  const uint8_t* base = p.segs + (int64_t)seg * p.seg_stride;
+  SegView v;
+  v.hdr = reinterpret_cast<const KSegHdr*>(base);
+  v.cols = reinterpret_cast<const KCol*>(base + sizeof(KSegHdr));
+  v.leaves = reinterpret_cast<const KLeaf*>(base + sizeof(KSegHdr) + sizeof(KCol) * p.num_cols);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t slot_init(int kind) {
+  if (kind == SLOT_MIN_KEY) return (uint64_t)INT64_MAX;
+  if (kind == SLOT_MAX_KEY) return (uint64_t)INT64_MIN;
+  return 0ull;
+}
+
+// Leaf descriptors of the current segment held in registers (reloaded only when the segment changes).
+constexpr int kFastLeaves = 4;
+struct LeafReg {
+  const uint32_t* fwd;
+  const uint32_t* set;
+  int32_t bits, kind, negate;
+  uint32_t lo, span;
+};
+
+__device__ __forceinline__ uint32_t leaf_mask_reg(const LeafReg& R, int64_t group) {
+  return leaf_eval(R.kind, R.negate, R.lo, R.span, R.set, R.fwd, R.bits, group);
+}
+
+__device__ __forceinline__ LeafReg load_leaf_reg(const KParams& p, const SegView& S, int l) {
+  LeafReg r;
+  const KLeaf& L = S.leaves[l];
+  const KCol& C = S.cols[p.leaf_col[l]];
+  r.fwd = C.fwd;
+  r.bits = C.bits;
+  r.kind = L.kind;
+  r.negate = L.negate;
+  r.lo = L.lo;
+  r.span = L.span;
+  r.set = L.set;
+  return r;
+}
+
+// Evaluates the filter program for this lane's 32-doc group.
+__device__ __forceinline__ uint32_t eval_filter(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
+                                                uint32_t* __restrict__ stack) {
+  if (p.num_ops == 0) return mask;
+  if (p.pure_and) {
+    for (int l = 0; l < p.num_leaves; ++l) {
+      if (!__any(mask != 0u)) break;  // wave-uniform early exit: AndDocIdIterator never scans past an empty child
+      mask &= leaf_mask(S.leaves[l], S.cols[p.leaf_col[l]], group);
+    }
+    return mask;
+  }
+  const int tid = threadIdx.x;
+  int sp = 0;
+  for (int k = 0; k < p.num_ops; ++k) {
+    const int op = p.ops[k] >> 16, arg = p.ops[k] & 0xFFFF;
+    if (op == OP_LEAF) {
+      stack[sp * kBlock + tid] = leaf_mask(S.leaves[arg], S.cols[p.leaf_col[arg]], group);
+      ++sp;
+    } else if (op == OP_NOT) {
+      stack[(sp - 1) * kBlock + tid] = ~stack[(sp - 1) * kBlock + tid];
+    } else {
+      uint32_t acc = stack[(sp - arg) * kBlock + tid];
+      for (int j = sp - arg + 1; j < sp; ++j) {
+        const uint32_t x = stack[j * kBlock + tid];
+        acc = (op == OP_AND) ? (acc & x) : (acc | x);
+      }
+      sp -= arg;
+      stack[sp * kBlock + tid] = acc;
+      ++sp;
+    }
+  }
+  return mask & stack[tid];
+}
+
+__device__ __forceinline__ int64_t hash_slot(unsigned long long* __restrict__ keys, int64_t cap, uint64_t key) {
+  uint64_t h = key * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 29;
+  int64_t s = (int64_t)(h & (uint64_t)(cap - 1));
+  for (;;) {
+    unsigned long long k = keys[s];
+    if (k == key) return s;
+    if (k == ~0ull) {
+      const unsigned long long prev = atomicCAS(&keys[s], ~0ull, (unsigned long long)key);
+      if (prev == ~0ull || prev == key) return s;
+    }
+    s = (s + 1) & (cap - 1);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void accumulate(uint64_t* __restrict__ base, int64_t idx, int kind, int64_t ikey,
+                                           double dval) {
+  unsigned long long* u = reinterpret_cast<unsigned long long*>(base + idx);
+  long long* s = reinterpret_cast<long long*>(base + idx);
+  switch (kind) {
+    case SLOT_COUNT: atomicAdd(u, 1ull); break;
+    case SLOT_SUM_I64: atomicAdd(u, (unsigned long long)ikey); break;
+    case SLOT_SUM_F64: atomicAdd(reinterpret_cast<double*>(base + idx), dval); break;
+    case SLOT_MIN_KEY: atomicMin(s, (long long)ikey); break;
+    default: atomicMax(s, (long long)ikey); break;
+  }
+}
+
+// Aggregates NB docs of one segment per lane with their gathers interleaved: every dependent level (forward-index
+// words -> dictId -> LUT / dictionary value) is issued for all NB docs before any is consumed, so a batch pays
+// each memory round trip once.  Docs with ok[b] == false read doc 0 (always in bounds) and add nothing.
+template <int MODE, int NB>
+__device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView& S, const int64_t (&doc)[NB],
+                                                const bool (&ok)[NB], uint64_t* __restrict__ tbl, int64_t G) {
+  int64_t key[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) key[b] = 0;
+  for (int j = 0; j < p.num_keys; ++j) {
+    const KCol& c = S.cols[p.key_col[j]];
+    const uint32_t* fwd = c.fwd;
+    const int32_t* lut = c.lut;
+    const int bits = c.bits;
+    uint32_t id[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) id[b] = gather_id(fwd, bits, ok[b] ? doc[b] : 0);
+    int32_t g[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) g[b] = lut[id[b]];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
+  }
+  int64_t idx[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    idx[b] = key[b];
+    if (MODE == MODE_HASH && ok[b]) idx[b] = hash_slot(p.hash_keys, G, (uint64_t)key[b]);
+  }
+  uint32_t id[NB];
+  int prev_col = -1;
+  for (int s = 0; s < p.num_slots; ++s) {
+    const int kind = p.slot_kind[s];
+    int64_t ikey[NB];
+    double dval[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) { ikey[b] = 0; dval[b] = 0.0; }
+    if (kind != SLOT_COUNT) {
+      const int col = p.slot_col[s];
+      const KCol& c = S.cols[col];
+      if (col != prev_col) {  // SUM/MIN/MAX of one column share the dictId gather
+#pragma unroll
+        for (int b = 0; b < NB; ++b) id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
+        prev_col = col;
+      }
+      if (kind == SLOT_SUM_F64) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) dval[b] = c.dval[id[b]];
+      } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) ikey[b] = c.dkey[id[b]];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (ok[b]) accumulate<MODE>(tbl, (int64_t)s * G + idx[b], kind, ikey[b], dval[b]);
+  }
+}
+
+// Drains a wave's queue of matched docs (all of segment S): 2 docs per lane per batch.
+template <int MODE>
+__device__ __forceinline__ void flush_wave_queue(const KParams& p, const SegView& S, const uint32_t* q, uint32_t qn,
+                                                 int lane, uint64_t* __restrict__ tbl, int64_t G) {
+  for (uint32_t base = 0; base < qn; base += 128) {
+    const uint32_t i0 = base + lane, i1 = base + 64 + lane;
+    int64_t doc[2];
+    bool ok[2];
+    ok[0] = i0 < qn;
+    ok[1] = i1 < qn;
+    doc[0] = ok[0] ? q[i0] : 0;
+    doc[1] = ok[1] ? q[i1] : 0;
+    aggregate_batch<MODE, 2>(p, S, doc, ok, tbl, G);
+  }
+}
+
+}  // namespace pgpu

@@ -28,6 +28,8 @@ constexpr int kMaxStack = 8;                // filter evaluation stack depth
 constexpr int kFwdPadWords = 4;
 constexpr int kMaxStage = 4;                // distinct filter columns staged into LDS per tile
 constexpr int kQueueCap = 1024;             // matched-doc queue entries per workgroup (LDS)
+constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
+constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
 
 enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };

@@ -804,7 +804,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   const int nslots = (int)P->slot_kind.size();
   constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
   constexpr int64_t kLdsBudget = 48 * 1024;
-  const size_t stack_bytes = pure_and ? 0 : (size_t)std::max(max_depth, 1) * kBlock * 4;
+  // direct kernel LDS: [table (MODE_LDS)] [filter stack (general programs)] [per-wave match queues]
+  const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * kWaveQ * 4;
   for (Segment* s : P->segs) P->total_docs += s->num_docs;
   if ((int64_t)nslots * G * 8 <= kLdsBudget) {
     P->mode = MODE_LDS;
@@ -892,8 +893,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     P->leaf_stage.push_back(sidx);
   }
-  static const bool scan_off = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '0';  // A/B switch for profiling
-  if ((int)P->stage_slot.size() <= kMaxStage && !scan_off) {
+  // The LDS-DMA staged kernel is kept as an A/B alternative (PGPU_SCAN=1); the direct-load kernel measured faster
+  // on MI355X (profiles/r01_ab_scan*.log).
+  static const bool scan_on = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '1';
+  if ((int)P->stage_slot.size() <= kMaxStage && scan_on) {
     const bool pure_and = P->pure_and && P->num_leaves <= 4;  // the staged fast path holds at most 4 leaves in registers
     for (Segment* s : P->segs) {
       int64_t bits = 0;

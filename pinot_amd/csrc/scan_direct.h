@@ -1,0 +1,122 @@
+// scan_direct.h — the fused filter / group-by / aggregation scan (K1+K2+K3) with direct loads: the kernel of
+// the path.  Instantiated once per accumulator mode in k_direct.hip.
+#pragma once
+#include "device.h"
+
+namespace pgpu {
+
+// ---------------------------------------------------------------------------------------------- K3 fused
+template <int MODE>
+#ifndef PGPU_MIN_WAVES
+#define PGPU_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t G = p.num_keys_total;
+  const int64_t table_words = (MODE == MODE_LDS) ? (int64_t)p.num_slots * G : 0;
+  uint32_t* stack = reinterpret_cast<uint32_t*>(lds + table_words);
+  // per-wave queue of sparse matches (docs of the current segment), after the filter stack
+  uint32_t* wq = stack + (p.pure_and ? 0 : kMaxStack * kBlock) + wave * kWaveQ;
+  uint32_t qn = 0;  // wave-uniform fill
+
+  if (MODE == MODE_LDS) {
+    for (int64_t i = tid; i < table_words; i += kBlock) lds[i] = slot_init(p.slot_kind[i / G]);
+    __syncthreads();
+  }
+  uint64_t* tbl = (MODE == MODE_LDS) ? lds : p.table;
+
+  // Each workgroup streams a contiguous range of tiles; the segment cursor only moves forward and the leaf
+  // descriptors stay in registers until the segment changes (no per-tile dependent descriptor loads).
+  unsigned long long matched = 0;
+  const int64_t T = p.num_tiles;
+  const int64_t t0 = (int64_t)blockIdx.x * T / gridDim.x;
+  const int64_t t1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+  const bool fast = p.pure_and && p.num_leaves <= kFastLeaves;
+  if (t0 < t1) {
+    int seg = p.tile_seg[t0];
+    SegView S = seg_view(p, seg);
+    int64_t tile_base = S.hdr->tile_base, tile_end = tile_base + S.hdr->num_tiles;
+    int nd = S.hdr->num_docs;
+    // named registers, not an array: a runtime-guarded array of structs lands in scratch
+    LeafReg R0{}, R1{}, R2{}, R3{};
+    const int nl = p.num_leaves;
+#define PGPU_LOAD_LEAVES()                      \
+  do {                                          \
+    if (nl > 0) R0 = load_leaf_reg(p, S, 0);    \
+    if (nl > 1) R1 = load_leaf_reg(p, S, 1);    \
+    if (nl > 2) R2 = load_leaf_reg(p, S, 2);    \
+    if (nl > 3) R3 = load_leaf_reg(p, S, 3);    \
+  } while (0)
+    if (fast) PGPU_LOAD_LEAVES();
+    for (int64_t t = t0; t < t1; ++t) {
+      if (t >= tile_end) {
+        if (qn) { flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G); qn = 0; }
+        S = seg_view(p, ++seg);
+        tile_base = S.hdr->tile_base;
+        tile_end = tile_base + S.hdr->num_tiles;
+        nd = S.hdr->num_docs;
+        if (fast) PGPU_LOAD_LEAVES();
+      }
+      const int64_t group = (t - tile_base) * kBlock + tid;
+      const int64_t ngroups = ((int64_t)nd + 31) >> 5;
+      const int64_t doc0 = group << 5;
+      uint32_t mask = doc0 >= nd ? 0u : (nd - doc0 >= 32 ? ~0u : ((1u << (nd - doc0)) - 1u));
+      const int64_t gclamp = group < ngroups ? group : ngroups - 1;
+      if (fast) {
+        for (int l = 0; l < nl; ++l) {
+          if (!__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
+          const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
+          mask &= leaf_mask_reg(r, gclamp);
+        }
+      } else {
+        mask = eval_filter(p, S, gclamp, mask, stack);
+      }
+      const uint32_t cnt = __popc(mask);
+      matched += cnt;
+      if (__any(cnt > 2u)) {
+        // dense: the lane's own 32-doc group, 2 matched docs per batch (the lines are already cached)
+        while (__any(mask != 0u)) {
+          int64_t doc[2];
+          bool ok[2];
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            ok[b] = mask != 0u;
+            doc[b] = ok[b] ? doc0 + (__ffs(mask) - 1) : 0;
+            mask &= mask - 1u;
+          }
+          aggregate_batch<MODE, 2>(p, S, doc, ok, tbl, G);
+        }
+      } else if (__any(mask != 0u)) {
+        // sparse: append to the wave's queue (<= 2 per lane, so <= 128 per tile), aggregate in batches
+        while (__any(mask != 0u)) {
+          const bool has = mask != 0u;
+          const uint64_t bal = __ballot(has);
+          if (has) {
+            const uint32_t pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            wq[pos] = (uint32_t)(doc0 + (__ffs(mask) - 1));
+            mask &= mask - 1u;
+          }
+          qn += (uint32_t)__popcll(bal);
+        }
+        if (qn >= (uint32_t)kFlushAt) {
+          flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G);
+          qn = 0;
+        }
+      }
+    }
+    if (qn) flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G);
+  }
+  // numDocsScanned: wave reduce, one atomic per wave.
+  for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
+  if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
+
+  if (MODE == MODE_LDS) {
+    __syncthreads();
+    uint64_t* out = p.slab + (int64_t)blockIdx.x * table_words;
+    for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
+  }
+}
+
+}  // namespace pgpu

@@ -1,0 +1,138 @@
+"""world_size-2 CPU test (gloo) of the multi-GPU combine: the code bench.py runs between ranks
+(pinot_amd/combine.py) merges per-rank dense group tables into the result of GroupByCombineOperator over the union
+of the ranks' segments (core/operator/combine/GroupByCombineOperator.java:113-160).
+
+Each rank owns a disjoint set of segments (weak scaling: segments shard).  The per-rank table is
+the plan layout the GPU writes ([slot][key] int64 words: COUNT, integer SUM, float64 SUM bits, MIN/MAX keys) in the
+table-global key space that union_dictionaries establishes; here it is filled from the oracle's per-rank result.
+The merged table must equal the oracle run over all segments: bit-exact for integer slots, 1e-9 relative for the
+float64 sum.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pinot_amd import _lib as L
+from pinot_amd.combine import allreduce_group_table, union_dictionaries
+from pinot_amd.query import parse_query
+
+SCHEMA = [("d", "INT"), ("f", "INT"), ("mi", "INT"), ("md", "DOUBLE")]
+SQL = "SELECT COUNT(*), SUM(mi), MIN(mi), MAX(mi), SUM(md) FROM t WHERE f < 40 GROUP BY d"
+KINDS = [L.SLOT_COUNT, L.SLOT_SUM_I64, L.SLOT_MIN_KEY, L.SLOT_MAX_KEY, L.SLOT_SUM_F64]
+WORLD = 2
+SEGS_PER_RANK = 2
+DOCS = 3000
+
+
+class _DictTable:
+    """The two GpuTable methods union_dictionaries uses, over a host dictionary (no device needed)."""
+
+    def __init__(self, dicts):
+        self.dicts = {k: sorted(set(v)) for k, v in dicts.items()}
+
+    def dictionary(self, column):
+        return list(self.dicts[column])
+
+    def add_dictionary_values(self, column, values):
+        self.dicts[column] = sorted(set(self.dicts[column]) | set(values))
+
+
+def _segment_columns(seg_index):
+    rng = np.random.default_rng(1000 + seg_index)
+    # every rank sees a different subset of group values, so the union of dictionaries matters
+    d = rng.integers(0, 12, DOCS) + 3 * (seg_index % 3)
+    return {"d": d.astype(np.int64), "f": rng.integers(0, 100, DOCS).astype(np.int64),
+            "mi": rng.integers(-5000, 70000, DOCS).astype(np.int64),
+            "md": rng.uniform(-1e6, 1e6, DOCS)}
+
+
+def _dense_table(groups, gdict):
+    """Oracle groups {(d,): [count, sum_mi, min_mi, max_mi, sum_md]} -> [5][G] int64 table in the global key space."""
+    G = len(gdict)
+    t = np.zeros((len(KINDS), G), dtype=np.int64)
+    t[2, :] = np.iinfo(np.int64).max
+    t[3, :] = np.iinfo(np.int64).min
+    f64 = t[4].view(np.float64)
+    f64[:] = 0.0
+    pos = {v: i for i, v in enumerate(gdict)}
+    for (d,), vals in groups.items():
+        k = pos[d]
+        t[0, k] = vals[0]
+        t[1, k] = int(vals[1])
+        t[2, k] = int(vals[2])
+        t[3, k] = int(vals[3])
+        f64[k] = vals[4]
+    return torch.from_numpy(t)
+
+
+def _worker(rank, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import _oracle
+        q = parse_query(SQL)
+        mine = [rank * SEGS_PER_RANK + i for i in range(SEGS_PER_RANK)]
+        cols = [_segment_columns(s) for s in mine]
+        segs = [_oracle.make_segment(SCHEMA, c) for c in cols]
+        local = _oracle.run_groupby(SCHEMA, segs, q, nthreads=2)
+        # global key space: union of the ranks' group-by dictionaries
+        table = _DictTable({"d": np.concatenate([c["d"] for c in cols]).tolist()})
+        union_dictionaries(table, ["d"])
+        gdict = table.dictionary("d")
+        dense = _dense_table(local.groups, gdict)
+        allreduce_group_table(dense, KINDS)
+        np.save(os.path.join(out_dir, "merged_%d.npy" % rank), dense.numpy())
+        np.save(os.path.join(out_dir, "dict_%d.npy" % rank), np.array(gdict, dtype=np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_combine_matches_oracle(oracle, tmp_path):
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    m0, m1 = np.load(tmp_path / "merged_0.npy"), np.load(tmp_path / "merged_1.npy")
+    d0, d1 = np.load(tmp_path / "dict_0.npy"), np.load(tmp_path / "dict_1.npy")
+    assert np.array_equal(d0, d1), "ranks disagree on the global key space"
+    assert np.array_equal(m0, m1), "all-reduce left ranks with different tables"
+    # oracle over the union of all segments (GroupByCombineOperator semantics)
+    q = parse_query(SQL)
+    segs = [oracle.make_segment(SCHEMA, _segment_columns(s)) for s in range(WORLD * SEGS_PER_RANK)]
+    exp = oracle.run_groupby(SCHEMA, segs, q, nthreads=2)
+    got = {}
+    f64 = m0[4].view(np.float64)
+    for k, d in enumerate(d0):
+        if m0[0, k] == 0:
+            continue
+        got[(int(d),)] = (int(m0[0, k]), int(m0[1, k]), int(m0[2, k]), int(m0[3, k]), float(f64[k]))
+    assert set(got) == set(exp.groups)
+    for key, vals in exp.groups.items():
+        c, s, mn, mx, sd = got[key]
+        assert c == vals[0] and s == int(vals[1]) and mn == int(vals[2]) and mx == int(vals[3]), key
+        assert sd == pytest.approx(vals[4], rel=1e-9, abs=1e-6), key
+
+
+def test_union_dictionaries_single_process_group(tmp_path):
+    """union_dictionaries is a no-op on values already shared (world_size 1, gloo)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        t = _DictTable({"d": [5, 1, 3]})
+        union_dictionaries(t, ["d"])
+        assert t.dictionary("d") == [1, 3, 5]
+    finally:
+        dist.destroy_process_group()

@@ -29,6 +29,7 @@ def parse_args():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="adanalytics")
+    p.add_argument("--sql", default=None, help="override the workload's query (same table)")
     p.add_argument("--segments-per-gpu", type=int, default=1000)
     p.add_argument("--docs-per-segment", type=int, default=1_000_000)
     p.add_argument("--cpu-sample-segments", type=int, default=64)
@@ -37,6 +38,7 @@ def parse_args():
     p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
     p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
     p.add_argument("--host-profile", action="store_true", help="report host time per phase of a step")
+    p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE passes (roofline.traffic)")
     return p.parse_args()
 
 
@@ -57,7 +59,11 @@ def compulsory_bytes(table, handles, query, docs_per_segment):
         width[n] = 4 if table.types[i] in (0, 2) else 8
     total = 0
     matched_total = 0
-    for h in handles:
+    with table.plan(handles, query) as plan:
+        scanned = plan.scanned_segments()
+    for h, sc in zip(handles, scanned):
+        if not sc:  # filter folded to always-false: the segment is not read (EmptyFilterOperator)
+            continue
         bm = table.filter_bitmap(h, query, docs_per_segment)
         bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:docs_per_segment]
         docs = np.nonzero(bits)[0].astype(np.int64)
@@ -89,6 +95,62 @@ def _col_info(table, h, c):
     L.check(table.lib.pgpu_segment_column_info(table.handle, h, table.index[c], ctypes.byref(card),
                                                ctypes.byref(bits), ctypes.byref(dl), ctypes.byref(fl)))
     return card.value, bits.value, dl.value, fl.value
+
+
+# Calibration query per workload: every segment is scanned, no document matches, and the only bytes read are the
+# full forward index of one column (two contradicting EQ leaves on it), so its bytes_alg is exact.
+CALIB_SQL = {
+    "adanalytics": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 17532 AND daysSinceEpoch = 17533 GROUP BY daysSinceEpoch",
+    "c1": "SELECT COUNT(*) FROM t WHERE filt = 1 AND filt = 2 GROUP BY dim",
+    "c2": "SELECT COUNT(*) FROM t WHERE f = 1 AND f = 2 GROUP BY d",
+    "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
+}
+SCAN_KERNELS = ("filter_groupby_kernel", "scan_kernel")
+
+
+def _fetch_per_launch(csv_path):
+    import csv
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(csv_path))
+            if r["Counter_Name"] == "FETCH_SIZE" and any(k in r["Kernel_Name"] for k in SCAN_KERNELS)]
+    return sum(vals) / len(vals) * 1024.0 if vals else None
+
+
+def pmc_traffic(args):
+    """roofline.traffic: HBM bytes per launch of the scan kernel from rocprofv3 FETCH_SIZE (KB units), measured in
+    two child runs of this script started before this process touches the GPU: the bench query, and a calibration
+    query of known bytes (CALIB_SQL) in the same access pattern.  FETCH_SIZE under-counts wide streaming reads on
+    gfx950 (MI355X_MICROARCH.md, HBM section); traffic = FETCH(main) x bytes_alg(calib) / FETCH(calib)."""
+    import shutil
+    import subprocess
+    import tempfile
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rocprof) or args.workload not in CALIB_SQL:
+        return None
+    base = [sys.executable, "-u", os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+            "--no-pmc", "--workload", args.workload, "--segments-per-gpu", str(args.segments_per_gpu),
+            "--docs-per-segment", str(args.docs_per_segment)]
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        for name, sql in (("main", args.sql), ("calib", CALIB_SQL[args.workload])):
+            cmd = [rocprof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", d, "-o", name, "--"] + base + \
+                (["--sql", sql] if sql else [])
+            try:
+                p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+            except subprocess.TimeoutExpired:
+                print("pmc pass %s timed out" % name, file=sys.stderr)
+                return None
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            csvs = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f == name + "_counter_collection.csv"]
+            if p.returncode != 0 or not line or not csvs:
+                print("pmc pass %s failed (rc %d): %s" % (name, p.returncode, p.stdout[-2000:]), file=sys.stderr)
+                return None
+            res[name] = (json.loads(line[-1]), _fetch_per_launch(csvs[0]))
+    (jm, fm), (jc, fc) = res["main"], res["calib"]
+    if not fm or not fc:
+        return None
+    factor = jc["roofline"]["bytes_alg_per_launch"] / fc
+    return {"traffic": fm * factor, "fetch_size_bytes": fm, "calib_factor": round(factor, 4),
+            "calib_bytes_alg": jc["roofline"]["bytes_alg_per_launch"], "calib_fetch_size_bytes": fc}
 
 
 def cpu_baseline(table, handles, query, workload, docs, args):
@@ -131,6 +193,12 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc = None
+    if world == 1 and not args.no_pmc and not args.no_bytes:
+        # before this process initialises the GPU: the profiled runs are children, not exec'd
+        from pinot_amd.build import build as _build
+        _build()
+        pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -154,6 +222,8 @@ def main():
         dist.barrier()
     L.load()
     w = WORKLOADS[args.workload]()
+    if args.sql:
+        w.sql = args.sql
     q = parse_query(w.sql)
     docs = args.docs_per_segment
     nseg = args.segments_per_gpu
@@ -230,6 +300,9 @@ def main():
                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                     "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
                     "matched_docs_per_gpu": int(matched)}
+        if pmc:
+            roofline["traffic"] = round(pmc["traffic"], 0)
+            roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(table, handles, q, w, docs, args)

@@ -158,8 +158,12 @@ typedef struct {
   const int32_t* group_by;    /* table column indices */
   const pgpu_agg* aggs;
   int32_t num_groups_limit;   /* InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000 (:70); <= 0 = unlimited */
-  int32_t reserved;
+  int32_t options;            /* PGPU_OPT_* bits */
 } pgpu_query;
+
+/* Query options: debug option useStarTree=false (StarTreeUtils.isStarTreeDisabled, core/startree/StarTreeUtils.java:
+ * 51-59) keeps the scan path on segments that carry a star-tree. */
+#define PGPU_OPT_NO_STAR_TREE 1
 
 /* A query compiled against a list of pinned segments (InstancePlanMakerImplV2.makeInstancePlan +
  * per-segment AggregationGroupByPlanNode: predicate evaluators per segment, group-key layout, accumulators). */
@@ -198,6 +202,10 @@ int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32
  * [0] whole execute, [1] the fused scan kernel, [2] number of fused-kernel launches. */
 int pgpu_plan_timing(pgpu_plan plan, double* out3);
 
+/* Per plan segment (plan order): 1 if the segment is scanned, 0 if its filter folds to always-false against the
+ * segment's dictionaries (EmptyFilterOperator, core/plan/FilterPlanNode.java:146-176).  out holds num_segments. */
+int pgpu_plan_scanned_segments(pgpu_plan plan, uint8_t* out);
+
 /* ---- results: AggregationGroupByResult (core/query/aggregation/groupby/AggregationGroupByResult.java:31-81) */
 int pgpu_result_num_groups(pgpu_result r, int64_t* n);
 /* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */
@@ -217,6 +225,56 @@ int pgpu_result_destroy(pgpu_result r);
 /* Docid match bitmap of one segment's filter (the FilterOperator's doc set, K2): bit d of 64-bit word d/64.
  * out_words must hold ceil(num_docs / 64) words. */
 int pgpu_filter_bitmap(pgpu_table table, int64_t segment_handle, const pgpu_query* q, uint64_t* out_words);
+
+/* ============================================================================ star-tree index */
+
+/* A star-tree of one segment (StarTreeV2: seglocal/startree/OffHeapStarTree.java:38-80 + the star-tree's own
+ * documents).  Dimension / metric columns are indexes into the segment's (= the table's) columns.
+ *   nodes      : num_nodes records of 7 little-endian int32 {dimensionId, dimensionValue, startDocId, endDocId,
+ *                aggregatedDocId, firstChildId, lastChildId} in BFS order (OffHeapStarTreeNode.java:28-64; the
+ *                node array of the star-tree file, after its header);
+ *   dim_fwd[d] : the star-tree documents' dictIds of dimension d, BIG_ENDIAN fixed-bit with the segment column's
+ *                bitsPerElement (StarTreeLoaderUtils.java:73-92); STAR = dictId 0 (StarTreeV2Constants.java:38);
+ *   metrics    : the function-column pairs (AggregationFunctionColumnPair, segspi/index/startree/
+ *                AggregationFunctionColumnPair.java:25-50); COUNT's column is -1;
+ *   metric_f64 : per pair, the pre-aggregated double per star-tree document (SUM / MIN / MAX, AVG's sum), NULL for
+ *                COUNT — the values of the PASS_THROUGH raw chunk column "fn__col" (BaseSingleTreeBuilder.java:
+ *                471-475), decoded by the caller;
+ *   metric_i64 : per pair, COUNT's long (and AVG's count) per star-tree document, NULL otherwise. */
+typedef struct {
+  int32_t num_dims;
+  int32_t num_metrics;
+  int32_t num_nodes;
+  int32_t num_docs;
+  const int32_t* dim_columns;
+  const uint8_t* nodes;
+  const uint8_t* const* dim_fwd;
+  const int64_t* dim_fwd_len;
+  const pgpu_agg* metrics;
+  const double* const* metric_f64;
+  const int64_t* const* metric_i64;
+} pgpu_startree_desc;
+
+/* Pins a star-tree for a pinned segment (StarTreeIndexContainer at ImmutableSegmentLoader.java:198-201).  Queries
+ * that fit it (StarTreeUtils.isFitForStarTree, core/startree/StarTreeUtils.java:151-176) then traverse it on the
+ * GPU (StarTreeFilterOperator, core/startree/operator/StarTreeFilterOperator.java:234-338) and aggregate the
+ * pre-aggregated documents (StarTreeGroupByExecutor, core/startree/executor/StarTreeGroupByExecutor.java:60-71). */
+int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_startree_desc* desc);
+
+/* Host-side star-tree builder (BaseSingleTreeBuilder + OnHeapSingleTreeBuilder, seglocal/startree/v2/builder/):
+ * builds the star-tree of a segment given in Pinot's byte format (the pgpu_segment_desc of pgpu_pin_segment;
+ * column_types per column), split order (column indexes), dimensions without star nodes (indexes into the split
+ * order), function-column pairs and maxLeafRecords (<= 0: StarTreeV2BuilderConfig default 10000).  Pure host code:
+ * no device is needed.  The result is read with pgpu_startree_get_desc and released with pgpu_startree_destroy. */
+typedef struct pgpu_startree_s* pgpu_startree;
+int pgpu_startree_build(const pgpu_segment_desc* segment, const int32_t* column_types, const int32_t* split_order,
+                        int32_t num_dims, const int32_t* skip_star_dims, int32_t num_skip, const pgpu_agg* pairs,
+                        int32_t num_pairs, int32_t max_leaf_records, pgpu_startree* out);
+int pgpu_startree_get_desc(pgpu_startree st, pgpu_startree_desc* out);
+/* Number of star-tree records that come straight from the segment (sorted + aggregated rows), before the star-node
+ * and aggregated documents. */
+int pgpu_startree_num_raw_records(pgpu_startree st, int32_t* n);
+int pgpu_startree_destroy(pgpu_startree st);
 
 /* ============================================================================ synthetic segments (bench) */
 

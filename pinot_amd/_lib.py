@@ -65,12 +65,19 @@ class QueryC(ctypes.Structure):
     _fields_ = [("num_predicates", c_i32), ("num_filter_ops", c_i32), ("predicates", ctypes.POINTER(PredicateC)),
                 ("filter", ctypes.POINTER(FilterOpC)), ("num_group_by", c_i32), ("num_aggs", c_i32),
                 ("group_by", c_i32p), ("aggs", ctypes.POINTER(AggC)), ("num_groups_limit", c_i32),
-                ("reserved", c_i32)]
+                ("options", c_i32)]
 
 
 class GenColumnC(ctypes.Structure):
     _fields_ = [("kind", c_i32), ("column_index", c_i32), ("lo", c_i64), ("hi", c_i64), ("n", c_i32),
                 ("reserved", c_i32), ("cdf", c_f64p), ("ids", c_i64p), ("table", c_f64p)]
+
+
+class StarTreeDescC(ctypes.Structure):
+    _fields_ = [("num_dims", c_i32), ("num_metrics", c_i32), ("num_nodes", c_i32), ("num_docs", c_i32),
+                ("dim_columns", c_i32p), ("nodes", c_u8p), ("dim_fwd", ctypes.POINTER(c_u8p)),
+                ("dim_fwd_len", c_i64p), ("metrics", ctypes.POINTER(AggC)),
+                ("metric_f64", ctypes.POINTER(c_f64p)), ("metric_i64", ctypes.POINTER(c_i64p))]
 
 
 class PinotGpuError(RuntimeError):
@@ -113,6 +120,13 @@ _PROTOS = {
     "pgpu_execute_groupby": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp,
                                      ctypes.POINTER(c_voidp)]),
     "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),
+    "pgpu_plan_scanned_segments": (c_int, [c_voidp, c_u8p]),
+    "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
+    "pgpu_startree_build": (c_int, [ctypes.POINTER(SegmentDesc), c_i32p, c_i32p, c_i32, c_i32p, c_i32,
+                                    ctypes.POINTER(AggC), c_i32, c_i32, ctypes.POINTER(c_voidp)]),
+    "pgpu_startree_get_desc": (c_int, [c_voidp, ctypes.POINTER(StarTreeDescC)]),
+    "pgpu_startree_num_raw_records": (c_int, [c_voidp, c_i32p]),
+    "pgpu_startree_destroy": (c_int, [c_voidp]),
     "pgpu_result_num_groups": (c_int, [c_voidp, c_i64p]),
     "pgpu_result_group_ids": (c_int, [c_voidp, c_i32p]),
     "pgpu_result_values": (c_int, [c_voidp, c_int, c_f64p]),

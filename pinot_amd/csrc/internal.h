@@ -95,6 +95,49 @@ struct KParams {
   unsigned long long* stats;      // [0] docs matched
 };
 
+// ---------------------------------------------------------------------------------------------- star-tree
+constexpr int kMaxStarDims = 16;
+
+// One star-tree segment of a plan (uploaded per query).  Dimension indexes are split-order positions.
+struct KStarSeg {
+  const int32_t* nodes;                   // num_nodes x 7 int32 (OffHeapStarTreeNode layout)
+  int32_t num_nodes;
+  int32_t num_docs;                       // star-tree documents
+  int32_t pred_mask;                      // dims with predicates (traversal's remaining predicate columns)
+  int32_t group_mask;                     // group-by dims without predicates
+  int32_t num_dims;
+  int32_t pad;
+  const uint32_t* dim_fwd[kMaxStarDims];  // star-tree documents' dictIds (MSB-first, padded)
+  int32_t dim_bits[kMaxStarDims];
+  const uint32_t* match[kMaxStarDims];    // matching-dictId bitset of each predicate dim
+  const int32_t* key_lut[kMaxKeys];       // local -> global dictId of each group-by key
+  int32_t key_dim[kMaxKeys];              // dim of each group-by key
+  const double* src_f[kMaxSlots];         // per slot: pre-aggregated double per document
+  const int64_t* src_c[kMaxSlots];        // per slot: pre-aggregated count per document (slot 0; null = 1)
+  int32_t* ranges;                        // scratch: 2 x num_nodes (startDocId, endDocId)
+  int64_t* prefix;                        // scratch: num_nodes + 1 prefix sums of range lengths
+  int32_t* frontier;                      // scratch: 2 x 3 x num_nodes
+  int32_t* out;                           // [0] ranges emitted, [1] remaining predicate dims (residual filter)
+};
+
+struct KStarParams {
+  const KStarSeg* segs;
+  int32_t num_segs;
+  int32_t chunks_per_seg;
+  int32_t num_keys;
+  int32_t num_slots;
+  int64_t key_stride[kMaxKeys];
+  int64_t num_keys_total;
+  int32_t slot_kind[kMaxSlots];
+  int32_t slot_int[kMaxSlots];            // 1: the slot's column is INT/LONG (MIN/MAX keys are the value)
+  int32_t lds_table_words;
+  int32_t pad;
+  uint64_t* table;                        // MODE_GLOBAL / MODE_HASH
+  uint64_t* slab;                         // MODE_LDS: this kernel's first slab
+  unsigned long long* hash_keys;
+  unsigned long long* stats;              // [0] docs matched, [1] entries scanned in filter
+};
+
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
@@ -108,6 +151,8 @@ int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int3
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
                    unsigned long long* counter, uint64_t* out, int64_t out_cap, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
+int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
+int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.
 int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,
                          const int32_t* code_to_pos, int32_t n_codes, int64_t row0, int32_t num_docs,

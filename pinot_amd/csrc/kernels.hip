@@ -229,6 +229,18 @@ int launch_staged_mode0(const KParams& p, int grid, size_t lds_bytes, void* stre
 int launch_staged_mode1(const KParams& p, int grid, size_t lds_bytes, void* stream);
 int launch_staged_mode2(const KParams& p, int grid, size_t lds_bytes, void* stream);
 
+int launch_startree_scan_mode0(const KStarParams& p, size_t lds_bytes, void* stream);
+int launch_startree_scan_mode1(const KStarParams& p, size_t lds_bytes, void* stream);
+int launch_startree_scan_mode2(const KStarParams& p, size_t lds_bytes, void* stream);
+
+int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream) {
+  switch (mode) {
+    case MODE_LDS: return launch_startree_scan_mode0(p, lds_bytes, stream);
+    case MODE_GLOBAL: return launch_startree_scan_mode1(p, lds_bytes, stream);
+    default: return launch_startree_scan_mode2(p, lds_bytes, stream);
+  }
+}
+
 int launch_filter_groupby(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream) {
   switch (mode) {
     case MODE_LDS: return launch_direct_mode0(p, grid, lds_bytes, stream);

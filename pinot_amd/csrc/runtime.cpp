@@ -22,9 +22,11 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/pinotgpu.h"
+#include "host_common.h"
 #include "internal.h"
 
 using namespace pgpu;
@@ -52,6 +54,20 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
+
+}  // namespace
+
+int pgpu::host_fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+namespace {
 
 #define HIP_TRY(expr)                                                                               \
   do {                                                                                              \
@@ -218,20 +234,46 @@ struct Column {
   double* d_val = nullptr;
 };
 
+// A pinned star-tree (pgpu_attach_startree): one device block holding the nodes, the star-tree documents'
+// dimension forward indexes and the pre-aggregated metric arrays.
+struct StarTreeDev {
+  int32_t num_dims = 0, num_nodes = 0, num_docs = 0;
+  std::vector<int32_t> dim_cols, dim_bits;
+  std::vector<pgpu_agg> metrics;
+  void* d_block = nullptr;
+  int64_t bytes = 0;
+  const int32_t* d_nodes = nullptr;
+  std::vector<const uint32_t*> d_dim_fwd;
+  std::vector<const double*> d_mf;
+  std::vector<const int64_t*> d_mc;
+  int dim_of(int col) const {
+    for (int d = 0; d < num_dims; ++d) if (dim_cols[d] == col) return d;
+    return -1;
+  }
+  int pair(int fn, int col) const {  // AggregationFunctionColumnPair lookup (COUNT: column ignored)
+    for (size_t m = 0; m < metrics.size(); ++m)
+      if (metrics[m].fn == fn && (fn == PGPU_AGG_COUNT || metrics[m].column == col)) return (int)m;
+    return -1;
+  }
+};
+
 struct Segment {
   int64_t handle = 0;
   int32_t num_docs = 0;
   void* d_block = nullptr;
   std::vector<Column> cols;
+  std::unique_ptr<StarTreeDev> star;
 };
 
 struct Scratch {
-  DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg;
-  HostPinned stage;
+  DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
+  HostPinned stage, starstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   void release() {
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
-    ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release();
+    ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
+    starstage.release();
+    starwork.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -350,66 +392,6 @@ bool merge_dict(Dict& dst, const Dict& src) {
 
 // BaseImmutableDictionary.insertionIndexOf behind PredicateUtils.getStoredValue (Dictionary.java:49-100,
 // BaseImmutableDictionary.java:97-230).  Returns false when the literal does not convert (BadQueryRequest).
-bool insertion_index_of(const Column& c, const char* lit, int* out) {
-  const Dict& d = c.dict;
-  int lo = 0, hi = (int)d.size() - 1;
-  switch (d.type) {
-    case PGPU_INT: case PGPU_LONG: {
-      int64_t v;
-      if (!parse_long(lit, d.type == PGPU_INT ? INT32_MIN : INT64_MIN, d.type == PGPU_INT ? INT32_MAX : INT64_MAX, &v))
-        return false;
-      while (lo <= hi) {
-        int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-        if (d.iv[mid] < v) lo = mid + 1;
-        else if (d.iv[mid] > v) hi = mid - 1;
-        else { *out = mid; return true; }
-      }
-      *out = -(lo + 1);
-      return true;
-    }
-    case PGPU_FLOAT: case PGPU_DOUBLE: {
-      double v;
-      if (!parse_double(lit, &v)) return false;
-      if (d.type == PGPU_FLOAT) v = (double)(float)v;
-      while (lo <= hi) {
-        int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-        if (d.dv[mid] < v) lo = mid + 1;
-        else if (d.dv[mid] > v) hi = mid - 1;
-        else { *out = mid; return true; }
-      }
-      *out = -(lo + 1);
-      return true;
-    }
-    default: {
-      const uint8_t* lv = reinterpret_cast<const uint8_t*>(lit);
-      size_t ln = strlen(lit);
-      if (c.padding == 0) {
-        while (lo <= hi) {
-          int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-          const std::string& m = d.sv[mid];
-          int r = cmp_bytes(reinterpret_cast<const uint8_t*>(m.data()), m.size(), lv, ln);
-          if (r < 0) lo = mid + 1;
-          else if (r > 0) hi = mid - 1;
-          else { *out = mid; return true; }
-        }
-      } else {  // legacy non-zero padding: padded comparison (BaseImmutableDictionary.java:215-228)
-        std::string padded(lit);
-        if ((int)padded.size() < c.entry_width) padded.append(c.entry_width - padded.size(), (char)c.padding);
-        while (lo <= hi) {
-          int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-          const uint8_t* m = c.raw_dict.data() + (int64_t)mid * c.entry_width;
-          int r = cmp_bytes(m, c.entry_width, reinterpret_cast<const uint8_t*>(padded.data()), padded.size());
-          if (r < 0) lo = mid + 1;
-          else if (r > 0) hi = mid - 1;
-          else { *out = mid; return true; }
-        }
-      }
-      *out = -(lo + 1);
-      return true;
-    }
-  }
-}
-
 int64_t global_index_of(const Dict& g, const Dict& local, size_t i) {
   if (is_int_type(g.type)) {
     auto it = std::lower_bound(g.iv.begin(), g.iv.end(), local.iv[i]);
@@ -476,6 +458,10 @@ void free_segment(pgpu_table_s* t, Segment* s) {
     t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) + (c.d_key ? 16 * std::max(c.card, 1) : 0);
   }
   if (s->d_block) hipFree(s->d_block);
+  if (s->star && s->star->d_block) {
+    hipFree(s->star->d_block);
+    t->device_bytes -= s->star->bytes;
+  }
 }
 
 int64_t padded_fwd_words(int64_t num_docs, int bits) {
@@ -529,6 +515,7 @@ struct pgpu_plan_s {
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
   int segments_matched_filter = 0;
+  std::vector<uint8_t> seg_scanned;       // per plan segment: 1 = scanned (filter not folded to empty)
   int grid = 0;
   size_t lds_bytes = 0;
   bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
@@ -541,6 +528,20 @@ struct pgpu_plan_s {
   bool executed = false;
   const void* d_table_used = nullptr;
   bool hash = false;
+  // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local
+  // cardinalities) exceeds the limit may drop groups in first-seen docId order (DictionaryBasedGroupKeyGenerator
+  // IntGroupIdMap :1101-1113).  If such a plan produces more than `limit` groups in total, Pinot's truncation could
+  // apply and the GPU result is not reported (PGPU_ERR_UNSUPPORTED: the caller runs Pinot's own operator).
+  int64_t num_groups_limit = 0;
+  bool limit_sensitive = false;
+  // star-tree segments (StarTreeFilterOperator + StarTreeGroupByExecutor instead of the scan)
+  std::vector<KStarSeg> star;                                // host images; pointers patched at execute
+  std::vector<std::tuple<int, int, int64_t>> star_match_fix; // (star seg, dim, word offset in set_words)
+  std::vector<int64_t> star_work_off;                        // per star seg: byte offset of its scratch
+  int64_t star_work_bytes = 0;
+  int star_chunks = 1;
+  size_t star_lds_bytes = 0;
+  int64_t star_segments = 0;
 };
 
 struct pgpu_result_s {
@@ -575,44 +576,121 @@ void release_scratch(pgpu_table_s* t, Scratch* s) {
   t->scratch_pool.emplace_back(s);
 }
 
+// A predicate literal converted once per query to the column's stored type (PredicateUtils.getStoredValue): the
+// per-segment translation below then only binary-searches.  `star` = RangePredicate.UNBOUNDED ("*").
+struct Literal {
+  bool star = false;
+  int64_t i = 0;
+  double d = 0.0;
+  std::string s;
+};
+struct ParsedPred {
+  std::vector<Literal> lits;
+};
+
+// Literal conversion per column type; false = BadQueryRequestException (PredicateEvaluatorProvider.java:85-88).
+bool parse_literal(int type, const char* lit, bool allow_star, Literal* out) {
+  if (allow_star && strcmp(lit, "*") == 0) { out->star = true; return true; }
+  switch (type) {
+    case PGPU_INT: return parse_long(lit, INT32_MIN, INT32_MAX, &out->i);
+    case PGPU_LONG: return parse_long(lit, INT64_MIN, INT64_MAX, &out->i);
+    case PGPU_FLOAT:
+      if (!parse_double(lit, &out->d)) return false;
+      out->d = (double)(float)out->d;
+      return true;
+    case PGPU_DOUBLE: return parse_double(lit, &out->d);
+    default: out->s = lit; return true;
+  }
+}
+
+// Dictionary.insertionIndexOf (BaseImmutableDictionary.java:86-120) of a converted literal: index if present,
+// else -(insertion point + 1).
+int insertion_index(const Column& c, const Literal& v) {
+  const Dict& d = c.dict;
+  int lo = 0, hi = (int)d.size() - 1;
+  switch (d.type) {
+    case PGPU_INT: case PGPU_LONG:
+      while (lo <= hi) {
+        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+        if (d.iv[mid] < v.i) lo = mid + 1;
+        else if (d.iv[mid] > v.i) hi = mid - 1;
+        else return mid;
+      }
+      return -(lo + 1);
+    case PGPU_FLOAT: case PGPU_DOUBLE:
+      while (lo <= hi) {
+        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+        if (d.dv[mid] < v.d) lo = mid + 1;
+        else if (d.dv[mid] > v.d) hi = mid - 1;
+        else return mid;
+      }
+      return -(lo + 1);
+    default: {
+      const uint8_t* lv = reinterpret_cast<const uint8_t*>(v.s.data());
+      const size_t ln = v.s.size();
+      if (c.padding == 0) {
+        while (lo <= hi) {
+          const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+          const std::string& m = d.sv[mid];
+          const int r = cmp_bytes(reinterpret_cast<const uint8_t*>(m.data()), m.size(), lv, ln);
+          if (r < 0) lo = mid + 1;
+          else if (r > 0) hi = mid - 1;
+          else return mid;
+        }
+      } else {  // legacy non-zero padding: padded comparison (BaseImmutableDictionary.java:215-228)
+        std::string padded(v.s);
+        if ((int)padded.size() < c.entry_width) padded.append(c.entry_width - padded.size(), (char)c.padding);
+        while (lo <= hi) {
+          const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+          const uint8_t* m = c.raw_dict.data() + (int64_t)mid * c.entry_width;
+          const int r = cmp_bytes(m, c.entry_width, reinterpret_cast<const uint8_t*>(padded.data()), padded.size());
+          if (r < 0) lo = mid + 1;
+          else if (r > 0) hi = mid - 1;
+          else return mid;
+        }
+      }
+      return -(lo + 1);
+    }
+  }
+}
+
+// Converts the literals of predicate `p` for a column of `type`.
+int parse_predicate(int type, const pgpu_predicate& p, ParsedPred* out) {
+  const int need = p.type == PGPU_PRED_RANGE ? 2 : 1;
+  if (p.num_values < need) return fail(PGPU_ERR_INVALID_ARGUMENT, "predicate on column %d needs %d value(s)", p.column, need);
+  out->lits.resize(p.num_values);
+  for (int i = 0; i < p.num_values; ++i)
+    if (!parse_literal(type, p.values[i], p.type == PGPU_PRED_RANGE, &out->lits[i]))
+      return fail(PGPU_ERR_BAD_QUERY, "BadQueryRequestException: cannot convert '%s' to the type of column %d",
+                  p.values[i], p.column);
+  return 0;
+}
+
 // Translates predicate `p` against one segment's column dictionary (dictionary-based PredicateEvaluators).
-int translate_predicate(const Column& c, const pgpu_predicate& p, LeafHost* L) {
+// `ids` is caller-owned scratch.
+int translate_predicate(const Column& c, const pgpu_predicate& p, const ParsedPred& pp, LeafHost* L,
+                        std::vector<int>& ids) {
   const int32_t card = c.card;
-  auto index_of = [&](const char* lit, int* id) -> bool {
-    int ins;
-    if (!insertion_index_of(c, lit, &ins)) return false;
-    *id = ins >= 0 ? ins : -1;  // BaseImmutableDictionary.indexOf (:81-84)
-    return true;
-  };
-  auto bad = [&](const char* lit) {
-    return fail(PGPU_ERR_BAD_QUERY, "BadQueryRequestException: cannot convert '%s' to the type of column %d", lit,
-                p.column);
-  };
   switch (p.type) {
     case PGPU_PRED_EQ: {  // EqualsPredicateEvaluatorFactory.java:86-99
-      if (p.num_values < 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "EQ needs a value");
-      int id;
-      if (!index_of(p.values[0], &id)) return bad(p.values[0]);
-      if (id < 0) L->kind = LEAF_NONE;
+      const int ins = insertion_index(c, pp.lits[0]);
+      if (ins < 0) L->kind = LEAF_NONE;
       else if (card == 1) L->kind = LEAF_ALL;
-      else { L->kind = LEAF_RANGE; L->lo = id; L->span = 1; }
+      else { L->kind = LEAF_RANGE; L->lo = ins; L->span = 1; }
       return 0;
     }
     case PGPU_PRED_NOT_EQ: {  // NotEqualsPredicateEvaluatorFactory.java:88-102
-      if (p.num_values < 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "NOT_EQ needs a value");
-      int id;
-      if (!index_of(p.values[0], &id)) return bad(p.values[0]);
-      if (id < 0) L->kind = LEAF_ALL;
+      const int ins = insertion_index(c, pp.lits[0]);
+      if (ins < 0) L->kind = LEAF_ALL;
       else if (card == 1) L->kind = LEAF_NONE;
-      else { L->kind = LEAF_RANGE; L->lo = id; L->span = 1; L->negate = 1; }
+      else { L->kind = LEAF_RANGE; L->lo = ins; L->span = 1; L->negate = 1; }
       return 0;
     }
     case PGPU_PRED_IN: case PGPU_PRED_NOT_IN: {  // InPredicateEvaluatorFactory.java:138-154, NotIn...:140-160
-      std::vector<int> ids;
-      for (int i = 0; i < p.num_values; ++i) {
-        int id;
-        if (!index_of(p.values[i], &id)) return bad(p.values[i]);
-        if (id >= 0) ids.push_back(id);
+      ids.clear();
+      for (const Literal& v : pp.lits) {
+        const int ins = insertion_index(c, v);
+        if (ins >= 0) ids.push_back(ins);
       }
       std::sort(ids.begin(), ids.end());
       ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
@@ -633,18 +711,15 @@ int translate_predicate(const Column& c, const pgpu_predicate& p, LeafHost* L) {
       return 0;
     }
     case PGPU_PRED_RANGE: {  // SortedDictionaryBasedRangePredicateEvaluator (RangePredicateEvaluatorFactory.java:115-159)
-      if (p.num_values < 2) return fail(PGPU_ERR_INVALID_ARGUMENT, "RANGE needs (lower, upper)");
       int start, end;
-      if (strcmp(p.values[0], "*") == 0) start = 0;
+      if (pp.lits[0].star) start = 0;
       else {
-        int ins;
-        if (!insertion_index_of(c, p.values[0], &ins)) return bad(p.values[0]);
+        const int ins = insertion_index(c, pp.lits[0]);
         start = ins < 0 ? -(ins + 1) : (p.lower_inclusive ? ins : ins + 1);
       }
-      if (strcmp(p.values[1], "*") == 0) end = card;
+      if (pp.lits[1].star) end = card;
       else {
-        int ins;
-        if (!insertion_index_of(c, p.values[1], &ins)) return bad(p.values[1]);
+        const int ins = insertion_index(c, pp.lits[1]);
         end = ins < 0 ? -(ins + 1) : (p.upper_inclusive ? ins + 1 : ins);
       }
       const int nm = end - start;
@@ -660,27 +735,184 @@ int translate_predicate(const Column& c, const pgpu_predicate& p, LeafHost* L) {
 
 // Constant folding of the program against the leaves' constants (FilterPlanNode.java:146-176).
 Tri fold_program(const std::vector<int32_t>& ops, const std::vector<Tri>& leaf) {
-  std::vector<Tri> st;
+  Tri st[kMaxOps];
+  int sp = 0;
   for (int32_t e : ops) {
     const int op = e >> 16, arg = e & 0xFFFF;
-    if (op == OP_LEAF) st.push_back(leaf[arg]);
+    if (op == OP_LEAF) st[sp++] = leaf[arg];
     else if (op == OP_NOT) {
-      Tri& x = st.back();
+      Tri& x = st[sp - 1];
       x = x == T_ALL ? T_NONE : x == T_NONE ? T_ALL : T_VAR;
     } else {
       bool any_none = false, any_all = false, all_all = true, all_none = true;
-      for (int j = (int)st.size() - arg; j < (int)st.size(); ++j) {
+      for (int j = sp - arg; j < sp; ++j) {
         any_none |= st[j] == T_NONE;
         any_all |= st[j] == T_ALL;
         all_all &= st[j] == T_ALL;
         all_none &= st[j] == T_NONE;
       }
-      st.resize(st.size() - arg);
-      if (op == OP_AND) st.push_back(any_none ? T_NONE : all_all ? T_ALL : T_VAR);
-      else st.push_back(any_all ? T_ALL : all_none ? T_NONE : T_VAR);
+      sp -= arg;
+      if (op == OP_AND) st[sp++] = any_none ? T_NONE : all_all ? T_ALL : T_VAR;
+      else st[sp++] = any_all ? T_ALL : all_none ? T_NONE : T_VAR;
     }
   }
-  return st.empty() ? T_ALL : st.back();
+  return sp == 0 ? T_ALL : st[sp - 1];
+}
+
+// ------------------------------------------------------------------------------------------------ star-tree plans
+// The filter as a star-tree sees it: composites (one leaf, or an OR of leaves on one column) that are ANDed
+// (StarTreeUtils.extractPredicateEvaluatorsMap / isOrClauseValidForStarTree, core/startree/StarTreeUtils.java:
+// 88-218).  False for other shapes (NOT, AND under OR, OR across columns): those segments use the scan path, which
+// returns the same result.
+bool star_composites(const std::vector<int32_t>& ops, const pgpu_query* q, std::vector<std::vector<int>>* out) {
+  struct Node {
+    int type;  // 0 leaf, 1 OR on one column, 2 AND
+    int col;
+    std::vector<int> leaves;
+    std::vector<std::vector<int>> comps;
+  };
+  std::vector<Node> st;
+  for (int32_t e : ops) {
+    const int op = e >> 16, arg = e & 0xFFFF;
+    if (op == OP_LEAF) {
+      st.push_back({0, q->predicates[arg].column, {arg}, {}});
+    } else if (op == OP_NOT) {
+      return false;
+    } else if (op == OP_OR) {
+      Node n{1, -1, {}, {}};
+      for (int j = (int)st.size() - arg; j < (int)st.size(); ++j) {
+        if (st[j].type == 2) return false;
+        if (n.col >= 0 && st[j].col != n.col) return false;
+        n.col = st[j].col;
+        n.leaves.insert(n.leaves.end(), st[j].leaves.begin(), st[j].leaves.end());
+      }
+      st.resize(st.size() - arg);
+      st.push_back(std::move(n));
+    } else {
+      Node n{2, -1, {}, {}};
+      for (int j = (int)st.size() - arg; j < (int)st.size(); ++j) {
+        if (st[j].type == 2) n.comps.insert(n.comps.end(), st[j].comps.begin(), st[j].comps.end());
+        else n.comps.push_back(st[j].leaves);
+      }
+      st.resize(st.size() - arg);
+      st.push_back(std::move(n));
+    }
+  }
+  out->clear();
+  if (st.empty()) return true;
+  if (st.back().type == 2) *out = st.back().comps;
+  else out->push_back(st.back().leaves);
+  return true;
+}
+
+// Matching dictIds of one translated leaf over [0, card) as a bitset (PredicateEvaluator.getMatchingDictIds).
+void leaf_bitset(const LeafHost& L, int32_t card, std::vector<uint32_t>& w) {
+  const size_t nw = ((size_t)card + 31) / 32;
+  w.assign(nw, 0u);
+  for (int32_t i = 0; i < card; ++i) {
+    bool m;
+    switch (L.kind) {
+      case LEAF_ALL: m = true; break;
+      case LEAF_NONE: m = false; break;
+      case LEAF_RANGE: m = (uint32_t)i >= L.lo && (uint32_t)i < L.lo + L.span; break;
+      default: m = (L.set[i >> 5] >> (i & 31)) & 1u; break;
+    }
+    if (L.kind == LEAF_RANGE || L.kind == LEAF_SET) m ^= L.negate != 0;
+    if (m) w[i >> 5] |= 1u << (i & 31);
+  }
+}
+
+// Plans segment `s` on its star-tree when the query fits it (StarTreeUtils.isFitForStarTree, :151-176, and the
+// function-column pairs of the aggregations, :67-86).  *used = false leaves the segment to the scan path.
+int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_query* q,
+                      const std::vector<std::vector<int>>& comps, const std::vector<LeafHost>& leaves,
+                      hipStream_t stream, bool* used) {
+  *used = false;
+  const StarTreeDev* st = s->star.get();
+  if (!st || st->num_dims > kMaxStarDims || st->num_nodes < 1) return 0;
+  bool has_avg = false;
+  int avg_col = -1;
+  for (int i = 0; i < q->num_aggs; ++i) {
+    if (st->pair(q->aggs[i].fn, q->aggs[i].column) < 0) return 0;
+    if (q->aggs[i].fn == PGPU_AGG_AVG) { has_avg = true; avg_col = q->aggs[i].column; }
+  }
+  for (int c : P->key_cols)
+    if (st->dim_of(c) < 0) return 0;
+  for (int l = 0; l < q->num_predicates; ++l)
+    if (st->dim_of(q->predicates[l].column) < 0) return 0;
+  KStarSeg k;
+  memset(&k, 0, sizeof k);
+  k.nodes = st->d_nodes;
+  k.num_nodes = st->num_nodes;
+  k.num_docs = st->num_docs;
+  k.num_dims = st->num_dims;
+  for (int d = 0; d < st->num_dims; ++d) {
+    k.dim_fwd[d] = st->d_dim_fwd[d];
+    k.dim_bits[d] = st->dim_bits[d];
+  }
+  // slot sources
+  const int cnt_pair = st->pair(PGPU_AGG_COUNT, -1);
+  if (cnt_pair >= 0) k.src_c[0] = st->d_mc[cnt_pair];
+  else if (has_avg) k.src_c[0] = st->d_mc[st->pair(PGPU_AGG_AVG, avg_col)];
+  for (size_t sl = 1; sl < P->slot_kind.size(); ++sl) {
+    const int col = P->slot_tcol[sl];
+    int m = -1;
+    switch (P->slot_kind[sl]) {
+      case SLOT_SUM_I64: case SLOT_SUM_F64:
+        m = st->pair(PGPU_AGG_SUM, col);
+        if (m < 0) m = st->pair(PGPU_AGG_AVG, col);
+        break;
+      case SLOT_MIN_KEY: m = st->pair(PGPU_AGG_MIN, col); break;
+      default: m = st->pair(PGPU_AGG_MAX, col); break;
+    }
+    if (m < 0 || !st->d_mf[m]) return 0;
+    k.src_f[sl] = st->d_mf[m];
+  }
+  // predicate dims: AND of the composites' matching dictIds; always-true composites are dropped
+  std::vector<std::vector<uint32_t>> match(st->num_dims);
+  std::vector<uint32_t> cw, lw;
+  for (const auto& comp : comps) {
+    const int col = q->predicates[comp[0]].column;
+    const int d = st->dim_of(col);
+    const int32_t card = s->cols[col].card;
+    const size_t nw = ((size_t)card + 31) / 32;
+    cw.assign(nw, 0u);
+    for (int l : comp) {
+      leaf_bitset(leaves[l], card, lw);
+      for (size_t i = 0; i < nw; ++i) cw[i] |= lw[i];
+    }
+    int64_t ones = 0;
+    for (uint32_t x : cw) ones += __builtin_popcount(x);
+    if (ones == card) continue;  // isAlwaysTrue: not a predicate column for the traversal
+    if (match[d].empty()) match[d].assign(nw, ~0u);
+    for (size_t i = 0; i < nw; ++i) match[d][i] &= cw[i];
+    k.pred_mask |= 1 << d;
+  }
+  *used = true;
+  for (int d = 0; d < st->num_dims; ++d) {
+    if (!(k.pred_mask & (1 << d))) continue;
+    int64_t ones = 0;
+    for (uint32_t x : match[d]) ones += __builtin_popcount(x);
+    if (ones == 0) return 0;  // no matching dictId: the traversal returns null (empty result for the segment)
+  }
+  for (size_t j = 0; j < P->key_cols.size(); ++j) {
+    const int c = P->key_cols[j];
+    TRY(ensure_lut(t, *s, c, stream));
+    k.key_lut[j] = s->cols[c].d_lut;
+    k.key_dim[j] = st->dim_of(c);
+    if (!(k.pred_mask & (1 << k.key_dim[j]))) k.group_mask |= 1 << k.key_dim[j];
+  }
+  const int idx = (int)P->star.size();
+  for (int d = 0; d < st->num_dims; ++d) {
+    if (!(k.pred_mask & (1 << d))) continue;
+    P->star_match_fix.emplace_back(idx, d, (int64_t)P->set_words.size());
+    P->set_words.insert(P->set_words.end(), match[d].begin(), match[d].end());
+  }
+  const int64_t nn = st->num_nodes;
+  P->star_work_off.push_back(P->star_work_bytes);
+  P->star_work_bytes += ((2 * nn * 4 + (nn + 1) * 8 + 6 * nn * 4 + 8) + 15) & ~int64_t(15);
+  P->star.push_back(k);
+  return 0;
 }
 
 int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P) {
@@ -790,6 +1022,17 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->num_projected = (int)(std::unique(proj.begin(), proj.end()) - proj.begin());
   }
 
+  P->num_groups_limit = q->num_groups_limit;
+  if (q->num_groups_limit > 0) {
+    for (Segment* s : P->segs) {
+      int64_t prod = 1;
+      for (int c : P->key_cols) {
+        const int64_t card = std::max<int64_t>(s->cols[c].card, 1);
+        prod = prod > INT64_MAX / card ? INT64_MAX : prod * card;
+      }
+      if (prod > q->num_groups_limit) P->limit_sensitive = true;
+    }
+  }
   // group-key layout over the table-global dictionaries (mixed radix, first column fastest: ArrayBasedHolder)
   bool overflow = false;
   int64_t G = 1;
@@ -833,17 +1076,31 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   std::vector<uint8_t> rec(P->seg_stride);
   std::vector<LeafHost> leaves(P->num_leaves);
   std::vector<Tri> tri(P->num_leaves);
+  std::vector<ParsedPred> parsed(P->num_leaves);
+  for (int l = 0; l < P->num_leaves; ++l)
+    TRY(parse_predicate(t->types[q->predicates[l].column], q->predicates[l], &parsed[l]));
+  std::vector<int> ids_scratch;
+  std::vector<std::vector<int>> star_comps;
+  const bool star_allowed = !(q->options & PGPU_OPT_NO_STAR_TREE) && star_composites(P->ops, q, &star_comps);
   int64_t tile_base = 0;
   std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
   for (Segment* s : P->segs) {
     for (int l = 0; l < P->num_leaves; ++l) {
-      leaves[l] = LeafHost();
-      TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], &leaves[l]));
+      LeafHost& lh = leaves[l];
+      lh.kind = LEAF_NONE; lh.negate = 0; lh.lo = 0; lh.span = 0;
+      TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], parsed[l], &lh, ids_scratch));
       tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
     }
     const Tri whole = P->num_leaves ? fold_program(P->ops, tri) : T_ALL;
+    P->seg_scanned.push_back(0);
     if (whole == T_NONE || s->num_docs == 0) continue;  // EmptyFilterOperator: the segment is not scanned
+    P->seg_scanned.back() = 1;
     P->segments_matched_filter++;
+    if (star_allowed && s->star) {
+      bool used = false;
+      TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
+      if (used) continue;
+    }
     for (int l = 0; l < P->num_leaves; ++l)
       if (tri[l] == T_VAR) P->scanned_entries_model += s->num_docs;
     for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
@@ -881,6 +1138,11 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   }
   P->num_tiles = tile_base;
   if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
+  P->star_segments = (int64_t)P->star.size();
+  if (!P->star.empty()) {
+    P->star_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, 1024 / (int64_t)P->star.size()));
+    P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
+  }
   P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));  // 4 workgroups per CU
   // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
   for (int l = 0; l < P->num_leaves; ++l) {
@@ -973,8 +1235,10 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   kp.num_slots = nslots;
   for (int s = 0; s < nslots; ++s) { kp.slot_kind[s] = P->slot_kind[s]; kp.slot_col[s] = P->slot_col[s]; }
   kp.stats = sc->stats.as<unsigned long long>();
+  const int scan_blocks = P->num_tiles > 0 ? P->grid : 0;
+  const int star_blocks = (int)P->star.size() * P->star_chunks;
   if (P->mode == MODE_LDS) {
-    TRY(sc->slab.ensure((size_t)P->grid * words * 8));
+    TRY(sc->slab.ensure((size_t)std::max(scan_blocks + star_blocks, 1) * words * 8));
     kp.slab = sc->slab.as<uint64_t>();
   } else {
     if (P->mode == MODE_HASH) {
@@ -1000,9 +1264,50 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
                              : launch_filter_groupby(kp, P->mode, P->grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
+  if (!P->star.empty()) {
+    // star-tree segments: K5 traversal then K6 residual scan + aggregation into the same group table
+    TRY(sc->starwork.ensure((size_t)P->star_work_bytes));
+    TRY(sc->starrec.ensure(P->star.size() * sizeof(KStarSeg)));
+    std::vector<KStarSeg> recs = P->star;
+    for (size_t i = 0; i < recs.size(); ++i) {
+      uint8_t* base = sc->starwork.as<uint8_t>() + P->star_work_off[i];
+      const int64_t nn = recs[i].num_nodes;
+      recs[i].ranges = reinterpret_cast<int32_t*>(base);
+      recs[i].prefix = reinterpret_cast<int64_t*>(base + ((2 * nn * 4 + 7) & ~int64_t(7)));
+      recs[i].frontier = reinterpret_cast<int32_t*>(base + ((2 * nn * 4 + 7) & ~int64_t(7)) + (nn + 1) * 8);
+      recs[i].out = recs[i].frontier + 6 * nn;
+    }
+    for (auto& f : P->star_match_fix)
+      recs[std::get<0>(f)].match[std::get<1>(f)] = sc->sets.as<uint32_t>() + std::get<2>(f);
+    TRY(sc->starstage.ensure(recs.size() * sizeof(KStarSeg)));
+    memcpy(sc->starstage.p, recs.data(), recs.size() * sizeof(KStarSeg));
+    HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, recs.size() * sizeof(KStarSeg), hipMemcpyHostToDevice,
+                           stream));
+    if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), stream))
+      return fail(PGPU_ERR_DEVICE, "star-tree traversal launch failed: %s", hipGetErrorString(hipGetLastError()));
+    KStarParams sp;
+    memset(&sp, 0, sizeof sp);
+    sp.segs = sc->starrec.as<KStarSeg>();
+    sp.num_segs = (int)recs.size();
+    sp.chunks_per_seg = P->star_chunks;
+    sp.num_keys = (int)P->key_cols.size();
+    for (size_t j = 0; j < P->key_cols.size(); ++j) sp.key_stride[j] = P->key_stride[j];
+    sp.num_keys_total = P->num_keys;
+    sp.num_slots = nslots;
+    for (int sl = 0; sl < nslots; ++sl) {
+      sp.slot_kind[sl] = P->slot_kind[sl];
+      sp.slot_int[sl] = sl > 0 && is_int_type(P->table->types[P->slot_tcol[sl]]) ? 1 : 0;
+    }
+    sp.table = kp.table;
+    sp.slab = P->mode == MODE_LDS ? kp.slab + (int64_t)scan_blocks * words : nullptr;
+    sp.hash_keys = kp.hash_keys;
+    sp.stats = kp.stats;
+    if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
+      return fail(PGPU_ERR_DEVICE, "star-tree scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
   if (P->mode == MODE_LDS) {
-    const int nb = P->num_tiles > 0 ? P->grid : 0;
+    const int nb = scan_blocks + star_blocks;
     if (nb == 0) {
       if (launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
@@ -1026,7 +1331,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
   std::vector<uint64_t> keys, slots;  // keys[n], slots[s * n + i]
   int64_t n = 0;
-  uint64_t matched = 0;
+  uint64_t matched = 0, star_scanned = 0;
   const int64_t words = (int64_t)nslots * P->num_keys;
   double t_sync1 = 0;
   if (!P->hash && words * 8 <= kHostCompactBytes) {
@@ -1034,10 +1339,11 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     matched = st[words];
+    star_scanned = st[words + 1];
     const int64_t G = P->num_keys;
     for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
     keys.resize(n);
@@ -1060,11 +1366,12 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
+    star_scanned = st[2];
     if (n > 0) {
       TRY(sc->stage.ensure((size_t)n * rec * 8));
       st = reinterpret_cast<uint64_t*>(sc->stage.p);
@@ -1079,6 +1386,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     }
   }
   const double t_sync2 = trace_on() ? now_us() : 0;
+  if (P->limit_sensitive && n > P->num_groups_limit)
+    return fail(PGPU_ERR_UNSUPPORTED,
+                "numGroupsLimit %lld reached (%lld groups): Pinot truncates per segment in first-seen order",
+                (long long)P->num_groups_limit, (long long)n);
   // order groups by composite key
   std::vector<int64_t> order(n);
   for (int64_t i = 0; i < n; ++i) order[i] = i;
@@ -1131,7 +1442,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
                         ((fn == PGPU_AGG_MIN || fn == PGPU_AGG_MAX) && is_int_type(P->table->types[P->agg_col[a]]));
     }
   R->stats[0] = (int64_t)matched;
-  R->stats[1] = P->scanned_entries_model;
+  R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned;
   R->stats[2] = (int64_t)matched * P->num_projected;
   R->stats[3] = P->total_docs;
   R->stats[4] = (int64_t)P->segs.size();
@@ -1291,6 +1602,87 @@ int pgpu_unpin_segment(pgpu_table t, int64_t h) {
   hipStreamSynchronize(t->stream);
   free_segment(t, it->second.get());
   t->segments.erase(it);
+  return 0;
+}
+
+int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
+  if (!t || !d) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  if (d->num_dims < 1 || d->num_dims > kMaxStarDims || d->num_nodes < 1 || d->num_docs < 0 || d->num_metrics < 1)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree shape (dims %d, nodes %d, docs %d, metrics %d)",
+                d->num_dims, d->num_nodes, d->num_docs, d->num_metrics);
+  DeviceGuard g(t->device);
+  std::lock_guard<std::mutex> lk(t->mu);
+  auto it = t->segments.find(h);
+  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+  Segment& seg = *it->second;
+  auto st = std::make_unique<StarTreeDev>();
+  st->num_dims = d->num_dims;
+  st->num_nodes = d->num_nodes;
+  st->num_docs = d->num_docs;
+  // layout: nodes | dim fwd (padded words) | metric doubles | metric counts
+  std::vector<int64_t> fwd_words(d->num_dims);
+  int64_t bytes = ((int64_t)d->num_nodes * 28 + 15) & ~int64_t(15);
+  for (int k = 0; k < d->num_dims; ++k) {
+    const int c = d->dim_columns[k];
+    if (c < 0 || c >= (int)seg.cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree dimension column");
+    const int bits = seg.cols[c].bits;
+    const int64_t need = ((int64_t)d->num_docs * bits + 7) / 8;
+    if (!d->dim_fwd[k] || d->dim_fwd_len[k] < need)
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree dimension %d forward index too short", k);
+    st->dim_cols.push_back(c);
+    st->dim_bits.push_back(bits);
+    fwd_words[k] = ((int64_t)d->num_docs * bits + 31) / 32 + kFwdPadWords;
+    bytes += ((fwd_words[k] * 4) + 15) & ~int64_t(15);
+  }
+  for (int m = 0; m < d->num_metrics; ++m) {
+    const pgpu_agg a = d->metrics[m];
+    if (a.fn < PGPU_AGG_COUNT || a.fn > PGPU_AGG_AVG) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad metric function");
+    const bool needs_f = a.fn != PGPU_AGG_COUNT, needs_c = a.fn == PGPU_AGG_COUNT || a.fn == PGPU_AGG_AVG;
+    if ((needs_f && !d->metric_f64[m]) || (needs_c && !d->metric_i64[m]))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %d values missing", m);
+    if (needs_f && (a.column < 0 || a.column >= (int)seg.cols.size()))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree metric column");
+    st->metrics.push_back(a);
+    bytes += (needs_f ? (int64_t)d->num_docs * 8 : 0) + (needs_c ? (int64_t)d->num_docs * 8 : 0) + 32;
+  }
+  HIP_TRY(hipMalloc(&st->d_block, bytes));
+  st->bytes = bytes;
+  std::vector<uint8_t> host(bytes, 0);
+  int64_t off = 0;
+  memcpy(host.data(), d->nodes, (size_t)d->num_nodes * 28);  // little-endian, as the file holds it
+  st->d_nodes = reinterpret_cast<const int32_t*>(st->d_block);
+  off = ((int64_t)d->num_nodes * 28 + 15) & ~int64_t(15);
+  for (int k = 0; k < d->num_dims; ++k) {
+    const int64_t nb = ((int64_t)d->num_docs * st->dim_bits[k] + 7) / 8;
+    memcpy(host.data() + off, d->dim_fwd[k], nb);
+    st->d_dim_fwd.push_back(reinterpret_cast<const uint32_t*>((uint8_t*)st->d_block + off));
+    off += ((fwd_words[k] * 4) + 15) & ~int64_t(15);
+  }
+  for (int m = 0; m < d->num_metrics; ++m) {
+    const pgpu_agg a = d->metrics[m];
+    const double* pf = nullptr;
+    const int64_t* pc = nullptr;
+    if (a.fn != PGPU_AGG_COUNT) {
+      memcpy(host.data() + off, d->metric_f64[m], (size_t)d->num_docs * 8);
+      pf = reinterpret_cast<const double*>((uint8_t*)st->d_block + off);
+      off += (int64_t)d->num_docs * 8 + 16;
+    }
+    if (a.fn == PGPU_AGG_COUNT || a.fn == PGPU_AGG_AVG) {
+      memcpy(host.data() + off, d->metric_i64[m], (size_t)d->num_docs * 8);
+      pc = reinterpret_cast<const int64_t*>((uint8_t*)st->d_block + off);
+      off += (int64_t)d->num_docs * 8 + 16;
+    }
+    st->d_mf.push_back(pf);
+    st->d_mc.push_back(pc);
+  }
+  HIP_TRY(hipMemcpyAsync(st->d_block, host.data(), bytes, hipMemcpyHostToDevice, t->stream));
+  HIP_TRY(hipStreamSynchronize(t->stream));
+  if (seg.star && seg.star->d_block) {
+    hipFree(seg.star->d_block);
+    t->device_bytes -= seg.star->bytes;
+  }
+  t->device_bytes += bytes;
+  seg.star = std::move(st);
   return 0;
 }
 
@@ -1461,6 +1853,12 @@ int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, co
   pgpu_plan_destroy(P);
   g_err = keep;
   return rc;
+}
+
+int pgpu_plan_scanned_segments(pgpu_plan P, uint8_t* out) {
+  if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  if (!P->seg_scanned.empty()) memcpy(out, P->seg_scanned.data(), P->seg_scanned.size());
+  return 0;
 }
 
 int pgpu_plan_timing(pgpu_plan P, double* out3) {

@@ -127,6 +127,11 @@ class GpuTable:
         self._dict_cache.clear()
         return h.value
 
+    def attach_startree(self, handle, star_tree):
+        """Pins a StarTree (pinot_amd.startree) for the pinned segment `handle`."""
+        from .startree import attach
+        attach(self, handle, star_tree)
+
     def unpin_segment(self, handle):
         L.check(self.lib.pgpu_unpin_segment(self.handle, handle))
         self._dict_cache.clear()
@@ -267,6 +272,7 @@ class Plan:
         L.check(self.lib.pgpu_plan_create(table.handle, L.ptr(hs, ctypes.c_int64), len(hs), ctypes.byref(q),
                                           ctypes.byref(h)))
         self.handle = h
+        self.num_segments = len(hs)
         del keep
 
     def close(self):
@@ -295,6 +301,12 @@ class Plan:
 
     def execute(self, stream=None, d_table=None):
         L.check(self.lib.pgpu_plan_execute(self.handle, ctypes.c_void_p(stream or 0), ctypes.c_void_p(d_table or 0)))
+
+    def scanned_segments(self):
+        """Per plan segment: True if scanned (its filter does not fold to always-false)."""
+        out = np.zeros(max(self.num_segments, 1), dtype=np.uint8)
+        L.check(self.lib.pgpu_plan_scanned_segments(self.handle, L.ptr(out, ctypes.c_uint8)))
+        return out[:self.num_segments].astype(bool)
 
     def timing_us(self):
         out = (ctypes.c_double * 3)()

@@ -93,8 +93,10 @@ class FilterContext:
 
 
 class QueryContext:
-    def __init__(self, group_by, aggregations, filter=None, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
+    def __init__(self, group_by, aggregations, filter=None, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT,
+                 use_star_tree=True):
         self.filter = filter
+        self.use_star_tree = use_star_tree  # debug option useStarTree (StarTreeUtils.java:51-59)
         self.group_by = list(group_by)
         self.aggregations = [(fn.upper(), col) for fn, col in aggregations]
         self.num_groups_limit = num_groups_limit
@@ -170,6 +172,7 @@ class QueryContext:
         q.num_aggs = len(self.aggregations)
         q.aggs = ac
         q.num_groups_limit = self.num_groups_limit
+        q.options = 0 if getattr(self, "use_star_tree", True) else 1  # PGPU_OPT_NO_STAR_TREE
         keep += [pc, oc, gb, ac]
         return q, keep
 

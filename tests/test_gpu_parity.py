@@ -315,3 +315,29 @@ def test_padding_segments_pin_and_query(gpu_lib, tmp_path):
             assert sum(v[0] for v in r2.as_dict().values()) == 2
         finally:
             t.close()
+
+
+def test_num_groups_limit_reached_declines(oracle, sv):
+    """InterSegmentAggregationSingleValueQueriesTest.java:534-545: GROUP BY column1 with numGroupsLimit 1000 makes
+    Pinot drop groups in first-seen order; the GPU path does not report a result that could differ (the caller
+    runs Pinot's operator), and the oracle confirms the limit is reached."""
+    seg, t, h = sv
+    q = QueryContext(["column1"], [("COUNT", "*")], None, num_groups_limit=1000)
+    assert oracle.run_groupby(K.SCHEMA, [seg], q, max_initial_capacity=1000).limit_reached
+    with pytest.raises(L.UnsupportedQueryError):
+        t.execute_groupby([h], q)
+
+
+def test_num_groups_limit_not_reached_is_exact(oracle, sv):
+    """A limit below the segment's key space but above the groups the filter leaves: no truncation happens in
+    Pinot, and the GPU result equals the oracle's under the same limit."""
+    seg, t, h = sv
+    flt = K.inner_query(["column9"], True).filter
+    q0 = QueryContext(["column9"], [("COUNT", "*"), ("SUM", "column1")], flt, num_groups_limit=10 ** 9)
+    ngroups = len(oracle.run_groupby(K.SCHEMA, [seg], q0).groups)
+    q = QueryContext(["column9"], [("COUNT", "*"), ("SUM", "column1")], flt, num_groups_limit=ngroups + 1)
+    assert seg.columns["column9"].cardinality > ngroups
+    o = oracle.run_groupby(K.SCHEMA, [seg], q, max_initial_capacity=min(10000, ngroups + 1))
+    assert not o.limit_reached
+    r = t.execute_groupby([h], q)
+    assert_same(r, o, q, K.SCHEMA)

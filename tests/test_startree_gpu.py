@@ -1,0 +1,92 @@
+"""GPU star-tree parity: K5 traversal + K6 pre-aggregated scan through the C ABI against the star-tree oracle
+(oracle/startree_oracle.py) and the scan oracle (BaseStarTreeV2Test's self-consistency rule,
+core-test/core/startree/v2/BaseStarTreeV2Test.java:219-295): exact for counts and integer SUM/MIN/MAX, 1e-9
+relative for double sums."""
+import numpy as np
+import pytest
+
+import startree_common as SC
+from pinot_amd.executor import GpuTable
+from pinot_amd.query import parse_query
+from pinot_amd.startree import StarTree
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(got, exp, q):
+    g = got.as_dict()
+    assert set(g) == set(exp), sorted(set(g) ^ set(exp))[:5]
+    for k, ev in exp.items():
+        for (fn, col), x, y in zip(q.aggregations, g[k], ev):
+            if fn == "AVG":
+                assert x.count == y.count and x.sum == pytest.approx(y.sum, rel=1e-12), k
+            elif col == "md":
+                assert x == pytest.approx(y, rel=1e-9, abs=1e-6), k
+            else:
+                assert x == y, (k, fn, x, y)
+
+
+@pytest.fixture(scope="module")
+def c4_gpu(oracle, gpu_lib):
+    rng = np.random.default_rng(404)
+    segs, stars = [], []
+    for i in range(3):
+        seg = oracle.make_segment(SC.C4_SCHEMA, SC.c4_columns(rng, 40000 + 7919 * i, cards=(40, 15, 8, 6)))
+        segs.append(seg)
+        stars.append(StarTree.build(SC.C4_SCHEMA, seg, SC.C4_SPLIT, SC.C4_PAIRS, max_leaf_records=300))
+    t = GpuTable(SC.C4_SCHEMA)
+    hs = [t.pin_segment(s) for s in segs]
+    for h, st in zip(hs, stars):
+        t.attach_startree(h, st)
+    yield segs, stars, t, hs
+    t.close()
+
+
+@pytest.mark.parametrize("sql", SC.C4_QUERIES)
+def test_startree_matches_oracles(oracle, c4_gpu, sql):
+    segs, stars, t, hs = c4_gpu
+    q = parse_query(sql, num_groups_limit=10 ** 9)
+    got = t.execute_groupby(hs, q)
+    # star-tree oracle, segment by segment: documents read off the star-tree
+    docs = 0
+    for seg, st in zip(segs, stars):
+        _, d, _ = SC.startree_answer(oracle, seg, SC.C4_SCHEMA, st.arrays(), q, SC.C4_SPLIT, SC.C4_PAIRS)
+        docs += d
+    assert got.stats.num_docs_scanned == docs
+    exp = oracle.run_groupby(SC.C4_SCHEMA, segs, q).groups
+    _check(got, exp, q)
+    # useStarTree=false: the scan path over the raw documents gives the same answer
+    q.use_star_tree = False
+    scan = t.execute_groupby(hs, q)
+    _check(scan, exp, q)
+    assert scan.stats.num_docs_scanned >= got.stats.num_docs_scanned
+
+
+def test_startree_mixed_with_scan_segments(oracle, c4_gpu):
+    """Segments without a star-tree run the scan path in the same plan (per-segment choice, as
+    AggregationGroupByPlanNode.run makes it, core/plan/AggregationGroupByPlanNode.java:66-67)."""
+    segs, stars, t, hs = c4_gpu
+    rng = np.random.default_rng(9)
+    plain = oracle.make_segment(SC.C4_SCHEMA, SC.c4_columns(rng, 25000, cards=(40, 15, 8, 6)))
+    h = t.pin_segment(plain)
+    try:
+        q = parse_query(SC.C4_QUERIES[0], num_groups_limit=10 ** 9)
+        got = t.execute_groupby(hs + [h], q)
+        _check(got, oracle.run_groupby(SC.C4_SCHEMA, segs + [plain], q).groups, q)
+    finally:
+        t.unpin_segment(h)
+
+
+def test_startree_large_key_space(oracle, c4_gpu):
+    """Group by every dimension: a key space past the LDS table (global table mode)."""
+    segs, stars, t, hs = c4_gpu
+    q = parse_query("SELECT SUM(m), COUNT(*) FROM t WHERE d2 < 6 GROUP BY d1, d2, d3, d4", num_groups_limit=10 ** 9)
+    got = t.execute_groupby(hs, q)
+    _check(got, oracle.run_groupby(SC.C4_SCHEMA, segs, q).groups, q)
+
+
+def test_startree_empty_match(oracle, c4_gpu):
+    segs, stars, t, hs = c4_gpu
+    q = parse_query("SELECT COUNT(*) FROM t WHERE d3 = 2 AND d3 = 3 GROUP BY d1", num_groups_limit=10 ** 9)
+    got = t.execute_groupby(hs, q)
+    assert len(got) == 0 and got.stats.num_docs_scanned == 0

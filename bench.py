@@ -224,7 +224,7 @@ def main():
     w = WORKLOADS[args.workload]()
     if args.sql:
         w.sql = args.sql
-    q = parse_query(w.sql)
+    q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
     docs = args.docs_per_segment
     nseg = args.segments_per_gpu
     table = GpuTable(w.schema, device=device)
@@ -236,6 +236,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
     if world > 1:
         union_dictionaries(table, q.group_by)
+    handles = np.array(handles, dtype=np.int64)
 
     stream = torch.cuda.current_stream().cuda_stream
     probe = table.plan(handles, q)

@@ -258,26 +258,27 @@ __device__ __forceinline__ void accumulate(uint64_t* __restrict__ base, int64_t 
   }
 }
 
-// Aggregates NB docs of one segment per lane with their gathers interleaved: every dependent level (forward-index
-// words -> dictId -> LUT / dictionary value) is issued for all NB docs before any is consumed, so a batch pays
-// each memory round trip once.  Docs with ok[b] == false read doc 0 (always in bounds) and add nothing.
+// Aggregates NB docs per lane (doc b of segment S[b]) with their gathers interleaved: every dependent level
+// (segment record -> forward-index words -> dictId -> LUT / dictionary value) is issued for all NB docs before any
+// is consumed, so a batch pays each memory round trip once.  Docs with ok[b] == false read doc 0 of their segment
+// (always in bounds) and add nothing.
 template <int MODE, int NB>
-__device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView& S, const int64_t (&doc)[NB],
+__device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView (&S)[NB], const int64_t (&doc)[NB],
                                                 const bool (&ok)[NB], uint64_t* __restrict__ tbl, int64_t G) {
   int64_t key[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) key[b] = 0;
   for (int j = 0; j < p.num_keys; ++j) {
-    const KCol& c = S.cols[p.key_col[j]];
-    const uint32_t* fwd = c.fwd;
-    const int32_t* lut = c.lut;
-    const int bits = c.bits;
+    const int kc = p.key_col[j];
     uint32_t id[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) id[b] = gather_id(fwd, bits, ok[b] ? doc[b] : 0);
+    for (int b = 0; b < NB; ++b) {
+      const KCol& c = S[b].cols[kc];
+      id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
+    }
     int32_t g[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) g[b] = lut[id[b]];
+    for (int b = 0; b < NB; ++b) g[b] = S[b].cols[kc].lut[id[b]];
 #pragma unroll
     for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
   }
@@ -297,18 +298,20 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView&
     for (int b = 0; b < NB; ++b) { ikey[b] = 0; dval[b] = 0.0; }
     if (kind != SLOT_COUNT) {
       const int col = p.slot_col[s];
-      const KCol& c = S.cols[col];
       if (col != prev_col) {  // SUM/MIN/MAX of one column share the dictId gather
 #pragma unroll
-        for (int b = 0; b < NB; ++b) id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
+        for (int b = 0; b < NB; ++b) {
+          const KCol& c = S[b].cols[col];
+          id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
+        }
         prev_col = col;
       }
       if (kind == SLOT_SUM_F64) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) dval[b] = c.dval[id[b]];
+        for (int b = 0; b < NB; ++b) dval[b] = S[b].cols[col].dval[id[b]];
       } else {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) ikey[b] = c.dkey[id[b]];
+        for (int b = 0; b < NB; ++b) ikey[b] = S[b].cols[col].dkey[id[b]];
       }
     }
 #pragma unroll
@@ -317,9 +320,9 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView&
   }
 }
 
-// Drains a wave's queue of matched docs (all of segment S): 2 docs per lane per batch.
+// Drains a wave's queue of matched (segment, doc) entries: 2 per lane per batch.
 template <int MODE>
-__device__ __forceinline__ void flush_wave_queue(const KParams& p, const SegView& S, const uint32_t* q, uint32_t qn,
+__device__ __forceinline__ void flush_wave_queue(const KParams& p, const uint32_t* qd, const uint32_t* qs, uint32_t qn,
                                                  int lane, uint64_t* __restrict__ tbl, int64_t G) {
   for (uint32_t base = 0; base < qn; base += 128) {
     const uint32_t i0 = base + lane, i1 = base + 64 + lane;
@@ -327,8 +330,9 @@ __device__ __forceinline__ void flush_wave_queue(const KParams& p, const SegView
     bool ok[2];
     ok[0] = i0 < qn;
     ok[1] = i1 < qn;
-    doc[0] = ok[0] ? q[i0] : 0;
-    doc[1] = ok[1] ? q[i1] : 0;
+    doc[0] = ok[0] ? qd[i0] : 0;
+    doc[1] = ok[1] ? qd[i1] : 0;
+    const SegView S[2] = {seg_view(p, ok[0] ? (int)qs[i0] : (int)qs[0]), seg_view(p, ok[1] ? (int)qs[i1] : (int)qs[0])};
     aggregate_batch<MODE, 2>(p, S, doc, ok, tbl, G);
   }
 }

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -289,7 +290,7 @@ struct pgpu_table_s {
   std::vector<std::string> names;
   std::vector<int32_t> types;
   std::mutex mu;
-  std::map<int64_t, std::unique_ptr<Segment>> segments;
+  std::unordered_map<int64_t, std::unique_ptr<Segment>> segments;
   int64_t next_handle = 1;
   std::vector<Dict> global;
   std::vector<uint64_t> global_version;
@@ -1048,7 +1049,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
   constexpr int64_t kLdsBudget = 48 * 1024;
   // direct kernel LDS: [table (MODE_LDS)] [filter stack (general programs)] [per-wave match queues]
-  const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * kWaveQ * 4;
+  const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * 2 * kWaveQ * 4;
   for (Segment* s : P->segs) P->total_docs += s->num_docs;
   if ((int64_t)nslots * G * 8 <= kLdsBudget) {
     P->mode = MODE_LDS;
@@ -1070,10 +1071,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
 
   // per-segment records
   const int nqc = (int)P->query_cols.size();
+  P->seg_scanned.reserve(P->segs.size());
   P->seg_stride = (int)(sizeof(KSegHdr) + sizeof(KCol) * nqc + sizeof(KLeaf) * std::max(P->num_leaves, 0));
   P->seg_stride = (P->seg_stride + 15) & ~15;
   hipStream_t stream = t->stream;
   std::vector<uint8_t> rec(P->seg_stride);
+  P->segrec.reserve(P->segs.size() * (size_t)P->seg_stride);
   std::vector<LeafHost> leaves(P->num_leaves);
   std::vector<Tri> tri(P->num_leaves);
   std::vector<ParsedPred> parsed(P->num_leaves);
@@ -1144,6 +1147,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
   }
   P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));  // 4 workgroups per CU
+  if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
   // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
   for (int l = 0; l < P->num_leaves; ++l) {
     int sidx = -1;

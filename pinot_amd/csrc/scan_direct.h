@@ -16,8 +16,9 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
   const int64_t G = p.num_keys_total;
   const int64_t table_words = (MODE == MODE_LDS) ? (int64_t)p.num_slots * G : 0;
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds + table_words);
-  // per-wave queue of sparse matches (docs of the current segment), after the filter stack
-  uint32_t* wq = stack + (p.pure_and ? 0 : kMaxStack * kBlock) + wave * kWaveQ;
+  // per-wave queue of sparse matches ((doc, segment) pairs), after the filter stack
+  uint32_t* wq = stack + (p.pure_and ? 0 : kMaxStack * kBlock) + wave * 2 * kWaveQ;
+  uint32_t* wqs = wq + kWaveQ;
   uint32_t qn = 0;  // wave-uniform fill
 
   if (MODE == MODE_LDS) {
@@ -26,18 +27,29 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
   }
   uint64_t* tbl = (MODE == MODE_LDS) ? lds : p.table;
 
-  // Each workgroup streams a contiguous range of tiles; the segment cursor only moves forward and the leaf
-  // descriptors stay in registers until the segment changes (no per-tile dependent descriptor loads).
+  // XCD-aware tile order: workgroups b and b+8 share an XCD (round-robin dispatch; speed only, never correctness),
+  // so XCD x sweeps its own contiguous eighth of the tile space with its workgroups side by side, one tile each.
+  // The tiles in flight on an XCD then come from ~one segment at a time and that segment's dictionaries / LUTs
+  // (the targets of the gathers) stay in the XCD's 4 MiB L2.
   unsigned long long matched = 0;
   const int64_t T = p.num_tiles;
-  const int64_t t0 = (int64_t)blockIdx.x * T / gridDim.x;
-  const int64_t t1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+  int64_t t_begin, t_end, t_step;
+  if (gridDim.x >= 64 && (gridDim.x & 7) == 0) {
+    const int64_t x = blockIdx.x & 7;
+    t_begin = x * T / 8 + (blockIdx.x >> 3);
+    t_end = (x + 1) * T / 8;
+    t_step = gridDim.x >> 3;
+  } else {
+    t_begin = (int64_t)blockIdx.x * T / gridDim.x;
+    t_end = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+    t_step = 1;
+  }
   const bool fast = p.pure_and && p.num_leaves <= kFastLeaves;
-  if (t0 < t1) {
-    int seg = p.tile_seg[t0];
-    SegView S = seg_view(p, seg);
-    int64_t tile_base = S.hdr->tile_base, tile_end = tile_base + S.hdr->num_tiles;
-    int nd = S.hdr->num_docs;
+  if (t_begin < t_end) {
+    int seg = -1;
+    SegView S{};
+    int64_t tile_base = 0;
+    int nd = 0;
     // named registers, not an array: a runtime-guarded array of structs lands in scratch
     LeafReg R0{}, R1{}, R2{}, R3{};
     const int nl = p.num_leaves;
@@ -48,13 +60,14 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
     if (nl > 2) R2 = load_leaf_reg(p, S, 2);    \
     if (nl > 3) R3 = load_leaf_reg(p, S, 3);    \
   } while (0)
-    if (fast) PGPU_LOAD_LEAVES();
-    for (int64_t t = t0; t < t1; ++t) {
-      if (t >= tile_end) {
-        if (qn) { flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G); qn = 0; }
-        S = seg_view(p, ++seg);
+    int next_seg = p.tile_seg[t_begin];
+    for (int64_t t = t_begin; t < t_end; t += t_step) {
+      const int cur_seg = next_seg;
+      if (t + t_step < t_end) next_seg = p.tile_seg[t + t_step];  // one tile ahead
+      if (cur_seg != seg) {
+        seg = cur_seg;
+        S = seg_view(p, seg);
         tile_base = S.hdr->tile_base;
-        tile_end = tile_base + S.hdr->num_tiles;
         nd = S.hdr->num_docs;
         if (fast) PGPU_LOAD_LEAVES();
       }
@@ -85,7 +98,8 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
             doc[b] = ok[b] ? doc0 + (__ffs(mask) - 1) : 0;
             mask &= mask - 1u;
           }
-          aggregate_batch<MODE, 2>(p, S, doc, ok, tbl, G);
+          const SegView SS[2] = {S, S};
+          aggregate_batch<MODE, 2>(p, SS, doc, ok, tbl, G);
         }
       } else if (__any(mask != 0u)) {
         // sparse: append to the wave's queue (<= 2 per lane, so <= 128 per tile), aggregate in batches
@@ -96,17 +110,18 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
             const uint32_t pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
             wq[pos] = (uint32_t)(doc0 + (__ffs(mask) - 1));
+            wqs[pos] = (uint32_t)seg;
             mask &= mask - 1u;
           }
           qn += (uint32_t)__popcll(bal);
         }
         if (qn >= (uint32_t)kFlushAt) {
-          flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G);
+          flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
           qn = 0;
         }
       }
     }
-    if (qn) flush_wave_queue<MODE>(p, S, wq, qn, lane, tbl, G);
+    if (qn) flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
   }
   // numDocsScanned: wave reduce, one atomic per wave.
   for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);

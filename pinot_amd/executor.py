@@ -266,14 +266,14 @@ class Plan:
         self.table = table
         self.query = query
         self.lib = table.lib
-        hs = np.ascontiguousarray(list(handles), dtype=np.int64)
+        hs = handles if isinstance(handles, np.ndarray) and handles.dtype == np.int64 else \
+            np.ascontiguousarray(list(handles), dtype=np.int64)
         q, keep = query.to_c(table.index)
         h = ctypes.c_void_p()
         L.check(self.lib.pgpu_plan_create(table.handle, L.ptr(hs, ctypes.c_int64), len(hs), ctypes.byref(q),
                                           ctypes.byref(h)))
         self.handle = h
         self.num_segments = len(hs)
-        del keep
 
     def close(self):
         if self.handle:

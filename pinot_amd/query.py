@@ -135,7 +135,18 @@ class QueryContext:
 
     # ---- C ABI form
     def to_c(self, column_index):
-        """Returns (QueryC, keepalive) for a table whose column name -> index map is `column_index`."""
+        """Returns (QueryC, keepalive) for a table whose column name -> index map is `column_index`.  The ctypes
+        form is built once per (query, table) and reused; options are refreshed on every call."""
+        cache = self.__dict__.get("_c_cache")
+        if cache is not None and cache[0] is column_index and cache[1] == self.num_groups_limit:
+            q, keep = cache[2], cache[3]
+            q.options = 0 if getattr(self, "use_star_tree", True) else 1
+            return q, keep
+        q, keep = self._build_c(column_index)
+        self._c_cache = (column_index, self.num_groups_limit, q, keep)
+        return q, keep
+
+    def _build_c(self, column_index):
         keep = []
         preds, ops = [], []
         if self.filter is not None:

@@ -33,12 +33,13 @@ def double_table(n, column_index, lo, hi):
 
 
 class Workload:
-    def __init__(self, name, schema, gen, sql, description):
+    def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000):
         self.name = name
         self.schema = schema          # [(column, type)]
         self.gen = gen                # generator spec per column (table column order)
         self.sql = sql
         self.description = description
+        self.num_groups_limit = num_groups_limit  # query option numGroupsLimit of the config
 
 
 def adanalytics():
@@ -88,7 +89,8 @@ def c5():
         {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 1000},
     ]
     sql = "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3"
-    return Workload("c5", schema, gen, sql, "C5 high-cardinality 3-column GROUP BY")
+    # run with num.groups.limit = 10M and server trim off
+    return Workload("c5", schema, gen, sql, "C5 high-cardinality 3-column GROUP BY", num_groups_limit=10_000_000)
 
 
 WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c5": c5}

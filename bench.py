@@ -23,6 +23,11 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
 
 
+def log(msg):
+    """Progress to stderr (long phases: segment generation, bytes_alg pass, CPU baseline)."""
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -32,7 +37,7 @@ def parse_args():
     p.add_argument("--sql", default=None, help="override the workload's query (same table)")
     p.add_argument("--segments-per-gpu", type=int, default=1000)
     p.add_argument("--docs-per-segment", type=int, default=1_000_000)
-    p.add_argument("--cpu-sample-segments", type=int, default=64)
+    p.add_argument("--cpu-sample-segments", type=int, default=None, help="default: the workload's sample size")
     p.add_argument("--cpu-target-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
@@ -160,7 +165,8 @@ def cpu_baseline(table, handles, query, workload, docs, args):
     import _oracle
     from pinot_amd.segment import ColumnData, SegmentBuffers
     types = dict(workload.schema)
-    sample = handles[:max(1, min(args.cpu_sample_segments, len(handles)))]
+    nsample = args.cpu_sample_segments or workload.cpu_sample_segments
+    sample = handles[:max(1, min(nsample, len(handles)))]
     segs = []
     from pinot_amd import _lib as L
     for h in sample:
@@ -171,11 +177,11 @@ def cpu_baseline(table, handles, query, workload, docs, args):
             cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
         segs.append(SegmentBuffers(docs, cols))
     threads = max(1, min(16, os.cpu_count() or 1))
-    _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads)  # warm-up
+    _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False)  # warm-up
     reps, elapsed = 0, 0.0
     t0 = time.perf_counter()
     while True:
-        _oracle.run_groupby(workload.schema, segs, query, nthreads=threads)
+        _oracle.run_groupby(workload.schema, segs, query, nthreads=threads, decode=False)
         reps += 1
         elapsed = time.perf_counter() - t0
         if elapsed >= args.cpu_target_seconds or reps >= 50:
@@ -234,6 +240,7 @@ def main():
         global_seg = rank * nseg + i
         handles.append(table.generate_segment(w.gen, row0=global_seg * docs, num_docs=docs))
     t_gen = time.perf_counter() - t_gen
+    log("rank %d: %d segments generated in %.1f s" % (rank, nseg, t_gen))
     if world > 1:
         union_dictionaries(table, q.group_by)
     handles = np.array(handles, dtype=np.int64)
@@ -244,7 +251,8 @@ def main():
     probe.close()
     d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
 
-    phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0}
+    phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0,
+              "decode": 0.0}
 
     def step():
         c0 = time.perf_counter()
@@ -258,9 +266,10 @@ def main():
         res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
         c4 = time.perf_counter()
         k_us = plan.timing_us()[1]
+        fc_us, dec_us = plan.finalize_us
         plan.close()
         c5 = time.perf_counter()
-        for k, v in zip(phases, (c1 - c0, c2 - c1, c3 - c2, c4 - c3, c5 - c4)):
+        for k, v in zip(phases, (c1 - c0, c2 - c1, c3 - c2, c4 - c3, c5 - c4, fc_us * 1e-6, dec_us * 1e-6)):
             phases[k] += v
         return res, k_us
 
@@ -293,6 +302,7 @@ def main():
     value = total_rows * args.steps / elapsed
     kernel_avg_us = float(np.mean(kernel_us)) if kernel_us else 0.0
 
+    log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
     if not args.no_bytes:
         bytes_alg, matched = compulsory_bytes(table, handles, q, docs)
@@ -306,6 +316,7 @@ def main():
             roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("bytes_alg pass done; CPU baseline")
         cpu = cpu_baseline(table, handles, q, w, docs, args)
 
     if rank == 0:

@@ -210,6 +210,14 @@ int pgpu_plan_scanned_segments(pgpu_plan plan, uint8_t* out);
 int pgpu_result_num_groups(pgpu_result r, int64_t* n);
 /* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */
 int pgpu_result_group_ids(pgpu_result r, int32_t* out);
+/* Column `key` of the above ([n] dictIds of group-by column `key`): a plain copy, the layout the result holds. */
+int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out);
+/* Zero-copy views valid until pgpu_result_destroy (a JNI caller wraps them in direct ByteBuffers):
+ * the [n] dictIds of group-by column `key`, and the [n] accumulator words of aggregation `agg` (agg = -1: the
+ * COUNT words, i.e. AvgPair.count) with their form: 0 = exact int64, 1 = IEEE double bits, 2 = order-preserving
+ * int64 key of a double (MIN/MAX over FLOAT/DOUBLE; pgpu_result_values converts it). */
+int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out);
+int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form);
 /* Per aggregation i (query order): value per group as Pinot's intermediate result holds it (double) — COUNT,
  * SUM, MIN, MAX, and AVG's AvgPair.sum; AVG's AvgPair.count via pgpu_result_avg_counts. */
 int pgpu_result_values(pgpu_result r, int agg, double* out);

@@ -129,6 +129,9 @@ _PROTOS = {
     "pgpu_startree_destroy": (c_int, [c_voidp]),
     "pgpu_result_num_groups": (c_int, [c_voidp, c_i64p]),
     "pgpu_result_group_ids": (c_int, [c_voidp, c_i32p]),
+    "pgpu_result_group_ids_column": (c_int, [c_voidp, c_int, c_i32p]),
+    "pgpu_result_group_ids_view": (c_int, [c_voidp, c_int, ctypes.POINTER(c_voidp)]),
+    "pgpu_result_words_view": (c_int, [c_voidp, c_int, ctypes.POINTER(c_voidp), c_i32p]),
     "pgpu_result_values": (c_int, [c_voidp, c_int, c_f64p]),
     "pgpu_result_avg_counts": (c_int, [c_voidp, c_int, c_i64p]),
     "pgpu_result_values_i64": (c_int, [c_voidp, c_int, c_i64p]),

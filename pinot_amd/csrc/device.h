@@ -320,6 +320,129 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
   }
 }
 
+// ---------------------------------------------------------------------------------------------- dense groups
+// Dense tiles: every 128-B line of the group-by / aggregated columns holds matches, so instead of per-doc gathers
+// each lane streams its whole 32-doc group of each such column (the same coalesced B-word read as a filter leaf),
+// decodes the 32 dictIds with compile-time shifts into registers, and issues the 32 dictionary / LUT lookups of a
+// column together (one memory round trip per column instead of one per doc pair).
+template <int B, int H, int... I>
+__device__ __forceinline__ void decode_half(const uint32_t (&w)[B + 1], uint32_t (&ids)[16],
+                                            std::integer_sequence<int, I...>) {
+  ((ids[I] = extract<B, H + I>(w)), ...);
+}
+
+template <int B, int H>
+__device__ __forceinline__ void decode_group_b(const uint32_t* __restrict__ words, uint32_t (&ids)[16]) {
+  uint32_t w[B + 1];
+  load_group<B>(words, w);
+  decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
+}
+
+// dictIds of docs [32*group + H, 32*group + H + 16) (PinotDataBitSet.readInt).
+template <int H>
+__device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, int bits, int64_t group,
+                                             uint32_t (&ids)[16]) {
+  const uint32_t* words = fwd + group * (int64_t)bits;
+  switch (bits) {
+#define PGPU_CASE(B) \
+  case B:            \
+    decode_group_b<B, H>(words, ids); \
+    break;
+    PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
+    PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
+    PGPU_CASE(16) PGPU_CASE(17) PGPU_CASE(18) PGPU_CASE(19) PGPU_CASE(20) PGPU_CASE(21) PGPU_CASE(22)
+    PGPU_CASE(23) PGPU_CASE(24) PGPU_CASE(25) PGPU_CASE(26) PGPU_CASE(27) PGPU_CASE(28) PGPU_CASE(29)
+    PGPU_CASE(30) PGPU_CASE(31)
+#undef PGPU_CASE
+    default:
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ids[i] = 0;
+      break;
+  }
+}
+
+// One half (docs H..H+15 of the lane's group) of aggregate_group.
+template <int MODE, int H>
+__device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
+                                               uint64_t* __restrict__ tbl, int64_t G) {
+  const uint32_t m = mask >> H;
+  uint32_t ids[16];
+  int32_t key[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) key[i] = 0;
+  for (int j = 0; j < p.num_keys; ++j) {
+    const KCol& c = S.cols[p.key_col[j]];
+    decode_group<H>(c.fwd, c.bits, group, ids);
+    const int32_t* __restrict__ lut = c.lut;
+    const int32_t stride = (int32_t)p.key_stride[j];
+    int32_t g[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
+  }
+  // Slots in runs of one column (SUM/MIN/MAX of a column share the decode and the dictionary lookups).
+  for (int s = 0; s < p.num_slots;) {
+    const int kind = p.slot_kind[s];
+    if (kind == SLOT_COUNT) {
+      uint64_t* __restrict__ row = tbl + (int64_t)s * G;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_COUNT, 0, 0.0);
+      ++s;
+      continue;
+    }
+    const int col = p.slot_col[s];
+    int e = s + 1;
+    bool need_i = kind != SLOT_SUM_F64, need_f = kind == SLOT_SUM_F64;
+    while (e < p.num_slots && p.slot_kind[e] != SLOT_COUNT && p.slot_col[e] == col) {
+      need_i |= p.slot_kind[e] != SLOT_SUM_F64;
+      need_f |= p.slot_kind[e] == SLOT_SUM_F64;
+      ++e;
+    }
+    const KCol& c = S.cols[col];
+    decode_group<H>(c.fwd, c.bits, group, ids);
+    if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
+      const int64_t* __restrict__ dk = c.dkey;
+      int64_t v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+      for (int r = s; r < e; ++r) {
+        const int kr = p.slot_kind[r];
+        if (kr == SLOT_SUM_F64) continue;
+        uint64_t* __restrict__ row = tbl + (int64_t)r * G;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], kr, v[i], 0.0);
+      }
+    }
+    if (need_f) {
+      const double* __restrict__ dv = c.dval;
+      double v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;
+      for (int r = s; r < e; ++r) {
+        if (p.slot_kind[r] != SLOT_SUM_F64) continue;
+        uint64_t* __restrict__ row = tbl + (int64_t)r * G;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_SUM_F64, 0, v[i]);
+      }
+    }
+    s = e;
+  }
+}
+
+// Aggregates the matched docs (bits of `mask`) of this lane's 32-doc group `group` of segment S, 16 docs at a
+// time.  Dense key spaces only (MODE_LDS / MODE_GLOBAL: composite keys < 2^31).  Docs beyond numDocs decode from
+// the zero padding to dictId 0 (in bounds) and are never in `mask`.
+template <int MODE>
+__device__ __forceinline__ void aggregate_group(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
+                                                uint64_t* __restrict__ tbl, int64_t G) {
+  if (mask & 0xFFFFu) aggregate_half<MODE, 0>(p, S, group, mask, tbl, G);
+  if (mask >> 16) aggregate_half<MODE, 16>(p, S, group, mask, tbl, G);
+}
+
 // Drains a wave's queue of matched (segment, doc) entries: 2 per lane per batch.
 template <int MODE>
 __device__ __forceinline__ void flush_wave_queue(const KParams& p, const uint32_t* qd, const uint32_t* qs, uint32_t qn,

@@ -30,6 +30,7 @@ constexpr int kMaxStage = 4;                // distinct filter columns staged in
 constexpr int kQueueCap = 1024;             // matched-doc queue entries per workgroup (LDS)
 constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
+constexpr int kDenseGroupMin = 256;         // matches per wave-tile (of 2048 docs) above which whole groups are decoded
 
 enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
@@ -144,12 +145,21 @@ int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, in
 int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                       unsigned long long* hash_keys, void* stream);
 int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg, void* stream);
-int launch_filter_groupby(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
+int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream);
+// Resident workgroups per CU of the direct kernel instance (< 0: query failed).
+int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes);
 int launch_scan(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
 int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int32_t num_slots, int64_t num_keys,
                         int32_t num_blocks, uint64_t* out, void* stream);
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
                    unsigned long long* counter, uint64_t* out, int64_t out_cap, void* stream);
+// Dense tables: groups with COUNT > 0 in ascending key order, columnar with row stride cap (even): int32 group-by
+// dictIds [num_key_cols][cap], then u64 slot words [num_slots][cap]; chunk_scratch holds
+// compact_ordered_chunks(num_keys) u32.
+int64_t compact_ordered_chunks(int64_t num_keys);
+int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int64_t* key_stride,
+                           const int64_t* key_card, int32_t num_key_cols, uint32_t* chunk_scratch,
+                           unsigned long long* total, void* out, int64_t cap, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);

@@ -9,10 +9,25 @@
 
 namespace pgpu {
 
-int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, int grid, size_t lds_bytes, void* stream) {
-  hipLaunchKernelGGL(filter_groupby_kernel<PGPU_MODE>, dim3(grid), dim3(kBlock), lds_bytes,
-                     reinterpret_cast<hipStream_t>(stream), p);
+int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream) {
+  if (dense)
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, true>), dim3(grid), dim3(kBlock), lds_bytes,
+                       reinterpret_cast<hipStream_t>(stream), p);
+  else
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, false>), dim3(grid), dim3(kBlock), lds_bytes,
+                       reinterpret_cast<hipStream_t>(stream), p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Resident workgroups per CU of the instance (registers and LDS): the persistent grid is sized to exactly fill
+// the chip, since its tile ranges are assigned statically.
+int PGPU_CAT(occupancy_direct_mode, PGPU_MODE)(bool dense, size_t lds_bytes) {
+  int n = 0;
+  const hipError_t e = dense ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                   &n, filter_groupby_kernel<PGPU_MODE, true>, kBlock, lds_bytes)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                   &n, filter_groupby_kernel<PGPU_MODE, false>, kBlock, lds_bytes);
+  return e == hipSuccess ? n : -1;
 }
 
 }  // namespace pgpu

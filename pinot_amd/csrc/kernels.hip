@@ -122,6 +122,94 @@ __global__ void compact_kernel(const uint64_t* __restrict__ table, const unsigne
   }
 }
 
+// Ordered compaction of a dense table (AggregationGroupByResult iteration in ascending key order, deterministic):
+// count per chunk -> one-workgroup exclusive scan -> scatter in key order.  Columnar output: keys[cap] then
+// slot s at out + (1 + s) * cap.
+constexpr int kCompactChunk = 4096;  // keys per workgroup (16 rounds of 256)
+
+__global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t* __restrict__ table, int64_t num_keys,
+                                                            uint32_t* __restrict__ chunk_cnt) {
+  __shared__ uint32_t wsum[4];
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
+  uint32_t c = 0;
+  for (int r = 0; r < kCompactChunk / 256; ++r) {
+    const int64_t k = base + r * 256 + threadIdx.x;
+    c += (k < num_keys && table[k] != 0) ? 1u : 0u;  // row 0 = COUNT
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// One workgroup: exclusive prefix of chunk_cnt (in place) and the total into *total.
+__global__ __launch_bounds__(1024) void compact_scan_kernel(uint32_t* __restrict__ chunk, int32_t n,
+                                                            unsigned long long* __restrict__ total) {
+  __shared__ uint32_t wsum[16];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + threadIdx.x;
+    const uint32_t v = i < n ? chunk[i] : 0u;
+    uint32_t x = v;  // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    const unsigned long long c = carry;
+    if (i < n) chunk[i] = (uint32_t)(c + before + x - v);
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = c + before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// Output (columnar, stride cap): group-by dictIds gid[j] = (key / stride[j]) % card[j] as int32 rows [num_keys][cap],
+// then the slot words as u64 rows [num_slots][cap] starting at byte offset num_keys * cap * 4 (8-aligned cap).
+struct KeyDecode {
+  int64_t stride[kMaxKeys];
+  int64_t card[kMaxKeys];
+  int32_t n;
+};
+__global__ __launch_bounds__(256) void compact_scatter_kernel(const uint64_t* __restrict__ table, int32_t num_slots,
+                                                              int64_t num_keys, const uint32_t* __restrict__ chunk_off,
+                                                              const KeyDecode kd, uint8_t* __restrict__ out,
+                                                              int64_t cap) {
+  __shared__ uint32_t wcnt[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
+  int32_t* gid = reinterpret_cast<int32_t*>(out);
+  uint64_t* words = reinterpret_cast<uint64_t*>(out + (int64_t)kd.n * cap * 4);
+  uint32_t pos = chunk_off[blockIdx.x];
+  for (int r = 0; r < kCompactChunk / 256; ++r) {
+    const int64_t k = base + r * 256 + threadIdx.x;
+    const bool f = k < num_keys && table[k] != 0;
+    const unsigned long long bal = __ballot(f);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (lane == 0) wcnt[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += wcnt[w];
+    const uint32_t round_total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (f) {
+      const int64_t j = (int64_t)pos + before + rank;
+      if (j < cap) {
+        for (int c = 0; c < kd.n; ++c) gid[(int64_t)c * cap + j] = (int32_t)((k / kd.stride[c]) % kd.card[c]);
+        for (int s = 0; s < num_slots; ++s) words[(int64_t)s * cap + j] = table[(int64_t)s * num_keys + k];
+      }
+    }
+    pos += round_total;
+    __syncthreads();
+  }
+}
+
 // K2 alone: the FilterOperator's docId bitmap of the plan's first segment, one 32-bit word per lane group.
 __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, uint32_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -222,9 +310,12 @@ int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slo
 }
 
 // One object per (kernel family, mode): k_direct.hip / k_staged.hip compiled with -DPGPU_MODE=0,1,2.
-int launch_direct_mode0(const KParams& p, int grid, size_t lds_bytes, void* stream);
-int launch_direct_mode1(const KParams& p, int grid, size_t lds_bytes, void* stream);
-int launch_direct_mode2(const KParams& p, int grid, size_t lds_bytes, void* stream);
+int launch_direct_mode0(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
+int launch_direct_mode1(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
+int launch_direct_mode2(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
+int occupancy_direct_mode0(bool dense, size_t lds_bytes);
+int occupancy_direct_mode1(bool dense, size_t lds_bytes);
+int occupancy_direct_mode2(bool dense, size_t lds_bytes);
 int launch_staged_mode0(const KParams& p, int grid, size_t lds_bytes, void* stream);
 int launch_staged_mode1(const KParams& p, int grid, size_t lds_bytes, void* stream);
 int launch_staged_mode2(const KParams& p, int grid, size_t lds_bytes, void* stream);
@@ -241,11 +332,19 @@ int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void*
   }
 }
 
-int launch_filter_groupby(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream) {
+int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream) {
   switch (mode) {
-    case MODE_LDS: return launch_direct_mode0(p, grid, lds_bytes, stream);
-    case MODE_GLOBAL: return launch_direct_mode1(p, grid, lds_bytes, stream);
-    default: return launch_direct_mode2(p, grid, lds_bytes, stream);
+    case MODE_LDS: return launch_direct_mode0(p, dense, grid, lds_bytes, stream);
+    case MODE_GLOBAL: return launch_direct_mode1(p, dense, grid, lds_bytes, stream);
+    default: return launch_direct_mode2(p, dense, grid, lds_bytes, stream);
+  }
+}
+
+int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes) {
+  switch (mode) {
+    case MODE_LDS: return occupancy_direct_mode0(dense, lds_bytes);
+    case MODE_GLOBAL: return occupancy_direct_mode1(dense, lds_bytes);
+    default: return occupancy_direct_mode2(dense, lds_bytes);
   }
 }
 
@@ -283,6 +382,23 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(compact_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_slots,
                      num_keys, counter, out, out_cap);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int64_t compact_ordered_chunks(int64_t num_keys) { return (num_keys + kCompactChunk - 1) / kCompactChunk; }
+
+int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int64_t* key_stride,
+                           const int64_t* key_card, int32_t num_key_cols, uint32_t* chunk_scratch,
+                           unsigned long long* total, void* out, int64_t cap, void* stream) {
+  const int64_t nch = compact_ordered_chunks(num_keys);
+  if (nch < 1 || nch > INT32_MAX || num_key_cols > kMaxKeys || (cap & 1)) return -1;
+  KeyDecode kd{};
+  kd.n = num_key_cols;
+  for (int j = 0; j < num_key_cols; ++j) { kd.stride[j] = key_stride[j]; kd.card[j] = key_card[j]; }
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);
+  hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_slots, num_keys,
+                     chunk_scratch, kd, reinterpret_cast<uint8_t*>(out), cap);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -138,6 +138,34 @@ struct HostPinned {
   }
 };
 
+// Pinned host buffers that hold finalized results, reused across queries (a result of ~10M groups is hundreds of
+// MB: pinning it per query would cost more than the scan).  Shared by a table and the results it produced, so a
+// result may outlive its table.
+struct ResultPool {
+  std::mutex mu;
+  std::vector<HostPinned> free;
+  ~ResultPool() {
+    for (auto& h : free) h.release();
+  }
+  HostPinned take() {
+    std::lock_guard<std::mutex> g(mu);
+    if (free.empty()) return HostPinned();
+    HostPinned h = free.back();
+    free.pop_back();
+    return h;
+  }
+  void give(HostPinned h) {
+    if (!h.p) return;
+    std::lock_guard<std::mutex> g(mu);
+    free.push_back(h);
+    if (free.size() > 4) {  // keep the largest few
+      auto it = std::min_element(free.begin(), free.end(), [](const HostPinned& a, const HostPinned& b) { return a.cap < b.cap; });
+      it->release();
+      free.erase(it);
+    }
+  }
+};
+
 // ================================================================================================ values
 inline uint32_t rd_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -297,6 +325,7 @@ struct pgpu_table_s {
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Scratch>> scratch_pool;
   GenScratch gen;
+  std::shared_ptr<ResultPool> result_pool = std::make_shared<ResultPool>();
   int64_t device_bytes = 0;
   int num_cus = 256;
 };
@@ -520,6 +549,9 @@ struct pgpu_plan_s {
   int grid = 0;
   size_t lds_bytes = 0;
   bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
+  bool dense = false;                     // direct kernel instance with whole-group decode (dense tiles)
+  double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
+  int64_t sel_docs = 0;
   std::vector<int32_t> stage_slot;        // query column slot of each staged filter column
   std::vector<int32_t> leaf_stage;        // staged column of each leaf
   int64_t stage_words = 0;                // one stage buffer (max over segments)
@@ -549,13 +581,30 @@ struct pgpu_result_s {
   int64_t n = 0;
   int num_keys = 0;
   int num_aggs = 0;
-  std::vector<int32_t> gids;              // [n][num_keys]
-  std::vector<double> values;             // [num_aggs][n]
-  std::vector<int64_t> avg_counts;        // [num_aggs][n]
-  std::vector<int64_t> exact;             // [num_aggs][n]
-  std::vector<uint8_t> has_exact;         // per agg
+  int num_slots = 0;
+  // Groups in ascending composite-key order, columnar in one pinned buffer: int32 group-by dictIds
+  // [num_keys][n], then (8-aligned) u64 accumulator words [num_slots][n]; slot 0 = COUNT.
+  HostPinned buf;
+  std::shared_ptr<ResultPool> pool;
+  std::vector<int32_t> agg_slot;          // per aggregation: its slot
+  std::vector<uint8_t> agg_conv;          // per aggregation: how the slot word reads (RCONV_*)
   int64_t stats[6] = {0, 0, 0, 0, 0, 0};
+  ~pgpu_result_s() {
+    if (pool) pool->give(buf);
+    else buf.release();
+  }
+  static size_t slot_offset(int nk, int64_t n) { return ((size_t)nk * n * 4 + 7) & ~size_t(7); }
+  int alloc(int nk, int ns, int64_t rows) {
+    num_keys = nk;
+    num_slots = ns;
+    n = rows;
+    if (pool && !buf.p) buf = pool->take();
+    return buf.ensure(std::max<size_t>(slot_offset(nk, rows) + (size_t)ns * rows * 8, 64));
+  }
+  int32_t* gid(int j) { return reinterpret_cast<int32_t*>(buf.p) + (size_t)j * n; }
+  uint64_t* slot(int s) { return reinterpret_cast<uint64_t*>((uint8_t*)buf.p + slot_offset(num_keys, n)) + (size_t)s * n; }
 };
+enum { RCONV_I64 = 0, RCONV_F64 = 1, RCONV_KEY_F64 = 2 };
 
 namespace {
 
@@ -735,6 +784,25 @@ int translate_predicate(const Column& c, const pgpu_predicate& p, const ParsedPr
 }
 
 // Constant folding of the program against the leaves' constants (FilterPlanNode.java:146-176).
+// Fraction of docs the filter program passes if every dictId were equally frequent (leaf fractions combined as
+// independent events).  Only picks the scan kernel instance (dense / sparse): never affects results.
+double estimate_selectivity(const std::vector<int32_t>& ops, const std::vector<double>& leaf) {
+  double st[kMaxOps];
+  int sp = 0;
+  for (int32_t e : ops) {
+    const int op = e >> 16, arg = e & 0xFFFF;
+    if (op == OP_LEAF) st[sp++] = leaf[arg];
+    else if (op == OP_NOT) st[sp - 1] = 1.0 - st[sp - 1];
+    else {
+      double x = op == OP_AND ? 1.0 : 0.0;
+      for (int j = sp - arg; j < sp; ++j) x = op == OP_AND ? x * st[j] : 1.0 - (1.0 - x) * (1.0 - st[j]);
+      sp -= arg;
+      st[sp++] = x;
+    }
+  }
+  return sp == 0 ? 1.0 : st[sp - 1];
+}
+
 Tri fold_program(const std::vector<int32_t>& ops, const std::vector<Tri>& leaf) {
   Tri st[kMaxOps];
   int sp = 0;
@@ -1106,6 +1174,22 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     for (int l = 0; l < P->num_leaves; ++l)
       if (tri[l] == T_VAR) P->scanned_entries_model += s->num_docs;
+    if (P->sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
+      std::vector<double> frac(P->num_leaves, 1.0);
+      for (int l = 0; l < P->num_leaves; ++l) {
+        const LeafHost& lh = leaves[l];
+        const double card = std::max(1, s->cols[q->predicates[l].column].card);
+        double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
+        if (lh.kind == LEAF_SET) {
+          int64_t ones = 0;
+          for (uint32_t w : lh.set) ones += __builtin_popcount(w);
+          f = ones / card;
+        }
+        frac[l] = lh.negate ? 1.0 - f : f;
+      }
+      P->sel_estimate = P->num_leaves ? estimate_selectivity(P->ops, frac) : 1.0;
+      P->sel_docs = s->num_docs;
+    }
     for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
     for (size_t k = 1; k < P->slot_kind.size(); ++k) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
     std::fill(rec.begin(), rec.end(), 0);
@@ -1146,7 +1230,23 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->star_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, 1024 / (int64_t)P->star.size()));
     P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
   }
-  P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, 1024));  // 4 workgroups per CU
+  // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
+  P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16;
+  {
+    static std::mutex occ_mu;
+    static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU
+    int per_cu;
+    {
+      std::lock_guard<std::mutex> g(occ_mu);
+      const auto k = std::make_tuple(t->device, (int)P->mode, (int)P->dense, P->lds_bytes);
+      auto it = occ_cache.find(k);
+      if (it == occ_cache.end()) it = occ_cache.emplace(k, occupancy_filter_groupby(P->mode, P->dense, P->lds_bytes)).first;
+      per_cu = it->second;
+    }
+    if (per_cu <= 0) per_cu = 1;
+    per_cu = std::min(per_cu, 4);
+    P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+  }
   if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
   // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
   for (int l = 0; l < P->num_leaves; ++l) {
@@ -1265,7 +1365,7 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   HIP_TRY(hipEventRecord(sc->ev[1], stream));
   if (P->num_tiles > 0) {
     const int rc = P->staged ? launch_scan(kp, P->mode, P->grid, P->lds_bytes, stream)
-                             : launch_filter_groupby(kp, P->mode, P->grid, P->lds_bytes, stream);
+                             : launch_filter_groupby(kp, P->mode, P->dense, P->grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   if (!P->star.empty()) {
@@ -1326,20 +1426,27 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   return 0;
 }
 
+// Group-by dictIds of composite key k: (k / stride[j]) % card[j] (DictionaryBasedGroupKeyGenerator.java:276-323).
+void decode_keys(const pgpu_plan_s* P, pgpu_result_s* R, int64_t row, uint64_t key) {
+  for (int j = 0; j < R->num_keys; ++j)
+    R->gid(j)[row] = (int32_t)((key / (uint64_t)P->key_stride[j]) % (uint64_t)P->key_card[j]);
+}
+
 int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, pgpu_result_s* R) {
   Scratch* sc = P->scratch;
   const double t_start = trace_on() ? now_us() : 0;
   if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   const uint64_t* table = reinterpret_cast<const uint64_t*>(d_table ? d_table : P->d_table_used);
   const int nslots = (int)P->slot_kind.size();
-  const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
-  std::vector<uint64_t> keys, slots;  // keys[n], slots[s * n + i]
+  const int nk = (int)P->key_cols.size();
+  const int64_t G = P->num_keys;
   int64_t n = 0;
   uint64_t matched = 0, star_scanned = 0;
-  const int64_t words = (int64_t)nslots * P->num_keys;
+  const int64_t words = (int64_t)nslots * G;
   double t_sync1 = 0;
+  R->pool = P->table->result_pool;
   if (!P->hash && words * 8 <= kHostCompactBytes) {
-    // small dense table: one copy (table + stats) and one sync, compacted on the host
+    // small dense table: one copy (table + stats) and one sync, compacted on the host in key order
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
@@ -1348,24 +1455,56 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     t_sync1 = trace_on() ? now_us() : 0;
     matched = st[words];
     star_scanned = st[words + 1];
-    const int64_t G = P->num_keys;
     for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
-    keys.resize(n);
-    slots.resize((size_t)n * nslots);
+    TRY(R->alloc(nk, nslots, n));
     int64_t j = 0;
     for (int64_t k = 0; k < G; ++k) {
       if (!st[k]) continue;
-      keys[j] = (uint64_t)k;
-      for (int s = 0; s < nslots; ++s) slots[(size_t)s * n + j] = st[(int64_t)s * G + k];
+      decode_keys(P, R, j, (uint64_t)k);
+      for (int s = 0; s < nslots; ++s) R->slot(s)[j] = st[(int64_t)s * G + k];
       ++j;
     }
+  } else if (!P->hash) {
+    // large dense table: ordered compaction on the device (count / scan / scatter, dictIds decoded there),
+    // copied back row by row into the pinned result buffer
+    int64_t cap = std::max<int64_t>(2, std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)));
+    cap = (cap + 1) & ~int64_t(1);
+    const int64_t nch = compact_ordered_chunks(G);
+    TRY(sc->counter.ensure(64));
+    TRY(sc->cslots.ensure((size_t)std::max<int64_t>(nch, 1) * 4));
+    TRY(sc->ckeys.ensure((size_t)cap * (4 * nk + 8 * nslots) + 8));
+    if (launch_compact_ordered(table, nslots, G, P->key_stride.data(), P->key_card.data(), nk,
+                               sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(), sc->ckeys.p, cap,
+                               stream))
+      return fail(PGPU_ERR_DEVICE, "compact launch failed: %s", hipGetErrorString(hipGetLastError()));
+    TRY(sc->stage.ensure(64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    t_sync1 = trace_on() ? now_us() : 0;
+    n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
+    matched = st[1];
+    star_scanned = st[2];
+    TRY(R->alloc(nk, nslots, n));
+    if (n > 0) {
+      const uint8_t* dev = sc->ckeys.as<uint8_t>();
+      for (int j = 0; j < nk; ++j)
+        HIP_TRY(hipMemcpyAsync(R->gid(j), dev + (size_t)j * cap * 4, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+      for (int s = 0; s < nslots; ++s)
+        HIP_TRY(hipMemcpyAsync(R->slot(s), dev + (size_t)nk * cap * 4 + (size_t)s * cap * 8, (size_t)n * 8,
+                               hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+    }
   } else {
-    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
+    // hash table: unordered compaction, then key order on the host
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)));
+    const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
     TRY(sc->counter.ensure(64));
     TRY(sc->ckeys.ensure((size_t)cap * 8 * rec));
     HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
-    if (launch_compact(table, P->hash ? sc->hash_keys.as<unsigned long long>() : nullptr, nslots, P->num_keys,
-                       sc->counter.as<unsigned long long>(), sc->ckeys.as<uint64_t>(), cap, stream))
+    if (launch_compact(table, sc->hash_keys.as<unsigned long long>(), nslots, G, sc->counter.as<unsigned long long>(),
+                       sc->ckeys.as<uint64_t>(), cap, stream))
       return fail(PGPU_ERR_DEVICE, "compact launch failed");
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
@@ -1382,11 +1521,14 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       HIP_TRY(hipMemcpyAsync(st, sc->ckeys.p, (size_t)n * rec * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
     }
-    keys.resize(n);
-    slots.resize((size_t)n * nslots);
-    for (int64_t j = 0; j < n; ++j) {
-      keys[j] = st[j * rec];
-      for (int s = 0; s < nslots; ++s) slots[(size_t)s * n + j] = st[j * rec + 1 + s];
+    std::vector<int64_t> order(n);
+    for (int64_t i = 0; i < n; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return st[a * rec] < st[b * rec]; });
+    TRY(R->alloc(nk, nslots, n));
+    for (int64_t r = 0; r < n; ++r) {
+      const uint64_t* e = st + order[r] * rec;
+      decode_keys(P, R, r, e[0]);
+      for (int s = 0; s < nslots; ++s) R->slot(s)[r] = e[1 + s];
     }
   }
   const double t_sync2 = trace_on() ? now_us() : 0;
@@ -1394,57 +1536,18 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     return fail(PGPU_ERR_UNSUPPORTED,
                 "numGroupsLimit %lld reached (%lld groups): Pinot truncates per segment in first-seen order",
                 (long long)P->num_groups_limit, (long long)n);
-  // order groups by composite key
-  std::vector<int64_t> order(n);
-  for (int64_t i = 0; i < n; ++i) order[i] = i;
-  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return keys[a] < keys[b]; });
-  const int nk = (int)P->key_cols.size();
   const int na = (int)P->agg_fn.size();
-  R->n = n;
-  R->num_keys = nk;
   R->num_aggs = na;
-  R->gids.resize((size_t)n * nk);
-  R->values.assign((size_t)na * n, 0.0);
-  R->avg_counts.assign((size_t)na * n, 0);
-  R->exact.assign((size_t)na * n, 0);
-  R->has_exact.assign(na, 0);
-  for (int64_t r = 0; r < n; ++r) {
-    const int64_t i = order[r];
-    uint64_t key = keys[i];
-    for (int j = 0; j < nk; ++j) R->gids[(size_t)r * nk + j] = (int32_t)((key / P->key_stride[j]) % P->key_card[j]);
-    const int64_t count = (int64_t)slots[i];
-    for (int a = 0; a < na; ++a) {
-      const int fn = P->agg_fn[a];
-      const int s = P->agg_slot[a];
-      const uint64_t w = slots[(size_t)s * n + i];
-      double v = 0.0;
-      int64_t ex = 0;
-      bool exact = false;
-      switch (fn) {
-        case PGPU_AGG_COUNT: v = (double)count; ex = count; exact = true; break;  // CountAggregationFunction: double count
-        case PGPU_AGG_SUM: case PGPU_AGG_AVG:
-          if (P->slot_kind[s] == SLOT_SUM_I64) { ex = (int64_t)w; v = (double)ex; exact = true; }
-          else memcpy(&v, &w, 8);
-          if (fn == PGPU_AGG_AVG) R->avg_counts[(size_t)a * n + r] = count;
-          break;
-        default: {  // MIN / MAX: ordered key -> value
-          const int type = P->table->types[P->agg_col[a]];
-          if (is_int_type(type)) { ex = (int64_t)w; v = (double)ex; exact = true; }
-          else v = key_double((int64_t)w);
-          break;
-        }
-      }
-      R->values[(size_t)a * n + r] = v;
-      R->exact[(size_t)a * n + r] = ex;
-      if (r == 0) R->has_exact[a] = exact;
-    }
+  R->agg_slot = P->agg_slot;
+  R->agg_conv.assign(na, RCONV_I64);
+  for (int a = 0; a < na; ++a) {
+    const int fn = P->agg_fn[a];
+    if (fn == PGPU_AGG_COUNT) continue;  // CountAggregationFunction: exact count (held as double by Pinot)
+    if (fn == PGPU_AGG_SUM || fn == PGPU_AGG_AVG)
+      R->agg_conv[a] = P->slot_kind[P->agg_slot[a]] == SLOT_SUM_I64 ? RCONV_I64 : RCONV_F64;
+    else
+      R->agg_conv[a] = is_int_type(P->table->types[P->agg_col[a]]) ? RCONV_I64 : RCONV_KEY_F64;
   }
-  if (n == 0)
-    for (int a = 0; a < na; ++a) {
-      const int fn = P->agg_fn[a];
-      R->has_exact[a] = fn == PGPU_AGG_COUNT || (P->slot_kind[P->agg_slot[a]] == SLOT_SUM_I64) ||
-                        ((fn == PGPU_AGG_MIN || fn == PGPU_AGG_MAX) && is_int_type(P->table->types[P->agg_col[a]]));
-    }
   R->stats[0] = (int64_t)matched;
   R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned;
   R->stats[2] = (int64_t)matched * P->num_projected;
@@ -1885,23 +1988,53 @@ int pgpu_result_num_groups(pgpu_result r, int64_t* n) {
 }
 int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
   if (!r || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  std::copy(r->gids.begin(), r->gids.end(), out);
+  const int nk = r->num_keys;
+  for (int j = 0; j < nk; ++j) {
+    const int32_t* g = r->gid(j);
+    for (int64_t i = 0; i < r->n; ++i) out[i * nk + j] = g[i];
+  }
+  return 0;
+}
+int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out) {
+  if (!r || key < 0 || key >= r->num_keys || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->n) memcpy(out, r->gid(key), (size_t)r->n * 4);
+  return 0;
+}
+int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out) {
+  if (!r || key < 0 || key >= r->num_keys || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *out = r->gid(key);
+  return 0;
+}
+int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form) {
+  if (!r || agg < -1 || agg >= r->num_aggs || !out || !form) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (agg == -1) {  // the COUNT slot (AvgPair.count of every AVG)
+    *out = r->slot(0);
+    *form = RCONV_I64;
+    return 0;
+  }
+  *out = r->slot(r->agg_slot[agg]);
+  *form = r->agg_conv[agg];
   return 0;
 }
 int pgpu_result_values(pgpu_result r, int agg, double* out) {
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  std::copy(r->values.begin() + (size_t)agg * r->n, r->values.begin() + (size_t)(agg + 1) * r->n, out);
+  const uint64_t* w = r->slot(r->agg_slot[agg]);
+  switch (r->agg_conv[agg]) {
+    case RCONV_I64: for (int64_t i = 0; i < r->n; ++i) out[i] = (double)(int64_t)w[i]; break;
+    case RCONV_F64: if (r->n) memcpy(out, w, (size_t)r->n * 8); break;
+    default: for (int64_t i = 0; i < r->n; ++i) out[i] = key_double((int64_t)w[i]); break;
+  }
   return 0;
 }
 int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) {
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  std::copy(r->avg_counts.begin() + (size_t)agg * r->n, r->avg_counts.begin() + (size_t)(agg + 1) * r->n, out);
+  if (r->n) memcpy(out, r->slot(0), (size_t)r->n * 8);  // slot 0 = COUNT = AvgPair.count
   return 0;
 }
 int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  if (!r->has_exact[agg]) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
-  std::copy(r->exact.begin() + (size_t)agg * r->n, r->exact.begin() + (size_t)(agg + 1) * r->n, out);
+  if (r->agg_conv[agg] != RCONV_I64) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
+  if (r->n) memcpy(out, r->slot(r->agg_slot[agg]), (size_t)r->n * 8);
   return 0;
 }
 int pgpu_result_stats(pgpu_result r, int64_t* out6) {

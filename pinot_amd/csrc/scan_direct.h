@@ -6,11 +6,14 @@
 namespace pgpu {
 
 // ---------------------------------------------------------------------------------------------- K3 fused
-template <int MODE>
+// DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
+// decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
+// path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
+template <int MODE, bool DENSE>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
-__global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
+__global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t G = p.num_keys_total;
@@ -87,7 +90,15 @@ __global__ __launch_bounds__(kBlock, PGPU_MIN_WAVES) void filter_groupby_kernel(
       }
       const uint32_t cnt = __popc(mask);
       matched += cnt;
-      if (__any(cnt > 2u)) {
+      uint32_t wave_cnt = 0;
+      if (DENSE && MODE != MODE_HASH) {
+        wave_cnt = cnt;
+        for (int off = 32; off > 0; off >>= 1) wave_cnt += __shfl_xor(wave_cnt, off);
+      }
+      if (DENSE && MODE != MODE_HASH && wave_cnt >= (uint32_t)kDenseGroupMin) {
+        // dense tile: whole-group decode of the group-by / aggregated columns
+        aggregate_group<MODE>(p, S, gclamp, mask, tbl, G);
+      } else if (__any(cnt > 2u)) {
         // dense: the lane's own 32-doc group, 2 matched docs per batch (the lines are already cached)
         while (__any(mask != 0u)) {
           int64_t doc[2];

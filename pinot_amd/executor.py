@@ -7,6 +7,7 @@ Plan          a compiled query over a segment list: execute (async, dense group 
 GroupByResult decoded groups {key tuple: [aggregation results]} + ExecutionStatistics.
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -47,11 +48,52 @@ class AvgPair:
 
 
 class GroupByResult:
-    def __init__(self, keys, values, stats, exact=None):
-        self.keys = keys            # list of key tuples (python values), ascending composite key
-        self.values = values        # list (per group) of lists (per aggregation)
+    """Groups in ascending composite-key order, held columnar (numpy) as the C ABI returns them; the Python form
+    ({key tuple: [aggregation results]}) is built on first use of `keys` / `values` / `as_dict()`."""
+
+    def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None):
         self.stats = stats
         self.exact = exact or {}    # agg index -> np.int64 array of exact integer accumulators
+        self._keys, self._values = keys, values
+        # columnar: (dicts, [per group-by column: [n] int32 dictIds], per-agg (fn, values f64 | None,
+        # exact i64 | None, counts | None), n) -- numpy views of the C result's pinned buffer
+        self._col = columnar
+        self._n = len(keys) if keys is not None else (columnar[3] if columnar is not None else 0)
+
+    @property
+    def gid_columns(self):
+        """Per group-by column, the [n] table-global dictIds of the groups (zero-copy)."""
+        return self._col[1]
+
+    @property
+    def gids(self):
+        """[n, num_group_by] table-global dictIds of the groups."""
+        cols = self._col[1]
+        return np.stack(cols, axis=1) if cols and self._n else np.zeros((self._n, len(cols)), dtype=np.int32)
+
+    @property
+    def keys(self):
+        if self._keys is None:
+            dicts, cols = self._col[0], self._col[1]
+            vals = [np.asarray(d)[c].tolist() if self._n else [] for d, c in zip(dicts, cols)]
+            self._keys = list(zip(*vals)) if vals else [()] * self._n
+        return self._keys
+
+    @property
+    def values(self):
+        if self._values is None:
+            cols = []
+            for fn, v, e, c in self._col[2]:
+                if v is None:
+                    v = e.astype(np.float64)
+                if fn == "AVG":
+                    cols.append([AvgPair(x, y) for x, y in zip(v.tolist(), c.tolist())])
+                elif fn == "COUNT":
+                    cols.append((e if e is not None else v.astype(np.int64)).tolist())
+                else:
+                    cols.append(v.tolist())
+            self._values = [list(r) for r in zip(*cols)] if cols else [[] for _ in range(self._n)]
+        return self._values
 
     def as_dict(self):
         return {k: v for k, v in zip(self.keys, self.values)}
@@ -61,7 +103,7 @@ class GroupByResult:
         return {"\0".join(_key_str(x) for x in k): v for k, v in zip(self.keys, self.values)}
 
     def __len__(self):
-        return len(self.keys)
+        return self._n
 
 
 def _key_str(x):
@@ -314,44 +356,75 @@ class Plan:
         return out[0], out[1]
 
     def finalize(self, stream=None, d_table=None):
+        """Waits for the execution, compacts the group table and returns the decoded result.  `finalize_us`
+        holds (C ABI finalize incl. the wait for the kernels, decode into numpy) in microseconds."""
         r = ctypes.c_void_p()
+        t0 = time.perf_counter()
         L.check(self.lib.pgpu_plan_finalize(self.handle, ctypes.c_void_p(stream or 0), ctypes.c_void_p(d_table or 0),
                                             ctypes.byref(r)))
-        try:
-            return _decode_result(self.table, self.query, r)
-        finally:
-            self.lib.pgpu_result_destroy(r)
+        t1 = time.perf_counter()
+        holder = _ResultHolder(self.lib, r)
+        res = _decode_result(self.table, self.query, holder)
+        self.finalize_us = ((t1 - t0) * 1e6, (time.perf_counter() - t1) * 1e6)
+        return res
 
 
-def _decode_result(table, query, r):
-    lib = table.lib
+class _ResultHolder:
+    """Owns a pgpu_result; numpy views of its pinned columns reference this object, so the C result lives until
+    the last view is gone."""
+
+    def __init__(self, lib, r):
+        self.lib, self.r = lib, r
+
+    def __del__(self):
+        if self.r:
+            self.lib.pgpu_result_destroy(self.r)
+            self.r = None
+
+
+class _View:
+    def __init__(self, owner, addr, n, typestr):
+        self.owner = owner
+        self.__array_interface__ = {"shape": (n,), "typestr": typestr, "data": (addr, True), "version": 3}
+
+
+def _view(holder, addr, n, dtype):
+    if n == 0 or not addr:
+        return np.zeros(0, dtype=dtype)
+    return np.asarray(_View(holder, addr, n, np.dtype(dtype).str))
+
+
+def _decode_result(table, query, holder):
+    """Columnar result over zero-copy views of the C result (pgpu_result_*_view)."""
+    lib, r = table.lib, holder.r
     n = ctypes.c_int64()
     L.check(lib.pgpu_result_num_groups(r, ctypes.byref(n)))
     n = n.value
     nk = len(query.group_by)
-    gids = np.zeros(max(n * nk, 1), dtype=np.int32)
-    L.check(lib.pgpu_result_group_ids(r, L.ptr(gids, ctypes.c_int32)))
-    gids = gids[:n * nk].reshape(n, nk) if n else np.zeros((0, nk), dtype=np.int32)
-    dicts = [table.dictionary(c) for c in query.group_by]
-    keys = [tuple(dicts[j][int(gids[i, j])] for j in range(nk)) for i in range(n)]
+    ptr = ctypes.c_void_p()
     cols = []
+    for j in range(nk):
+        L.check(lib.pgpu_result_group_ids_view(r, j, ctypes.byref(ptr)))
+        cols.append(_view(holder, ptr.value, n, np.int32))
+    dicts = [table.dictionary(c) for c in query.group_by]
+    aggs = []
     exact = {}
+    form = ctypes.c_int32()
     for a, (fn, _) in enumerate(query.aggregations):
-        v = np.zeros(max(n, 1), dtype=np.float64)
-        L.check(lib.pgpu_result_values(r, a, L.ptr(v, ctypes.c_double)))
-        v = v[:n]
-        e = np.zeros(max(n, 1), dtype=np.int64)
-        if lib.pgpu_result_values_i64(r, a, L.ptr(e, ctypes.c_int64)) == L.PGPU_OK:
-            exact[a] = e[:n].copy()
-        if fn == "AVG":
-            c = np.zeros(max(n, 1), dtype=np.int64)
-            L.check(lib.pgpu_result_avg_counts(r, a, L.ptr(c, ctypes.c_int64)))
-            cols.append([AvgPair(v[i], c[i]) for i in range(n)])
-        elif fn == "COUNT":
-            cols.append([int(x) for x in e[:n]] if a in exact else [int(x) for x in v])
+        L.check(lib.pgpu_result_words_view(r, a, ctypes.byref(ptr), ctypes.byref(form)))
+        e = v = c = None
+        if form.value == 0:
+            exact[a] = e = _view(holder, ptr.value, n, np.int64)
+        elif form.value == 1:
+            v = _view(holder, ptr.value, n, np.float64)
         else:
-            cols.append([float(x) for x in v])
-    values = [[cols[a][i] for a in range(len(cols))] for i in range(n)]
+            v = np.empty(max(n, 1), dtype=np.float64)
+            L.check(lib.pgpu_result_values(r, a, L.ptr(v, ctypes.c_double)))
+            v = v[:n]
+        if fn == "AVG":
+            L.check(lib.pgpu_result_words_view(r, -1, ctypes.byref(ptr), ctypes.byref(form)))
+            c = _view(holder, ptr.value, n, np.int64)
+        aggs.append((fn, v, e, c))
     st = np.zeros(6, dtype=np.int64)
     L.check(lib.pgpu_result_stats(r, L.ptr(st, ctypes.c_int64)))
-    return GroupByResult(keys, values, ExecutionStatistics(st), exact)
+    return GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n))

@@ -33,13 +33,14 @@ def double_table(n, column_index, lo, hi):
 
 
 class Workload:
-    def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000):
+    def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000, cpu_sample_segments=64):
         self.name = name
         self.schema = schema          # [(column, type)]
         self.gen = gen                # generator spec per column (table column order)
         self.sql = sql
         self.description = description
         self.num_groups_limit = num_groups_limit  # query option numGroupsLimit of the config
+        self.cpu_sample_segments = cpu_sample_segments  # bench CPU-baseline sample (~10-30 s of oracle work)
 
 
 def adanalytics():
@@ -90,7 +91,8 @@ def c5():
     ]
     sql = "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3"
     # run with num.groups.limit = 10M and server trim off
-    return Workload("c5", schema, gen, sql, "C5 high-cardinality 3-column GROUP BY", num_groups_limit=10_000_000)
+    return Workload("c5", schema, gen, sql, "C5 high-cardinality 3-column GROUP BY", num_groups_limit=10_000_000,
+                    cpu_sample_segments=16)
 
 
 WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c5": c5}

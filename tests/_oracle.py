@@ -227,7 +227,8 @@ def _decode_key(blob, types):
     return tuple(out)
 
 
-def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000):
+def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000, decode=True):
+    """decode=False: run the operator + combine only and return the group count (bench timing leg)."""
     o = lib()
     segs = [_OrSeg(schema, s) for s in segments]
     arr = (OrSegment * max(len(segs), 1))(*[s.seg for s in segs])
@@ -238,6 +239,8 @@ def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capac
     if rc != 0:
         raise RuntimeError("oracle error %d: %s" % (rc, msg.value.decode()))
     try:
+        if not decode:
+            return res.num_groups
         types = {n: (L.TYPE_NAMES[t] if isinstance(t, str) else t) for n, t in schema}
         ktypes = [types[c] for c in q.group_by]
         n = res.num_groups

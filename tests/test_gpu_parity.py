@@ -341,3 +341,31 @@ def test_num_groups_limit_not_reached_is_exact(oracle, sv):
     assert not o.limit_reached
     r = t.execute_groupby([h], q)
     assert_same(r, o, q, K.SCHEMA)
+
+
+@pytest.mark.parametrize("docs", [1, 4097, 150_000])
+def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs):
+    """C5 shape (3-column composite key over a ~10^6 key space, INT_MAP holder in Pinot): the dense global table
+    and its ordered device compaction (count / scan / scatter) give the oracle's groups in ascending key order,
+    across chunk boundaries and with fewer docs than keys."""
+    rng = np.random.default_rng(docs)
+    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE")]
+    segs = []
+    for _ in range(2):
+        segs.append(oracle.make_segment(schema, {"k1": rng.integers(0, 400, size=docs),
+                                                 "k2": rng.integers(0, 60, size=docs),
+                                                 "k3": rng.integers(0, 50, size=docs),
+                                                 "m": rng.integers(0, 1000, size=docs),
+                                                 "x": rng.uniform(-1e6, 1e6, size=docs)}))
+    t, hs = gpu_table(schema, segs)
+    try:
+        q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
+                        num_groups_limit=10 ** 7)
+        r = t.execute_groupby(hs, q)
+        o = oracle.run_groupby(schema, segs, q, combine=False, max_initial_capacity=10000)
+        assert_same(r, o, q, schema)
+        g = r.gids.astype(np.int64)  # key = d0 + d1*c0 + d2*c0*c1 (DictionaryBasedGroupKeyGenerator.java:276-323)
+        comp = (g[:, 2] * 10 ** 6 + g[:, 1]) * 10 ** 6 + g[:, 0]
+        assert np.all(np.diff(comp) > 0)
+    finally:
+        t.close()

@@ -20,6 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+SHARD_BYTES = 16 << 20  # group tables at least this large are reduce-scattered across ranks, not all-reduced
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
 
 
@@ -184,7 +185,7 @@ def cpu_baseline(table, handles, query, workload, docs, args):
         _oracle.run_groupby(workload.schema, segs, query, nthreads=threads, decode=False)
         reps += 1
         elapsed = time.perf_counter() - t0
-        if elapsed >= args.cpu_target_seconds or reps >= 50:
+        if elapsed >= args.cpu_target_seconds or reps >= 1000:
             break
     rows = reps * len(segs) * docs
     _ = types
@@ -217,7 +218,7 @@ def main():
 
     from pinot_amd import _lib as L
     from pinot_amd.build import build
-    from pinot_amd.combine import allreduce_group_table, union_dictionaries
+    from pinot_amd.combine import allreduce_group_table, reduce_scatter_group_table, union_dictionaries
     from pinot_amd.executor import GpuTable
     from pinot_amd.query import parse_query
     from pinot_amd.workloads import WORKLOADS
@@ -250,6 +251,8 @@ def main():
     nslots, nkeys, kinds = probe.layout()
     probe.close()
     d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
+    # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
+    sharded = world > 1 and nslots * nkeys * 8 >= SHARD_BYTES
 
     phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0,
               "decode": 0.0}
@@ -260,10 +263,15 @@ def main():
         c1 = time.perf_counter()
         plan.execute(stream, d_table.data_ptr() if nkeys > 0 else None)
         c2 = time.perf_counter()
-        if world > 1:
+        if sharded:
+            shard, k0, kn = reduce_scatter_group_table(d_table, kinds)
+        elif world > 1:
             allreduce_group_table(d_table, kinds)
         c3 = time.perf_counter()
-        res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
+        if sharded:
+            res = plan.finalize_range(stream, shard.data_ptr(), k0, kn)
+        else:
+            res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
         c4 = time.perf_counter()
         k_us = plan.timing_us()[1]
         fc_us, dec_us = plan.finalize_us
@@ -298,6 +306,11 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    ngroups = len(first) if first is not None else 0
+    if sharded:  # disjoint per-rank shards: the query's groups are their sum
+        g = torch.tensor([ngroups], dtype=torch.int64, device="cuda")
+        dist.all_reduce(g)
+        ngroups = int(g.item())
     total_rows = float(nseg) * docs * world
     value = total_rows * args.steps / elapsed
     kernel_avg_us = float(np.mean(kernel_us)) if kernel_us else 0.0
@@ -335,7 +348,8 @@ def main():
             "data": "synthetic (BASELINE.md §3 generators, built on the device)",
             "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
-                       "groups": len(first) if first is not None else None, "setup_s": round(t_gen, 1)},
+                       "groups": ngroups, "setup_s": round(t_gen, 1),
+                       "combine": "reduce_scatter" if sharded else ("all_reduce" if world > 1 else "none")},
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,

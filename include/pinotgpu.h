@@ -194,6 +194,14 @@ int pgpu_plan_execute(pgpu_plan plan, void* stream, void* d_table);
  * dictionary ids and finished aggregation values.  Synchronises `stream`. */
 int pgpu_plan_finalize(pgpu_plan plan, void* stream, const void* d_table, pgpu_result* out);
 
+/* Finalize of one key-range shard of a dense group table: d_table_shard is [num_slots][key_count] words holding
+ * the composite keys [key_begin, key_begin + key_count) -- a rank's part after a reduce-scatter of the per-GPU
+ * tables (the multi-GPU combine of large key spaces; every rank then returns its own disjoint groups, as Pinot
+ * servers return partial tables).  PGPU_ERR_UNSUPPORTED for hash-mode tables and for queries whose
+ * numGroupsLimit is below the key space (those finalize the whole table). */
+int pgpu_plan_finalize_range(pgpu_plan plan, void* stream, const void* d_table_shard, int64_t key_begin,
+                             int64_t key_count, pgpu_result* out);
+
 /* One-call form: plan + execute + finalize (the whole per-server query path). */
 int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,
                          void* stream, pgpu_result* out);

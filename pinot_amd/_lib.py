@@ -117,6 +117,7 @@ _PROTOS = {
     "pgpu_plan_layout": (c_int, [c_voidp, c_i32p, c_i64p, c_i32p]),
     "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
     "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
+    "pgpu_plan_finalize_range": (c_int, [c_voidp, c_voidp, c_voidp, c_i64, c_i64, ctypes.POINTER(c_voidp)]),
     "pgpu_execute_groupby": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp,
                                      ctypes.POINTER(c_voidp)]),
     "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),

@@ -157,8 +157,9 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
 // dictIds [num_key_cols][cap], then u64 slot words [num_slots][cap]; chunk_scratch holds
 // compact_ordered_chunks(num_keys) u32.
 int64_t compact_ordered_chunks(int64_t num_keys);
-int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int64_t* key_stride,
-                           const int64_t* key_card, int32_t num_key_cols, uint32_t* chunk_scratch,
+int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
+                           const int64_t* key_stride, const int64_t* key_card, int32_t num_key_cols,
+                           uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);

@@ -176,6 +176,7 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(uint32_t* __restrict
 struct KeyDecode {
   int64_t stride[kMaxKeys];
   int64_t card[kMaxKeys];
+  int64_t base;  // composite key of table column 0 (a key-range shard of the table)
   int32_t n;
 };
 __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint64_t* __restrict__ table, int32_t num_slots,
@@ -201,7 +202,8 @@ __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint64_t* __
     if (f) {
       const int64_t j = (int64_t)pos + before + rank;
       if (j < cap) {
-        for (int c = 0; c < kd.n; ++c) gid[(int64_t)c * cap + j] = (int32_t)((k / kd.stride[c]) % kd.card[c]);
+        for (int c = 0; c < kd.n; ++c)
+          gid[(int64_t)c * cap + j] = (int32_t)(((kd.base + k) / kd.stride[c]) % kd.card[c]);
         for (int s = 0; s < num_slots; ++s) words[(int64_t)s * cap + j] = table[(int64_t)s * num_keys + k];
       }
     }
@@ -387,13 +389,15 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
 
 int64_t compact_ordered_chunks(int64_t num_keys) { return (num_keys + kCompactChunk - 1) / kCompactChunk; }
 
-int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int64_t* key_stride,
-                           const int64_t* key_card, int32_t num_key_cols, uint32_t* chunk_scratch,
+int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
+                           const int64_t* key_stride, const int64_t* key_card, int32_t num_key_cols,
+                           uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream) {
   const int64_t nch = compact_ordered_chunks(num_keys);
   if (nch < 1 || nch > INT32_MAX || num_key_cols > kMaxKeys || (cap & 1)) return -1;
   KeyDecode kd{};
   kd.n = num_key_cols;
+  kd.base = key_base;
   for (int j = 0; j < num_key_cols; ++j) { kd.stride[j] = key_stride[j]; kd.card[j] = key_card[j]; }
   hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch);
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);

@@ -1432,14 +1432,17 @@ void decode_keys(const pgpu_plan_s* P, pgpu_result_s* R, int64_t row, uint64_t k
     R->gid(j)[row] = (int32_t)((key / (uint64_t)P->key_stride[j]) % (uint64_t)P->key_card[j]);
 }
 
-int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, pgpu_result_s* R) {
+// key_begin / key_count: a shard [slots][key_count] of the dense table holding keys [key_begin, key_begin +
+// key_count) (after a reduce-scatter across GPUs); the whole table is (0, num_keys).
+int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, int64_t key_begin, int64_t key_count,
+                       pgpu_result_s* R) {
   Scratch* sc = P->scratch;
   const double t_start = trace_on() ? now_us() : 0;
   if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   const uint64_t* table = reinterpret_cast<const uint64_t*>(d_table ? d_table : P->d_table_used);
   const int nslots = (int)P->slot_kind.size();
   const int nk = (int)P->key_cols.size();
-  const int64_t G = P->num_keys;
+  const int64_t G = key_count;
   int64_t n = 0;
   uint64_t matched = 0, star_scanned = 0;
   const int64_t words = (int64_t)nslots * G;
@@ -1460,7 +1463,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     int64_t j = 0;
     for (int64_t k = 0; k < G; ++k) {
       if (!st[k]) continue;
-      decode_keys(P, R, j, (uint64_t)k);
+      decode_keys(P, R, j, (uint64_t)(key_begin + k));
       for (int s = 0; s < nslots; ++s) R->slot(s)[j] = st[(int64_t)s * G + k];
       ++j;
     }
@@ -1473,7 +1476,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->counter.ensure(64));
     TRY(sc->cslots.ensure((size_t)std::max<int64_t>(nch, 1) * 4));
     TRY(sc->ckeys.ensure((size_t)cap * (4 * nk + 8 * nslots) + 8));
-    if (launch_compact_ordered(table, nslots, G, P->key_stride.data(), P->key_card.data(), nk,
+    if (launch_compact_ordered(table, nslots, G, key_begin, P->key_stride.data(), P->key_card.data(), nk,
                                sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(), sc->ckeys.p, cap,
                                stream))
       return fail(PGPU_ERR_DEVICE, "compact launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1945,7 +1948,22 @@ int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_resu
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   auto R = std::make_unique<pgpu_result_s>();
-  TRY(plan_finalize_impl(P, s, d_table, R.get()));
+  TRY(plan_finalize_impl(P, s, d_table, 0, P->num_keys, R.get()));
+  *out = R.release();
+  return 0;
+}
+
+int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shard, int64_t key_begin,
+                             int64_t key_count, pgpu_result* out) {
+  if (!P || !out || !d_table_shard || key_begin < 0 || key_count < 0 || key_begin + key_count > P->num_keys)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (P->hash) return fail(PGPU_ERR_UNSUPPORTED, "hash-mode group tables are not key-range shardable");
+  if (P->limit_sensitive)
+    return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit below the key space: finalize the whole table");
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  auto R = std::make_unique<pgpu_result_s>();
+  TRY(plan_finalize_impl(P, s, d_table_shard, key_begin, key_count, R.get()));
   *out = R.release();
   return 0;
 }

@@ -368,6 +368,22 @@ class Plan:
         self.finalize_us = ((t1 - t0) * 1e6, (time.perf_counter() - t1) * 1e6)
         return res
 
+    def finalize_range(self, stream, d_shard, key_begin, key_count):
+        """Finalize of this rank's key-range shard of the merged dense table (combine.reduce_scatter_group_table):
+        the groups with keys in [key_begin, key_begin + key_count)."""
+        return _finalize_range(self, stream, d_shard, key_begin, key_count)
+
+
+def _finalize_range(plan, stream, d_shard, key_begin, key_count):
+    r = ctypes.c_void_p()
+    t0 = time.perf_counter()
+    L.check(plan.lib.pgpu_plan_finalize_range(plan.handle, ctypes.c_void_p(stream or 0), ctypes.c_void_p(d_shard),
+                                              key_begin, key_count, ctypes.byref(r)))
+    t1 = time.perf_counter()
+    res = _decode_result(plan.table, plan.query, _ResultHolder(plan.lib, r))
+    plan.finalize_us = ((t1 - t0) * 1e6, (time.perf_counter() - t1) * 1e6)
+    return res
+
 
 class _ResultHolder:
     """Owns a pgpu_result; numpy views of its pinned columns reference this object, so the C result lives until

@@ -369,3 +369,36 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs):
         assert np.all(np.diff(comp) > 0)
     finally:
         t.close()
+
+
+def test_finalize_key_range_shards(oracle, gpu_lib):
+    """pgpu_plan_finalize_range over the key-range shards a reduce-scatter leaves on each rank: the union of the
+    shards' groups is the whole table's result (the multi-GPU combine of large key spaces, combine.py)."""
+    import torch
+    from pinot_amd.combine import shard_range
+    rng = np.random.default_rng(7)
+    schema = [("a", "INT"), ("b", "INT"), ("m", "INT")]
+    n = 120_000
+    seg = oracle.make_segment(schema, {"a": rng.integers(0, 300, n), "b": rng.integers(0, 200, n),
+                                       "m": rng.integers(0, 1000, n)})
+    t, hs = gpu_table(schema, [seg])
+    try:
+        q = parse_query("SELECT COUNT(*), SUM(m) FROM t WHERE m < 900 GROUP BY a, b", num_groups_limit=10 ** 6)
+        stream = torch.cuda.current_stream().cuda_stream
+        with t.plan(hs, q) as plan:
+            nslots, nkeys, kinds = plan.layout()
+            d = torch.empty((nslots, nkeys), dtype=torch.int64, device="cuda")
+            plan.execute(stream, d.data_ptr())
+            full = plan.finalize(stream, d.data_ptr())
+            merged = {}
+            for r in range(3):
+                k0, kn, _ = shard_range(nkeys, 3, r)
+                shard = d[:, k0:k0 + kn].contiguous()
+                part = plan.finalize_range(stream, shard.data_ptr(), k0, kn)
+                assert not (set(part.as_dict()) & set(merged))
+                merged.update(part.as_dict())
+        assert merged == full.as_dict()
+        o = oracle.run_groupby(schema, [seg], q, combine=False, max_initial_capacity=10000)
+        assert_same(full, o, q, schema)
+    finally:
+        t.close()

@@ -18,7 +18,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from pinot_amd import _lib as L
-from pinot_amd.combine import allreduce_group_table, union_dictionaries
+from pinot_amd.combine import allreduce_group_table, reduce_scatter_group_table, shard_range, union_dictionaries
 from pinot_amd.query import parse_query
 
 SCHEMA = [("d", "INT"), ("f", "INT"), ("mi", "INT"), ("md", "DOUBLE")]
@@ -86,6 +86,9 @@ def _worker(rank, port, out_dir):
         union_dictionaries(table, ["d"])
         gdict = table.dictionary("d")
         dense = _dense_table(local.groups, gdict)
+        shard, k0, kn = reduce_scatter_group_table(dense.clone(), KINDS)
+        np.save(os.path.join(out_dir, "shard_%d.npy" % rank), shard.numpy())
+        np.save(os.path.join(out_dir, "range_%d.npy" % rank), np.array([k0, kn], dtype=np.int64))
         allreduce_group_table(dense, KINDS)
         np.save(os.path.join(out_dir, "merged_%d.npy" % rank), dense.numpy())
         np.save(os.path.join(out_dir, "dict_%d.npy" % rank), np.array(gdict, dtype=np.int64))
@@ -108,6 +111,15 @@ def test_two_rank_combine_matches_oracle(oracle, tmp_path):
     d0, d1 = np.load(tmp_path / "dict_0.npy"), np.load(tmp_path / "dict_1.npy")
     assert np.array_equal(d0, d1), "ranks disagree on the global key space"
     assert np.array_equal(m0, m1), "all-reduce left ranks with different tables"
+    # reduce-scatter (the large-table combine): rank r holds exactly its key range of the merged table
+    covered = 0
+    for r in range(WORLD):
+        shard, (k0, kn) = np.load(tmp_path / ("shard_%d.npy" % r)), np.load(tmp_path / ("range_%d.npy" % r))
+        assert (k0, kn) == shard_range(m0.shape[1], WORLD, r)[:2]
+        assert shard.shape == (m0.shape[0], kn)
+        assert np.array_equal(shard, m0[:, k0:k0 + kn]), r
+        covered += kn
+    assert covered == m0.shape[1]
     # oracle over the union of all segments (GroupByCombineOperator semantics)
     q = parse_query(SQL)
     segs = [oracle.make_segment(SCHEMA, _segment_columns(s)) for s in range(WORLD * SEGS_PER_RANK)]

@@ -1089,6 +1089,18 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   }
   r->in_filter = pool_scanned(&pool);
   r->post_filter = r->docs_scanned * nproj; /* AggregationGroupByOperator.java:94 */
+  if (g.nk == 0 && root->type == FN_ALL) {
+    /* Aggregation-only over a match-all filter (AggregationPlanNode.java:165-183): COUNT-only queries are answered
+     * from segment metadata (MetadataBasedAggregationOperator.java:89-92), MIN/MAX-only from the dictionaries
+     * (DictionaryBasedAggregationOperator.java:171-173) -- same values as the scan, statistics
+     * (numTotalDocs, 0, 0, numTotalDocs). */
+    int all_count = 1, all_minmax = 1;
+    for (int a = 0; a < q->num_aggs; a++) {
+      all_count &= q->aggs[a].fn == OR_AGG_COUNT;
+      all_minmax &= q->aggs[a].fn == OR_AGG_MIN || q->aggs[a].fn == OR_AGG_MAX;
+    }
+    if (all_count || all_minmax) r->post_filter = 0;
+  }
 
   /* Emit groups through getStringGroupKeys order: ARRAY ascending raw key; maps in id order (iteration order of
    * hash maps is not observable after the combine). */
@@ -1155,7 +1167,9 @@ static uint64_t hash_bytes(const uint8_t* p, int64_t n) {
 int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int nthreads, or_result* out,
                        char* msg, int msg_len) {
   memset(out, 0, sizeof *out);
-  if (q->num_group_by < 1 || q->num_group_by > 16) { snprintf(msg, msg_len, "need 1..16 group-by columns"); return -1; }
+  /* num_group_by == 0: aggregation-only (AggregationOperator / DefaultAggregationExecutor): one group with the empty
+   * key, emitted when a doc matched; the caller supplies the functions' defaults for an empty result. */
+  if (q->num_group_by < 0 || q->num_group_by > 16) { snprintf(msg, msg_len, "need 0..16 group-by columns"); return -1; }
   /* DictionaryBasedGroupKeyGenerator ctor: assert numGroupsLimit >= arrayBasedThreshold (:99) */
   if (q->num_groups_limit < q->max_initial_result_holder_capacity) {
     snprintf(msg, msg_len, "numGroupsLimit must be >= maxInitialResultHolderCapacity");

@@ -103,7 +103,7 @@ typedef struct {
   const or_predicate* predicates;
   int32_t num_filter_ops;        /* postfix program; 0 = no filter (MatchAll) */
   const or_filter_op* filter;
-  int32_t num_group_by;          /* 0 = aggregation-only is not on this path; must be >= 1 */
+  int32_t num_group_by;          /* 0 = aggregation-only (AggregationOperator): one group with the empty key */
   const int32_t* group_by;
   int32_t num_aggs;
   const or_agg* aggs;

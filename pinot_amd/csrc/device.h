@@ -258,6 +258,66 @@ __device__ __forceinline__ void accumulate(uint64_t* __restrict__ base, int64_t 
   }
 }
 
+// ---- single-row tables (aggregation-only queries, G == 1): every matched doc updates the same word, so each
+// lane folds its docs, the wave folds its lanes (xor butterfly) and one lane issues the atomic.  Requires the
+// whole wave to be converged at the call.
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+__device__ __forceinline__ double wave_sum_f64(double x) {
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
+  for (int off = 32; off > 0; off >>= 1) { const int64_t y = __shfl_xor(x, off); x = y < x ? y : x; }
+  return x;
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t x) {
+  for (int off = 32; off > 0; off >>= 1) { const int64_t y = __shfl_xor(x, off); x = y > x ? y : x; }
+  return x;
+}
+
+// Lane partials of one slot (cnt docs; isum / fsum sums; imin / imax extremes) -> one atomic on `word`.
+__device__ __forceinline__ void accumulate_wave(uint64_t* __restrict__ word, int kind, int64_t cnt, int64_t ival,
+                                                double fval) {
+  const bool leader = (threadIdx.x & 63) == 0;
+  const int64_t total = wave_sum_i64(cnt);
+  if (total == 0) return;  // wave-uniform
+  switch (kind) {
+    case SLOT_COUNT:
+      if (leader) atomicAdd(reinterpret_cast<unsigned long long*>(word), (unsigned long long)total);
+      break;
+    case SLOT_SUM_I64: {
+      const int64_t v = wave_sum_i64(ival);
+      if (leader) atomicAdd(reinterpret_cast<unsigned long long*>(word), (unsigned long long)v);
+      break;
+    }
+    case SLOT_SUM_F64: {
+      const double v = wave_sum_f64(fval);
+      if (leader) atomicAdd(reinterpret_cast<double*>(word), v);
+      break;
+    }
+    case SLOT_MIN_KEY: {
+      const int64_t v = wave_min_i64(ival);
+      if (leader) atomicMin(reinterpret_cast<long long*>(word), (long long)v);
+      break;
+    }
+    default: {
+      const int64_t v = wave_max_i64(ival);
+      if (leader) atomicMax(reinterpret_cast<long long*>(word), (long long)v);
+      break;
+    }
+  }
+}
+// Identity of a slot's lane partial.
+__device__ __forceinline__ int64_t slot_identity(int kind) {
+  return kind == SLOT_MIN_KEY ? INT64_MAX : kind == SLOT_MAX_KEY ? INT64_MIN : 0;
+}
+__device__ __forceinline__ int64_t slot_fold(int kind, int64_t a, int64_t v) {
+  return kind == SLOT_MIN_KEY ? (v < a ? v : a) : kind == SLOT_MAX_KEY ? (v > a ? v : a) : a + v;
+}
+
 // Aggregates NB docs per lane (doc b of segment S[b]) with their gathers interleaved: every dependent level
 // (segment record -> forward-index words -> dictId -> LUT / dictionary value) is issued for all NB docs before any
 // is consumed, so a batch pays each memory round trip once.  Docs with ok[b] == false read doc 0 of their segment
@@ -314,6 +374,15 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
         for (int b = 0; b < NB; ++b) ikey[b] = S[b].cols[col].dkey[id[b]];
       }
     }
+    if (G == 1) {  // single row: fold the lane's docs, then the wave
+      int64_t cnt = 0, iacc = slot_identity(kind);
+      double facc = 0.0;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (ok[b]) { ++cnt; iacc = slot_fold(kind, iacc, ikey[b]); facc += dval[b]; }
+      accumulate_wave(tbl + s, kind, cnt, iacc, facc);
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
       if (ok[b]) accumulate<MODE>(tbl, (int64_t)s * G + idx[b], kind, ikey[b], dval[b]);
@@ -365,7 +434,7 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
 template <int MODE, int H>
 __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
                                                uint64_t* __restrict__ tbl, int64_t G) {
-  const uint32_t m = mask >> H;
+  const uint32_t m = (mask >> H) & 0xFFFFu;
   uint32_t ids[16];
   int32_t key[16];
 #pragma unroll
@@ -386,9 +455,12 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     const int kind = p.slot_kind[s];
     if (kind == SLOT_COUNT) {
       uint64_t* __restrict__ row = tbl + (int64_t)s * G;
+      if (G == 1) accumulate_wave(row, SLOT_COUNT, __popc(m), 0, 0.0);
+      else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_COUNT, 0, 0.0);
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_COUNT, 0, 0.0);
+      }
       ++s;
       continue;
     }
@@ -411,6 +483,14 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
         const int kr = p.slot_kind[r];
         if (kr == SLOT_SUM_F64) continue;
         uint64_t* __restrict__ row = tbl + (int64_t)r * G;
+        if (G == 1) {
+          int64_t acc = slot_identity(kr);
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) acc = slot_fold(kr, acc, v[i]);
+          accumulate_wave(row, kr, __popc(m), acc, 0.0);
+          continue;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if ((m >> i) & 1u) accumulate<MODE>(row, key[i], kr, v[i], 0.0);
@@ -424,6 +504,14 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       for (int r = s; r < e; ++r) {
         if (p.slot_kind[r] != SLOT_SUM_F64) continue;
         uint64_t* __restrict__ row = tbl + (int64_t)r * G;
+        if (G == 1) {
+          double acc = 0.0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) acc += v[i];
+          accumulate_wave(row, SLOT_SUM_F64, __popc(m), 0, acc);
+          continue;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_SUM_F64, 0, v[i]);
@@ -439,8 +527,9 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
 template <int MODE>
 __device__ __forceinline__ void aggregate_group(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
                                                 uint64_t* __restrict__ tbl, int64_t G) {
-  if (mask & 0xFFFFu) aggregate_half<MODE, 0>(p, S, group, mask, tbl, G);
-  if (mask >> 16) aggregate_half<MODE, 16>(p, S, group, mask, tbl, G);
+  // wave-uniform conditions: the single-row (G == 1) fold inside uses cross-lane shuffles
+  if (__any((mask & 0xFFFFu) != 0u)) aggregate_half<MODE, 0>(p, S, group, mask, tbl, G);
+  if (__any((mask >> 16) != 0u)) aggregate_half<MODE, 16>(p, S, group, mask, tbl, G);
 }
 
 // Drains a wave's queue of matched (segment, doc) entries: 2 per lane per batch.

@@ -139,6 +139,23 @@ struct KStarParams {
   unsigned long long* stats;              // [0] docs matched, [1] entries scanned in filter
 };
 
+// ---------------------------------------------------------------------------------------------- partitioned
+// Parameters of the partitioned group-by of large dense key spaces (partition.h, k_partition.hip).
+struct KPartParams {
+  KParams base;                     // segments, filter program, key layout (num_keys_total = G), slots
+  int32_t pshift;                   // keys per partition = 1 << pshift (<= 65536: u16 record keys)
+  int32_t num_parts;
+  int32_t num_streams;              // 8-byte operand streams of a record
+  int32_t stream_col[kMaxSlots];    // query column slot of each stream
+  int32_t stream_f64[kMaxSlots];    // 1: the column's dval (double), 0: its dkey (int64 value / ordered key)
+  int32_t slot_stream[kMaxSlots];   // per slot: its operand stream (-1: COUNT)
+  uint32_t* part_start;             // [num_parts + 1]: K8a totals, scanned in place into run starts by K8b
+  uint32_t* block_off;              // [gridDim][num_parts]: a workgroup's offset inside each partition run
+  uint16_t* rec_key;                // [rec_cap]
+  uint64_t* rec_val;                // [num_streams][rec_cap]
+  int64_t rec_cap;
+};
+
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
@@ -161,6 +178,11 @@ int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num
                            const int64_t* key_stride, const int64_t* key_card, int32_t num_key_cols,
                            uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream);
+// Partitioned group-by (k_partition.hip): K8a count, scan, K8c scatter, K8d aggregate into p.base.table.
+int occupancy_part_pass(size_t lds_bytes);
+int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* stream);
+// In-place exclusive prefix sum of n u32 (one workgroup; n up to a few 10^4).
+int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);

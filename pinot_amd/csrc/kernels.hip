@@ -168,7 +168,7 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(uint32_t* __restrict
     if (threadIdx.x == 1023) carry = c + before + x;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *total = carry;
+  if (threadIdx.x == 0 && total) *total = carry;
 }
 
 // Output (columnar, stride cap): group-by dictIds gid[j] = (key / stride[j]) % card[j] as int32 rows [num_keys][cap],
@@ -384,6 +384,13 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(compact_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_slots,
                      num_keys, counter, out, out_cap);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream) {
+  if (n < 1) return 0;
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), data, n,
+                     static_cast<unsigned long long*>(nullptr));
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -12,6 +12,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -38,6 +41,10 @@ namespace {
 thread_local std::string g_err;
 
 // PGPU_TRACE=1: per-phase host timings on stderr (diagnostics only).
+bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '1';
+}
 bool trace_on() {
   static const bool on = getenv("PGPU_TRACE") && getenv("PGPU_TRACE")[0] == '1';
   return on;
@@ -166,6 +173,86 @@ struct ResultPool {
   }
 };
 
+// Host worker pool for per-query planning of long segment lists (the per-segment predicate translation that
+// Pinot runs on its query worker threads, one task per segment: BaseCombineOperator.java:85-115).  Workers are
+// started once and parked on a condition variable; run() executes fn(0..n-1) on the workers and the caller.
+class HostPool {
+ public:
+  explicit HostPool(int workers) {
+    for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& th : threads_) th.join();
+  }
+  int size() const { return (int)threads_.size(); }
+  void run(int n, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> serial(run_mu_);  // one batch at a time
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    int mine = 0;
+    for (int i; (i = next_.fetch_add(1)) < n;) { fn(i); ++mine; }
+    std::unique_lock<std::mutex> g(mu_);
+    done_ += mine;
+    done_cv_.wait(g, [&] { return done_ >= n_; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* fn;
+      int n;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        fn = fn_;
+        n = n_;
+      }
+      int mine = 0;
+      for (int i; (i = next_.fetch_add(1)) < n;) { (*fn)(i); ++mine; }
+      std::lock_guard<std::mutex> g(mu_);
+      done_ += mine;
+      if (done_ >= n_) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, done_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+HostPool& host_pool() {
+  static HostPool pool(std::max(1, std::min(7, (int)std::thread::hardware_concurrency() - 1)));
+  return pool;
+}
+// Segments per planning task.  Measured on MI355X hosts: translating the 1000 segments of C3 takes ~90 us on one
+// thread, and waking pool workers costs more than it saves below a few thousand segments, so lists shorter than
+// this are planned on the calling thread.  PGPU_PLAN_CHUNK_SEGS overrides it (tests).
+size_t plan_chunk_segs() {
+  const char* v = getenv("PGPU_PLAN_CHUNK_SEGS");
+  const long n = v ? atol(v) : 0;
+  return n > 0 ? (size_t)n : 4096;
+}
+
 // ================================================================================================ values
 inline uint32_t rd_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -192,6 +279,10 @@ inline double key_double(int64_t k) {
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
 constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr size_t kMaxScanLds = 128 * 1024;          // larger staging falls back to the direct-load kernel
+constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
+constexpr int64_t kPartLds = 64 * 1024;              // K8d accumulators per partition (LDS)
+constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
+constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
 
 bool is_int_type(int t) { return t == PGPU_INT || t == PGPU_LONG; }
 bool is_fp_type(int t) { return t == PGPU_FLOAT || t == PGPU_DOUBLE; }
@@ -296,6 +387,7 @@ struct Segment {
 
 struct Scratch {
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
+  DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
   HostPinned stage, starstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   void release() {
@@ -303,6 +395,7 @@ struct Scratch {
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
     starstage.release();
     starwork.release();
+    part_start.release(); block_off.release(); rec_key.release(); rec_val.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -544,12 +637,17 @@ struct pgpu_plan_s {
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
+  int64_t post_exempt_docs = 0;           // aggregation-only: docs of segments answered from metadata / dictionary
   int segments_matched_filter = 0;
   std::vector<uint8_t> seg_scanned;       // per plan segment: 1 = scanned (filter not folded to empty)
   int grid = 0;
   size_t lds_bytes = 0;
   bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
   bool dense = false;                     // direct kernel instance with whole-group decode (dense tiles)
+  bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
+  int part_shift = 0, num_parts = 0, part_grid = 0;
+  size_t part_lds = 0;
+  std::vector<int32_t> stream_col, stream_f64, slot_stream;
   double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
   int64_t sel_docs = 0;
   std::vector<int32_t> stage_slot;        // query column slot of each staged filter column
@@ -988,13 +1086,19 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
   const double t_start = trace_on() ? now_us() : 0;
   const int ncols = (int)t->names.size();
-  if (q->num_group_by < 1) return fail(PGPU_ERR_UNSUPPORTED, "aggregation without GROUP BY is not on this path");
+  // num_group_by == 0: aggregation-only (AggregationOperator, core/operator/query/AggregationOperator.java:58-95):
+  // one accumulator row (key space G = 1), reduced per wave before any atomic.
+  if (q->num_group_by < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "negative group-by count");
   if (q->num_group_by > kMaxKeys) return fail(PGPU_ERR_UNSUPPORTED, "more than %d group-by columns", kMaxKeys);
   if (q->num_predicates > kMaxLeaves) return fail(PGPU_ERR_UNSUPPORTED, "more than %d predicates", kMaxLeaves);
   if (q->num_filter_ops > kMaxOps) return fail(PGPU_ERR_UNSUPPORTED, "filter program longer than %d", kMaxOps);
   P->table = t;
+  double tr[8] = {0};
+  int ntr = 0;
+  auto mark = [&] { if (trace_on() && ntr < 8) tr[ntr++] = now_us(); };
   {
     std::lock_guard<std::mutex> g(t->mu);
+    P->segs.reserve(nsegs);
     for (int i = 0; i < nsegs; ++i) {
       auto it = t->segments.find(handles[i]);
       if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)handles[i]);
@@ -1143,85 +1247,151 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   P->seg_stride = (int)(sizeof(KSegHdr) + sizeof(KCol) * nqc + sizeof(KLeaf) * std::max(P->num_leaves, 0));
   P->seg_stride = (P->seg_stride + 15) & ~15;
   hipStream_t stream = t->stream;
-  std::vector<uint8_t> rec(P->seg_stride);
   P->segrec.reserve(P->segs.size() * (size_t)P->seg_stride);
-  std::vector<LeafHost> leaves(P->num_leaves);
-  std::vector<Tri> tri(P->num_leaves);
   std::vector<ParsedPred> parsed(P->num_leaves);
   for (int l = 0; l < P->num_leaves; ++l)
     TRY(parse_predicate(t->types[q->predicates[l].column], q->predicates[l], &parsed[l]));
-  std::vector<int> ids_scratch;
   std::vector<std::vector<int>> star_comps;
-  const bool star_allowed = !(q->options & PGPU_OPT_NO_STAR_TREE) && star_composites(P->ops, q, &star_comps);
-  int64_t tile_base = 0;
+  const bool star_allowed = q->num_group_by > 0 && !(q->options & PGPU_OPT_NO_STAR_TREE) &&
+                            star_composites(P->ops, q, &star_comps);
+  // Aggregation-only over a match-all segment: COUNT-only is answered from metadata, MIN/MAX-only from the
+  // dictionaries (AggregationPlanNode.java:165-183) -- same values, numEntriesScannedPostFilter 0
+  // (MetadataBasedAggregationOperator.java:89-92, DictionaryBasedAggregationOperator.java:171-173).
+  bool exempt_kind = false;
+  if (q->num_group_by == 0 && q->num_aggs > 0) {
+    bool all_count = true, all_minmax = true;
+    for (int i = 0; i < q->num_aggs; ++i) {
+      all_count &= q->aggs[i].fn == PGPU_AGG_COUNT;
+      all_minmax &= q->aggs[i].fn == PGPU_AGG_MIN || q->aggs[i].fn == PGPU_AGG_MAX;
+    }
+    exempt_kind = all_count || all_minmax;
+  }
   std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
+  bool any_star = false;
+  mark();
   for (Segment* s : P->segs) {
-    for (int l = 0; l < P->num_leaves; ++l) {
-      LeafHost& lh = leaves[l];
-      lh.kind = LEAF_NONE; lh.negate = 0; lh.lo = 0; lh.span = 0;
-      TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], parsed[l], &lh, ids_scratch));
-      tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
-    }
-    const Tri whole = P->num_leaves ? fold_program(P->ops, tri) : T_ALL;
-    P->seg_scanned.push_back(0);
-    if (whole == T_NONE || s->num_docs == 0) continue;  // EmptyFilterOperator: the segment is not scanned
-    P->seg_scanned.back() = 1;
-    P->segments_matched_filter++;
-    if (star_allowed && s->star) {
-      bool used = false;
-      TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
-      if (used) continue;
-    }
-    for (int l = 0; l < P->num_leaves; ++l)
-      if (tri[l] == T_VAR) P->scanned_entries_model += s->num_docs;
-    if (P->sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
-      std::vector<double> frac(P->num_leaves, 1.0);
-      for (int l = 0; l < P->num_leaves; ++l) {
-        const LeafHost& lh = leaves[l];
-        const double card = std::max(1, s->cols[q->predicates[l].column].card);
-        double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
-        if (lh.kind == LEAF_SET) {
-          int64_t ones = 0;
-          for (uint32_t w : lh.set) ones += __builtin_popcount(w);
-          f = ones / card;
-        }
-        frac[l] = lh.negate ? 1.0 - f : f;
-      }
-      P->sel_estimate = P->num_leaves ? estimate_selectivity(P->ops, frac) : 1.0;
-      P->sel_docs = s->num_docs;
-    }
+    any_star |= star_allowed && s->star != nullptr;
+    // device LUT / value arrays of the referenced columns (built once per segment, rebuilt when the global
+    // dictionary grows); done up front so the per-segment translation below only reads segment state
     for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
     for (size_t k = 1; k < P->slot_kind.size(); ++k) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
-    std::fill(rec.begin(), rec.end(), 0);
-    KSegHdr* h = reinterpret_cast<KSegHdr*>(rec.data());
-    h->num_docs = s->num_docs;
-    h->tile_base = (int32_t)tile_base;
-    h->num_tiles = (int32_t)((s->num_docs + kTileDocs - 1) / kTileDocs);
-    KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
-    for (int j = 0; j < nqc; ++j) {
-      const Column& c = s->cols[P->query_cols[j]];
-      kc[j].fwd = c.d_fwd;
-      kc[j].lut = c.d_lut;
-      kc[j].dkey = c.d_key;
-      kc[j].dval = c.d_val;
-      kc[j].bits = c.bits;
-    }
-    KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
-    const int64_t rec_off = (int64_t)P->segrec.size();
-    for (int l = 0; l < P->num_leaves; ++l) {
-      kl[l].kind = leaves[l].kind;
-      kl[l].negate = leaves[l].negate;
-      kl[l].lo = leaves[l].lo;
-      kl[l].span = leaves[l].span;
-      kl[l].set = nullptr;
-      if (leaves[l].kind == LEAF_SET) {
-        const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[l].set - rec.data());
-        P->set_fix.emplace_back(field, (int64_t)P->set_words.size());
-        P->set_words.insert(P->set_words.end(), leaves[l].set.begin(), leaves[l].set.end());
+  }
+  // Per-segment translation (PredicateEvaluatorProvider + FilterPlanNode per segment) in contiguous chunks,
+  // on the host worker pool for large segment lists; records carry chunk-relative tile / set offsets, fixed up
+  // when the chunks are concatenated in segment order.
+  struct Chunk {
+    std::vector<uint8_t> rec;
+    std::vector<uint32_t> set_words;
+    std::vector<std::pair<int64_t, int64_t>> set_fix;
+    std::vector<uint8_t> scanned;
+    int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
+    double sel = 1.0;
+    int rc = 0;
+    std::string err;
+  };
+  auto plan_range = [&](size_t b, size_t e, Chunk& C) -> int {
+    std::vector<LeafHost> leaves(P->num_leaves);
+    std::vector<Tri> tri(P->num_leaves);
+    std::vector<int> ids_scratch;
+    std::vector<uint8_t> rec(P->seg_stride);
+    for (size_t i = b; i < e; ++i) {
+      Segment* s = P->segs[i];
+      for (int l = 0; l < P->num_leaves; ++l) {
+        LeafHost& lh = leaves[l];
+        lh.kind = LEAF_NONE; lh.negate = 0; lh.lo = 0; lh.span = 0;
+        TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], parsed[l], &lh, ids_scratch));
+        tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
       }
+      const Tri whole = P->num_leaves ? fold_program(P->ops, tri) : T_ALL;
+      C.scanned.push_back(0);
+      if (whole == T_NONE || s->num_docs == 0) continue;  // EmptyFilterOperator: the segment is not scanned
+      C.scanned.back() = 1;
+      C.matched++;
+      if (exempt_kind && whole == T_ALL) C.exempt += s->num_docs;
+      if (star_allowed && s->star) {  // only on the sequential path (any_star)
+        bool used = false;
+        TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
+        if (used) continue;
+      }
+      for (int l = 0; l < P->num_leaves; ++l)
+        if (tri[l] == T_VAR) C.entries += s->num_docs;
+      if (C.sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
+        std::vector<double> frac(P->num_leaves, 1.0);
+        for (int l = 0; l < P->num_leaves; ++l) {
+          const LeafHost& lh = leaves[l];
+          const double card = std::max(1, s->cols[q->predicates[l].column].card);
+          double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
+          if (lh.kind == LEAF_SET) {
+            int64_t ones = 0;
+            for (uint32_t w : lh.set) ones += __builtin_popcount(w);
+            f = ones / card;
+          }
+          frac[l] = lh.negate ? 1.0 - f : f;
+        }
+        C.sel = P->num_leaves ? estimate_selectivity(P->ops, frac) : 1.0;
+        C.sel_docs = s->num_docs;
+      }
+      std::fill(rec.begin(), rec.end(), 0);
+      KSegHdr* h = reinterpret_cast<KSegHdr*>(rec.data());
+      h->num_docs = s->num_docs;
+      h->tile_base = (int32_t)C.tiles;  // chunk-relative
+      h->num_tiles = (int32_t)((s->num_docs + kTileDocs - 1) / kTileDocs);
+      KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
+      for (int j = 0; j < nqc; ++j) {
+        const Column& c = s->cols[P->query_cols[j]];
+        kc[j].fwd = c.d_fwd;
+        kc[j].lut = c.d_lut;
+        kc[j].dkey = c.d_key;
+        kc[j].dval = c.d_val;
+        kc[j].bits = c.bits;
+      }
+      KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
+      const int64_t rec_off = (int64_t)C.rec.size();
+      for (int l = 0; l < P->num_leaves; ++l) {
+        kl[l].kind = leaves[l].kind;
+        kl[l].negate = leaves[l].negate;
+        kl[l].lo = leaves[l].lo;
+        kl[l].span = leaves[l].span;
+        kl[l].set = nullptr;
+        if (leaves[l].kind == LEAF_SET) {
+          const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[l].set - rec.data());
+          C.set_fix.emplace_back(field, (int64_t)C.set_words.size());
+          C.set_words.insert(C.set_words.end(), leaves[l].set.begin(), leaves[l].set.end());
+        }
+      }
+      C.rec.insert(C.rec.end(), rec.begin(), rec.end());
+      C.tiles += h->num_tiles;
     }
-    P->segrec.insert(P->segrec.end(), rec.begin(), rec.end());
-    tile_base += h->num_tiles;
+    return 0;
+  };
+  const size_t nseg = P->segs.size();
+  const int nchunks = any_star ? 1 : (int)std::min<size_t>(host_pool().size() + 1, (nseg + plan_chunk_segs() - 1) / plan_chunk_segs());
+  std::vector<Chunk> chunks(std::max(nchunks, 1));
+  auto run_chunk = [&](int c) {
+    Chunk& C = chunks[c];
+    C.rec.reserve((nseg / chunks.size() + 1) * (size_t)P->seg_stride);
+    C.rc = plan_range(nseg * c / chunks.size(), nseg * (c + 1) / chunks.size(), C);
+    if (C.rc) C.err = g_err;
+  };
+  mark();
+  if (chunks.size() == 1) run_chunk(0);
+  else host_pool().run((int)chunks.size(), run_chunk);
+  mark();
+  int64_t tile_base = 0;
+  for (Chunk& C : chunks) {
+    if (C.rc) return fail(C.rc, "%s", C.err.c_str());
+    const int64_t rec0 = (int64_t)P->segrec.size(), set0 = (int64_t)P->set_words.size();
+    for (size_t r = 0; r < C.rec.size(); r += P->seg_stride)
+      reinterpret_cast<KSegHdr*>(C.rec.data() + r)->tile_base += (int32_t)tile_base;
+    for (auto& f : C.set_fix) P->set_fix.emplace_back(rec0 + f.first, set0 + f.second);
+    P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
+    P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
+    P->seg_scanned.insert(P->seg_scanned.end(), C.scanned.begin(), C.scanned.end());
+    P->segments_matched_filter += C.matched;
+    P->scanned_entries_model += C.entries;
+    P->post_exempt_docs += C.exempt;
+    if (P->sel_docs == 0 && C.sel_docs) { P->sel_estimate = C.sel; P->sel_docs = C.sel_docs; }
+    tile_base += C.tiles;
   }
   P->num_tiles = tile_base;
   if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
@@ -1248,6 +1418,36 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
   }
   if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
+  // Large dense tables: partitioned group-by (partition.h) instead of random global atomics.
+  if (P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes && P->star.empty() && tile_base > 0 &&
+      P->total_docs < (int64_t)UINT32_MAX && !getenv_flag("PGPU_NO_PARTITION")) {
+    int shift = 16;
+    while (shift > 8 && ((int64_t)nslots << shift) * 8 > kPartLds) --shift;
+    const int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
+    std::vector<int32_t> scol, sf64, sstream(nslots, -1);
+    for (int sl = 1; sl < nslots; ++sl) {
+      const int f64 = P->slot_kind[sl] == SLOT_SUM_F64 ? 1 : 0;
+      int k = -1;
+      for (size_t j = 0; j < scol.size(); ++j)
+        if (scol[j] == P->slot_col[sl] && sf64[j] == f64) k = (int)j;
+      if (k < 0) { scol.push_back(P->slot_col[sl]); sf64.push_back(f64); k = (int)scol.size() - 1; }
+      sstream[sl] = k;
+    }
+    const int64_t rec_bytes = P->total_docs * (2 + 8 * (int64_t)scol.size());
+    const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
+    if (parts <= kMaxParts && rec_bytes <= kPartMaxRecordBytes && pass_lds <= 96 * 1024) {
+      P->partitioned = true;
+      P->part_shift = shift;
+      P->num_parts = (int)parts;
+      P->stream_col = scol;
+      P->stream_f64 = sf64;
+      P->slot_stream = sstream;
+      P->part_lds = pass_lds;
+      int per_cu = occupancy_part_pass(pass_lds);
+      per_cu = std::max(1, std::min(per_cu, 4));
+      P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+    }
+  }
   // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
   for (int l = 0; l < P->num_leaves; ++l) {
     int sidx = -1;
@@ -1280,7 +1480,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
     }
   }
-  if (trace_on()) fprintf(stderr, "[pgpu] plan_create: %.1f us (%zu segments)\n", now_us() - t_start, P->segs.size());
+  if (trace_on())
+    fprintf(stderr, "[pgpu] plan_create: %.1f us (%zu segments; setup %.1f, ensure %.1f, translate %.1f, rest %.1f)\n",
+            now_us() - t_start, P->segs.size(), tr[0] - t_start, tr[1] - tr[0], tr[2] - tr[1], now_us() - tr[2]);
   return 0;
 }
 
@@ -1349,7 +1551,8 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
       TRY(sc->hash_keys.ensure((size_t)P->num_keys * 8));
       kp.hash_keys = sc->hash_keys.as<unsigned long long>();
     }
-    if (launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, kp.hash_keys, stream))
+    if (!P->partitioned &&  // the partitioned path stores every table word itself
+        launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, kp.hash_keys, stream))
       return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
     kp.table = table;
   }
@@ -1363,7 +1566,28 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   kp.stage_words = (int32_t)P->stage_words;
   kp.lds_table_words = P->lds_table_words;
   HIP_TRY(hipEventRecord(sc->ev[1], stream));
-  if (P->num_tiles > 0) {
+  if (P->num_tiles > 0 && P->partitioned) {
+    KPartParams pp;
+    memset(&pp, 0, sizeof pp);
+    pp.base = kp;
+    pp.pshift = P->part_shift;
+    pp.num_parts = P->num_parts;
+    pp.num_streams = (int)P->stream_col.size();
+    for (size_t j = 0; j < P->stream_col.size(); ++j) { pp.stream_col[j] = P->stream_col[j]; pp.stream_f64[j] = P->stream_f64[j]; }
+    for (int sl = 0; sl < nslots; ++sl) pp.slot_stream[sl] = P->slot_stream[sl];
+    const int64_t cap = std::max<int64_t>(P->total_docs, 1);
+    TRY(sc->part_start.ensure((size_t)(P->num_parts + 1) * 4));
+    TRY(sc->block_off.ensure((size_t)P->part_grid * P->num_parts * 4));
+    TRY(sc->rec_key.ensure((size_t)cap * 2));
+    TRY(sc->rec_val.ensure(std::max<size_t>((size_t)cap * 8 * pp.num_streams, 8)));
+    pp.part_start = sc->part_start.as<uint32_t>();
+    pp.block_off = sc->block_off.as<uint32_t>();
+    pp.rec_key = sc->rec_key.as<uint16_t>();
+    pp.rec_val = sc->rec_val.as<uint64_t>();
+    pp.rec_cap = cap;
+    if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
+      return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
+  } else if (P->num_tiles > 0) {
     const int rc = P->staged ? launch_scan(kp, P->mode, P->grid, P->lds_bytes, stream)
                              : launch_filter_groupby(kp, P->mode, P->dense, P->grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1553,7 +1777,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   }
   R->stats[0] = (int64_t)matched;
   R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned;
-  R->stats[2] = (int64_t)matched * P->num_projected;
+  R->stats[2] = ((int64_t)matched - P->post_exempt_docs) * P->num_projected;
   R->stats[3] = P->total_docs;
   R->stats[4] = (int64_t)P->segs.size();
   R->stats[5] = P->segments_matched_filter;

@@ -106,6 +106,29 @@ class GroupByResult:
         return self._n
 
 
+def aggregation_defaults(aggregations):
+    """Results of aggregation functions over no documents: their result holders' initial values
+    (SumAggregationFunction.java:33 0.0, MinAggregationFunction.java:33 +inf, MaxAggregationFunction.java:33 -inf,
+    CountAggregationFunction.java:38 0, AvgAggregationFunction: AvgPair(0.0, 0))."""
+    out = []
+    for fn, _ in aggregations:
+        out.append({"COUNT": 0, "SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}.get(fn, None)
+                   if fn != "AVG" else AvgPair(0.0, 0))
+    return out
+
+
+class AggregationResult:
+    """Aggregation-only result (AggregationOperator / AggregationOnlyCombineOperator): one value per function in
+    query order, and ExecutionStatistics."""
+
+    def __init__(self, values, stats):
+        self.values = values
+        self.stats = stats
+
+    def __repr__(self):
+        return "AggregationResult(%r, %r)" % (self.values, self.stats)
+
+
 def _key_str(x):
     if isinstance(x, float):
         return repr(x)
@@ -291,6 +314,14 @@ class GpuTable:
         return out
 
     # ------------------------------------------------------------------ queries
+    def execute_aggregation(self, handles, query, stream=None):
+        """Aggregation-only query (no GROUP BY) over the segments: AggregationOperator per segment +
+        AggregationOnlyCombineOperator (core/operator/query/AggregationOperator.java:58-95)."""
+        assert not query.group_by, "execute_aggregation takes a query without GROUP BY"
+        r = self.execute_groupby(handles, query, stream)
+        vals = r.values[0] if len(r) else aggregation_defaults(query.aggregations)
+        return AggregationResult(list(vals), r.stats)
+
     def plan(self, handles, query):
         return Plan(self, handles, query)
 

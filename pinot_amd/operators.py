@@ -6,6 +6,9 @@ names and result shapes as Pinot's own operators:
                                   (group keys + per-function results) and ExecutionStatistics.
   GpuGroupByCombineOperator       GroupByCombineOperator (core/operator/combine/GroupByCombineOperator.java:75-223):
                                   all segments of a server in one GPU pass, merged in the table-global key space.
+  GpuAggregationOperator          AggregationOperator (core/operator/query/AggregationOperator.java:58-95):
+                                  aggregation-only queries (no GROUP BY), one result per function.
+  GpuAggregationOnlyCombineOperator  AggregationOnlyCombineOperator: the same over all segments in one pass.
 Errors follow the reference: a bad literal raises BadQueryRequestException; a shape outside the GPU path raises
 UnsupportedQueryError (the Java shim keeps Pinot's CPU operator for it).
 """
@@ -25,6 +28,17 @@ class IntermediateResultsBlock:
 
     def get_group_by_result(self):
         return self._result
+
+
+class AggregationResultsBlock:
+    """IntermediateResultsBlock in its aggregation-only form (IntermediateResultsBlock.java:78-86)."""
+
+    def __init__(self, aggregation_functions, result):
+        self.aggregation_functions = aggregation_functions
+        self._result = result
+
+    def get_aggregation_result(self):
+        return self._result.values
 
 
 class _GpuOperatorBase:
@@ -53,3 +67,21 @@ class GpuAggregationGroupByOperator(_GpuOperatorBase):
 
 class GpuGroupByCombineOperator(_GpuOperatorBase):
     OPERATOR_NAME = "GroupByCombineOperator"
+
+
+class _GpuAggregationBase(_GpuOperatorBase):
+    def next_block(self):
+        result = self.table.execute_aggregation(self.segments, self.query)
+        self._stats = result.stats
+        return AggregationResultsBlock(self.query.aggregations, result)
+
+
+class GpuAggregationOperator(_GpuAggregationBase):
+    OPERATOR_NAME = "AggregationOperator"
+
+    def __init__(self, table, segment_handle, query):
+        super().__init__(table, [segment_handle], query)
+
+
+class GpuAggregationOnlyCombineOperator(_GpuAggregationBase):
+    OPERATOR_NAME = "AggregationOnlyCombineOperator"

@@ -45,3 +45,44 @@ def check_inner_values(vals, expected):
     assert int(mn) == expected[3]
     assert int(avg.sum) == expected[4]
     assert avg.count == expected[5]
+
+
+# InterSegmentAggregationSingleValueQueriesTest KATs (tests/golden/kat_inter_agg.json): SUM/COUNT/MIN/MAX/AVG over
+# 4 copies of the segment, aggregation-only and GROUP BY column9 (PQL: the top group per function).
+KAT_AGG = json.load(open(os.path.join(HERE, "golden", "kat_inter_agg.json")))
+
+
+def agg_case_query(case):
+    from pinot_amd.query import parse_query
+    q = parse_query(case["query"])
+    if case["filter"]:
+        q.filter = QueryContext.filter_from_json(KAT["query_filter"])
+    if case["group_by"]:
+        q.group_by = [KAT_AGG["group_by_column"]]
+    return q
+
+
+def pql_value(fn, v):
+    """Broker formatting of an aggregation result (PQL): COUNT as a long, everything else '%.5f'; AVG is final."""
+    if fn == "AVG":
+        v = v.final() if hasattr(v, "final") else v
+    return str(int(v)) if fn == "COUNT" else "%.5f" % float(v)
+
+
+def top_group_values(q, groups):
+    """AggregationGroupByTrimmingService order per function: MIN ascending, the others descending; the broker's
+    first row per function."""
+    out = []
+    for a, (fn, _) in enumerate(q.aggregations):
+        vals = [(g[a].final() if fn == "AVG" else g[a]) for g in groups]
+        out.append(min(vals) if fn == "MIN" else max(vals))
+    return out
+
+
+def check_agg_case(case, q, stats, values):
+    docs, in_filter, post, total = case["stats"]
+    assert (stats[0], stats[2], stats[3]) == (docs, post, total), (case["test"], case["variant"], stats)
+    if not case["filter"]:
+        assert stats[1] == in_filter
+    got = [pql_value(fn, v) for (fn, _), v in zip(q.aggregations, values)]
+    assert got == case["values"], (case["test"], case["variant"], got)

@@ -343,11 +343,15 @@ def test_num_groups_limit_not_reached_is_exact(oracle, sv):
     assert_same(r, o, q, K.SCHEMA)
 
 
+@pytest.mark.parametrize("partitioned", [True, False], ids=["partitioned", "atomics"])
 @pytest.mark.parametrize("docs", [1, 4097, 150_000])
-def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs):
+def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned, monkeypatch):
     """C5 shape (3-column composite key over a ~10^6 key space, INT_MAP holder in Pinot): the dense global table
-    and its ordered device compaction (count / scan / scatter) give the oracle's groups in ascending key order,
-    across chunk boundaries and with fewer docs than keys."""
+    -- built by the partitioned group-by (partition.h) or by global atomics -- and its ordered device compaction
+    (count / scan / scatter) give the oracle's groups in ascending key order, across chunk boundaries and with
+    fewer docs than keys."""
+    if not partitioned:
+        monkeypatch.setenv("PGPU_NO_PARTITION", "1")
     rng = np.random.default_rng(docs)
     schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE")]
     segs = []
@@ -362,6 +366,11 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs):
         q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
                         num_groups_limit=10 ** 7)
         r = t.execute_groupby(hs, q)
+        rf = t.execute_groupby(hs, parse_query("SELECT COUNT(*), SUM(m), MIN(m), MAX(x), SUM(x) FROM t WHERE m < 500 OR x > 0 "
+                                               "GROUP BY k1, k2, k3", num_groups_limit=10 ** 7))
+        qf = parse_query("SELECT COUNT(*), SUM(m), MIN(m), MAX(x), SUM(x) FROM t WHERE m < 500 OR x > 0 GROUP BY k1, k2, k3",
+                         num_groups_limit=10 ** 7)
+        assert_same(rf, oracle.run_groupby(schema, segs, qf, combine=False, max_initial_capacity=10000), qf, schema)
         o = oracle.run_groupby(schema, segs, q, combine=False, max_initial_capacity=10000)
         assert_same(r, o, q, schema)
         g = r.gids.astype(np.int64)  # key = d0 + d1*c0 + d2*c0*c1 (DictionaryBasedGroupKeyGenerator.java:276-323)
@@ -402,3 +411,93 @@ def test_finalize_key_range_shards(oracle, gpu_lib):
         assert_same(full, o, q, schema)
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("chunk", [0, 64], ids=["one_thread", "chunks_of_64"])
+def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, monkeypatch):
+    """Plans over hundreds of segments translate their predicates in parallel chunks (host worker pool); the
+    concatenated records (tile offsets, IN-set bitsets) must give the oracle's combined result, including
+    segments the filter prunes (EmptyFilterOperator) in the middle of a chunk."""
+    if chunk:
+        monkeypatch.setenv("PGPU_PLAN_CHUNK_SEGS", str(chunk))
+    rng = np.random.default_rng(11)
+    schema = [("g", "INT"), ("f", "INT"), ("v", "LONG")]
+    segs = []
+    for i in range(300):
+        n = int(rng.integers(1, 3000))
+        lo = 0 if i % 7 else 5000  # every 7th segment has no f value below 5000: pruned by the range leaf
+        segs.append(oracle.make_segment(schema, {"g": rng.integers(0, 40, n), "f": rng.integers(lo, lo + 200, n),
+                                                 "v": rng.integers(-10 ** 9, 10 ** 9, n)}))
+    t, hs = gpu_table(schema, segs)
+    try:
+        q = parse_query("SELECT COUNT(*), SUM(v), MIN(v) FROM t WHERE f < 150 AND g IN (1, 3, 5, 17, 39) GROUP BY g")
+        r = t.execute_groupby(hs, q)
+        o = oracle.run_groupby(schema, segs, q)
+        assert_same(r, o, q, schema)
+        assert r.stats.num_docs_scanned == o.stats[0]
+        assert r.stats.num_segments_matched == sum(1 for i in range(300) if i % 7)
+    finally:
+        t.close()
+
+
+# ------------------------------------------------------------------------------------------------ aggregation-only
+@pytest.mark.parametrize("case", K.KAT_AGG["cases"], ids=lambda c: "%s_%s" % (c["test"], c["variant"]))
+def test_kat_inter_segment_aggregation(sv, case):
+    """InterSegmentAggregationSingleValueQueriesTest SUM/COUNT/MIN/MAX/AVG (4 segments), aggregation-only and
+    GROUP BY column9, values and statistics, through the GPU path."""
+    seg, t, h = sv
+    q = K.agg_case_query(case)
+    if q.group_by:
+        r = t.execute_groupby([h] * 4, q)
+        values = K.top_group_values(q, r.values)
+    else:
+        r = t.execute_aggregation([h] * 4, q)
+        values = r.values
+    K.check_agg_case(case, q, r.stats.as_tuple(), values)
+
+
+@pytest.mark.parametrize("seed", list(range(6)))
+def test_random_aggregation_only_vs_oracle(oracle, gpu_lib, seed):
+    """Aggregation-only queries (single-row table, wave-folded accumulation) against the oracle, dense and sparse
+    filters, including filters that match nothing (the functions' defaults)."""
+    from pinot_amd.executor import aggregation_defaults
+    rng = np.random.default_rng(2000 + seed)
+    segs = [_random_segment(oracle, rng, SCHEMA_R, int(rng.integers(1, 60000))) for _ in range(int(rng.integers(1, 4)))]
+    t, hs = gpu_table(SCHEMA_R, segs)
+    try:
+        for qi in range(5):
+            aggs = [("COUNT", "*"), ("SUM", "a"), ("MIN", "d"), ("MAX", "c"), ("AVG", "f"), ("SUM", "d"), ("MIN", "b")]
+            flt = None if qi == 0 else _random_filter(rng, segs[0])
+            if qi == 4:
+                flt = FilterContext.and_(FilterContext.pred(Predicate.eq("a", "1")),
+                                         FilterContext.pred(Predicate.not_eq("a", "1")))
+            q = QueryContext([], aggs, flt)
+            r = t.execute_aggregation(hs, q)
+            o = oracle.run_groupby(SCHEMA_R, segs, q)
+            exp = o.groups[()] if o.groups else aggregation_defaults(aggs)
+            for (fn, col), x, y in zip(aggs, r.values, exp):
+                fp = col != "*" and dict(SCHEMA_R)[col] in ("FLOAT", "DOUBLE")
+                if fn == "AVG":
+                    assert x.count == y.count
+                    assert x.sum == pytest.approx(y.sum, rel=REL, abs=1e-6)
+                elif fp and fn == "SUM":
+                    assert x == pytest.approx(y, rel=REL, abs=1e-6)
+                else:
+                    assert x == y, (fn, col, x, y)
+            st = r.stats.as_tuple()
+            assert (st[0], st[2], st[3]) == (o.stats[0], o.stats[2], o.stats[3]), (r.stats, o.stats)
+    finally:
+        t.close()
+
+
+def test_aggregation_only_operators(sv):
+    """GpuAggregationOperator / GpuAggregationOnlyCombineOperator return Pinot's aggregation result list."""
+    from pinot_amd.operators import GpuAggregationOnlyCombineOperator, GpuAggregationOperator
+    seg, t, h = sv
+    op = GpuAggregationOperator(t, h, "SELECT COUNT(*), MAX(column3) FROM testTable")
+    blk = op.next_block()
+    assert blk.get_aggregation_result() == [30000, 2147419555.0]
+    assert op.get_execution_statistics().as_tuple() == (30000, 0, 30000, 30000)
+    comb = GpuAggregationOnlyCombineOperator(t, [h, h], "SELECT COUNT(*) FROM testTable")
+    assert comb.next_block().get_aggregation_result() == [60000]
+    assert comb.get_execution_statistics().as_tuple() == (60000, 0, 0, 60000)

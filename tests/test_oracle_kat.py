@@ -72,3 +72,32 @@ def test_num_groups_limit(oracle, sv_segment):
     assert r.limit_reached
     q = QueryContext(["column1"], [("COUNT", "*")])
     assert not oracle.run_groupby(K.SCHEMA, [sv_segment] * 4, q, combine=True).limit_reached
+
+
+@pytest.mark.parametrize("with_filter", [False, True], ids=["no_filter", "filter"])
+def test_aggregation_only_inner_segment(oracle, sv_segment, with_filter):
+    """InnerSegmentAggregationSingleValueQueriesTest.java:55-75: a true aggregation-only query (no GROUP BY):
+    one group with the empty key, AggregationOperator statistics."""
+    q = K.inner_query([], with_filter)
+    r = oracle.run_groupby(K.SCHEMA, [sv_segment], q, combine=False)
+    exp = K.KAT["inner_segment_aggregation_only"]["filter" if with_filter else "no_filter"]
+    assert list(r.groups) == [()]
+    K.check_inner_values(r.groups[()], exp["values"])
+    docs, in_filter, post, total = exp["stats"]
+    assert (r.stats[0], r.stats[2], r.stats[3]) == (docs, post, total)
+    if not with_filter:
+        assert r.stats[1] == in_filter
+
+
+@pytest.mark.parametrize("case", K.KAT_AGG["cases"], ids=lambda c: "%s_%s" % (c["test"], c["variant"]))
+def test_inter_segment_aggregation(oracle, sv_segment, case):
+    """InterSegmentAggregationSingleValueQueriesTest SUM/COUNT/MIN/MAX/AVG KATs (values and statistics; the
+    metadata / dictionary-based operators' zero post-filter entries included)."""
+    from pinot_amd.executor import aggregation_defaults
+    q = K.agg_case_query(case)
+    r = oracle.run_groupby(K.SCHEMA, [sv_segment] * 4, q, combine=True)
+    if q.group_by:
+        values = K.top_group_values(q, list(r.groups.values()))
+    else:
+        values = r.groups[()] if r.groups else aggregation_defaults(q.aggregations)
+    K.check_agg_case(case, q, r.stats, values)

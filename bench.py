@@ -45,6 +45,7 @@ def parse_args():
     p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
     p.add_argument("--host-profile", action="store_true", help="report host time per phase of a step")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE passes (roofline.traffic)")
+    p.add_argument("--no-star-tree", action="store_true", help="query option useStarTree=false (scan path)")
     return p.parse_args()
 
 
@@ -159,6 +160,34 @@ def pmc_traffic(args):
             "calib_bytes_alg": jc["roofline"]["bytes_alg_per_launch"], "calib_fetch_size_bytes": fc}
 
 
+def attach_star_trees(table, handles, workload, docs):
+    """Builds each segment's star-tree on the host (pgpu_startree_build: BaseSingleTreeBuilder restatement) from
+    the segment's Pinot bytes and pins it beside the segment (worker threads; the builder releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from pinot_amd import _lib as L
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    from pinot_amd.startree import StarTree
+    spec = workload.star_tree
+
+    def build(seg):
+        return StarTree.build(workload.schema, seg, spec["split_order"], spec["pairs"], spec["max_leaf_records"])
+
+    handles = list(handles)
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        for i in range(0, len(handles), 8):
+            segs = []
+            for h in handles[i:i + 8]:  # segment bytes back from HBM (the table's stream: one thread)
+                cols = {}
+                for name, typ in workload.schema:
+                    card, bits, d, f = table.segment_column_bytes(h, name)
+                    tcode = L.TYPE_NAMES[typ]
+                    cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
+                segs.append(SegmentBuffers(docs, cols))
+            for h, st in zip(handles[i:i + 8], ex.map(build, segs)):
+                table.attach_startree(h, st)
+                st.close()
+
+
 def cpu_baseline(table, handles, query, workload, docs, args):
     """The oracle (C restatement of Pinot's per-segment operator + combine, one task per segment) timed on the
     host cores over a bounded sample of the same segments (bytes pulled back from HBM)."""
@@ -232,6 +261,8 @@ def main():
     if args.sql:
         w.sql = args.sql
     q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+    if args.no_star_tree:
+        q.use_star_tree = False
     docs = args.docs_per_segment
     nseg = args.segments_per_gpu
     table = GpuTable(w.schema, device=device)
@@ -242,6 +273,10 @@ def main():
         handles.append(table.generate_segment(w.gen, row0=global_seg * docs, num_docs=docs))
     t_gen = time.perf_counter() - t_gen
     log("rank %d: %d segments generated in %.1f s" % (rank, nseg, t_gen))
+    if w.star_tree:
+        t_st = time.perf_counter()
+        attach_star_trees(table, handles, w, docs)
+        log("rank %d: star-trees built and pinned in %.1f s" % (rank, time.perf_counter() - t_st))
     if world > 1:
         union_dictionaries(table, q.group_by)
     handles = np.array(handles, dtype=np.int64)
@@ -317,7 +352,7 @@ def main():
 
     log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
-    if not args.no_bytes:
+    if not args.no_bytes and not w.star_tree:  # scan-path bytes model; star-tree plans: n/a
         bytes_alg, matched = compulsory_bytes(table, handles, q, docs)
         achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -328,7 +363,7 @@ def main():
             roofline["traffic"] = round(pmc["traffic"], 0)
             roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not w.star_tree:
         log("bytes_alg pass done; CPU baseline")
         cpu = cpu_baseline(table, handles, q, w, docs, args)
 

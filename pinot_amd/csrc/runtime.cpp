@@ -1219,7 +1219,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   if (overflow) return fail(PGPU_ERR_UNSUPPORTED, "group key space exceeds 64 bits (ARRAY_MAP holder)");
   const int nslots = (int)P->slot_kind.size();
   constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
-  constexpr int64_t kLdsBudget = 48 * 1024;
+  // LDS-privatised tables up to 112 KB (one workgroup per CU at the top end): measured on MI355X, an 80 KB table
+  // (C4: 5000 groups x 2 slots) runs 2.1x faster in LDS than with global atomics.  PGPU_LDS_BUDGET: A/B knob.
+  const char* lb = getenv("PGPU_LDS_BUDGET");
+  const int64_t kLdsBudget = lb && atol(lb) > 0 ? atol(lb) : 112 * 1024;
   // direct kernel LDS: [table (MODE_LDS)] [filter stack (general programs)] [per-wave match queues]
   const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * 2 * kWaveQ * 4;
   for (Segment* s : P->segs) P->total_docs += s->num_docs;

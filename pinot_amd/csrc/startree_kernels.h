@@ -134,45 +134,85 @@ __global__ __launch_bounds__(256) void startree_scan_kernel(const KStarParams p)
   const int64_t lo = (int64_t)chunk * T / p.chunks_per_seg, hi = (int64_t)(chunk + 1) * T / p.chunks_per_seg;
   unsigned long long matched = 0, scanned = 0;
   const int nrem = __popc(rem);
-  for (int64_t pos = lo + tid; pos < hi; pos += blockDim.x) {
-    int a = 0, b = nr - 1;  // last range with prefix <= pos
+  // Each lane walks positions lo + tid + k * 256 in batches of NB, every dependent level (range -> doc ->
+  // residual dictIds -> group keys / pre-aggregated values) issued for the whole batch before it is consumed.
+  // The range index only moves forward, so the binary search runs once per lane.
+  constexpr int NB = 4;
+  int a = 0;
+  {
+    int b = nr - 1;
+    const int64_t pos = lo + tid;
     while (a < b) {
       const int mid = (a + b + 1) >> 1;
       if (S.prefix[mid] <= pos) a = mid;
       else b = mid - 1;
     }
-    const int64_t doc = S.ranges[2 * a] + (pos - S.prefix[a]);
-    bool ok = true;
+  }
+  for (int64_t base = lo + tid; base < hi; base += (int64_t)NB * blockDim.x) {
+    int64_t doc[NB];
+    bool ok[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int64_t pos = base + (int64_t)k * blockDim.x;
+      ok[k] = pos < hi;
+      if (ok[k]) {
+        while (a + 1 < nr && S.prefix[a + 1] <= pos) ++a;
+        doc[k] = S.ranges[2 * a] + (pos - S.prefix[a]);
+      } else {
+        doc[k] = S.ranges[0];
+      }
+      scanned += ok[k] ? nrem : 0;
+    }
     for (int r = rem; r; r &= r - 1) {
       const int d = __ffs(r) - 1;
-      const uint32_t id = gather_id(S.dim_fwd[d], S.dim_bits[d], doc);
-      ok &= ((S.match[d][id >> 5] >> (id & 31)) & 1u) != 0;
+      uint32_t id[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) id[k] = gather_id(S.dim_fwd[d], S.dim_bits[d], doc[k]);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) ok[k] = ok[k] && ((S.match[d][id[k] >> 5] >> (id[k] & 31)) & 1u) != 0;
     }
-    scanned += nrem;
-    if (!ok) continue;
-    ++matched;
-    int64_t key = 0;
+    int64_t key[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) { key[k] = 0; matched += ok[k] ? 1 : 0; }
     for (int j = 0; j < p.num_keys; ++j) {
       const int d = S.key_dim[j];
-      key += (int64_t)S.key_lut[j][gather_id(S.dim_fwd[d], S.dim_bits[d], doc)] * p.key_stride[j];
+      uint32_t id[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) id[k] = gather_id(S.dim_fwd[d], S.dim_bits[d], doc[k]);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) key[k] += (int64_t)S.key_lut[j][id[k]] * p.key_stride[j];
     }
-    int64_t idx = key;
-    if (MODE == MODE_HASH) idx = hash_slot(p.hash_keys, G, (uint64_t)key);
+    int64_t idx[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      idx[k] = key[k];
+      if (MODE == MODE_HASH && ok[k]) idx[k] = hash_slot(p.hash_keys, G, (uint64_t)key[k]);
+    }
     for (int s = 0; s < p.num_slots; ++s) {
       const int kind = p.slot_kind[s];
-      int64_t ikey = 0;
-      double dval = 0.0;
       if (kind == SLOT_COUNT) {
         // COUNT adds the pre-aggregated count (1 per document when the tree has none)
-        const int64_t c = S.src_c[0] ? S.src_c[0][doc] : 1;
-        atomicAdd(reinterpret_cast<unsigned long long*>(tbl + (int64_t)s * G + idx), (unsigned long long)c);
+        int64_t c[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) c[k] = S.src_c[0] ? S.src_c[0][doc[k]] : 1;
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+          if (ok[k]) atomicAdd(reinterpret_cast<unsigned long long*>(tbl + (int64_t)s * G + idx[k]), (unsigned long long)c[k]);
         continue;
       }
-      const double v = S.src_f[s][doc];
-      if (kind == SLOT_SUM_F64) dval = v;
-      else if (kind == SLOT_SUM_I64) ikey = (int64_t)v;  // sums of integers are exact in double (< 2^53)
-      else ikey = p.slot_int[s] ? (int64_t)v : double_key_dev(v);
-      accumulate<MODE>(tbl, (int64_t)s * G + idx, kind, ikey, dval);
+      double v[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) v[k] = S.src_f[s][doc[k]];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        if (!ok[k]) continue;
+        int64_t ikey = 0;
+        double dval = 0.0;
+        if (kind == SLOT_SUM_F64) dval = v[k];
+        else if (kind == SLOT_SUM_I64) ikey = (int64_t)v[k];  // sums of integers are exact in double (< 2^53)
+        else ikey = p.slot_int[s] ? (int64_t)v[k] : double_key_dev(v[k]);
+        accumulate<MODE>(tbl, (int64_t)s * G + idx[k], kind, ikey, dval);
+      }
     }
   }
   for (int off = 32; off > 0; off >>= 1) {

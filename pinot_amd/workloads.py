@@ -33,7 +33,8 @@ def double_table(n, column_index, lo, hi):
 
 
 class Workload:
-    def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000, cpu_sample_segments=64):
+    def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000, cpu_sample_segments=64,
+                 star_tree=None):
         self.name = name
         self.schema = schema          # [(column, type)]
         self.gen = gen                # generator spec per column (table column order)
@@ -41,6 +42,7 @@ class Workload:
         self.description = description
         self.num_groups_limit = num_groups_limit  # query option numGroupsLimit of the config
         self.cpu_sample_segments = cpu_sample_segments  # bench CPU-baseline sample (~10-30 s of oracle work)
+        self.star_tree = star_tree    # None, or {split_order, pairs, max_leaf_records}: built per segment at setup
 
 
 def adanalytics():
@@ -95,4 +97,21 @@ def c5():
                     cpu_sample_segments=16)
 
 
-WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c5": c5}
+def c4():
+    """C4: star-tree query: per segment d1 U[0,100), d2 U[0,50), d3 U[0,20), d4 U[0,10),
+    m U[0,1000); star-tree split order [d1, d2, d3, d4], pairs SUM__m and COUNT__*, maxLeafRecords 10 000."""
+    schema = [("d1", "INT"), ("d2", "INT"), ("d3", "INT"), ("d4", "INT"), ("m", "INT")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 100},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 50},
+        {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 20},
+        {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 10},
+        {"kind": "UNIFORM", "column_index": 4, "lo": 0, "hi": 1000},
+    ]
+    sql = "SELECT SUM(m), COUNT(*) FROM t WHERE d3 IN (1, 5, 7) GROUP BY d1, d2"
+    star = {"split_order": ["d1", "d2", "d3", "d4"], "pairs": [("SUM", "m"), ("COUNT", "*")],
+            "max_leaf_records": 10_000}
+    return Workload("c4", schema, gen, sql, "C4 star-tree multi-dim GROUP BY", star_tree=star)
+
+
+WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c4": c4, "c5": c5}

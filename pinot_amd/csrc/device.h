@@ -137,8 +137,24 @@ __device__ __forceinline__ uint32_t leaf_eval_words(int kind, int negate, uint32
   return negate ? ~m : m;
 }
 
+// Docs [32*group, 32*group + 32) inside [lo, lo + span): bit i = doc 32*group + i.
+__device__ __forceinline__ uint32_t docrange_mask(int64_t group, uint32_t lo, uint32_t span) {
+  const int64_t doc0 = group << 5;
+  int64_t a = (int64_t)lo - doc0, b = (int64_t)lo + span - doc0;
+  a = a < 0 ? 0 : (a > 32 ? 32 : a);
+  b = b < 0 ? 0 : (b > 32 ? 32 : b);
+  if (b <= a) return 0u;
+  const uint32_t upto_b = b >= 32 ? ~0u : ((1u << b) - 1u);
+  const uint32_t below_a = a >= 32 ? ~0u : ((1u << a) - 1u);
+  return upto_b & ~below_a;
+}
+
 __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo, uint32_t span, const uint32_t* set,
                                               const uint32_t* fwd, int bits, int64_t group) {
+  if (kind == LEAF_DOCRANGE) {
+    const uint32_t m = docrange_mask(group, lo, span);
+    return negate ? ~m : m;
+  }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
 }
 

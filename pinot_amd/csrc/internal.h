@@ -32,13 +32,15 @@ constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of 
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
 constexpr int kDenseGroupMin = 256;         // matches per wave-tile (of 2048 docs) above which whole groups are decoded
 
-enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3 };
+// LEAF_DOCRANGE: a predicate on a sorted column (SortedIndexBasedFilterOperator, core/operator/filter/
+// SortedIndexBasedFilterOperator.java:51-125): docIds [lo, lo + span), evaluated without reading any column.
+enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
 enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
 enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };
 
 // One predicate leaf evaluated against one segment: dictId in [lo, lo + span) (RANGE), bit set in `set`
-// (SET), constant (ALL / NONE); `negate` flips the result (NOT_EQ / NOT_IN).
+// (SET), docId in [lo, lo + span) (DOCRANGE), constant (ALL / NONE); `negate` flips the result (NOT_EQ / NOT_IN).
 struct KLeaf {
   int32_t kind;
   int32_t negate;

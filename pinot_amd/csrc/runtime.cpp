@@ -346,6 +346,8 @@ struct Column {
   uint32_t* d_fwd = nullptr;        // inside the segment's allocation
   int64_t fwd_words = 0;            // padded words
   Dict dict;                        // parsed local dictionary
+  bool sorted = false;              // SortedIndexReaderImpl column: docIds of dictId i are [sorted_start[i], sorted_start[i+1])
+  std::vector<int32_t> sorted_start;
   std::vector<uint8_t> raw_dict;    // BIG_ENDIAN bytes as pinned (string padding semantics, column_bytes)
   // lazily built device arrays
   int32_t* d_lut = nullptr;
@@ -605,6 +607,7 @@ int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
 struct LeafHost {
   int32_t kind = LEAF_NONE, negate = 0;
   uint32_t lo = 0, span = 0;
+  uint32_t dict_lo = 0, dict_span = 0;  // LEAF_DOCRANGE: the dictId range it came from (star-tree matching)
   std::vector<uint32_t> set;  // bitset words for LEAF_SET
 };
 
@@ -816,8 +819,28 @@ int parse_predicate(int type, const pgpu_predicate& p, ParsedPred* out) {
 
 // Translates predicate `p` against one segment's column dictionary (dictionary-based PredicateEvaluators).
 // `ids` is caller-owned scratch.
+int translate_predicate_dict(const Column& c, const pgpu_predicate& p, const ParsedPred& pp, LeafHost* L,
+                             std::vector<int>& ids);
+
+// Dictionary-space translation, then on a sorted column a dictId range becomes the docId range of the
+// SortedIndexBasedFilterOperator (SortedIndexBasedFilterOperator.java:51-125; dictIds [lo, hi) own docs
+// [start(lo), start(hi)) of the SortedIndexReaderImpl pairs).
 int translate_predicate(const Column& c, const pgpu_predicate& p, const ParsedPred& pp, LeafHost* L,
                         std::vector<int>& ids) {
+  TRY(translate_predicate_dict(c, p, pp, L, ids));
+  if (c.sorted && L->kind == LEAF_RANGE) {
+    const int32_t d0 = c.sorted_start[L->lo], d1 = c.sorted_start[L->lo + L->span];
+    L->dict_lo = L->lo;
+    L->dict_span = L->span;
+    L->kind = LEAF_DOCRANGE;
+    L->lo = (uint32_t)d0;
+    L->span = (uint32_t)std::max(0, d1 - d0);
+  }
+  return 0;
+}
+
+int translate_predicate_dict(const Column& c, const pgpu_predicate& p, const ParsedPred& pp, LeafHost* L,
+                             std::vector<int>& ids) {
   const int32_t card = c.card;
   switch (p.type) {
     case PGPU_PRED_EQ: {  // EqualsPredicateEvaluatorFactory.java:86-99
@@ -982,9 +1005,10 @@ void leaf_bitset(const LeafHost& L, int32_t card, std::vector<uint32_t>& w) {
       case LEAF_ALL: m = true; break;
       case LEAF_NONE: m = false; break;
       case LEAF_RANGE: m = (uint32_t)i >= L.lo && (uint32_t)i < L.lo + L.span; break;
+      case LEAF_DOCRANGE: m = (uint32_t)i >= L.dict_lo && (uint32_t)i < L.dict_lo + L.dict_span; break;
       default: m = (L.set[i >> 5] >> (i & 31)) & 1u; break;
     }
-    if (L.kind == LEAF_RANGE || L.kind == LEAF_SET) m ^= L.negate != 0;
+    if (L.kind == LEAF_RANGE || L.kind == LEAF_SET || L.kind == LEAF_DOCRANGE) m ^= L.negate != 0;
     if (m) w[i >> 5] |= 1u << (i & 31);
   }
 }
@@ -1292,6 +1316,25 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     int rc = 0;
     std::string err;
   };
+  // Pure-AND programs evaluate their leaves in order with a wave-uniform early exit (AndDocIdIterator); leaves on
+  // columns sorted in every segment go first (FilterOperatorUtils orders index-based children first,
+  // FilterOperatorUtils.java:143-178) -- their docId-range masks cost no memory traffic and let whole waves skip
+  // the scan leaves' bytes.
+  std::vector<int> perm(P->num_leaves);
+  for (int l = 0; l < P->num_leaves; ++l) perm[l] = l;
+  if (P->pure_and && P->num_leaves > 1) {
+    std::vector<int> first, rest;
+    for (int l = 0; l < P->num_leaves; ++l) {
+      bool all_sorted = !P->segs.empty();
+      for (Segment* s : P->segs) all_sorted &= s->cols[q->predicates[l].column].sorted;
+      (all_sorted ? first : rest).push_back(l);
+    }
+    first.insert(first.end(), rest.begin(), rest.end());
+    perm = first;
+    std::vector<int32_t> slots(P->num_leaves);
+    for (int k = 0; k < P->num_leaves; ++k) slots[k] = P->leaf_slot[perm[k]];
+    P->leaf_slot = slots;
+  }
   auto plan_range = [&](size_t b, size_t e, Chunk& C) -> int {
     std::vector<LeafHost> leaves(P->num_leaves);
     std::vector<Tri> tri(P->num_leaves);
@@ -1316,14 +1359,15 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
         if (used) continue;
       }
-      for (int l = 0; l < P->num_leaves; ++l)
-        if (tri[l] == T_VAR) C.entries += s->num_docs;
+      for (int l = 0; l < P->num_leaves; ++l)  // sorted columns go through the sorted index: no entries scanned
+        if (tri[l] == T_VAR && !s->cols[q->predicates[l].column].sorted) C.entries += s->num_docs;
       if (C.sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
         std::vector<double> frac(P->num_leaves, 1.0);
         for (int l = 0; l < P->num_leaves; ++l) {
           const LeafHost& lh = leaves[l];
           const double card = std::max(1, s->cols[q->predicates[l].column].card);
           double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
+          if (lh.kind == LEAF_DOCRANGE) f = (double)lh.span / std::max(1, s->num_docs);
           if (lh.kind == LEAF_SET) {
             int64_t ones = 0;
             for (uint32_t w : lh.set) ones += __builtin_popcount(w);
@@ -1350,16 +1394,17 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       }
       KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
       const int64_t rec_off = (int64_t)C.rec.size();
-      for (int l = 0; l < P->num_leaves; ++l) {
-        kl[l].kind = leaves[l].kind;
-        kl[l].negate = leaves[l].negate;
-        kl[l].lo = leaves[l].lo;
-        kl[l].span = leaves[l].span;
-        kl[l].set = nullptr;
-        if (leaves[l].kind == LEAF_SET) {
-          const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[l].set - rec.data());
+      for (int k = 0; k < P->num_leaves; ++k) {
+        const LeafHost& lh = leaves[perm[k]];
+        kl[k].kind = lh.kind;
+        kl[k].negate = lh.negate;
+        kl[k].lo = lh.lo;
+        kl[k].span = lh.span;
+        kl[k].set = nullptr;
+        if (lh.kind == LEAF_SET) {
+          const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           C.set_fix.emplace_back(field, (int64_t)C.set_words.size());
-          C.set_words.insert(C.set_words.end(), leaves[l].set.begin(), leaves[l].set.end());
+          C.set_words.insert(C.set_words.end(), lh.set.begin(), lh.set.end());
         }
       }
       C.rec.insert(C.rec.end(), rec.begin(), rec.end());
@@ -1889,9 +1934,15 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
       col.fwd_bytes = ((int64_t)d->num_docs * col.bits + 7) / 8;
       std::vector<uint32_t>& w = sorted_expansion[c];
       w.assign(padded_fwd_words(d->num_docs, col.bits), 0u);
+      col.sorted = true;
+      col.sorted_start.assign((size_t)cb.cardinality + 1, d->num_docs);
+      int32_t prev_end = -1;
       for (int32_t id = 0; id < cb.cardinality; ++id) {
         const int32_t s = (int32_t)rd_be32(cb.fwd + (int64_t)id * 8), e = (int32_t)rd_be32(cb.fwd + (int64_t)id * 8 + 4);
         if (s < 0 || e >= d->num_docs || (e < s && e != s - 1)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad sorted pair");
+        if (s != prev_end + 1) return fail(PGPU_ERR_INVALID_ARGUMENT, "sorted pairs are not contiguous");
+        prev_end = e;
+        col.sorted_start[id] = s;
         for (int32_t doc = s; doc <= e; ++doc) {  // PinotDataBitSet.writeInt into BE words
           const uint64_t bit = (uint64_t)doc * col.bits;
           for (int b = 0; b < col.bits; ++b)
@@ -1901,6 +1952,8 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
             }
         }
       }
+      if (d->num_docs > 0 && prev_end != d->num_docs - 1)
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "sorted pairs do not cover every doc");
       for (auto& x : w) x = __builtin_bswap32(x);  // the device reads the forward index as big-endian bytes
     } else {
       return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad forward-index format", c);

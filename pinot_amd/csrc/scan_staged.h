@@ -87,7 +87,11 @@ __device__ __forceinline__ void issue_tile(const KParams& p, const StageRegs& R,
 }
 
 __device__ __forceinline__ uint32_t staged_leaf(const StageRegs& R, int sidx, const LeafRegs& L, const uint32_t* sbuf,
-                                                int tid) {
+                                                int tid, int64_t group) {
+  if (L.kind == LEAF_DOCRANGE) {
+    const uint32_t m = docrange_mask(group, L.lo, L.span);
+    return L.negate ? ~m : m;
+  }
   const int b = sidx == 0 ? R.b0 : sidx == 1 ? R.b1 : sidx == 2 ? R.b2 : R.b3;
   const int off = sidx == 0 ? 0 : sidx == 1 ? R.o1 : sidx == 2 ? R.o2 : R.o3;
   return leaf_eval_words(L.kind, L.negate, L.lo, L.span, L.set, sbuf + off + tid * b, b);
@@ -188,17 +192,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(const KParams p) {
       uint32_t mask = doc0 >= nd ? 0u : (nd - doc0 >= 32 ? ~0u : ((1u << (nd - doc0)) - 1u));
       if (p.num_ops > 0) {
         if (p.pure_and) {
-          if (nl > 0 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[0], L0, sbuf, tid);
-          if (nl > 1 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[1], L1, sbuf, tid);
-          if (nl > 2 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[2], L2, sbuf, tid);
-          if (nl > 3 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[3], L3, sbuf, tid);
+          if (nl > 0 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[0], L0, sbuf, tid, group);
+          if (nl > 1 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[1], L1, sbuf, tid, group);
+          if (nl > 2 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[2], L2, sbuf, tid, group);
+          if (nl > 3 && __any(mask != 0u)) mask &= staged_leaf(R, p.leaf_stage[3], L3, sbuf, tid, group);
         } else {
           int sp = 0;
           for (int k = 0; k < p.num_ops; ++k) {
             const int op = p.ops[k] >> 16, arg = p.ops[k] & 0xFFFF;
             if (op == OP_LEAF) {
               const LeafRegs Lk = load_leaf_regs(p, seg, arg);
-              stack[sp * kBlock + tid] = staged_leaf(R, p.leaf_stage[arg], Lk, sbuf, tid);
+              stack[sp * kBlock + tid] = staged_leaf(R, p.leaf_stage[arg], Lk, sbuf, tid, group);
               ++sp;
             } else if (op == OP_NOT) {
               stack[(sp - 1) * kBlock + tid] = ~stack[(sp - 1) * kBlock + tid];

@@ -501,3 +501,62 @@ def test_aggregation_only_operators(sv):
     comb = GpuAggregationOnlyCombineOperator(t, [h, h], "SELECT COUNT(*) FROM testTable")
     assert comb.next_block().get_aggregation_result() == [60000]
     assert comb.get_execution_statistics().as_tuple() == (60000, 0, 0, 60000)
+
+
+# ------------------------------------------------------------------------------------------------ sorted columns
+def _sorted_pair_segment(oracle, schema, cols, sorted_col):
+    """The oracle's fixed-bit segment and the same segment with `sorted_col` in SortedIndexReaderImpl pair format."""
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    seg = oracle.make_segment(schema, cols)
+    c = seg.columns[sorted_col]
+    n = seg.num_docs
+    ids = np.zeros(max(n, 1), dtype=np.int32)
+    buf = ctypes.create_string_buffer(bytes(c.fwd_bytes), max(len(c.fwd_bytes), 1))
+    oracle.lib().or_bitset_read_ints(buf, ctypes.c_int64(0), c.bits_per_element, n, ids.ctypes.data)
+    ids = ids[:n]
+    assert np.all(np.diff(ids) >= 0)
+    pairs = b""
+    for i in range(c.cardinality):
+        w = np.nonzero(ids == i)[0]
+        pairs += int(w[0]).to_bytes(4, "big") + int(w[-1]).to_bytes(4, "big")
+    out = dict(seg.columns)
+    out[sorted_col] = ColumnData(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.dict_bytes, pairs,
+                                 fwd_format=L.FWD_SORTED_PAIRS, is_sorted=True)
+    return seg, SegmentBuffers(n, out)
+
+
+SORTED_QUERIES = [
+    "SELECT COUNT(*), SUM(v) FROM t WHERE s = 40 GROUP BY g",
+    "SELECT COUNT(*), SUM(v), MIN(v) FROM t WHERE s BETWEEN 10 AND 70 AND v < 500 GROUP BY g",
+    "SELECT COUNT(*), MAX(v) FROM t WHERE v < 500 AND s <> 30 GROUP BY g",
+    "SELECT COUNT(*) FROM t WHERE s IN (10, 50, 90) OR v > 900 GROUP BY g",
+    "SELECT COUNT(*), SUM(v) FROM t WHERE NOT (s < 55) GROUP BY s",
+    "SELECT COUNT(*) FROM t WHERE s > 1000 GROUP BY g",
+    "SELECT COUNT(*), SUM(v) FROM t WHERE s IN (20, 30, 40) AND g < 5 GROUP BY s, g",
+]
+
+
+@pytest.mark.parametrize("n", [1, 777, 50_000])
+def test_sorted_column_docrange_leaves(oracle, gpu_lib, n):
+    """Predicates on sorted columns become docId ranges (SortedIndexBasedFilterOperator: no column read, no
+    entries scanned); results equal the oracle's scan over the same data; pure-AND programs evaluate them first."""
+    rng = np.random.default_rng(n)
+    schema = [("s", "INT"), ("v", "INT"), ("g", "INT")]
+    cols = {"s": np.sort(rng.integers(0, 100, n)), "v": rng.integers(0, 1000, n), "g": rng.integers(0, 10, n)}
+    seg, sseg = _sorted_pair_segment(oracle, schema, cols, "s")
+    t, hs = gpu_table(schema, [sseg, sseg])
+    try:
+        for sql in SORTED_QUERIES:
+            q = parse_query(sql)
+            r = t.execute_groupby(hs, q)
+            o = oracle.run_groupby(schema, [seg, seg], q)
+            assert_same(r, o, q, schema)
+            assert r.stats.num_docs_scanned == o.stats[0], sql
+        # the sorted leaf scans no entries; the v leaf scans every doc of both segments
+        r = t.execute_groupby(hs, parse_query(SORTED_QUERIES[1]))
+        if n > 1:
+            assert r.stats.num_entries_scanned_in_filter == 2 * n
+        bm = t.filter_bitmap(hs[0], parse_query(SORTED_QUERIES[2]), n)
+        np.testing.assert_array_equal(bm, oracle.filter_bitmap(schema, seg, parse_query(SORTED_QUERIES[2])))
+    finally:
+        t.close()

@@ -152,10 +152,20 @@ struct KPartParams {
   int32_t stream_f64[kMaxSlots];    // 1: the column's dval (double), 0: its dkey (int64 value / ordered key)
   int32_t slot_stream[kMaxSlots];   // per slot: its operand stream (-1: COUNT)
   uint32_t* part_start;             // [num_parts + 1]: K8a totals, scanned in place into run starts by K8b
-  uint32_t* block_off;              // [gridDim][num_parts]: a workgroup's offset inside each partition run
-  uint16_t* rec_key;                // [rec_cap]
+  uint32_t* block_off;              // [gridDim][num_coarse]: a workgroup's offset inside each coarse run
+  uint16_t* rec_key;                // [rec_cap] final layout: key within its partition
   uint64_t* rec_val;                // [num_streams][rec_cap]
   int64_t rec_cap;
+  // Two-level scatter (num_parts > 64): K8c writes runs of 2^cshift partitions ("coarse" partitions, few enough
+  // that every workgroup's open output lines stay in L2), K8e splits each coarse run into its partitions.
+  int32_t cshift;                   // 0: single level (K8c writes the final layout)
+  int32_t num_coarse;               // ceil(num_parts / 2^cshift)
+  int32_t chunks_per_coarse;        // K8e workgroups per coarse run
+  int32_t pad;
+  uint32_t* coarse_fill;            // [num_coarse] K8a reservation counters
+  uint32_t* fine_fill;              // [num_parts] K8e reservation counters
+  uint32_t* mid_key;                // [rec_cap] coarse layout: key within its coarse range
+  uint64_t* mid_val;                // [num_streams][rec_cap]
 };
 
 // Host-callable launchers (kernels.hip).

@@ -6,11 +6,17 @@
 // partition (a key range whose accumulators fit in LDS) is aggregated by one workgroup with LDS atomics and
 // written to the dense table with plain coalesced stores:
 //
-//   K8a part_count    : filter + key per matched doc; per-workgroup LDS histogram over partitions; each
-//                       workgroup reserves its run in every partition with one atomic per non-empty partition.
-//   K8b (scan)        : exclusive scan of the partition totals (compact_scan_kernel).
-//   K8c part_scatter  : the same docs again (same tile assignment); each record (key mod partition width as u16,
-//                       one 8-byte operand per value stream) goes to its partition run via an LDS cursor.
+//   K8a part_count    : filter + key per matched doc; per-workgroup LDS histogram over partitions; partition
+//                       totals by one atomic per non-empty partition; each workgroup reserves its run inside every
+//                       coarse partition (2^cshift consecutive partitions).
+//   K8b (scan)        : exclusive scan of the partition totals (compact_scan_kernel): the final layout, in which
+//                       a coarse partition is the contiguous run of its partitions.
+//   K8c part_scatter  : the same docs again (same tile assignment); each record (key within its coarse range,
+//                       one 8-byte operand per value stream) goes to its coarse run via an LDS cursor.  With <= 64
+//                       coarse runs, every workgroup's open output lines fit in L2 and fill before eviction (2442
+//                       single-level runs did not: partial-line write-backs made this pass 3 ms on C5).
+//   K8e part_split    : per coarse run (split over several workgroups): LDS histogram over its partitions,
+//                       reservation, and the records rewritten into the final layout (u16 key within partition).
 //   K8d part_aggregate: one workgroup per partition: LDS table, LDS atomics over its records, then the
 //                       partition's slice of every table row stored whole (no table init, no global atomics).
 //
@@ -55,20 +61,23 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   const KParams& p = pp.base;
   int32_t key[16];
   part_keys<H>(p, S, group, key);
+  const int cbits = pp.pshift + pp.cshift;  // key bits within a coarse partition
+  const bool two = pp.cshift > 0;
   uint32_t pos[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     pos[i] = 0;
     if ((m >> i) & 1u) {
-      pos[i] = atomicAdd(&cursor[key[i] >> pp.pshift], 1u);
-      pp.rec_key[pos[i]] = (uint16_t)(key[i] & ((1 << pp.pshift) - 1));
+      pos[i] = atomicAdd(&cursor[key[i] >> cbits], 1u);
+      if (two) pp.mid_key[pos[i]] = (uint32_t)(key[i] & ((1 << cbits) - 1));
+      else pp.rec_key[pos[i]] = (uint16_t)(key[i] & ((1 << pp.pshift) - 1));
     }
   }
   uint32_t ids[16];
   for (int s = 0; s < pp.num_streams; ++s) {
     const KCol& c = S.cols[pp.stream_col[s]];
     decode_group<H>(c.fwd, c.bits, group, ids);
-    uint64_t* __restrict__ out = pp.rec_val + (int64_t)s * pp.rec_cap;
+    uint64_t* __restrict__ out = (two ? pp.mid_val : pp.rec_val) + (int64_t)s * pp.rec_cap;
     if (pp.stream_f64[s]) {
       const double* __restrict__ dv = c.dval;
       double v[16];
@@ -107,8 +116,12 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   const int tid = threadIdx.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
   uint32_t* stack = hist + ((pp.num_parts + 3) & ~3);
-  for (int i = tid; i < pp.num_parts; i += kBlock)
-    hist[i] = SCATTER ? pp.part_start[i] + pp.block_off[(int64_t)blockIdx.x * pp.num_parts + i] : 0u;
+  if (SCATTER) {
+    for (int c = tid; c < pp.num_coarse; c += kBlock)
+      hist[c] = pp.part_start[c << pp.cshift] + pp.block_off[(int64_t)blockIdx.x * pp.num_coarse + c];
+  } else {
+    for (int i = tid; i < pp.num_parts; i += kBlock) hist[i] = 0u;
+  }
   __syncthreads();
   int64_t t0, t1;
   part_tiles(p.num_tiles, t0, t1);
@@ -145,10 +158,70 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
     for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
     if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
     __syncthreads();
-    // reserve this workgroup's run inside every partition it touches
-    for (int i = tid; i < pp.num_parts; i += kBlock) {
-      const uint32_t h = hist[i];
-      pp.block_off[(int64_t)blockIdx.x * pp.num_parts + i] = h ? atomicAdd(&pp.part_start[i], h) : 0u;
+    // partition totals, and this workgroup's run inside every coarse partition it touches
+    for (int i = tid; i < pp.num_parts; i += kBlock)
+      if (hist[i]) atomicAdd(&pp.part_start[i], hist[i]);
+    for (int c = tid; c < pp.num_coarse; c += kBlock) {
+      const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift);
+      uint32_t h = 0;
+      for (int i = p0; i < p1; ++i) h += hist[i];
+      pp.block_off[(int64_t)blockIdx.x * pp.num_coarse + c] = h ? atomicAdd(&pp.coarse_fill[c], h) : 0u;
+    }
+  }
+}
+
+// K8e: workgroup (coarse run c, chunk j) moves its share of run c into the final per-partition layout.
+// LDS: [2^cshift] counters / cursors.
+__global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
+  const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
+  const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
+  const uint32_t r0 = cs + (uint32_t)((uint64_t)(ce - cs) * j / pp.chunks_per_coarse);
+  const uint32_t r1 = cs + (uint32_t)((uint64_t)(ce - cs) * (j + 1) / pp.chunks_per_coarse);
+  for (int i = tid; i < np; i += kBlock) cnt[i] = 0u;
+  __syncthreads();
+  constexpr int NB = 8;  // records per lane per step: loads, then LDS atomics, then stores, each issued together
+  for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
+    uint32_t k[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t r = base + b * kBlock;
+      k[b] = r < r1 ? pp.mid_key[r] : ~0u;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (k[b] != ~0u) atomicAdd(&cnt[k[b] >> pp.pshift], 1u);
+  }
+  __syncthreads();
+  for (int i = tid; i < np; i += kBlock) {
+    const uint32_t h = cnt[i];
+    cnt[i] = h ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
+  }
+  __syncthreads();
+  const uint32_t low = (1u << pp.pshift) - 1u;
+  for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
+    uint32_t k[NB], pos[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t r = base + b * kBlock;
+      k[b] = r < r1 ? pp.mid_key[r] : ~0u;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) pos[b] = k[b] != ~0u ? atomicAdd(&cnt[k[b] >> pp.pshift], 1u) : 0u;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (k[b] != ~0u) pp.rec_key[pos[b]] = (uint16_t)(k[b] & low);
+    for (int s = 0; s < pp.num_streams; ++s) {
+      uint64_t v[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        v[b] = k[b] != ~0u ? pp.mid_val[(int64_t)s * pp.rec_cap + base + b * kBlock] : 0ull;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (k[b] != ~0u) pp.rec_val[(int64_t)s * pp.rec_cap + pos[b]] = v[b];
     }
   }
 }
@@ -163,13 +236,27 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   for (int i = tid; i < ns * PR; i += kBlock) lds[i] = slot_init(p.slot_kind[i / PR]);
   __syncthreads();
   const uint32_t r0 = pp.part_start[blockIdx.x], r1 = pp.part_start[blockIdx.x + 1];
-  for (uint32_t r = r0 + tid; r < r1; r += kBlock) {
-    const int k = pp.rec_key[r];
+  constexpr int NB = 4;  // records per lane per step, their loads issued together
+  for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
+    int k[NB];
+    bool ok[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t r = base + b * kBlock;
+      ok[b] = r < r1;
+      k[b] = ok[b] ? pp.rec_key[r] : 0;
+    }
     for (int s = 0; s < ns; ++s) {
       const int kind = p.slot_kind[s];
       const int st = pp.slot_stream[s];
-      const uint64_t w = st >= 0 ? pp.rec_val[(int64_t)st * pp.rec_cap + r] : 0ull;
-      accumulate<MODE_LDS>(lds + (int64_t)s * PR, k, kind, (int64_t)w, __longlong_as_double((long long)w));
+      uint64_t w[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        w[b] = (st >= 0 && ok[b]) ? pp.rec_val[(int64_t)st * pp.rec_cap + base + b * kBlock] : 0ull;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (ok[b])
+          accumulate<MODE_LDS>(lds + (int64_t)s * PR, k[b], kind, (int64_t)w[b], __longlong_as_double((long long)w[b]));
     }
   }
   __syncthreads();

@@ -390,6 +390,7 @@ struct Segment {
 struct Scratch {
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
+  DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   HostPinned stage, starstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   void release() {
@@ -398,6 +399,7 @@ struct Scratch {
     starstage.release();
     starwork.release();
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release();
+    coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -1625,7 +1627,22 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
     for (int sl = 0; sl < nslots; ++sl) pp.slot_stream[sl] = P->slot_stream[sl];
     const int64_t cap = std::max<int64_t>(P->total_docs, 1);
     TRY(sc->part_start.ensure((size_t)(P->num_parts + 1) * 4));
-    TRY(sc->block_off.ensure((size_t)P->part_grid * P->num_parts * 4));
+    int cshift = 0;
+    while ((P->num_parts + (1 << cshift) - 1) >> cshift > 64) ++cshift;
+    pp.cshift = cshift;
+    pp.num_coarse = (P->num_parts + (1 << cshift) - 1) >> cshift;
+    pp.chunks_per_coarse = std::max(1, 1024 / pp.num_coarse);
+    TRY(sc->block_off.ensure((size_t)P->part_grid * pp.num_coarse * 4));
+    TRY(sc->coarse_fill.ensure((size_t)pp.num_coarse * 4));
+    TRY(sc->fine_fill.ensure((size_t)P->num_parts * 4));
+    if (cshift > 0) {
+      TRY(sc->mid_key.ensure((size_t)cap * 4));
+      TRY(sc->mid_val.ensure(std::max<size_t>((size_t)cap * 8 * pp.num_streams, 8)));
+      pp.mid_key = sc->mid_key.as<uint32_t>();
+      pp.mid_val = sc->mid_val.as<uint64_t>();
+    }
+    pp.coarse_fill = sc->coarse_fill.as<uint32_t>();
+    pp.fine_fill = sc->fine_fill.as<uint32_t>();
     TRY(sc->rec_key.ensure((size_t)cap * 2));
     TRY(sc->rec_val.ensure(std::max<size_t>((size_t)cap * 8 * pp.num_streams, 8)));
     pp.part_start = sc->part_start.as<uint32_t>();

@@ -237,10 +237,17 @@ def main():
         pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # PGPU_BENCH_BACKEND=gloo: rehearsal of the multi-rank control flow on a box with fewer GPUs than ranks (ranks
+    # share devices, collectives staged through host memory); the measured configuration is RCCL, one GPU per rank.
+    backend = os.environ.get("PGPU_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local_rank = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     device = local_rank if world > 1 else 0
@@ -338,12 +345,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ngroups = len(first) if first is not None else 0
     if sharded:  # disjoint per-rank shards: the query's groups are their sum
-        g = torch.tensor([ngroups], dtype=torch.int64, device="cuda")
+        g = torch.tensor([ngroups], dtype=torch.int64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(g)
         ngroups = int(g.item())
     total_rows = float(nseg) * docs * world

@@ -26,9 +26,19 @@ _OPS = {
 }
 
 
+def _staged(group):
+    """gloo collectives on device tensors go through host copies (CPU tests use host tensors directly)."""
+    return dist.get_backend(group) == "gloo"
+
+
 def allreduce_group_table(table, slot_kinds, group=None):
     """In-place all-reduce of a [num_slots, num_keys] int64 tensor holding a plan's dense group table."""
     assert table.dtype == torch.int64 and table.dim() == 2 and table.shape[0] == len(slot_kinds)
+    if table.is_cuda and _staged(group):
+        host = table.cpu()
+        allreduce_group_table(host, slot_kinds, group)
+        table.copy_(host)
+        return table
     kinds = list(slot_kinds)
     s = 0
     while s < len(kinds):
@@ -56,6 +66,9 @@ def reduce_scatter_group_table(table, slot_kinds, group=None):
     """Reduce-scatter of a [num_slots, num_keys] int64 dense group table by key range.  Returns (shard, key_begin,
     key_count): shard is a contiguous [num_slots, key_count] tensor with this rank's merged keys."""
     assert table.dtype == torch.int64 and table.dim() == 2 and table.shape[0] == len(slot_kinds)
+    if table.is_cuda and _staged(group):
+        shard, begin, count = reduce_scatter_group_table(table.cpu(), slot_kinds, group)
+        return shard.to(table.device), begin, count
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     nslots, G = table.shape

@@ -301,10 +301,10 @@ def main():
 
     def step():
         c0 = time.perf_counter()
-        plan = table.plan(handles, q)
+        # plan + execute streamed: segment chunks are launched while the rest of the list is still planned
+        plan = table.plan_execute(handles, q, stream, d_table.data_ptr() if nkeys > 0 else None)
         c1 = time.perf_counter()
-        plan.execute(stream, d_table.data_ptr() if nkeys > 0 else None)
-        c2 = time.perf_counter()
+        c2 = c1
         if sharded:
             shard, k0, kn = reduce_scatter_group_table(d_table, kinds)
         elif world > 1:
@@ -315,7 +315,8 @@ def main():
         else:
             res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
         c4 = time.perf_counter()
-        k_us = plan.timing_us()[1]
+        tm = plan.timing_us()
+        k_us = (tm[1], max(int(tm[2]), 1))  # scan launches of this query: summed duration, count
         fc_us, dec_us = plan.finalize_us
         plan.close()
         c5 = time.perf_counter()
@@ -355,17 +356,20 @@ def main():
         ngroups = int(g.item())
     total_rows = float(nseg) * docs * world
     value = total_rows * args.steps / elapsed
-    kernel_avg_us = float(np.mean(kernel_us)) if kernel_us else 0.0
+    launches = kernel_us[0][1] if kernel_us else 1
+    kernel_avg_us = float(np.mean([k for k, _ in kernel_us])) / launches if kernel_us else 0.0  # per launch
 
     log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
     if not args.no_bytes and not w.star_tree:  # scan-path bytes model; star-tree plans: n/a
         bytes_alg, matched = compulsory_bytes(table, handles, q, docs)
+        bytes_alg /= launches  # equal chunks of statistically identical segments: per-launch share
         achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                     "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
-                    "matched_docs_per_gpu": int(matched)}
+                    "matched_docs_per_gpu": int(matched), "launches_per_query": launches,
+                    "kernel_us_per_query": round(kernel_avg_us * launches, 2)}
         if pmc:
             roofline["traffic"] = round(pmc["traffic"], 0)
             roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}

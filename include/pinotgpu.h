@@ -206,8 +206,15 @@ int pgpu_plan_finalize_range(pgpu_plan plan, void* stream, const void* d_table_s
 int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,
                          void* stream, pgpu_result* out);
 
-/* Timing of the last pgpu_plan_execute of this plan (HIP events on the execution stream), microseconds:
- * [0] whole execute, [1] the fused scan kernel, [2] number of fused-kernel launches. */
+/* Plan + execute in one call, streamed: the segment list is planned in equal chunks and each chunk's scan is
+ * launched as soon as it is planned, so the GPU scans while the host still translates predicates for the next
+ * chunk (one launch per chunk; plans with star-tree segments, partitioned or staged scans run as one launch).
+ * The plan is returned executed: finalize (or merge across GPUs, then finalize) as after pgpu_plan_execute. */
+int pgpu_plan_create_execute(pgpu_table table, const int64_t* segment_handles, int32_t num_segments,
+                             const pgpu_query* q, void* stream, void* d_table, pgpu_plan* out);
+
+/* Timing of the last execution of this plan (HIP events on the execution stream), microseconds:
+ * [0] whole execute, [1] the scan kernel launches (summed), [2] number of scan launches. */
 int pgpu_plan_timing(pgpu_plan plan, double* out3);
 
 /* Per plan segment (plan order): 1 if the segment is scanned, 0 if its filter folds to always-false against the

@@ -114,6 +114,8 @@ _PROTOS = {
     "pgpu_unpack_fixed_bit_device": (c_int, [c_voidp, c_i64, c_i32, c_i64, c_i64, c_voidp, c_voidp]),
     "pgpu_plan_create": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), ctypes.POINTER(c_voidp)]),
     "pgpu_plan_destroy": (c_int, [c_voidp]),
+    "pgpu_plan_create_execute": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp, c_voidp,
+                                         ctypes.POINTER(c_voidp)]),
     "pgpu_plan_layout": (c_int, [c_voidp, c_i32p, c_i64p, c_i32p]),
     "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
     "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),

@@ -247,6 +247,17 @@ HostPool& host_pool() {
 // Segments per planning task.  Measured on MI355X hosts: translating the 1000 segments of C3 takes ~90 us on one
 // thread, and waking pool workers costs more than it saves below a few thousand segments, so lists shorter than
 // this are planned on the calling thread.  PGPU_PLAN_CHUNK_SEGS overrides it (tests).
+// Launches of a streamed plan: equal chunks, so every launch of the scan kernel covers the same work (the
+// roofline's per-launch bytes and rocprof's average launch agree).  Measured on MI355X (C3, 1000 segments): four
+// streamed launches took 1.115 ms per query against 0.950 ms for one -- each launch boundary costs the scan's
+// ramp and tail (~33 us) plus the in-stream record upload, more than the ~130 us of planning it hides -- so plans
+// run as one launch unless PGPU_STREAM_CHUNKS asks for more (tests exercise the streamed path with it).
+int stream_chunk_count(size_t nseg) {
+  const char* v = getenv("PGPU_STREAM_CHUNKS");
+  if (v && atoi(v) > 0) return std::min<int>(atoi(v), (int)std::max<size_t>(nseg, 1));
+  return 1;
+}
+
 size_t plan_chunk_segs() {
   const char* v = getenv("PGPU_PLAN_CHUNK_SEGS");
   const long n = v ? atol(v) : 0;
@@ -393,7 +404,10 @@ struct Scratch {
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   HostPinned stage, starstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
   void release() {
+    for (auto& e : cev) if (e) hipEventDestroy(e);
+    cev.clear();
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
     starstage.release();
@@ -615,6 +629,19 @@ struct LeafHost {
 
 enum Tri { T_NONE = 0, T_ALL = 1, T_VAR = 2 };
 
+// One scan launch of a plan: a contiguous run of segment records (tile_base relative to tile_begin), the set_fix
+// entries and SET bitset words they own.
+struct LaunchChunk {
+  int64_t rec_begin = 0, num_recs = 0, tile_begin = 0, num_tiles = 0;
+  int64_t fix_begin = 0, fix_end = 0, set_begin = 0, set_end = 0;
+};
+
+// Streamed execution requested by pgpu_plan_create_execute.
+struct StreamExec {
+  hipStream_t stream = nullptr;
+  void* d_table = nullptr;
+};
+
 }  // namespace
 
 struct pgpu_plan_s {
@@ -650,6 +677,10 @@ struct pgpu_plan_s {
   bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
   bool dense = false;                     // direct kernel instance with whole-group decode (dense tiles)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
+  std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
+  int launches_done = 0;
+  int64_t set_words_bound = 0;            // streamed plans: upper bound of the SET bitset words
+  int64_t tile_bound = 0;                 // streamed plans: upper bound of the tiles
   int part_shift = 0, num_parts = 0, part_grid = 0;
   size_t part_lds = 0;
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
@@ -1108,7 +1139,22 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
   return 0;
 }
 
-int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P) {
+struct ExecCtx {
+  KParams kp;
+  uint64_t* table = nullptr;
+  int64_t words = 0;
+  int nslots = 0;
+  double t_start = 0;
+  int64_t slabs_used = 0;  // MODE_LDS: slabs written by the scan launches so far (launches pack them back to back)
+};
+
+int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X);
+int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C);
+int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
+int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
+
+int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P,
+                     const StreamExec* se = nullptr) {
   if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
   const double t_start = trace_on() ? now_us() : 0;
   const int ncols = (int)t->names.size();
@@ -1280,6 +1326,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   std::vector<ParsedPred> parsed(P->num_leaves);
   for (int l = 0; l < P->num_leaves; ++l)
     TRY(parse_predicate(t->types[q->predicates[l].column], q->predicates[l], &parsed[l]));
+  static const bool scan_on = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '1';  // staged A/B kernel
   std::vector<std::vector<int>> star_comps;
   const bool star_allowed = q->num_group_by > 0 && !(q->options & PGPU_OPT_NO_STAR_TREE) &&
                             star_composites(P->ops, q, &star_comps);
@@ -1414,7 +1461,163 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     return 0;
   };
+  // Launch configuration once the tiles are known (tile_base: their number, or an upper bound for streamed plans).
+  auto configure = [&](int64_t tile_base) -> int {
+    P->num_tiles = tile_base;
+    if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
+    P->star_segments = (int64_t)P->star.size();
+    if (!P->star.empty()) {
+      P->star_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, 1024 / (int64_t)P->star.size()));
+      P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
+    }
+    // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
+    P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16;
+    {
+      static std::mutex occ_mu;
+      static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU
+      int per_cu;
+      {
+        std::lock_guard<std::mutex> g(occ_mu);
+        const auto k = std::make_tuple(t->device, (int)P->mode, (int)P->dense, P->lds_bytes);
+        auto it = occ_cache.find(k);
+        if (it == occ_cache.end()) it = occ_cache.emplace(k, occupancy_filter_groupby(P->mode, P->dense, P->lds_bytes)).first;
+        per_cu = it->second;
+      }
+      if (per_cu <= 0) per_cu = 1;
+      per_cu = std::min(per_cu, 4);
+      P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+    }
+    if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
+    // Large dense tables: partitioned group-by (partition.h) instead of random global atomics.
+    if (P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes && P->star.empty() && tile_base > 0 &&
+        P->total_docs < (int64_t)UINT32_MAX && !getenv_flag("PGPU_NO_PARTITION")) {
+      int shift = 16;
+      while (shift > 8 && ((int64_t)nslots << shift) * 8 > kPartLds) --shift;
+      const int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
+      std::vector<int32_t> scol, sf64, sstream(nslots, -1);
+      for (int sl = 1; sl < nslots; ++sl) {
+        const int f64 = P->slot_kind[sl] == SLOT_SUM_F64 ? 1 : 0;
+        int k = -1;
+        for (size_t j = 0; j < scol.size(); ++j)
+          if (scol[j] == P->slot_col[sl] && sf64[j] == f64) k = (int)j;
+        if (k < 0) { scol.push_back(P->slot_col[sl]); sf64.push_back(f64); k = (int)scol.size() - 1; }
+        sstream[sl] = k;
+      }
+      const int64_t rec_bytes = P->total_docs * (2 + 8 * (int64_t)scol.size());
+      const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
+      if (parts <= kMaxParts && rec_bytes <= kPartMaxRecordBytes && pass_lds <= 96 * 1024) {
+        P->partitioned = true;
+        P->part_shift = shift;
+        P->num_parts = (int)parts;
+        P->stream_col = scol;
+        P->stream_f64 = sf64;
+        P->slot_stream = sstream;
+        P->part_lds = pass_lds;
+        int per_cu = occupancy_part_pass(pass_lds);
+        per_cu = std::max(1, std::min(per_cu, 4));
+        P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+      }
+    }
+    // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
+    for (int l = 0; l < P->num_leaves; ++l) {
+      int sidx = -1;
+      for (size_t k = 0; k < P->stage_slot.size(); ++k)
+        if (P->stage_slot[k] == P->leaf_slot[l]) sidx = (int)k;
+      if (sidx < 0) {
+        P->stage_slot.push_back(P->leaf_slot[l]);
+        sidx = (int)P->stage_slot.size() - 1;
+      }
+      P->leaf_stage.push_back(sidx);
+    }
+    // The LDS-DMA staged kernel is kept as an A/B alternative (PGPU_SCAN=1); the direct-load kernel measured faster
+    // on MI355X (profiles/r01_ab_scan*.log).
+    if ((int)P->stage_slot.size() <= kMaxStage && scan_on) {
+      const bool pure_and = P->pure_and && P->num_leaves <= 4;  // the staged fast path holds at most 4 leaves in registers
+      for (Segment* s : P->segs) {
+        int64_t bits = 0;
+        for (int slot : P->stage_slot) bits += s->cols[P->query_cols[slot]].bits;
+        P->stage_words = std::max<int64_t>(P->stage_words, bits * kBlock);
+      }
+      P->lds_table_words = P->mode == MODE_LDS ? (int)((nslots * G + 1) & ~int64_t(1)) : 0;
+      const size_t lds = (size_t)P->lds_table_words * 8 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + 16 +
+                         (size_t)kQueueCap * 8 + (size_t)P->stage_words * 2 * 4;
+      if (lds <= kMaxScanLds) {
+        P->staged = true;
+        P->pure_and = pure_and;
+        P->lds_bytes = lds;
+        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, kLdsPerCu / lds));
+        P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
+      }
+    }
+    return 0;
+  };
+  // Appends a planned chunk to the plan; tile_shift is added to its records' chunk-relative tile_base (0 keeps
+  // them relative, as a streamed launch of the chunk reads them).
+  auto merge_chunk = [&](Chunk& C, int64_t tile_shift) {
+    const int64_t rec0 = (int64_t)P->segrec.size(), set0 = (int64_t)P->set_words.size();
+    if (tile_shift)
+      for (size_t r = 0; r < C.rec.size(); r += P->seg_stride)
+        reinterpret_cast<KSegHdr*>(C.rec.data() + r)->tile_base += (int32_t)tile_shift;
+    for (auto& f : C.set_fix) P->set_fix.emplace_back(rec0 + f.first, set0 + f.second);
+    P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
+    P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
+    P->seg_scanned.insert(P->seg_scanned.end(), C.scanned.begin(), C.scanned.end());
+    P->segments_matched_filter += C.matched;
+    P->scanned_entries_model += C.entries;
+    P->post_exempt_docs += C.exempt;
+    if (P->sel_docs == 0 && C.sel_docs) { P->sel_estimate = C.sel; P->sel_docs = C.sel_docs; }
+  };
   const size_t nseg = P->segs.size();
+  // Streamed plan (pgpu_plan_create_execute): equal chunks of segments, each launched as soon as it is planned,
+  // so the GPU scans chunk c while the host translates chunk c + 1 (Pinot plans and runs each segment's
+  // operator on its own worker thread, BaseCombineOperator.java:85-115).
+  const bool part_eligible = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes &&
+                             !getenv_flag("PGPU_NO_PARTITION");
+  const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
+  if (se && !any_star && !scan_on && !part_eligible && stream_chunks > 1) {
+    for (Segment* s : P->segs) {
+      P->tile_bound += (s->num_docs + kTileDocs - 1) / kTileDocs;
+      for (int l = 0; l < P->num_leaves; ++l) {
+        const int ty = q->predicates[l].type;
+        if (ty == PGPU_PRED_IN || ty == PGPU_PRED_NOT_IN)
+          P->set_words_bound += ((int64_t)s->cols[q->predicates[l].column].card + 31) / 32;
+      }
+    }
+    if (!P->scratch) return fail(PGPU_ERR_INVALID_ARGUMENT, "streamed plan without scratch");
+    ExecCtx X;
+    int64_t tile_off = 0;
+    mark();
+    for (int c = 0; c < stream_chunks; ++c) {
+      Chunk C;
+      C.rec.reserve((nseg / stream_chunks + 1) * (size_t)P->seg_stride);
+      TRY(plan_range(nseg * c / stream_chunks, nseg * (c + 1) / stream_chunks, C));
+      LaunchChunk L;
+      L.rec_begin = (int64_t)(P->segrec.size() / P->seg_stride);
+      L.fix_begin = (int64_t)P->set_fix.size();
+      L.set_begin = (int64_t)P->set_words.size();
+      L.tile_begin = tile_off;
+      merge_chunk(C, 0);
+      L.num_recs = (int64_t)(P->segrec.size() / P->seg_stride) - L.rec_begin;
+      L.fix_end = (int64_t)P->set_fix.size();
+      L.set_end = (int64_t)P->set_words.size();
+      L.num_tiles = C.tiles;
+      tile_off += C.tiles;
+      P->chunks.push_back(L);
+      if (c == 0) {
+        TRY(configure(P->tile_bound));
+        TRY(exec_prologue(P, se->stream, se->d_table, stream_chunks, X));
+      }
+      TRY(exec_upload_chunk(P, se->stream, L));
+      TRY(exec_launch_chunk(P, se->stream, X, L, c));
+    }
+    mark();
+    P->num_tiles = tile_off;
+    TRY(exec_epilogue(P, se->stream, X));
+    if (trace_on())
+      fprintf(stderr, "[pgpu] plan_create (streamed, %d launches): %.1f us (%zu segments)\n", stream_chunks,
+              now_us() - t_start, P->segs.size());
+    return 0;
+  }
   const int nchunks = any_star ? 1 : (int)std::min<size_t>(host_pool().size() + 1, (nseg + plan_chunk_segs() - 1) / plan_chunk_segs());
   std::vector<Chunk> chunks(std::max(nchunks, 1));
   auto run_chunk = [&](int c) {
@@ -1430,151 +1633,53 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   int64_t tile_base = 0;
   for (Chunk& C : chunks) {
     if (C.rc) return fail(C.rc, "%s", C.err.c_str());
-    const int64_t rec0 = (int64_t)P->segrec.size(), set0 = (int64_t)P->set_words.size();
-    for (size_t r = 0; r < C.rec.size(); r += P->seg_stride)
-      reinterpret_cast<KSegHdr*>(C.rec.data() + r)->tile_base += (int32_t)tile_base;
-    for (auto& f : C.set_fix) P->set_fix.emplace_back(rec0 + f.first, set0 + f.second);
-    P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
-    P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
-    P->seg_scanned.insert(P->seg_scanned.end(), C.scanned.begin(), C.scanned.end());
-    P->segments_matched_filter += C.matched;
-    P->scanned_entries_model += C.entries;
-    P->post_exempt_docs += C.exempt;
-    if (P->sel_docs == 0 && C.sel_docs) { P->sel_estimate = C.sel; P->sel_docs = C.sel_docs; }
+    merge_chunk(C, tile_base);
     tile_base += C.tiles;
   }
-  P->num_tiles = tile_base;
-  if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
-  P->star_segments = (int64_t)P->star.size();
-  if (!P->star.empty()) {
-    P->star_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, 1024 / (int64_t)P->star.size()));
-    P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
-  }
-  // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
-  P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16;
-  {
-    static std::mutex occ_mu;
-    static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU
-    int per_cu;
-    {
-      std::lock_guard<std::mutex> g(occ_mu);
-      const auto k = std::make_tuple(t->device, (int)P->mode, (int)P->dense, P->lds_bytes);
-      auto it = occ_cache.find(k);
-      if (it == occ_cache.end()) it = occ_cache.emplace(k, occupancy_filter_groupby(P->mode, P->dense, P->lds_bytes)).first;
-      per_cu = it->second;
-    }
-    if (per_cu <= 0) per_cu = 1;
-    per_cu = std::min(per_cu, 4);
-    P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
-  }
-  if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
-  // Large dense tables: partitioned group-by (partition.h) instead of random global atomics.
-  if (P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes && P->star.empty() && tile_base > 0 &&
-      P->total_docs < (int64_t)UINT32_MAX && !getenv_flag("PGPU_NO_PARTITION")) {
-    int shift = 16;
-    while (shift > 8 && ((int64_t)nslots << shift) * 8 > kPartLds) --shift;
-    const int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
-    std::vector<int32_t> scol, sf64, sstream(nslots, -1);
-    for (int sl = 1; sl < nslots; ++sl) {
-      const int f64 = P->slot_kind[sl] == SLOT_SUM_F64 ? 1 : 0;
-      int k = -1;
-      for (size_t j = 0; j < scol.size(); ++j)
-        if (scol[j] == P->slot_col[sl] && sf64[j] == f64) k = (int)j;
-      if (k < 0) { scol.push_back(P->slot_col[sl]); sf64.push_back(f64); k = (int)scol.size() - 1; }
-      sstream[sl] = k;
-    }
-    const int64_t rec_bytes = P->total_docs * (2 + 8 * (int64_t)scol.size());
-    const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
-    if (parts <= kMaxParts && rec_bytes <= kPartMaxRecordBytes && pass_lds <= 96 * 1024) {
-      P->partitioned = true;
-      P->part_shift = shift;
-      P->num_parts = (int)parts;
-      P->stream_col = scol;
-      P->stream_f64 = sf64;
-      P->slot_stream = sstream;
-      P->part_lds = pass_lds;
-      int per_cu = occupancy_part_pass(pass_lds);
-      per_cu = std::max(1, std::min(per_cu, 4));
-      P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
-    }
-  }
-  // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
-  for (int l = 0; l < P->num_leaves; ++l) {
-    int sidx = -1;
-    for (size_t k = 0; k < P->stage_slot.size(); ++k)
-      if (P->stage_slot[k] == P->leaf_slot[l]) sidx = (int)k;
-    if (sidx < 0) {
-      P->stage_slot.push_back(P->leaf_slot[l]);
-      sidx = (int)P->stage_slot.size() - 1;
-    }
-    P->leaf_stage.push_back(sidx);
-  }
-  // The LDS-DMA staged kernel is kept as an A/B alternative (PGPU_SCAN=1); the direct-load kernel measured faster
-  // on MI355X (profiles/r01_ab_scan*.log).
-  static const bool scan_on = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '1';
-  if ((int)P->stage_slot.size() <= kMaxStage && scan_on) {
-    const bool pure_and = P->pure_and && P->num_leaves <= 4;  // the staged fast path holds at most 4 leaves in registers
-    for (Segment* s : P->segs) {
-      int64_t bits = 0;
-      for (int slot : P->stage_slot) bits += s->cols[P->query_cols[slot]].bits;
-      P->stage_words = std::max<int64_t>(P->stage_words, bits * kBlock);
-    }
-    P->lds_table_words = P->mode == MODE_LDS ? (int)((nslots * G + 1) & ~int64_t(1)) : 0;
-    const size_t lds = (size_t)P->lds_table_words * 8 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + 16 +
-                       (size_t)kQueueCap * 8 + (size_t)P->stage_words * 2 * 4;
-    if (lds <= kMaxScanLds) {
-      P->staged = true;
-      P->pure_and = pure_and;
-      P->lds_bytes = lds;
-      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, kLdsPerCu / lds));
-      P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
-    }
-  }
+  TRY(configure(tile_base));
+  P->chunks.assign(1, LaunchChunk{0, (int64_t)(P->segrec.size() / std::max(P->seg_stride, 1)), 0, P->num_tiles, 0,
+                                  (int64_t)P->set_fix.size(), 0, (int64_t)P->set_words.size()});
   if (trace_on())
     fprintf(stderr, "[pgpu] plan_create: %.1f us (%zu segments; setup %.1f, ensure %.1f, translate %.1f, rest %.1f)\n",
             now_us() - t_start, P->segs.size(), tr[0] - t_start, tr[1] - tr[0], tr[2] - tr[1], now_us() - tr[2]);
   return 0;
 }
 
-int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
-  const double t_start = trace_on() ? now_us() : 0;
+// ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
+// (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
+// (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
+int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X) {
+  X.t_start = trace_on() ? now_us() : 0;
   Scratch* sc = P->scratch;
-  const int nslots = (int)P->slot_kind.size();
-  const int64_t words = (int64_t)nslots * P->num_keys;
+  X.nslots = (int)P->slot_kind.size();
+  const int nslots = X.nslots;
+  X.words = (int64_t)nslots * P->num_keys;
   for (auto& e : sc->ev)
     if (!e) HIP_TRY(hipEventCreate(&e));
-  HIP_TRY(hipEventRecord(sc->ev[0], stream));
-  // uploads: segment records (with SET pointers patched) and SET bitsets
-  TRY(sc->sets.ensure(std::max<size_t>(P->set_words.size() * 4, 16)));
-  std::vector<uint8_t>& rec = P->segrec;
-  for (auto& f : P->set_fix) {
-    const uint32_t* p = sc->sets.as<uint32_t>() + f.second;
-    memcpy(rec.data() + f.first, &p, sizeof p);
+  if ((int)sc->cev.size() < 2 * max_chunks) {
+    const size_t old = sc->cev.size();
+    sc->cev.resize(2 * max_chunks, nullptr);
+    for (size_t i = old; i < sc->cev.size(); ++i) HIP_TRY(hipEventCreate(&sc->cev[i]));
   }
-  const size_t up = rec.size() + P->set_words.size() * 4;
-  TRY(sc->stage.ensure(std::max<size_t>(up, 16)));
-  memcpy(sc->stage.p, rec.data(), rec.size());
-  if (!P->set_words.empty()) memcpy((uint8_t*)sc->stage.p + rec.size(), P->set_words.data(), P->set_words.size() * 4);
-  TRY(sc->segrec.ensure(std::max<size_t>(rec.size(), 16)));
-  if (!rec.empty()) HIP_TRY(hipMemcpyAsync(sc->segrec.p, sc->stage.p, rec.size(), hipMemcpyHostToDevice, stream));
-  if (!P->set_words.empty())
-    HIP_TRY(hipMemcpyAsync(sc->sets.p, (uint8_t*)sc->stage.p + rec.size(), P->set_words.size() * 4,
-                           hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipEventRecord(sc->ev[0], stream));
+  TRY(sc->sets.ensure(std::max<size_t>(std::max<size_t>(P->set_words.size(), (size_t)P->set_words_bound) * 4, 16)));
+  const size_t rec_cap = std::max<size_t>((size_t)P->segs.size() * P->seg_stride, P->segrec.size());
+  TRY(sc->segrec.ensure(std::max<size_t>(rec_cap, 16)));
+  TRY(sc->stage.ensure(std::max<size_t>(rec_cap + (size_t)std::max<int64_t>(P->set_words_bound,
+                                                                             (int64_t)P->set_words.size()) * 4, 16)));
   TRY(sc->stats.ensure(64));
   HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
   uint64_t* table = reinterpret_cast<uint64_t*>(d_table);
   if (!table) {
-    TRY(sc->table.ensure((size_t)words * 8));
+    TRY(sc->table.ensure((size_t)X.words * 8));
     table = sc->table.as<uint64_t>();
   }
+  X.table = table;
   P->d_table_used = table;
-  KParams kp;
+  KParams& kp = X.kp;
   memset(&kp, 0, sizeof kp);
-  kp.segs = sc->segrec.as<uint8_t>();
   kp.seg_stride = P->seg_stride;
   kp.num_cols = (int)P->query_cols.size();
-  kp.num_segs = (int)(P->segrec.size() / std::max(P->seg_stride, 1));
-  kp.num_tiles = (int32_t)P->num_tiles;
   kp.num_ops = (int)P->ops.size();
   kp.pure_and = P->pure_and ? 1 : 0;
   for (size_t i = 0; i < P->ops.size(); ++i) kp.ops[i] = P->ops[i];
@@ -1589,12 +1694,11 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   }
   kp.num_keys_total = P->num_keys;
   kp.num_slots = nslots;
-  for (int s = 0; s < nslots; ++s) { kp.slot_kind[s] = P->slot_kind[s]; kp.slot_col[s] = P->slot_col[s]; }
+  for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = sc->stats.as<unsigned long long>();
-  const int scan_blocks = P->num_tiles > 0 ? P->grid : 0;
   const int star_blocks = (int)P->star.size() * P->star_chunks;
   if (P->mode == MODE_LDS) {
-    TRY(sc->slab.ensure((size_t)std::max(scan_blocks + star_blocks, 1) * words * 8));
+    TRY(sc->slab.ensure((size_t)std::max(max_chunks * P->grid + star_blocks, 1) * X.words * 8));
     kp.slab = sc->slab.as<uint64_t>();
   } else {
     if (P->mode == MODE_HASH) {
@@ -1606,17 +1710,56 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
       return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
     kp.table = table;
   }
-  TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(P->num_tiles, 1) * 4));
-  kp.tile_seg = sc->tile_seg.as<int32_t>();
-  if (launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>(), stream))
-    return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
+  TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
   kp.num_stage = (int)P->stage_slot.size();
   for (size_t k = 0; k < P->stage_slot.size() && k < (size_t)kMaxStage; ++k) kp.stage_col[k] = P->stage_slot[k];
   for (size_t l = 0; l < P->leaf_stage.size(); ++l) kp.leaf_stage[l] = P->leaf_stage[l];
   kp.stage_words = (int32_t)P->stage_words;
   kp.lds_table_words = P->lds_table_words;
-  HIP_TRY(hipEventRecord(sc->ev[1], stream));
-  if (P->num_tiles > 0 && P->partitioned) {
+  P->launches_done = 0;
+  return 0;
+}
+
+// Uploads chunk c's records (SET pointers patched to the device bitsets) and its bitset words.
+int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C) {
+  Scratch* sc = P->scratch;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(sc->stage.p);
+  const size_t r0 = (size_t)C.rec_begin * P->seg_stride, rn = (size_t)C.num_recs * P->seg_stride;
+  if (rn) memcpy(stage + r0, P->segrec.data() + r0, rn);
+  for (int64_t i = C.fix_begin; i < C.fix_end; ++i) {
+    const auto& f = P->set_fix[i];
+    const uint32_t* ptr = sc->sets.as<uint32_t>() + f.second;
+    memcpy(stage + f.first, &ptr, sizeof ptr);
+  }
+  if (rn) HIP_TRY(hipMemcpyAsync(sc->segrec.as<uint8_t>() + r0, stage + r0, rn, hipMemcpyHostToDevice, stream));
+  if (C.set_end > C.set_begin) {
+    const size_t set_off = (size_t)P->segs.size() * P->seg_stride + (size_t)C.set_begin * 4;
+    const size_t bytes = (size_t)(C.set_end - C.set_begin) * 4;
+    if (set_off + bytes > sc->stage.cap) return fail(PGPU_ERR_DEVICE, "set staging overflow");
+    memcpy(stage + set_off, P->set_words.data() + C.set_begin, bytes);
+    HIP_TRY(hipMemcpyAsync(sc->sets.as<uint32_t>() + C.set_begin, stage + set_off, bytes, hipMemcpyHostToDevice,
+                           stream));
+  }
+  return 0;
+}
+
+// Launches the scan of chunk c (records already uploaded): tile map of its records, then the scan kernel (or the
+// partitioned group-by) over its tiles into slab region c.
+int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c) {
+  Scratch* sc = P->scratch;
+  KParams kp = X.kp;
+  kp.segs = sc->segrec.as<uint8_t>() + (size_t)C.rec_begin * P->seg_stride;
+  kp.num_segs = (int)C.num_recs;
+  kp.num_tiles = (int32_t)C.num_tiles;
+  kp.tile_seg = sc->tile_seg.as<int32_t>() + C.tile_begin;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->grid, C.num_tiles));
+  if (P->mode == MODE_LDS) kp.slab = X.kp.slab + X.slabs_used * X.words;
+  if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>() + C.tile_begin, stream))
+    return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (c == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
+  HIP_TRY(hipEventRecord(sc->cev[2 * c], stream));
+  if (C.num_tiles > 0 && P->partitioned) {
+    const int nslots = X.nslots;
     KPartParams pp;
     memset(&pp, 0, sizeof pp);
     pp.base = kp;
@@ -1652,11 +1795,24 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
     pp.rec_cap = cap;
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
-  } else if (P->num_tiles > 0) {
-    const int rc = P->staged ? launch_scan(kp, P->mode, P->grid, P->lds_bytes, stream)
-                             : launch_filter_groupby(kp, P->mode, P->dense, P->grid, P->lds_bytes, stream);
+  } else if (C.num_tiles > 0) {
+    const int rc = P->staged ? launch_scan(kp, P->mode, grid, P->lds_bytes, stream)
+                             : launch_filter_groupby(kp, P->mode, P->dense, grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
+  HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
+  if (C.num_tiles > 0 && !P->partitioned && P->mode == MODE_LDS) X.slabs_used += grid;
+  P->launches_done = c + 1;
+  return 0;
+}
+
+int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
+  Scratch* sc = P->scratch;
+  const int nslots = X.nslots;
+  const int64_t words = X.words;
+  KParams& kp = X.kp;
+  const int nl = P->launches_done;
+  if (nl == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   if (!P->star.empty()) {
     // star-tree segments: K5 traversal then K6 residual scan + aggregation into the same group table
     TRY(sc->starwork.ensure((size_t)P->star_work_bytes));
@@ -1692,7 +1848,7 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
       sp.slot_int[sl] = sl > 0 && is_int_type(P->table->types[P->slot_tcol[sl]]) ? 1 : 0;
     }
     sp.table = kp.table;
-    sp.slab = P->mode == MODE_LDS ? kp.slab + (int64_t)scan_blocks * words : nullptr;
+    sp.slab = P->mode == MODE_LDS ? kp.slab + X.slabs_used * words : nullptr;
     sp.hash_keys = kp.hash_keys;
     sp.stats = kp.stats;
     if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
@@ -1700,19 +1856,31 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   }
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
   if (P->mode == MODE_LDS) {
-    const int nb = scan_blocks + star_blocks;
-    if (nb == 0) {
-      if (launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
+    // fold every slab written: the scan launches' (back to back) and the star-tree chunks' after them
+    const int64_t all = X.slabs_used + (int64_t)P->star.size() * P->star_chunks;
+    if (all == 0) {
+      if (launch_table_init(X.table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
-    } else if (launch_reduce_slabs(kp.slab, P->slot_kind.data(), nslots, P->num_keys, nb, table, stream)) {
+    } else if (launch_reduce_slabs(kp.slab, P->slot_kind.data(), nslots, P->num_keys, (int32_t)all, X.table, stream)) {
       return fail(PGPU_ERR_DEVICE, "reduce launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
   }
   HIP_TRY(hipEventRecord(sc->ev[3], stream));
   P->last_stream = stream;
   P->executed = true;
-  if (trace_on()) fprintf(stderr, "[pgpu] execute: %.1f us host\n", now_us() - t_start);
+  if (trace_on()) fprintf(stderr, "[pgpu] execute: %.1f us host\n", now_us() - X.t_start);
   return 0;
+}
+
+int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
+  const int nl = (int)P->chunks.size();
+  ExecCtx X;
+  TRY(exec_prologue(P, stream, d_table, std::max(nl, 1), X));
+  for (int c = 0; c < nl; ++c) {
+    TRY(exec_upload_chunk(P, stream, P->chunks[c]));
+    TRY(exec_launch_chunk(P, stream, X, P->chunks[c], c));
+  }
+  return exec_epilogue(P, stream, X);
 }
 
 // Group-by dictIds of composite key k: (k / stride[j]) % card[j] (DictionaryBasedGroupKeyGenerator.java:276-323).
@@ -2232,6 +2400,32 @@ int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t
   return 0;
 }
 
+int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
+                             void* d_table, pgpu_plan* out) {
+  if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(t->device);
+  auto P = std::make_unique<pgpu_plan_s>();
+  StreamExec se;
+  se.stream = stream ? reinterpret_cast<hipStream_t>(stream) : t->stream;
+  se.d_table = d_table;
+  P->scratch = acquire_scratch(t);  // before plan_create_impl takes the table lock (acquire_scratch locks it too)
+  int rc = plan_create_impl(t, handles, nsegs, q, P.get(), &se);
+  if (!rc && !P->executed) {
+    if (P->hash && d_table) rc = fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
+    else rc = plan_execute_impl(P.get(), se.stream, d_table);
+  }
+  if (rc) {
+    if (P->scratch) {
+      hipStreamSynchronize(se.stream);  // no launch of this plan may still use its scratch
+      release_scratch(t, P->scratch);
+      P->scratch = nullptr;
+    }
+    return rc;
+  }
+  *out = P.release();
+  return 0;
+}
+
 int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   if (P->hash && d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
@@ -2268,9 +2462,8 @@ int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shar
 int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
                          pgpu_result* out) {
   pgpu_plan P = nullptr;
-  TRY(pgpu_plan_create(t, handles, nsegs, q, &P));
-  int rc = pgpu_plan_execute(P, stream, nullptr);
-  if (!rc) rc = pgpu_plan_finalize(P, stream, nullptr, out);
+  TRY(pgpu_plan_create_execute(t, handles, nsegs, q, stream, nullptr, &P));
+  int rc = pgpu_plan_finalize(P, stream, nullptr, out);
   std::string keep = g_err;
   pgpu_plan_destroy(P);
   g_err = keep;
@@ -2287,12 +2480,17 @@ int pgpu_plan_timing(pgpu_plan P, double* out3) {
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   Scratch* sc = P->scratch;
   HIP_TRY(hipEventSynchronize(sc->ev[3]));
-  float a = 0, b = 0;
+  float a = 0;
   HIP_TRY(hipEventElapsedTime(&a, sc->ev[0], sc->ev[3]));
-  HIP_TRY(hipEventElapsedTime(&b, sc->ev[1], sc->ev[2]));
+  double k = 0;
+  for (int c = 0; c < P->launches_done; ++c) {  // scan launches only (no host gaps between streamed launches)
+    float b = 0;
+    HIP_TRY(hipEventElapsedTime(&b, sc->cev[2 * c], sc->cev[2 * c + 1]));
+    k += b;
+  }
   out3[0] = a * 1000.0;
-  out3[1] = b * 1000.0;
-  out3[2] = P->num_tiles > 0 ? 1.0 : 0.0;
+  out3[1] = k * 1000.0;
+  out3[2] = P->num_tiles > 0 ? (double)P->launches_done : 0.0;
   return 0;
 }
 

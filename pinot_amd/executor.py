@@ -326,13 +326,18 @@ class GpuTable:
         return Plan(self, handles, query)
 
     def execute_groupby(self, handles, query, stream=None):
-        with Plan(self, handles, query) as p:
-            p.execute(stream)
+        with Plan(self, handles, query, execute=(stream, None)) as p:
             return p.finalize(stream)
+
+    def plan_execute(self, handles, query, stream=None, d_table=None):
+        """Plan + execute, streamed (pgpu_plan_create_execute): chunks of segments are launched while the rest
+        is still being planned.  Returns the executed Plan (finalize it, or merge across GPUs first)."""
+        return Plan(self, handles, query, execute=(stream, d_table))
 
 
 class Plan:
-    def __init__(self, table, handles, query):
+    def __init__(self, table, handles, query, execute=None):
+        """execute=(stream, d_table): create and execute in one streamed call (pgpu_plan_create_execute)."""
         if isinstance(query, str):
             from .query import parse_query
             query = parse_query(query)
@@ -343,8 +348,14 @@ class Plan:
             np.ascontiguousarray(list(handles), dtype=np.int64)
         q, keep = query.to_c(table.index)
         h = ctypes.c_void_p()
-        L.check(self.lib.pgpu_plan_create(table.handle, L.ptr(hs, ctypes.c_int64), len(hs), ctypes.byref(q),
-                                          ctypes.byref(h)))
+        if execute is None:
+            L.check(self.lib.pgpu_plan_create(table.handle, L.ptr(hs, ctypes.c_int64), len(hs), ctypes.byref(q),
+                                              ctypes.byref(h)))
+        else:
+            stream, d_table = execute
+            L.check(self.lib.pgpu_plan_create_execute(table.handle, L.ptr(hs, ctypes.c_int64), len(hs),
+                                                      ctypes.byref(q), ctypes.c_void_p(stream or 0),
+                                                      ctypes.c_void_p(d_table or 0), ctypes.byref(h)))
         self.handle = h
         self.num_segments = len(hs)
 
@@ -384,7 +395,7 @@ class Plan:
     def timing_us(self):
         out = (ctypes.c_double * 3)()
         L.check(self.lib.pgpu_plan_timing(self.handle, out))
-        return out[0], out[1]
+        return out[0], out[1], out[2]
 
     def finalize(self, stream=None, d_table=None):
         """Waits for the execution, compacts the group table and returns the decoded result.  `finalize_us`

@@ -186,7 +186,9 @@ def _random_filter(rng, seg, depth=0):
 
 
 @pytest.mark.parametrize("seed", list(range(12)))
-def test_random_queries_vs_oracle(oracle, gpu_lib, seed):
+def test_random_queries_vs_oracle(oracle, gpu_lib, seed, monkeypatch):
+    if seed % 2:  # streamed plans: every segment its own launch, planned while the previous ones run
+        monkeypatch.setenv("PGPU_STREAM_CHUNKS", "4")
     rng = np.random.default_rng(1000 + seed)
     nseg = int(rng.integers(1, 5))
     segs = [_random_segment(oracle, rng, SCHEMA_R, int(rng.integers(1, 40000))) for _ in range(nseg)]
@@ -414,12 +416,14 @@ def test_finalize_key_range_shards(oracle, gpu_lib):
 
 
 @pytest.mark.parametrize("chunk", [0, 64], ids=["one_thread", "chunks_of_64"])
-def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, monkeypatch):
+@pytest.mark.parametrize("launches", [1, 4, 7])
+def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, launches, monkeypatch):
     """Plans over hundreds of segments translate their predicates in parallel chunks (host worker pool); the
     concatenated records (tile offsets, IN-set bitsets) must give the oracle's combined result, including
     segments the filter prunes (EmptyFilterOperator) in the middle of a chunk."""
     if chunk:
         monkeypatch.setenv("PGPU_PLAN_CHUNK_SEGS", str(chunk))
+    monkeypatch.setenv("PGPU_STREAM_CHUNKS", str(launches))
     rng = np.random.default_rng(11)
     schema = [("g", "INT"), ("f", "INT"), ("v", "LONG")]
     segs = []

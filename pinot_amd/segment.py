@@ -62,7 +62,8 @@ def load_v1_segment_dir(path):
     num_docs = int(props["segment.total.docs"])
     pad = _padding_byte(props)
     cols = {}
-    names = sorted({k.split(".")[1] for k in props if k.startswith("column.") and k.endswith(".cardinality")})
+    names = sorted({k[len("column."):-len(".cardinality")] for k in props
+                    if k.startswith("column.") and k.endswith(".cardinality")})  # names may contain '.'
     for name in names:
         p = "column.%s." % name
         dtype = L.TYPE_NAMES[props[p + "dataType"]]

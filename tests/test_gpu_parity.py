@@ -564,3 +564,47 @@ def test_sorted_column_docrange_leaves(oracle, gpu_lib, n):
         np.testing.assert_array_equal(bm, oracle.filter_bitmap(schema, seg, parse_query(SORTED_QUERIES[2])))
     finally:
         t.close()
+
+
+def _fixed_bit_view(seg):
+    """The same segment with SortedIndexReaderImpl pair columns expanded to the fixed-bit forward index."""
+    from dataclasses import replace
+    from pinot_amd.segment import SegmentBuffers
+    from pinot_amd.segment_files import pack_msb_first
+    cols = {}
+    for name, c in seg.columns.items():
+        if c.fwd_format == L.FWD_SORTED_PAIRS:
+            pairs = np.frombuffer(c.fwd_bytes, dtype=">i4").reshape(-1, 2).astype(np.int64)
+            ids = np.repeat(np.arange(c.cardinality), np.maximum(pairs[:, 1] - pairs[:, 0] + 1, 0))
+            c = replace(c, fwd_bytes=pack_msb_first(ids, c.bits_per_element), fwd_format=L.FWD_FIXED_BIT,
+                        is_sorted=False)
+        cols[name] = c
+    return SegmentBuffers(seg.num_docs, cols)
+
+
+def test_v3_segment_files_pin_and_query(oracle, gpu_lib, tmp_path):
+    """Segments written as Pinot v1 directories, converted to v3 (columns.psf + index_map) and loaded back pin and
+    answer like the oracle over the same bytes (sorted time column, LONG and STRING group keys)."""
+    from pinot_amd.segment_files import convert_v1_to_v3, load_segment_dir, write_v1_segment_dir
+    schema = [("day", "INT"), ("acct", "LONG"), ("clicks", "INT"), ("name", "STRING")]
+    segs = []
+    for s in range(3):
+        rng = np.random.default_rng(40 + s)
+        n = [20000, 8193, 1][s]
+        vals = {"day": np.sort(rng.integers(17000, 17030, n)).tolist(), "acct": rng.integers(0, 500, n).tolist(),
+                "clicks": rng.integers(0, 1000, n).tolist(), "name": ["n%d" % v for v in rng.integers(0, 7, n)]}
+        path = str(tmp_path / ("seg%d" % s))
+        write_v1_segment_dir(path, schema, vals, sorted_columns=("day",))
+        convert_v1_to_v3(path)
+        segs.append(load_segment_dir(path))
+    orc = [_fixed_bit_view(s) for s in segs]  # the oracle reads fixed-bit forward indexes only
+    t, hs = gpu_table(schema, segs)
+    try:
+        for sql in ("SELECT SUM(clicks), COUNT(*), MAX(clicks) FROM t WHERE day BETWEEN 17005 AND 17020 "
+                    "AND acct IN (3, 7, 11, 499) GROUP BY day",
+                    "SELECT AVG(clicks), MIN(acct) FROM t WHERE clicks < 500 GROUP BY name, day",
+                    "SELECT SUM(acct) FROM t WHERE name IN ('n1', 'n4') OR day = 17029 GROUP BY acct"):
+            q = parse_query(sql)
+            assert_same(t.execute_groupby(hs, q), oracle.run_groupby(schema, orc, q), q, schema)
+    finally:
+        t.close()

@@ -284,6 +284,18 @@ typedef struct {
  * pre-aggregated documents (StarTreeGroupByExecutor, core/startree/executor/StarTreeGroupByExecutor.java:60-71). */
 int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_startree_desc* desc);
 
+/* Pins the bitmap inverted index of one column of a pinned segment: `bytes` is the `<column>.bitmap.inv` file
+ * (v1) or the column's `inverted_index` buffer of columns.psf (v3) verbatim -- (cardinality + 1) big-endian int32
+ * bitmap offsets, then one portable-format RoaringBitmap per dictId (BitmapInvertedIndexWriter /
+ * BitmapInvertedIndexReader, seglocal/segment/index/readers/BitmapInvertedIndexReader.java:40-70; the reader the
+ * DefaultIndexReaderProvider hands to the DataSource).  From then on EQ / NOT_EQ / IN / NOT_IN predicates on an
+ * unsorted column of that segment are BitmapBasedFilterOperator leaves (FilterOperatorUtils.java:72-79): the
+ * matching dictIds' containers are ORed into a docId bitmap on the device per query, and the leaf scans no
+ * forward-index entries.  Malformed bitmaps (bad cookie, overruns, docIds >= numDocs) return
+ * PGPU_ERR_INVALID_ARGUMENT. */
+int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
+                               int64_t num_bytes);
+
 /* Host-side star-tree builder (BaseSingleTreeBuilder + OnHeapSingleTreeBuilder, seglocal/startree/v2/builder/):
  * builds the star-tree of a segment given in Pinot's byte format (the pgpu_segment_desc of pgpu_pin_segment;
  * column_types per column), split order (column indexes), dimensions without star nodes (indexes into the split

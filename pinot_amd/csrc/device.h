@@ -155,6 +155,10 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
     const uint32_t m = docrange_mask(group, lo, span);
     return negate ? ~m : m;
   }
+  if (kind == LEAF_BITMAP) {
+    const uint32_t m = set[group];
+    return negate ? ~m : m;
+  }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
 }
 

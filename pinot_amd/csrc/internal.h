@@ -34,7 +34,10 @@ constexpr int kDenseGroupMin = 256;         // matches per wave-tile (of 2048 do
 
 // LEAF_DOCRANGE: a predicate on a sorted column (SortedIndexBasedFilterOperator, core/operator/filter/
 // SortedIndexBasedFilterOperator.java:51-125): docIds [lo, lo + span), evaluated without reading any column.
-enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4 };
+// LEAF_BITMAP: a predicate on a column with a bitmap inverted index (BitmapBasedFilterOperator, core/operator/filter/
+// BitmapBasedFilterOperator.java:63-100): `set` is the segment's materialised docId bitmap (bit i of word g = doc
+// 32g + i), the OR of the matching dictIds' Roaring bitmaps, built per query by inv_materialize_kernel.
+enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4, LEAF_BITMAP = 5 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
 enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
 enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };
@@ -168,6 +171,20 @@ struct KPartParams {
   uint64_t* mid_val;                // [num_streams][rec_cap]
 };
 
+// ---------------------------------------------------------------------------------------------- inverted index
+// One Roaring container of a pinned inverted index ORed into a query's docId bitmap.  Containers are kept on the
+// device as ARRAY (n sorted u16 low halves, two per u32 word, little-endian) or BITMAP (2048 u32 words: bit v of
+// the container = bit (v & 31) of word v >> 5, Roaring's long[1024] read as u32); run containers are converted at
+// attach time.  dst = word of the container's first doc (key << 16) in the plan's docbits buffer.
+enum ContainerType : int32_t { CONT_ARRAY = 0, CONT_BITMAP = 1 };
+constexpr int kContainerWords = 2048;
+struct KBitTask {
+  const uint32_t* payload;
+  int32_t type;
+  int32_t n;
+  int64_t dst;
+};
+
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
@@ -196,6 +213,7 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
 // In-place exclusive prefix sum of n u32 (one workgroup; n up to a few 10^4).
 int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
+int launch_inv_materialize(const KBitTask* tasks, int64_t num_tasks, uint32_t* docbits, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.

@@ -30,6 +30,28 @@ __global__ void gather_ids_kernel(const uint32_t* __restrict__ fwd, int32_t bits
   if (i < n) out[i] = (int32_t)gather_id(fwd, bits, docs[i]);
 }
 
+// BitmapBasedFilterOperator's OR of the matching dictIds' bitmaps (BitmapBasedFilterOperator.java:85-98), one
+// workgroup per Roaring container: BITMAP containers OR 2048 words (coalesced, zero words skipped), ARRAY containers
+// set one bit per value.  Atomic ORs: the containers of several dictIds of one IN leaf share docbits words.
+__global__ void inv_materialize_kernel(const KBitTask* __restrict__ tasks, int64_t num_tasks,
+                                       uint32_t* __restrict__ docbits) {
+  for (int64_t t = blockIdx.x; t < num_tasks; t += gridDim.x) {
+    const KBitTask T = tasks[t];
+    uint32_t* dst = docbits + T.dst;
+    if (T.type == CONT_BITMAP) {
+      for (int w = threadIdx.x; w < kContainerWords; w += blockDim.x) {
+        const uint32_t v = T.payload[w];
+        if (v) atomicOr(dst + w, v);
+      }
+    } else {
+      for (int i = threadIdx.x; i < T.n; i += blockDim.x) {
+        const uint32_t v = (T.payload[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+        atomicOr(dst + (v >> 5), 1u << (v & 31));
+      }
+    }
+  }
+}
+
 // tile -> segment map of a plan (one workgroup per segment record).
 __global__ void expand_tiles_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride, int32_t num_segs,
                                     int32_t* __restrict__ tile_seg) {
@@ -289,6 +311,13 @@ int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, i
   if (n <= 0) return 0;
   const int64_t grid = (n + 255) / 256;
   hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), fwd, bits, start, n, out);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_inv_materialize(const KBitTask* tasks, int64_t num_tasks, uint32_t* docbits, void* stream) {
+  if (num_tasks <= 0) return 0;
+  const int64_t grid = num_tasks < 65536 ? num_tasks : 65536;
+  hipLaunchKernelGGL(inv_materialize_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), tasks, num_tasks, docbits);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -351,6 +351,17 @@ struct Dict {
   size_t size() const { return is_int_type(type) ? iv.size() : is_fp_type(type) ? dv.size() : sv.size(); }
 };
 
+// A pinned bitmap inverted index (pgpu_attach_inverted_index; BitmapInvertedIndexReader): the Roaring containers
+// of every dictId in one device block (ARRAY / BITMAP payloads, internal.h), their directory kept on the host.
+struct InvIndex {
+  struct Cont { int64_t word; int32_t type, n, key; };
+  void* d_block = nullptr;
+  int64_t bytes = 0;
+  std::vector<int32_t> cont_begin;  // card + 1: containers of dictId i are [cont_begin[i], cont_begin[i + 1])
+  std::vector<Cont> conts;
+  std::vector<int64_t> docs;        // docs of each dictId (Roaring cardinality)
+};
+
 struct Column {
   int32_t card = 0, bits = 0, entry_width = 0, padding = 0;
   int64_t fwd_bytes = 0;            // Pinot byte length of the forward index
@@ -365,6 +376,7 @@ struct Column {
   uint64_t lut_version = ~0ull;
   int64_t* d_key = nullptr;
   double* d_val = nullptr;
+  std::shared_ptr<InvIndex> inv;    // bitmap inverted index, if attached
 };
 
 // A pinned star-tree (pgpu_attach_startree): one device block holding the nodes, the star-tree documents'
@@ -399,6 +411,7 @@ struct Segment {
 };
 
 struct Scratch {
+  DevBuf docbits, bittasks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
@@ -408,6 +421,7 @@ struct Scratch {
   void release() {
     for (auto& e : cev) if (e) hipEventDestroy(e);
     cev.clear();
+    docbits.release(); bittasks.release();
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
     starstage.release();
@@ -596,6 +610,11 @@ void free_segment(pgpu_table_s* t, Segment* s) {
     if (c.d_lut) hipFree(c.d_lut);
     if (c.d_key) hipFree(c.d_key);
     if (c.d_val) hipFree(c.d_val);
+    if (c.inv && c.inv->d_block) {
+      hipFree(c.inv->d_block);
+      t->device_bytes -= c.inv->bytes;
+      c.inv->d_block = nullptr;
+    }
     t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) + (c.d_key ? 16 * std::max(c.card, 1) : 0);
   }
   if (s->d_block) hipFree(s->d_block);
@@ -625,6 +644,8 @@ struct LeafHost {
   uint32_t lo = 0, span = 0;
   uint32_t dict_lo = 0, dict_span = 0;  // LEAF_DOCRANGE: the dictId range it came from (star-tree matching)
   std::vector<uint32_t> set;  // bitset words for LEAF_SET
+  std::vector<int32_t> inv_ids;  // LEAF_BITMAP: matching dictIds whose inverted-index bitmaps are ORed
+  double inv_frac = 0;           // LEAF_BITMAP: fraction of the segment's docs in those bitmaps
 };
 
 enum Tri { T_NONE = 0, T_ALL = 1, T_VAR = 2 };
@@ -666,6 +687,10 @@ struct pgpu_plan_s {
   int seg_stride = 0;
   std::vector<uint32_t> set_words;        // all SET bitsets back to back
   std::vector<std::pair<int64_t, int64_t>> set_fix;  // (offset of KLeaf.set field in segrec, word offset)
+  bool no_inverted = false;               // keep scan leaves (pgpu_filter_bitmap's single-segment path)
+  int64_t docbit_words = 0;               // LEAF_BITMAP docId bitmaps of the plan (device words)
+  std::vector<std::pair<int64_t, int64_t>> bit_fix;  // (offset of KLeaf.set field in segrec, docbits word offset)
+  std::vector<KBitTask> bit_tasks;        // containers ORed into the docbits by inv_materialize_kernel
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
@@ -848,6 +873,28 @@ int parse_predicate(int type, const pgpu_predicate& p, ParsedPred* out) {
       return fail(PGPU_ERR_BAD_QUERY, "BadQueryRequestException: cannot convert '%s' to the type of column %d",
                   p.values[i], p.column);
   return 0;
+}
+
+// FilterOperatorUtils.getLeafFilterOperator (FilterOperatorUtils.java:72-79): an EQ / NOT_EQ / IN / NOT_IN
+// predicate on a column with an inverted index (and not sorted: the sorted index wins) becomes a
+// BitmapBasedFilterOperator.  The leaf keeps its negate flag: flip(OR(bitmaps of the literals' dictIds)) over
+// [0, numDocs) equals the reference's OR over the non-matching dictIds (BitmapBasedFilterOperator.java:73-98).
+void to_inverted_leaf(const Column& c, const pgpu_predicate& p, const Segment& s, LeafHost* L) {
+  if (!c.inv || c.sorted || (L->kind != LEAF_RANGE && L->kind != LEAF_SET)) return;
+  if (p.type != PGPU_PRED_EQ && p.type != PGPU_PRED_NOT_EQ && p.type != PGPU_PRED_IN && p.type != PGPU_PRED_NOT_IN)
+    return;
+  L->inv_ids.clear();
+  if (L->kind == LEAF_RANGE) {
+    for (uint32_t i = 0; i < L->span; ++i) L->inv_ids.push_back((int32_t)(L->lo + i));
+  } else {
+    for (size_t w = 0; w < L->set.size(); ++w)
+      for (uint32_t bits = L->set[w]; bits; bits &= bits - 1)
+        L->inv_ids.push_back((int32_t)(w * 32 + __builtin_ctz(bits)));
+  }
+  int64_t docs = 0;
+  for (int32_t id : L->inv_ids) docs += c.inv->docs[id];
+  L->inv_frac = (double)docs / std::max(1, s.num_docs);
+  L->kind = LEAF_BITMAP;
 }
 
 // Translates predicate `p` against one segment's column dictionary (dictionary-based PredicateEvaluators).
@@ -1343,10 +1390,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     exempt_kind = all_count || all_minmax;
   }
   std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
-  bool any_star = false;
+  bool any_star = false, any_inv = false;
   mark();
   for (Segment* s : P->segs) {
     any_star |= star_allowed && s->star != nullptr;
+    for (int l = 0; l < q->num_predicates; ++l)
+      any_inv |= s->cols[q->predicates[l].column].inv != nullptr;
     // device LUT / value arrays of the referenced columns (built once per segment, rebuilt when the global
     // dictionary grows); done up front so the per-segment translation below only reads segment state
     for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
@@ -1359,6 +1408,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<uint8_t> rec;
     std::vector<uint32_t> set_words;
     std::vector<std::pair<int64_t, int64_t>> set_fix;
+    std::vector<std::pair<int64_t, int64_t>> bit_fix;
+    std::vector<KBitTask> bit_tasks;
+    int64_t docbit_words = 0;
     std::vector<uint8_t> scanned;
     int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
     double sel = 1.0;
@@ -1395,6 +1447,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         LeafHost& lh = leaves[l];
         lh.kind = LEAF_NONE; lh.negate = 0; lh.lo = 0; lh.span = 0;
         TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], parsed[l], &lh, ids_scratch));
+        if (!P->no_inverted && !s->star) to_inverted_leaf(s->cols[q->predicates[l].column], q->predicates[l], *s, &lh);
         tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
       }
       const Tri whole = P->num_leaves ? fold_program(P->ops, tri) : T_ALL;
@@ -1409,7 +1462,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         if (used) continue;
       }
       for (int l = 0; l < P->num_leaves; ++l)  // sorted columns go through the sorted index: no entries scanned
-        if (tri[l] == T_VAR && !s->cols[q->predicates[l].column].sorted) C.entries += s->num_docs;
+        if (tri[l] == T_VAR && !s->cols[q->predicates[l].column].sorted && leaves[l].kind != LEAF_BITMAP)
+          C.entries += s->num_docs;  // index leaves (sorted, inverted) scan no entries
       if (C.sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
         std::vector<double> frac(P->num_leaves, 1.0);
         for (int l = 0; l < P->num_leaves; ++l) {
@@ -1417,6 +1471,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           const double card = std::max(1, s->cols[q->predicates[l].column].card);
           double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
           if (lh.kind == LEAF_DOCRANGE) f = (double)lh.span / std::max(1, s->num_docs);
+          if (lh.kind == LEAF_BITMAP) f = lh.inv_frac;
           if (lh.kind == LEAF_SET) {
             int64_t ones = 0;
             for (uint32_t w : lh.set) ones += __builtin_popcount(w);
@@ -1454,6 +1509,22 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           C.set_fix.emplace_back(field, (int64_t)C.set_words.size());
           C.set_words.insert(C.set_words.end(), lh.set.begin(), lh.set.end());
+        }
+        if (lh.kind == LEAF_BITMAP) {  // docId bitmap region: whole 65536-doc containers
+          const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
+          const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
+          C.bit_fix.emplace_back(field, C.docbit_words);
+          for (int32_t id : lh.inv_ids)
+            for (int32_t ci = inv.cont_begin[id]; ci < inv.cont_begin[id + 1]; ++ci) {
+              const InvIndex::Cont& ct = inv.conts[ci];
+              KBitTask task;
+              task.payload = reinterpret_cast<const uint32_t*>(inv.d_block) + ct.word;
+              task.type = ct.type;
+              task.n = ct.n;
+              task.dst = C.docbit_words + (int64_t)ct.key * kContainerWords;
+              C.bit_tasks.push_back(task);
+            }
+          C.docbit_words += (((int64_t)s->num_docs + 65535) >> 16) * kContainerWords;
         }
       }
       C.rec.insert(C.rec.end(), rec.begin(), rec.end());
@@ -1559,6 +1630,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       for (size_t r = 0; r < C.rec.size(); r += P->seg_stride)
         reinterpret_cast<KSegHdr*>(C.rec.data() + r)->tile_base += (int32_t)tile_shift;
     for (auto& f : C.set_fix) P->set_fix.emplace_back(rec0 + f.first, set0 + f.second);
+    for (auto& f : C.bit_fix) P->bit_fix.emplace_back(rec0 + f.first, P->docbit_words + f.second);
+    for (KBitTask task : C.bit_tasks) {
+      task.dst += P->docbit_words;
+      P->bit_tasks.push_back(task);
+    }
+    P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
     P->seg_scanned.insert(P->seg_scanned.end(), C.scanned.begin(), C.scanned.end());
@@ -1574,7 +1651,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   const bool part_eligible = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes &&
                              !getenv_flag("PGPU_NO_PARTITION");
   const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
-  if (se && !any_star && !scan_on && !part_eligible && stream_chunks > 1) {
+  if (se && !any_star && !any_inv && !scan_on && !part_eligible && stream_chunks > 1) {
     for (Segment* s : P->segs) {
       P->tile_bound += (s->num_docs + kTileDocs - 1) / kTileDocs;
       for (int l = 0; l < P->num_leaves; ++l) {
@@ -1669,6 +1746,19 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
   TRY(sc->stats.ensure(64));
   HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
+  if (P->docbit_words > 0) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
+    TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
+    HIP_TRY(hipMemsetAsync(sc->docbits.p, 0, (size_t)P->docbit_words * 4, stream));
+    if (!P->bit_tasks.empty()) {
+      TRY(sc->bittasks.ensure(P->bit_tasks.size() * sizeof(KBitTask)));
+      HIP_TRY(hipMemcpyAsync(sc->bittasks.p, P->bit_tasks.data(), P->bit_tasks.size() * sizeof(KBitTask),
+                             hipMemcpyHostToDevice, stream));
+      if (launch_inv_materialize(sc->bittasks.as<KBitTask>(), (int64_t)P->bit_tasks.size(), sc->docbits.as<uint32_t>(),
+                                 stream))
+        return fail(PGPU_ERR_DEVICE, "inverted-index materialise launch failed: %s",
+                    hipGetErrorString(hipGetLastError()));
+    }
+  }
   uint64_t* table = reinterpret_cast<uint64_t*>(d_table);
   if (!table) {
     TRY(sc->table.ensure((size_t)X.words * 8));
@@ -1731,6 +1821,11 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C) 
     const uint32_t* ptr = sc->sets.as<uint32_t>() + f.second;
     memcpy(stage + f.first, &ptr, sizeof ptr);
   }
+  for (const auto& f : P->bit_fix)
+    if (f.first >= (int64_t)r0 && f.first < (int64_t)(r0 + rn)) {
+      const uint32_t* ptr = sc->docbits.as<uint32_t>() + f.second;
+      memcpy(stage + f.first, &ptr, sizeof ptr);
+    }
   if (rn) HIP_TRY(hipMemcpyAsync(sc->segrec.as<uint8_t>() + r0, stage + r0, rn, hipMemcpyHostToDevice, stream));
   if (C.set_end > C.set_begin) {
     const size_t set_off = (size_t)P->segs.size() * P->seg_stride + (size_t)C.set_begin * 4;
@@ -2180,6 +2275,141 @@ int pgpu_unpin_segment(pgpu_table t, int64_t h) {
   return 0;
 }
 
+namespace {
+// Portable RoaringBitmap deserialisation (RoaringBitmap 0.9.x RoaringArray.deserialize, little-endian): cookie
+// 12346 (no run containers; u32 size follows) or 12347 | (size - 1) << 16 (with a run-container bitmap); per
+// container (u16 key, u16 card - 1); offsets (u32, skipped) unless a run-cookie bitmap has < 4 containers; then
+// ARRAY (card <= 4096: u16 values), BITMAP (1024 u64) or RUN (u16 count, (u16 start, u16 length - 1) pairs).
+// Appends device-layout payload words and container entries; returns false on malformed input.
+bool parse_roaring(const uint8_t* b, int64_t n, int32_t num_docs, std::vector<uint32_t>& words,
+                   std::vector<InvIndex::Cont>& conts, int64_t* docs) {
+  auto u16 = [&](int64_t o) { return (uint32_t)b[o] | ((uint32_t)b[o + 1] << 8); };
+  auto u32 = [&](int64_t o) { return u16(o) | (u16(o + 2) << 16); };
+  if (n < 4) return false;
+  const uint32_t cookie = u32(0);
+  int64_t pos, size;
+  const uint8_t* runbits = nullptr;
+  bool offsets;
+  if ((cookie & 0xFFFF) == 12347) {
+    size = (cookie >> 16) + 1;
+    runbits = b + 4;
+    pos = 4 + (size + 7) / 8;
+    offsets = size >= 4;
+  } else if (cookie == 12346) {
+    if (n < 8) return false;
+    size = u32(4);
+    pos = 8;
+    offsets = true;
+  } else {
+    return false;
+  }
+  if (size < 0 || size > 65536 || pos + size * 4 > n) return false;
+  const int64_t desc = pos;
+  pos += size * 4 + (offsets ? size * 4 : 0);
+  *docs = 0;
+  int32_t prev_key = -1;
+  std::vector<uint32_t> vals;
+  for (int64_t i = 0; i < size; ++i) {
+    const int32_t key = (int32_t)u16(desc + 4 * i);
+    const int32_t card = (int32_t)u16(desc + 4 * i + 2) + 1;
+    if (key <= prev_key || ((int64_t)key << 16) >= num_docs) return false;
+    prev_key = key;
+    const bool run = runbits && ((runbits[i >> 3] >> (i & 7)) & 1);
+    vals.clear();
+    std::vector<uint32_t> bm;
+    if (run) {
+      if (pos + 2 > n) return false;
+      const int64_t nruns = u16(pos);
+      pos += 2;
+      if (pos + nruns * 4 > n) return false;
+      for (int64_t r = 0; r < nruns; ++r) {
+        const uint32_t start = u16(pos + 4 * r), len = u16(pos + 4 * r + 2);
+        if (start + len > 65535) return false;
+        for (uint32_t v = start; v <= start + len; ++v) vals.push_back(v);
+      }
+      pos += nruns * 4;
+    } else if (card <= 4096) {
+      if (pos + (int64_t)card * 2 > n) return false;
+      for (int32_t k = 0; k < card; ++k) vals.push_back(u16(pos + 2 * k));
+      pos += (int64_t)card * 2;
+    } else {
+      if (pos + 8192 > n) return false;
+      bm.resize(kContainerWords);
+      for (int w = 0; w < kContainerWords; ++w) bm[w] = u32(pos + 4 * w);
+      pos += 8192;
+    }
+    int64_t c = 0;
+    if (bm.empty()) {
+      if ((int64_t)vals.size() != card) return false;
+      if (vals.size() > 4096) {  // long runs: bitmap form
+        bm.assign(kContainerWords, 0);
+        for (uint32_t v : vals) bm[v >> 5] |= 1u << (v & 31);
+      }
+    }
+    if (!bm.empty()) {
+      int32_t top = -1;
+      for (int w = 0; w < kContainerWords; ++w)
+        if (bm[w]) { c += __builtin_popcount(bm[w]); top = w * 32 + 31 - __builtin_clz(bm[w]); }
+      if (((int64_t)key << 16) + top >= num_docs) return false;
+      conts.push_back({(int64_t)words.size(), CONT_BITMAP, (int32_t)c, key});
+      words.insert(words.end(), bm.begin(), bm.end());
+    } else {
+      for (size_t k = 1; k < vals.size(); ++k)
+        if (vals[k] <= vals[k - 1]) return false;
+      if (!vals.empty() && ((int64_t)key << 16) + vals.back() >= num_docs) return false;
+      c = (int64_t)vals.size();
+      conts.push_back({(int64_t)words.size(), CONT_ARRAY, (int32_t)c, key});
+      for (size_t k = 0; k < vals.size(); k += 2)
+        words.push_back(vals[k] | (k + 1 < vals.size() ? vals[k + 1] << 16 : 0u));
+    }
+    *docs += c;
+  }
+  return pos <= n;
+}
+}  // namespace
+
+int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
+  if (!t || (!bytes && num_bytes)) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  DeviceGuard g(t->device);
+  std::lock_guard<std::mutex> lk(t->mu);
+  auto it = t->segments.find(h);
+  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+  Segment& seg = *it->second;
+  if (column < 0 || column >= (int)seg.cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column %d", column);
+  Column& col = seg.cols[column];
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(bytes);
+  const int64_t card = col.card, hdr = (card + 1) * 4;
+  if (num_bytes < hdr) return fail(PGPU_ERR_INVALID_ARGUMENT, "inverted index shorter than its offset header");
+  auto be32 = [&](int64_t o) {
+    return (int64_t)(int32_t)(((uint32_t)b[o] << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) | b[o + 3]);
+  };
+  auto inv = std::make_shared<InvIndex>();
+  inv->cont_begin.assign(card + 1, 0);
+  inv->docs.assign(card, 0);
+  std::vector<uint32_t> words;
+  const int64_t first = be32(0);
+  for (int64_t id = 0; id < card; ++id) {
+    const int64_t off = be32(id * 4) - first, end = be32((id + 1) * 4) - first;
+    inv->cont_begin[id] = (int32_t)inv->conts.size();
+    if (off < 0 || end < off || hdr + end > num_bytes)
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "bitmap %lld of column %d overruns the index", (long long)id, column);
+    if (!parse_roaring(b + hdr + off, end - off, seg.num_docs, words, inv->conts, &inv->docs[id]))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed Roaring bitmap for dictId %lld of column %d", (long long)id,
+                  column);
+  }
+  inv->cont_begin[card] = (int32_t)inv->conts.size();
+  inv->bytes = (int64_t)std::max<size_t>(words.size(), 1) * 4;
+  HIP_TRY(hipMalloc(&inv->d_block, inv->bytes));
+  if (!words.empty()) HIP_TRY(hipMemcpy(inv->d_block, words.data(), words.size() * 4, hipMemcpyHostToDevice));
+  if (col.inv && col.inv->d_block) {
+    hipFree(col.inv->d_block);
+    t->device_bytes -= col.inv->bytes;
+  }
+  t->device_bytes += inv->bytes;
+  col.inv = inv;
+  return 0;
+}
+
 int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
   if (!t || !d) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (d->num_dims < 1 || d->num_dims > kMaxStarDims || d->num_nodes < 1 || d->num_docs < 0 || d->num_metrics < 1)
@@ -2571,6 +2801,7 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
   fq.num_aggs = 0;
   fq.aggs = nullptr;
   auto P = std::make_unique<pgpu_plan_s>();
+  P->no_inverted = true;  // the standalone filter kernel reads scan / sorted leaves only
   TRY(plan_create_impl(t, &h, 1, &fq, P.get()));
   Segment* s = P->segs[0];
   const int64_t ngroups = ((int64_t)s->num_docs + 31) / 32;

@@ -92,6 +92,10 @@ __device__ __forceinline__ uint32_t staged_leaf(const StageRegs& R, int sidx, co
     const uint32_t m = docrange_mask(group, L.lo, L.span);
     return L.negate ? ~m : m;
   }
+  if (L.kind == LEAF_BITMAP) {
+    const uint32_t m = L.set[group];
+    return L.negate ? ~m : m;
+  }
   const int b = sidx == 0 ? R.b0 : sidx == 1 ? R.b1 : sidx == 2 ? R.b2 : R.b3;
   const int off = sidx == 0 ? 0 : sidx == 1 ? R.o1 : sidx == 2 ? R.o2 : R.o3;
   return leaf_eval_words(L.kind, L.negate, L.lo, L.span, L.set, sbuf + off + tid * b, b);

@@ -23,6 +23,7 @@ class ColumnData:
     padding_byte: int = 0
     fwd_format: int = L.FWD_FIXED_BIT
     is_sorted: bool = False
+    inv_bytes: bytes = None  # bitmap inverted index (<column>.bitmap.inv), if the column has one
 
 
 @dataclass
@@ -81,6 +82,11 @@ def load_v1_segment_dir(path):
             with open(os.path.join(path, name + ".sv.unsorted.fwd"), "rb") as f:
                 fwd = f.read()
             fmt = L.FWD_FIXED_BIT
+        inv_path = os.path.join(path, name + ".bitmap.inv")
+        inv = None
+        if os.path.exists(inv_path):
+            with open(inv_path, "rb") as f:
+                inv = f.read()
         cols[name] = ColumnData(dtype, card, bits, width, d, fwd, pad if dtype == L.STRING else 0, fmt,
-                                props.get(p + "isSorted", "false") == "true")
+                                props.get(p + "isSorted", "false") == "true", inv)
     return SegmentBuffers(num_docs, cols)

@@ -94,6 +94,77 @@ def build_column(data_type, values, pad_byte=0, is_sorted=None):
                       pad_byte if data_type == L.STRING else 0, fmt, bool(is_sorted))
 
 
+def serialize_roaring(doc_ids, run_optimize=False):
+    """Portable RoaringBitmap serialisation (RoaringBitmap 0.9.x `serialize`, little-endian) of sorted docIds:
+    containers per 65536-doc key, ARRAY when cardinality <= 4096 else BITMAP (1024 u64); with `run_optimize` a
+    container is stored as RUN when that is smaller (`runOptimize`), which switches to the 12347 cookie."""
+    docs = np.asarray(doc_ids, dtype=np.int64)
+    keys = np.unique(docs >> 16)
+    conts = []
+    for k in keys:
+        low = (docs[(docs >> 16) == k] & 0xFFFF).astype(np.int64)
+        card = low.size
+        plain = low.astype("<u2").tobytes() if card <= 4096 else None
+        if plain is None:
+            bm = np.zeros(2048, dtype=np.uint32)
+            np.bitwise_or.at(bm, low >> 5, (np.uint32(1) << (low & 31).astype(np.uint32)))
+            plain = bm.astype("<u4").tobytes()
+        kind, payload = "plain", plain
+        if run_optimize:
+            breaks = np.nonzero(np.diff(low) != 1)[0]
+            starts = np.concatenate([[0], breaks + 1])
+            ends = np.concatenate([breaks, [card - 1]])
+            runs = np.stack([low[starts], low[ends] - low[starts]], axis=1).astype("<u2")
+            run_bytes = struct.pack("<H", len(runs)) + runs.tobytes()
+            if len(run_bytes) < len(plain):
+                kind, payload = "run", run_bytes
+        conts.append((int(k), card, kind, payload))
+    size = len(conts)
+    has_run = any(c[2] == "run" for c in conts)
+    out = bytearray()
+    if has_run:
+        out += struct.pack("<I", 12347 | ((size - 1) << 16))
+        rb = bytearray((size + 7) // 8)
+        for i, c in enumerate(conts):
+            if c[2] == "run":
+                rb[i >> 3] |= 1 << (i & 7)
+        out += rb
+    else:
+        out += struct.pack("<II", 12346, size)
+    for k, card, _, _ in conts:
+        out += struct.pack("<HH", k, card - 1)
+    if not has_run or size >= 4:
+        off = len(out) + 4 * size
+        for _, _, _, payload in conts:
+            out += struct.pack("<I", off)
+            off += len(payload)
+    for c in conts:
+        out += c[3]
+    return bytes(out)
+
+
+def build_inverted_index(dict_ids, cardinality, run_optimize=False):
+    """BitmapInvertedIndexWriter (seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:37-75): big-endian
+    int32 offsets of the (cardinality + 1) bitmap boundaries, counted from the start of the file, then each dictId's
+    serialised RoaringBitmap of docIds."""
+    ids = np.asarray(dict_ids, dtype=np.int64)
+    order = np.argsort(ids, kind="stable")
+    bounds = np.searchsorted(ids[order], np.arange(cardinality + 1))
+    bitmaps = [serialize_roaring(np.sort(order[bounds[i]:bounds[i + 1]]), run_optimize) for i in range(cardinality)]
+    offs = np.cumsum([4 * (cardinality + 1)] + [len(b) for b in bitmaps])
+    return offs.astype(">i4").tobytes() + b"".join(bitmaps)
+
+
+def _dict_ids(c, num_docs):
+    """dictIds of every doc of a column (fixed-bit or sorted pairs)."""
+    if c.fwd_format == L.FWD_SORTED_PAIRS:
+        pairs = np.frombuffer(c.fwd_bytes, dtype=">i4").reshape(-1, 2).astype(np.int64)
+        return np.repeat(np.arange(c.cardinality), np.maximum(pairs[:, 1] - pairs[:, 0] + 1, 0))
+    b = c.bits_per_element
+    bits = np.unpackbits(np.frombuffer(c.fwd_bytes, dtype=np.uint8))[: num_docs * b].reshape(num_docs, b)
+    return (bits.astype(np.int64) << np.arange(b - 1, -1, -1)).sum(axis=1)
+
+
 def _fwd_file_name(name, col):
     return name + (".sv.sorted.fwd" if col.fwd_format == L.FWD_SORTED_PAIRS else ".sv.unsorted.fwd")
 
@@ -125,11 +196,12 @@ def _metadata_lines(segment_name, table_name, num_docs, columns, pad_byte, versi
 
 
 def write_v1_segment_dir(path, schema, values, segment_name="segment_0", table_name="table", pad_byte=0,
-                         sorted_columns=()):
+                         sorted_columns=(), inverted_columns=(), run_optimize=False):
     """Creates a v1 segment directory from column values; returns its SegmentBuffers.
 
     schema: [(name, "INT"|"LONG"|"FLOAT"|"DOUBLE"|"STRING")]; values: {name: sequence}. Columns named in
-    `sorted_columns` are written with the sorted forward index (their values must be non-decreasing)."""
+    `sorted_columns` are written with the sorted forward index (their values must be non-decreasing); columns named
+    in `inverted_columns` also get a bitmap inverted index (`<column>.bitmap.inv`)."""
     os.makedirs(path, exist_ok=True)
     num_docs = len(values[schema[0][0]]) if schema else 0
     cols = {}
@@ -142,6 +214,10 @@ def write_v1_segment_dir(path, schema, values, segment_name="segment_0", table_n
             pairs = np.frombuffer(c.fwd_bytes, dtype=">i4").reshape(-1, 2)
             if np.any(pairs[1:, 0] != pairs[:-1, 1] + 1):
                 raise ValueError("column %s is not sorted in doc order" % name)
+        if name in inverted_columns:
+            c.inv_bytes = build_inverted_index(_dict_ids(c, num_docs), c.cardinality, run_optimize)
+            with open(os.path.join(path, name + ".bitmap.inv"), "wb") as f:
+                f.write(c.inv_bytes)
         cols[name] = c
         with open(os.path.join(path, name + ".dict"), "wb") as f:
             f.write(c.dict_bytes)
@@ -169,6 +245,14 @@ def convert_v1_to_v3(path):
                 index_map.append("%s.%s.startOffset = %d" % (name, index_name, offset))
                 index_map.append("%s.%s.size = %d" % (name, index_name, len(buf) + len(marker)))
                 offset += len(buf) + len(marker)
+        for name in sorted(v1.columns):  # inverted indexes follow every column's dictionary + forward index
+            c = v1.columns[name]
+            if c.inv_bytes is not None:
+                psf.write(marker)
+                psf.write(c.inv_bytes)
+                index_map.append("%s.inverted_index.startOffset = %d" % (name, offset))
+                index_map.append("%s.inverted_index.size = %d" % (name, len(c.inv_bytes) + len(marker)))
+                offset += len(c.inv_bytes) + len(marker)
     with open(os.path.join(v3, INDEX_MAP_FILE_NAME), "w") as f:
         f.write("\n".join(index_map) + "\n")
     with open(os.path.join(path, METADATA_FILE_NAME)) as f:
@@ -227,7 +311,8 @@ def load_v3_segment_dir(v3_path):
         cols[name] = ColumnData(dtype, int(props[p + "cardinality"]), int(props[p + "bitsPerElement"]), width,
                                 buffer(name, "dictionary"), buffer(name, "forward_index"),
                                 pad if dtype == L.STRING else 0,
-                                L.FWD_SORTED_PAIRS if is_sorted else L.FWD_FIXED_BIT, is_sorted)
+                                L.FWD_SORTED_PAIRS if is_sorted else L.FWD_FIXED_BIT, is_sorted,
+                                buffer(name, "inverted_index") if (name, "inverted_index") in entries else None)
     return SegmentBuffers(num_docs, cols)
 
 

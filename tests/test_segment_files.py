@@ -159,3 +159,75 @@ def test_v3_corrupt_marker_and_overrun(tmp_path):
     open(psf_path, "wb").write(bytes(raw[:-4]))
     with pytest.raises(ValueError, match="overruns"):
         load_segment_dir(path)
+
+
+# ------------------------------------------------------------------------------------------- inverted index
+def _decode_roaring(b):
+    """Independent portable-format Roaring reader (the spec the writer and the C++ attach parser follow)."""
+    cookie = struct.unpack_from("<I", b, 0)[0]
+    if cookie & 0xFFFF == 12347:
+        size = (cookie >> 16) + 1
+        runbits = b[4:4 + (size + 7) // 8]
+        pos = 4 + (size + 7) // 8
+        offsets = size >= 4
+    else:
+        assert cookie == 12346
+        size = struct.unpack_from("<I", b, 4)[0]
+        runbits, pos, offsets = None, 8, True
+    desc = [struct.unpack_from("<HH", b, pos + 4 * i) for i in range(size)]
+    pos += 4 * size + (4 * size if offsets else 0)
+    out = []
+    for i, (key, c1) in enumerate(desc):
+        card = c1 + 1
+        if runbits is not None and (runbits[i >> 3] >> (i & 7)) & 1:
+            nruns = struct.unpack_from("<H", b, pos)[0]
+            runs = np.frombuffer(b, dtype="<u2", count=2 * nruns, offset=pos + 2).reshape(-1, 2)
+            vals = np.concatenate([np.arange(int(s), int(s) + int(l) + 1) for s, l in runs])
+            pos += 2 + 4 * nruns
+        elif card <= 4096:
+            vals = np.frombuffer(b, dtype="<u2", count=card, offset=pos).astype(np.int64)
+            pos += 2 * card
+        else:
+            words = np.frombuffer(b, dtype="<u4", count=2048, offset=pos)
+            vals = np.nonzero(np.unpackbits(words.view(np.uint8), bitorder="little"))[0]
+            pos += 8192
+        assert len(vals) == card
+        out.append((key << 16) + np.asarray(vals, dtype=np.int64))
+    assert pos == len(b)
+    return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+
+@pytest.mark.parametrize("run_optimize", [False, True])
+def test_roaring_serialisation_round_trip(run_optimize):
+    from pinot_amd.segment_files import serialize_roaring
+    rng = np.random.default_rng(3)
+    cases = [np.array([0]), np.arange(70000), np.sort(rng.choice(300000, 5000, replace=False)),
+             np.concatenate([np.arange(100, 9000), np.arange(65536 * 3 + 5, 65536 * 3 + 40)]),
+             np.sort(rng.choice(200000, 150000, replace=False)), np.array([], dtype=np.int64)]
+    for docs in cases:
+        b = serialize_roaring(docs, run_optimize)
+        np.testing.assert_array_equal(_decode_roaring(b), docs)
+
+
+def test_inverted_index_files(tmp_path):
+    from pinot_amd.segment_files import build_inverted_index
+    rng = np.random.default_rng(4)
+    n = 140000
+    vals = {"a": rng.integers(0, 9, n).tolist(), "b": rng.integers(0, 3000, n).tolist()}
+    path = str(tmp_path / "inv")
+    seg = write_v1_segment_dir(path, [("a", "INT"), ("b", "INT")], vals, inverted_columns=("a", "b"),
+                               run_optimize=True)
+    for col in ("a", "b"):
+        c = seg.columns[col]
+        assert os.path.exists(os.path.join(path, col + ".bitmap.inv"))
+        offs = np.frombuffer(c.inv_bytes[:4 * (c.cardinality + 1)], dtype=">i4")
+        assert offs[0] == 4 * (c.cardinality + 1) and offs[-1] == len(c.inv_bytes)
+        uniq = np.unique(vals[col])
+        for d in (0, c.cardinality // 2, c.cardinality - 1):
+            docs = _decode_roaring(c.inv_bytes[offs[d]:offs[d + 1]])
+            np.testing.assert_array_equal(docs, np.nonzero(np.asarray(vals[col]) == uniq[d])[0])
+    assert load_v1_segment_dir(path).columns == seg.columns
+    convert_v1_to_v3(path)
+    assert "a.inverted_index.startOffset" in open(os.path.join(path, "v3", "index_map")).read()
+    assert load_segment_dir(path).columns == seg.columns
+    assert build_inverted_index([], 0) == struct.pack(">i", 4)

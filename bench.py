@@ -49,15 +49,19 @@ def parse_args():
     return p.parse_args()
 
 
-def compulsory_bytes(table, handles, query, docs_per_segment):
+def compulsory_bytes(table, handles, query, docs_per_segment, inverted_columns=()):
     """bytes_alg (compulsory-traffic form): full forward-index bytes of every filter column, plus
     the 128-B lines of every other referenced column's forward index that hold >= 1 matched doc, plus the 128-B
-    lines of the group-by / aggregated columns' dictionaries that hold >= 1 matched dictId."""
-    from pinot_amd.query import FilterContext  # noqa: F401
+    lines of the group-by / aggregated columns' dictionaries that hold >= 1 matched dictId.  A filter column whose
+    predicates are all inverted-index leaves (EQ / NOT_EQ / IN / NOT_IN on a column with a bitmap inverted index)
+    costs the scan kernel its materialised docId bitmap, N/8 bytes, instead of its forward index."""
+    from pinot_amd.query import EQ, IN, NOT_EQ, NOT_IN
     preds = []
     if query.filter is not None:
         query.filter.postfix(preds, [])
     filter_cols = sorted({p.column for p in preds})
+    bitmap_cols = {c for c in filter_cols if c in inverted_columns and
+                   all(p.type in (EQ, NOT_EQ, IN, NOT_IN) for p in preds if p.column == c)}
     other_cols = [c for c in query.columns() if c not in filter_cols]
     dict_cols = [c for c in query.group_by] + [c for _, c in query.aggregations if c != "*"]
     dict_cols = sorted(set(dict_cols))
@@ -80,7 +84,7 @@ def compulsory_bytes(table, handles, query, docs_per_segment):
             card, b, dlen, flen = _col_info(table, h, c)
             info[c] = (card, b, flen)
         for c in filter_cols:
-            total += info[c][2]
+            total += ((docs_per_segment + 31) // 32) * 4 if c in bitmap_cols else info[c][2]
         for c in other_cols:
             b = info[c][1]
             if len(docs):
@@ -108,6 +112,7 @@ def _col_info(table, h, c):
 # full forward index of one column (two contradicting EQ leaves on it), so its bytes_alg is exact.
 CALIB_SQL = {
     "adanalytics": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 17532 AND daysSinceEpoch = 17533 GROUP BY daysSinceEpoch",
+    "adanalytics_inv": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 17532 AND daysSinceEpoch = 17533 GROUP BY daysSinceEpoch",
     "c1": "SELECT COUNT(*) FROM t WHERE filt = 1 AND filt = 2 GROUP BY dim",
     "c2": "SELECT COUNT(*) FROM t WHERE f = 1 AND f = 2 GROUP BY d",
     "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
@@ -186,6 +191,25 @@ def attach_star_trees(table, handles, workload, docs):
             for h, st in zip(handles[i:i + 8], ex.map(build, segs)):
                 table.attach_startree(h, st)
                 st.close()
+
+
+def attach_inverted_indexes(table, handles, workload, docs):
+    """Bitmap inverted indexes of the workload's columns: each segment's forward index is read back, the host
+    creator (pgpu_build_inverted_index) writes Pinot's .bitmap.inv bytes, and pgpu_attach_inverted_index pins them."""
+    from concurrent.futures import ThreadPoolExecutor
+    from pinot_amd.segment_files import build_inverted_index_native
+
+    def one(h):
+        out = []
+        for name in workload.inverted_columns:
+            card, bits, _, fwd = table.segment_column_bytes(h, name)
+            out.append((name, build_inverted_index_native(fwd, bits, docs, card)))
+        return h, out
+
+    with ThreadPoolExecutor(8) as ex:
+        for h, out in ex.map(one, handles):
+            for name, inv in out:
+                table.attach_inverted_index(h, name, inv)
 
 
 def cpu_baseline(table, handles, query, workload, docs, args):
@@ -284,6 +308,10 @@ def main():
         t_st = time.perf_counter()
         attach_star_trees(table, handles, w, docs)
         log("rank %d: star-trees built and pinned in %.1f s" % (rank, time.perf_counter() - t_st))
+    if w.inverted_columns:
+        t_inv = time.perf_counter()
+        attach_inverted_indexes(table, handles, w, docs)
+        log("rank %d: inverted indexes built and pinned in %.1f s" % (rank, time.perf_counter() - t_inv))
     if world > 1:
         union_dictionaries(table, q.group_by)
     handles = np.array(handles, dtype=np.int64)
@@ -362,7 +390,7 @@ def main():
     log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
     if not args.no_bytes and not w.star_tree:  # scan-path bytes model; star-tree plans: n/a
-        bytes_alg, matched = compulsory_bytes(table, handles, q, docs)
+        bytes_alg, matched = compulsory_bytes(table, handles, q, docs, w.inverted_columns)
         bytes_alg /= launches  # equal chunks of statistically identical segments: per-launch share
         achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -296,6 +296,13 @@ int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_st
 int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
                                int64_t num_bytes);
 
+/* Host-side bitmap inverted-index creator (OffHeapBitmapInvertedIndexCreator + BitmapInvertedIndexWriter,
+ * seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:60-78) over a fixed-bit forward index: writes
+ * the `<column>.bitmap.inv` bytes (portable Roaring without run containers) into `out` (capacity out_cap) and their
+ * length into *out_len; out == NULL only reports the length.  Pure host code, for segment fixtures and benches. */
+int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, int32_t num_docs, int32_t cardinality,
+                              void* out, int64_t out_cap, int64_t* out_len);
+
 /* Host-side star-tree builder (BaseSingleTreeBuilder + OnHeapSingleTreeBuilder, seglocal/startree/v2/builder/):
  * builds the star-tree of a segment given in Pinot's byte format (the pgpu_segment_desc of pgpu_pin_segment;
  * column_types per column), split order (column indexes), dimensions without star nodes (indexes into the split

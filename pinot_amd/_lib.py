@@ -126,6 +126,7 @@ _PROTOS = {
     "pgpu_plan_scanned_segments": (c_int, [c_voidp, c_u8p]),
     "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_attach_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),
+    "pgpu_build_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32, c_voidp, c_i64, c_i64p]),
     "pgpu_startree_build": (c_int, [ctypes.POINTER(SegmentDesc), c_i32p, c_i32p, c_i32, c_i32p, c_i32,
                                     ctypes.POINTER(AggC), c_i32, c_i32, ctypes.POINTER(c_voidp)]),
     "pgpu_startree_get_desc": (c_int, [c_voidp, ctypes.POINTER(StarTreeDescC)]),

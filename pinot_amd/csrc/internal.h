@@ -184,6 +184,13 @@ struct KBitTask {
   int32_t n;
   int64_t dst;
 };
+// One 2048-word (65536-doc) block of a docbits region: the OR of its tasks [task_begin, task_begin + num_tasks),
+// zero when it has none.  Every block of every region is listed, so the kernel writes the whole buffer.
+struct KBitBlock {
+  int64_t dst;
+  int32_t task_begin;
+  int32_t num_tasks;
+};
 
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
@@ -213,7 +220,8 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
 // In-place exclusive prefix sum of n u32 (one workgroup; n up to a few 10^4).
 int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
-int launch_inv_materialize(const KBitTask* tasks, int64_t num_tasks, uint32_t* docbits, void* stream);
+int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
+                           void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.

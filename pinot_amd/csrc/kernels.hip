@@ -31,24 +31,40 @@ __global__ void gather_ids_kernel(const uint32_t* __restrict__ fwd, int32_t bits
 }
 
 // BitmapBasedFilterOperator's OR of the matching dictIds' bitmaps (BitmapBasedFilterOperator.java:85-98), one
-// workgroup per Roaring container: BITMAP containers OR 2048 words (coalesced, zero words skipped), ARRAY containers
-// set one bit per value.  Atomic ORs: the containers of several dictIds of one IN leaf share docbits words.
-__global__ void inv_materialize_kernel(const KBitTask* __restrict__ tasks, int64_t num_tasks,
-                                       uint32_t* __restrict__ docbits) {
-  for (int64_t t = blockIdx.x; t < num_tasks; t += gridDim.x) {
-    const KBitTask T = tasks[t];
-    uint32_t* dst = docbits + T.dst;
-    if (T.type == CONT_BITMAP) {
-      for (int w = threadIdx.x; w < kContainerWords; w += blockDim.x) {
-        const uint32_t v = T.payload[w];
-        if (v) atomicOr(dst + w, v);
-      }
-    } else {
-      for (int i = threadIdx.x; i < T.n; i += blockDim.x) {
-        const uint32_t v = (T.payload[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
-        atomicOr(dst + (v >> 5), 1u << (v & 31));
+// workgroup per 65536-doc block of a docbits region: BITMAP containers are ORed into registers (thread t owns words
+// t, t + 256, ...), ARRAY containers set bits in an LDS copy of the block, and the block is stored once, coalesced
+// -- no global atomics and no separate zero fill.
+__global__ void __launch_bounds__(256) inv_materialize_kernel(const KBitBlock* __restrict__ blocks, int64_t num_blocks,
+                                                              const KBitTask* __restrict__ tasks,
+                                                              uint32_t* __restrict__ docbits) {
+  __shared__ uint32_t lds[kContainerWords];
+  constexpr int kPer = kContainerWords / 256;
+  for (int64_t b = blockIdx.x; b < num_blocks; b += gridDim.x) {
+    const KBitBlock B = blocks[b];
+    uint32_t acc[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      acc[k] = 0u;
+      lds[threadIdx.x + 256 * k] = 0u;
+    }
+    __syncthreads();
+    for (int32_t i = 0; i < B.num_tasks; ++i) {
+      const KBitTask T = tasks[B.task_begin + i];
+      if (T.type == CONT_BITMAP) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) acc[k] |= T.payload[threadIdx.x + 256 * k];
+      } else {
+        for (int j = threadIdx.x; j < T.n; j += 256) {
+          const uint32_t v = (T.payload[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+          atomicOr(&lds[v >> 5], 1u << (v & 31));
+        }
       }
     }
+    __syncthreads();
+    uint32_t* dst = docbits + B.dst;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) dst[threadIdx.x + 256 * k] = acc[k] | lds[threadIdx.x + 256 * k];
+    __syncthreads();
   }
 }
 
@@ -314,10 +330,12 @@ int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, i
   return PGPU_HIP_OK(hipGetLastError());
 }
 
-int launch_inv_materialize(const KBitTask* tasks, int64_t num_tasks, uint32_t* docbits, void* stream) {
-  if (num_tasks <= 0) return 0;
-  const int64_t grid = num_tasks < 65536 ? num_tasks : 65536;
-  hipLaunchKernelGGL(inv_materialize_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), tasks, num_tasks, docbits);
+int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
+                           void* stream) {
+  if (num_blocks <= 0) return 0;
+  const int64_t grid = num_blocks < 65536 ? num_blocks : 65536;
+  hipLaunchKernelGGL(inv_materialize_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), blocks, num_blocks, tasks,
+                     docbits);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -411,20 +411,21 @@ struct Segment {
 };
 
 struct Scratch {
-  DevBuf docbits, bittasks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
+  DevBuf docbits, bittasks, bitblocks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
-  HostPinned stage, starstage;
+  HostPinned stage, starstage, bitstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
   void release() {
     for (auto& e : cev) if (e) hipEventDestroy(e);
     cev.clear();
-    docbits.release(); bittasks.release();
+    docbits.release(); bittasks.release(); bitblocks.release();
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
     starstage.release();
+    bitstage.release();
     starwork.release();
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
@@ -691,6 +692,7 @@ struct pgpu_plan_s {
   int64_t docbit_words = 0;               // LEAF_BITMAP docId bitmaps of the plan (device words)
   std::vector<std::pair<int64_t, int64_t>> bit_fix;  // (offset of KLeaf.set field in segrec, docbits word offset)
   std::vector<KBitTask> bit_tasks;        // containers ORed into the docbits by inv_materialize_kernel
+  std::vector<KBitBlock> bit_blocks;      // every 65536-doc block of the docbits, with its tasks
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
@@ -1410,6 +1412,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<std::pair<int64_t, int64_t>> set_fix;
     std::vector<std::pair<int64_t, int64_t>> bit_fix;
     std::vector<KBitTask> bit_tasks;
+    std::vector<KBitBlock> bit_blocks;
     int64_t docbit_words = 0;
     std::vector<uint8_t> scanned;
     int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
@@ -1424,12 +1427,21 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   std::vector<int> perm(P->num_leaves);
   for (int l = 0; l < P->num_leaves; ++l) perm[l] = l;
   if (P->pure_and && P->num_leaves > 1) {
-    std::vector<int> first, rest;
+    // FilterOperatorUtils.reorderAndFilterChildOperators (:143-178): sorted-index leaves, then bitmap
+    // (inverted-index) leaves, then scans.
+    std::vector<int> first, second, rest;
     for (int l = 0; l < P->num_leaves; ++l) {
-      bool all_sorted = !P->segs.empty();
-      for (Segment* s : P->segs) all_sorted &= s->cols[q->predicates[l].column].sorted;
-      (all_sorted ? first : rest).push_back(l);
+      const pgpu_predicate& pr = q->predicates[l];
+      const bool eq_in = pr.type == PGPU_PRED_EQ || pr.type == PGPU_PRED_NOT_EQ || pr.type == PGPU_PRED_IN ||
+                         pr.type == PGPU_PRED_NOT_IN;
+      bool all_sorted = !P->segs.empty(), all_inv = !P->segs.empty() && eq_in && !P->no_inverted;
+      for (Segment* s : P->segs) {
+        all_sorted &= s->cols[pr.column].sorted;
+        all_inv &= s->cols[pr.column].inv != nullptr && !s->star;
+      }
+      (all_sorted ? first : all_inv ? second : rest).push_back(l);
     }
+    first.insert(first.end(), second.begin(), second.end());
     first.insert(first.end(), rest.begin(), rest.end());
     perm = first;
     std::vector<int32_t> slots(P->num_leaves);
@@ -1514,6 +1526,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
           C.bit_fix.emplace_back(field, C.docbit_words);
+          const int64_t nblk = ((int64_t)s->num_docs + 65535) >> 16;
+          const size_t t0 = C.bit_tasks.size();
           for (int32_t id : lh.inv_ids)
             for (int32_t ci = inv.cont_begin[id]; ci < inv.cont_begin[id + 1]; ++ci) {
               const InvIndex::Cont& ct = inv.conts[ci];
@@ -1524,7 +1538,18 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
               task.dst = C.docbit_words + (int64_t)ct.key * kContainerWords;
               C.bit_tasks.push_back(task);
             }
-          C.docbit_words += (((int64_t)s->num_docs + 65535) >> 16) * kContainerWords;
+          std::stable_sort(C.bit_tasks.begin() + t0, C.bit_tasks.end(),
+                           [](const KBitTask& x, const KBitTask& y) { return x.dst < y.dst; });
+          size_t ti = t0;
+          for (int64_t kb = 0; kb < nblk; ++kb) {
+            KBitBlock blk;
+            blk.dst = C.docbit_words + kb * kContainerWords;
+            blk.task_begin = (int32_t)ti;
+            while (ti < C.bit_tasks.size() && C.bit_tasks[ti].dst == blk.dst) ++ti;
+            blk.num_tasks = (int32_t)(ti - blk.task_begin);
+            C.bit_blocks.push_back(blk);
+          }
+          C.docbit_words += nblk * kContainerWords;
         }
       }
       C.rec.insert(C.rec.end(), rec.begin(), rec.end());
@@ -1631,10 +1656,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         reinterpret_cast<KSegHdr*>(C.rec.data() + r)->tile_base += (int32_t)tile_shift;
     for (auto& f : C.set_fix) P->set_fix.emplace_back(rec0 + f.first, set0 + f.second);
     for (auto& f : C.bit_fix) P->bit_fix.emplace_back(rec0 + f.first, P->docbit_words + f.second);
-    for (KBitTask task : C.bit_tasks) {
-      task.dst += P->docbit_words;
-      P->bit_tasks.push_back(task);
+    for (KBitBlock blk : C.bit_blocks) {
+      blk.dst += P->docbit_words;
+      blk.task_begin += (int32_t)P->bit_tasks.size();
+      P->bit_blocks.push_back(blk);
     }
+    P->bit_tasks.insert(P->bit_tasks.end(), C.bit_tasks.begin(), C.bit_tasks.end());
     P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
@@ -1748,16 +1775,20 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
   if (P->docbit_words > 0) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
     TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
-    HIP_TRY(hipMemsetAsync(sc->docbits.p, 0, (size_t)P->docbit_words * 4, stream));
-    if (!P->bit_tasks.empty()) {
-      TRY(sc->bittasks.ensure(P->bit_tasks.size() * sizeof(KBitTask)));
-      HIP_TRY(hipMemcpyAsync(sc->bittasks.p, P->bit_tasks.data(), P->bit_tasks.size() * sizeof(KBitTask),
-                             hipMemcpyHostToDevice, stream));
-      if (launch_inv_materialize(sc->bittasks.as<KBitTask>(), (int64_t)P->bit_tasks.size(), sc->docbits.as<uint32_t>(),
-                                 stream))
-        return fail(PGPU_ERR_DEVICE, "inverted-index materialise launch failed: %s",
-                    hipGetErrorString(hipGetLastError()));
-    }
+    TRY(sc->bittasks.ensure(std::max<size_t>(P->bit_tasks.size(), 1) * sizeof(KBitTask)));
+    TRY(sc->bitblocks.ensure(P->bit_blocks.size() * sizeof(KBitBlock)));
+    // staged through pinned memory: asynchronous copies (pageable sources would block the host)
+    const size_t tb = P->bit_tasks.size() * sizeof(KBitTask), bb = P->bit_blocks.size() * sizeof(KBitBlock);
+    TRY(sc->bitstage.ensure(tb + bb));
+    uint8_t* hs = reinterpret_cast<uint8_t*>(sc->bitstage.p);
+    if (tb) memcpy(hs, P->bit_tasks.data(), tb);
+    memcpy(hs + tb, P->bit_blocks.data(), bb);
+    if (tb) HIP_TRY(hipMemcpyAsync(sc->bittasks.p, hs, tb, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(sc->bitblocks.p, hs + tb, bb, hipMemcpyHostToDevice, stream));
+    if (launch_inv_materialize(sc->bitblocks.as<KBitBlock>(), (int64_t)P->bit_blocks.size(),
+                               sc->bittasks.as<KBitTask>(), sc->docbits.as<uint32_t>(), stream))
+      return fail(PGPU_ERR_DEVICE, "inverted-index materialise launch failed: %s",
+                  hipGetErrorString(hipGetLastError()));
   }
   uint64_t* table = reinterpret_cast<uint64_t*>(d_table);
   if (!table) {
@@ -2367,6 +2398,93 @@ bool parse_roaring(const uint8_t* b, int64_t n, int32_t num_docs, std::vector<ui
   return pos <= n;
 }
 }  // namespace
+
+namespace {
+void put_le16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); }
+void put_le32(std::vector<uint8_t>& o, uint32_t v) { put_le16(o, v & 0xFFFF); put_le16(o, v >> 16); }
+
+// RoaringBitmap.serialize of a sorted docId list without run containers (cookie 12346).
+void serialize_roaring_plain(const int32_t* docs, int64_t n, std::vector<uint8_t>& o) {
+  std::vector<std::pair<int64_t, int64_t>> conts;  // [begin, end) per key
+  for (int64_t i = 0; i < n;) {
+    int64_t j = i;
+    while (j < n && (docs[j] >> 16) == (docs[i] >> 16)) ++j;
+    conts.emplace_back(i, j);
+    i = j;
+  }
+  const size_t base = o.size();
+  put_le32(o, 12346);
+  put_le32(o, (uint32_t)conts.size());
+  for (auto& c : conts) {
+    put_le16(o, (uint32_t)(docs[c.first] >> 16));
+    put_le16(o, (uint32_t)(c.second - c.first - 1));
+  }
+  uint32_t off = (uint32_t)(o.size() - base + 4 * conts.size());
+  for (auto& c : conts) {
+    put_le32(o, off);
+    const int64_t card = c.second - c.first;
+    off += card <= 4096 ? (uint32_t)(2 * card) : 8192u;
+  }
+  for (auto& c : conts) {
+    const int64_t card = c.second - c.first;
+    if (card <= 4096) {
+      for (int64_t k = c.first; k < c.second; ++k) put_le16(o, (uint32_t)(docs[k] & 0xFFFF));
+    } else {
+      std::vector<uint32_t> bm(kContainerWords, 0);
+      for (int64_t k = c.first; k < c.second; ++k) bm[(docs[k] & 0xFFFF) >> 5] |= 1u << (docs[k] & 31);
+      for (uint32_t w : bm) put_le32(o, w);
+    }
+  }
+}
+}  // namespace
+
+// Host-side inverted-index creator (OffHeapBitmapInvertedIndexCreator + BitmapInvertedIndexWriter,
+// seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:60-78): dictIds of the MSB-first fixed-bit
+// forward index -> per dictId the sorted docIds -> (card + 1) BE offsets + serialised bitmaps.
+int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, int32_t num_docs, int32_t cardinality,
+                              void* out, int64_t out_cap, int64_t* out_len) {
+  if (!fwd || !out_len || bits < 1 || bits > 31 || num_docs < 0 || cardinality < 1 ||
+      fwd_len < ((int64_t)num_docs * bits + 7) / 8)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad inverted-index build arguments");
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(fwd);
+  std::vector<int32_t> ids(num_docs);
+  for (int64_t d = 0; d < num_docs; ++d) {
+    const int64_t bit = d * bits;
+    uint64_t w = 0;
+    for (int k = 0; k < 5; ++k) {
+      const int64_t byte = (bit >> 3) + k;
+      w = (w << 8) | (byte < fwd_len ? b[byte] : 0);
+    }
+    ids[d] = (int32_t)((w >> (40 - (bit & 7) - bits)) & ((1u << bits) - 1u));
+    if (ids[d] >= cardinality) return fail(PGPU_ERR_INVALID_ARGUMENT, "dictId %d >= cardinality", ids[d]);
+  }
+  std::vector<int64_t> start(cardinality + 1, 0);
+  for (int32_t id : ids) start[id + 1]++;
+  for (int32_t i = 0; i < cardinality; ++i) start[i + 1] += start[i];
+  std::vector<int32_t> docs(num_docs);
+  {
+    std::vector<int64_t> fill(start.begin(), start.end() - 1);
+    for (int32_t d = 0; d < num_docs; ++d) docs[fill[ids[d]]++] = d;
+  }
+  std::vector<uint8_t> body;
+  std::vector<uint32_t> offs(cardinality + 1);
+  const uint32_t hdr = 4u * (uint32_t)(cardinality + 1);
+  for (int32_t i = 0; i < cardinality; ++i) {
+    offs[i] = hdr + (uint32_t)body.size();
+    serialize_roaring_plain(docs.data() + start[i], start[i + 1] - start[i], body);
+  }
+  offs[cardinality] = hdr + (uint32_t)body.size();
+  *out_len = (int64_t)hdr + (int64_t)body.size();
+  if (!out) return 0;
+  if (out_cap < *out_len) return fail(PGPU_ERR_INVALID_ARGUMENT, "output buffer too small");
+  uint8_t* o = reinterpret_cast<uint8_t*>(out);
+  for (int32_t i = 0; i <= cardinality; ++i) {
+    o[4 * i] = (uint8_t)(offs[i] >> 24); o[4 * i + 1] = (uint8_t)(offs[i] >> 16);
+    o[4 * i + 2] = (uint8_t)(offs[i] >> 8); o[4 * i + 3] = (uint8_t)offs[i];
+  }
+  memcpy(o + hdr, body.data(), body.size());
+  return 0;
+}
 
 int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
   if (!t || (!bytes && num_bytes)) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");

@@ -155,6 +155,19 @@ def build_inverted_index(dict_ids, cardinality, run_optimize=False):
     return offs.astype(">i4").tobytes() + b"".join(bitmaps)
 
 
+def build_inverted_index_native(fwd_bytes, bits, num_docs, cardinality):
+    """The same file from the library's host creator (pgpu_build_inverted_index; no GPU involved)."""
+    import ctypes
+    lib = L.load()
+    fwd = ctypes.create_string_buffer(bytes(fwd_bytes), max(len(fwd_bytes), 1))
+    n = ctypes.c_int64()
+    L.check(lib.pgpu_build_inverted_index(fwd, len(fwd_bytes), bits, num_docs, cardinality, None, 0, ctypes.byref(n)))
+    out = ctypes.create_string_buffer(max(n.value, 1))
+    L.check(lib.pgpu_build_inverted_index(fwd, len(fwd_bytes), bits, num_docs, cardinality, out, n.value,
+                                          ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
 def _dict_ids(c, num_docs):
     """dictIds of every doc of a column (fixed-bit or sorted pairs)."""
     if c.fwd_format == L.FWD_SORTED_PAIRS:

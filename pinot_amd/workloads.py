@@ -34,7 +34,7 @@ def double_table(n, column_index, lo, hi):
 
 class Workload:
     def __init__(self, name, schema, gen, sql, description, num_groups_limit=100_000, cpu_sample_segments=64,
-                 star_tree=None):
+                 star_tree=None, inverted_columns=()):
         self.name = name
         self.schema = schema          # [(column, type)]
         self.gen = gen                # generator spec per column (table column order)
@@ -43,6 +43,7 @@ class Workload:
         self.num_groups_limit = num_groups_limit  # query option numGroupsLimit of the config
         self.cpu_sample_segments = cpu_sample_segments  # bench CPU-baseline sample (~10-30 s of oracle work)
         self.star_tree = star_tree    # None, or {split_order, pairs, max_leaf_records}: built per segment at setup
+        self.inverted_columns = tuple(inverted_columns)  # bitmap inverted indexes built per segment at setup
 
 
 def adanalytics():
@@ -58,6 +59,16 @@ def adanalytics():
     sql = ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN 17849 AND 17856 "
            "AND accountId IN (123456789) GROUP BY daysSinceEpoch TOP 100")
     return Workload("adanalytics", schema, gen, sql, "C3 AdAnalytics filtered GROUP BY day")
+
+
+def adanalytics_inv():
+    """C3 over a production-style table: a bitmap inverted index on accountId (BitmapBasedFilterOperator leaf,
+    evaluated before the daysSinceEpoch scan)."""
+    w = adanalytics()
+    w.name = "adanalytics_inv"
+    w.description = "C3 AdAnalytics with an inverted index on accountId"
+    w.inverted_columns = ("accountId",)
+    return w
 
 
 def c1():
@@ -114,4 +125,4 @@ def c4():
     return Workload("c4", schema, gen, sql, "C4 star-tree multi-dim GROUP BY", star_tree=star)
 
 
-WORKLOADS = {"adanalytics": adanalytics, "c1": c1, "c2": c2, "c4": c4, "c5": c5}
+WORKLOADS = {"adanalytics": adanalytics, "adanalytics_inv": adanalytics_inv, "c1": c1, "c2": c2, "c4": c4, "c5": c5}

@@ -231,3 +231,14 @@ def test_inverted_index_files(tmp_path):
     assert "a.inverted_index.startOffset" in open(os.path.join(path, "v3", "index_map")).read()
     assert load_segment_dir(path).columns == seg.columns
     assert build_inverted_index([], 0) == struct.pack(">i", 4)
+
+
+def test_native_inverted_index_builder_matches_writer():
+    """pgpu_build_inverted_index (host code of the library) writes the same bytes as the Python creator."""
+    from pinot_amd.segment_files import build_column, build_inverted_index, build_inverted_index_native
+    rng = np.random.default_rng(6)
+    for n, card in ((1, 1), (5000, 3), (140000, 9), (70001, 2000)):
+        c = build_column(L.INT, rng.integers(0, card, n).tolist(), is_sorted=False)
+        ids = _unpack(c.fwd_bytes, c.bits_per_element, n)
+        native = build_inverted_index_native(c.fwd_bytes, c.bits_per_element, n, c.cardinality)
+        assert native == build_inverted_index(ids, c.cardinality)

@@ -1538,8 +1538,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
               task.dst = C.docbit_words + (int64_t)ct.key * kContainerWords;
               C.bit_tasks.push_back(task);
             }
-          std::stable_sort(C.bit_tasks.begin() + t0, C.bit_tasks.end(),
-                           [](const KBitTask& x, const KBitTask& y) { return x.dst < y.dst; });
+          if (lh.inv_ids.size() > 1)  // one dictId's containers are already in key order
+            std::stable_sort(C.bit_tasks.begin() + t0, C.bit_tasks.end(),
+                             [](const KBitTask& x, const KBitTask& y) { return x.dst < y.dst; });
           size_t ti = t0;
           for (int64_t kb = 0; kb < nblk; ++kb) {
             KBitBlock blk;

@@ -816,26 +816,41 @@ bool parse_literal(int type, const char* lit, bool allow_star, Literal* out) {
 
 // Dictionary.insertionIndexOf (BaseImmutableDictionary.java:86-120) of a converted literal: index if present,
 // else -(insertion point + 1).
+// Search of a sorted, duplicate-free numeric dictionary: up to 3 interpolation probes narrow [lo, hi] (dictionaries
+// of dense ids / days / uniformly spread values resolve in one probe, touching one cache line instead of the ~14
+// of a cold binary search -- planning does one lookup per predicate per segment), then the binary search of
+// BaseImmutableDictionary.insertionIndexOf on what is left.  Same result as the plain binary search: probes only
+// move the bounds past values known to be smaller / larger.
+template <class T>
+int sorted_search(const std::vector<T>& a, T v) {
+  int lo = 0, hi = (int)a.size() - 1;
+  for (int round = 0; round < 3 && lo < hi; ++round) {
+    const T a_lo = a[lo], a_hi = a[hi];
+    if (!(v > a_lo) || !(v < a_hi)) break;  // at or outside the ends (NaN-free dictionaries)
+    const double f = ((double)v - (double)a_lo) / ((double)a_hi - (double)a_lo);
+    int pos = lo + (int)(f * (double)(hi - lo));
+    pos = pos < lo + 1 ? lo + 1 : (pos > hi - 1 ? hi - 1 : pos);
+    if (a[pos] < v) lo = pos + 1;
+    else if (a[pos] > v) hi = pos - 1;
+    else return pos;
+  }
+  while (lo <= hi) {
+    const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+    if (a[mid] < v) lo = mid + 1;
+    else if (a[mid] > v) hi = mid - 1;
+    else return mid;
+  }
+  return -(lo + 1);
+}
+
 int insertion_index(const Column& c, const Literal& v) {
   const Dict& d = c.dict;
   int lo = 0, hi = (int)d.size() - 1;
   switch (d.type) {
     case PGPU_INT: case PGPU_LONG:
-      while (lo <= hi) {
-        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-        if (d.iv[mid] < v.i) lo = mid + 1;
-        else if (d.iv[mid] > v.i) hi = mid - 1;
-        else return mid;
-      }
-      return -(lo + 1);
+      return sorted_search<int64_t>(d.iv, v.i);
     case PGPU_FLOAT: case PGPU_DOUBLE:
-      while (lo <= hi) {
-        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-        if (d.dv[mid] < v.d) lo = mid + 1;
-        else if (d.dv[mid] > v.d) hi = mid - 1;
-        else return mid;
-      }
-      return -(lo + 1);
+      return sorted_search<double>(d.dv, v.d);
     default: {
       const uint8_t* lv = reinterpret_cast<const uint8_t*>(v.s.data());
       const size_t ln = v.s.size();

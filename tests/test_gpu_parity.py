@@ -648,10 +648,16 @@ def test_inverted_index_leaves(oracle, gpu_lib, tmp_path, run_optimize):
         assert seg.columns["a"].inv_bytes is not None
         segs.append(seg)
         orc.append(_fixed_bit_view(seg))
-    t, hs = gpu_table(schema, segs)
-    plain = GpuTable(schema)  # the same segments without inverted indexes: scan leaves
     from dataclasses import replace
     from pinot_amd.segment import SegmentBuffers
+    t, hs = gpu_table(schema, segs)
+    # a mixed table: the same data once more, this time with segment 1 lacking the indexes (bitmap leaves in some
+    # segments, scan leaves in others, one plan)
+    mixed = GpuTable(schema)
+    hm = [mixed.pin_segment(s if k != 1 else
+                            SegmentBuffers(s.num_docs, {c: replace(d, inv_bytes=None) for c, d in s.columns.items()}))
+          for k, s in enumerate(segs)]
+    plain = GpuTable(schema)  # the same segments without inverted indexes: scan leaves
     hp = [plain.pin_segment(SegmentBuffers(s.num_docs, {c: replace(d, inv_bytes=None) for c, d in s.columns.items()}))
           for s in segs]
     try:
@@ -662,10 +668,21 @@ def test_inverted_index_leaves(oracle, gpu_lib, tmp_path, run_optimize):
             rp = plain.execute_groupby(hp, q)
             assert r.stats.num_docs_scanned == rp.stats.num_docs_scanned, sql
             assert r.stats.num_entries_scanned_in_filter <= rp.stats.num_entries_scanned_in_filter, sql
+            assert_same(mixed.execute_groupby(hm, q), oracle.run_groupby(schema, orc, q), q, schema)
         r = t.execute_groupby(hs, parse_query("SELECT COUNT(*) FROM t WHERE a IN (2, 3) GROUP BY g"))
         assert r.stats.num_entries_scanned_in_filter == 0
+        for sql in ("SELECT COUNT(*), SUM(v), MIN(v), MAX(g) FROM t WHERE a = 3",
+                    "SELECT COUNT(*), SUM(v) FROM t WHERE b NOT IN (5, 6) AND a IN (1, 3, 7)",
+                    "SELECT COUNT(*) FROM t WHERE a = 3 AND a <> 3"):
+            q = parse_query(sql)
+            o = oracle.run_groupby(schema, orc, q)
+            from pinot_amd.executor import aggregation_defaults
+            exp = o.groups[()] if o.groups else aggregation_defaults(q.aggregations)
+            assert t.execute_aggregation(hs, q).values == list(exp), sql
+            assert mixed.execute_aggregation(hm, q).values == list(exp), sql
     finally:
         t.close()
+        mixed.close()
         plain.close()
 
 

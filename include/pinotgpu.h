@@ -293,7 +293,8 @@ int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_st
  * matching dictIds' containers are ORed into a docId bitmap on the device per query, and the leaf scans no
  * forward-index entries.  Malformed bitmaps (bad cookie, overruns, docIds >= numDocs) return
  * PGPU_ERR_INVALID_ARGUMENT.  Attach at segment load, before queries reference the segment (as Pinot builds its
- * DataSource readers): re-attaching replaces the column's index and must not race queries on that segment. */
+ * DataSource readers): re-attaching replaces the column's index and must not race plan creation on that segment;
+ * plans created before a re-attach (or an unpin) keep the index they were planned on alive until destroyed. */
 int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
                                int64_t num_bytes);
 

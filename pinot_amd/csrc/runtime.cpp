@@ -355,6 +355,9 @@ struct Dict {
 // of every dictId in one device block (ARRAY / BITMAP payloads, internal.h), their directory kept on the host.
 struct InvIndex {
   struct Cont { int64_t word; int32_t type, n, key; };
+  // Owned: freed with the last owner (the segment column, or a plan whose bitmap tasks point into it), so a
+  // re-attach or an unpin never frees memory an existing plan still reads.
+  ~InvIndex() { if (d_block) hipFree(d_block); }
   void* d_block = nullptr;
   int64_t bytes = 0;
   // Per dictId, in one 16-byte record so planning takes one cache miss per (segment, dictId): its containers
@@ -613,10 +616,9 @@ void free_segment(pgpu_table_s* t, Segment* s) {
     if (c.d_lut) hipFree(c.d_lut);
     if (c.d_key) hipFree(c.d_key);
     if (c.d_val) hipFree(c.d_val);
-    if (c.inv && c.inv->d_block) {
-      hipFree(c.inv->d_block);
+    if (c.inv) {
       t->device_bytes -= c.inv->bytes;
-      c.inv->d_block = nullptr;
+      c.inv.reset();
     }
     t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) + (c.d_key ? 16 * std::max(c.card, 1) : 0);
   }
@@ -695,6 +697,7 @@ struct pgpu_plan_s {
   std::vector<std::pair<int64_t, int64_t>> bit_fix;  // (offset of KLeaf.set field in segrec, docbits word offset)
   std::vector<KBitTask> bit_tasks;        // containers ORed into the docbits by inv_materialize_kernel
   std::vector<KBitBlock> bit_blocks;      // every 65536-doc block of the docbits, with its tasks
+  std::vector<std::shared_ptr<InvIndex>> inv_refs;  // inverted indexes the bit tasks point into (kept alive)
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
@@ -829,7 +832,10 @@ int sorted_search(const std::vector<T>& a, T v) {
   for (int round = 0; round < 3 && lo < hi; ++round) {
     const T a_lo = a[lo], a_hi = a[hi];
     if (!(v > a_lo) || !(v < a_hi)) break;  // at or outside the ends (NaN-free dictionaries)
+    // LONG values past 2^53 can round to equal doubles, and +-inf ends give inf / inf: interpolation only while
+    // the fraction is a finite number in [0, 1] (the binary search below finishes the job either way).
     const double f = ((double)v - (double)a_lo) / ((double)a_hi - (double)a_lo);
+    if (!(f >= 0.0 && f <= 1.0)) break;
     int pos = lo + (int)(f * (double)(hi - lo));
     pos = pos < lo + 1 ? lo + 1 : (pos > hi - 1 ? hi - 1 : pos);
     if (a[pos] < v) lo = pos + 1;
@@ -1214,6 +1220,18 @@ struct ExecCtx {
   int64_t slabs_used = 0;  // MODE_LDS: slabs written by the scan launches so far (launches pack them back to back)
 };
 
+// True when an int64 accumulator cannot overflow for SUM / AVG over integer column `col` of these segments.
+bool int_sum_fits(const std::vector<Segment*>& segs, int col) {
+  long double bound = 0;
+  for (const Segment* s : segs) {
+    const Dict& d = s->cols[col].dict;
+    if (d.iv.empty()) continue;
+    const long double m = std::max(std::fabs((long double)d.iv.front()), std::fabs((long double)d.iv.back()));
+    bound += m * (long double)s->num_docs;
+  }
+  return bound < 0x1p62L;
+}
+
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X);
 int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C);
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
@@ -1317,7 +1335,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     if (type == PGPU_STRING) return fail(PGPU_ERR_UNSUPPORTED, "numeric aggregation over a STRING column");
     int kind;
     switch (a.fn) {
-      case PGPU_AGG_SUM: case PGPU_AGG_AVG: kind = is_int_type(type) ? SLOT_SUM_I64 : SLOT_SUM_F64; break;
+      case PGPU_AGG_SUM: case PGPU_AGG_AVG:
+        // Integer columns sum exactly in int64 unless the plan could overflow it: |sum| <= sum over segments of
+        // numDocs x max |value| (the sorted dictionary's ends).  Past 2^62 the slot accumulates the doubles of
+        // the values (Pinot's own arithmetic, SumAggregationFunction.java:66-73) instead of wrapping.
+        kind = is_int_type(type) && int_sum_fits(P->segs, a.column) ? SLOT_SUM_I64 : SLOT_SUM_F64;
+        break;
       case PGPU_AGG_MIN: kind = SLOT_MIN_KEY; break;
       case PGPU_AGG_MAX: kind = SLOT_MAX_KEY; break;
       default: return fail(PGPU_ERR_UNSUPPORTED, "aggregation function %d", a.fn);
@@ -1430,6 +1453,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<std::pair<int64_t, int64_t>> bit_fix;
     std::vector<KBitTask> bit_tasks;
     std::vector<KBitBlock> bit_blocks;
+    std::vector<std::shared_ptr<InvIndex>> inv_refs;
     int64_t docbit_words = 0;
     std::vector<uint8_t> scanned;
     int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
@@ -1542,6 +1566,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         if (lh.kind == LEAF_BITMAP) {  // docId bitmap region: whole 65536-doc containers
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
+          C.inv_refs.push_back(s->cols[q->predicates[perm[k]].column].inv);
           C.bit_fix.emplace_back(field, C.docbit_words);
           const int64_t nblk = ((int64_t)s->num_docs + 65535) >> 16;
           const size_t t0 = C.bit_tasks.size();
@@ -1682,6 +1707,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->bit_blocks.push_back(blk);
     }
     P->bit_tasks.insert(P->bit_tasks.end(), C.bit_tasks.begin(), C.bit_tasks.end());
+    P->inv_refs.insert(P->inv_refs.end(), C.inv_refs.begin(), C.inv_refs.end());
     P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
@@ -2376,6 +2402,8 @@ bool parse_roaring(const uint8_t* b, int64_t n, int32_t num_docs, std::vector<ui
       for (int64_t r = 0; r < nruns; ++r) {
         const uint32_t start = u16(pos + 4 * r), len = u16(pos + 4 * r + 2);
         if (start + len > 65535) return false;
+        // the runs may not hold more values than the declared cardinality (bounds the expansion)
+        if ((int64_t)vals.size() + len + 1 > card) return false;
         for (uint32_t v = start; v <= start + len; ++v) vals.push_back(v);
       }
       pos += nruns * 4;
@@ -2402,6 +2430,7 @@ bool parse_roaring(const uint8_t* b, int64_t n, int32_t num_docs, std::vector<ui
       for (int w = 0; w < kContainerWords; ++w)
         if (bm[w]) { c += __builtin_popcount(bm[w]); top = w * 32 + 31 - __builtin_clz(bm[w]); }
       if (((int64_t)key << 16) + top >= num_docs) return false;
+      if (c != card) return false;  // overlapping runs / a bitmap whose popcount is not its cardinality
       conts.push_back({(int64_t)words.size(), CONT_BITMAP, (int32_t)c, key});
       words.insert(words.end(), bm.begin(), bm.end());
     } else {
@@ -2540,10 +2569,7 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
   inv->bytes = (int64_t)std::max<size_t>(words.size(), 1) * 4;
   HIP_TRY(hipMalloc(&inv->d_block, inv->bytes));
   if (!words.empty()) HIP_TRY(hipMemcpy(inv->d_block, words.data(), words.size() * 4, hipMemcpyHostToDevice));
-  if (col.inv && col.inv->d_block) {
-    hipFree(col.inv->d_block);
-    t->device_bytes -= col.inv->bytes;
-  }
+  if (col.inv) t->device_bytes -= col.inv->bytes;  // freed when the last plan using it is destroyed
   t->device_bytes += inv->bytes;
   col.inv = inv;
   return 0;

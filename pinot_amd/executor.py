@@ -190,10 +190,14 @@ class GpuTable:
         h = ctypes.c_int64()
         L.check(self.lib.pgpu_pin_segment(self.handle, ctypes.byref(desc), ctypes.byref(h)))
         self._dict_cache.clear()
-        for name in self.names:
-            inv = getattr(seg.columns[name], "inv_bytes", None)
-            if inv is not None:
-                self.attach_inverted_index(h.value, name, inv)
+        try:
+            for name in self.names:
+                inv = getattr(seg.columns[name], "inv_bytes", None)
+                if inv is not None:
+                    self.attach_inverted_index(h.value, name, inv)
+        except Exception:
+            self.lib.pgpu_unpin_segment(self.handle, h.value)  # no half-loaded segment stays pinned
+            raise
         return h.value
 
     def attach_inverted_index(self, handle, column, inv_bytes):

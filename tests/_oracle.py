@@ -266,6 +266,43 @@ def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capac
         o.or_free_result(ctypes.byref(res))
 
 
+def run_groupby_arrays(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000):
+    """run_groupby for numeric group-by keys, returned as numpy arrays (large results: millions of groups):
+    (keys [n, num_group_by] int64 / float64, values [num_aggs, n] float64, avg_counts [num_aggs, n] int64, stats)."""
+    o = lib()
+    types = {n: (L.TYPE_NAMES[t] if isinstance(t, str) else t) for n, t in schema}
+    ktypes = [types[c] for c in q.group_by]
+    assert all(t != L.STRING for t in ktypes), "numeric group-by keys only"
+    segs = [_OrSeg(schema, s) for s in segments]
+    arr = (OrSegment * max(len(segs), 1))(*[s.seg for s in segs])
+    oq, keep = _or_query(schema, q, combine, max_initial_capacity)
+    res = OrResult()
+    msg = ctypes.create_string_buffer(512)
+    rc = o.or_execute_groupby(arr, len(segs), ctypes.byref(oq), nthreads, ctypes.byref(res), msg, 512)
+    if rc != 0:
+        raise RuntimeError("oracle error %d: %s" % (rc, msg.value.decode()))
+    try:
+        n, nk, na = res.num_groups, len(ktypes), len(q.aggregations)
+        raw = np.frombuffer(ctypes.string_at(res.key_blob, n * nk * 8), dtype=np.uint8) if n and nk else \
+            np.zeros(0, dtype=np.uint8)
+        keys = np.zeros((n, nk), dtype=object if len(set(ktypes)) > 1 else np.float64)
+        words = raw.view(np.int64).reshape(n, nk) if n and nk else np.zeros((n, nk), dtype=np.int64)
+        if all(t in (L.INT, L.LONG) for t in ktypes):
+            keys = words.copy()
+        else:
+            keys = np.stack([words[:, j] if t in (L.INT, L.LONG) else words[:, j].view(np.float64)
+                             for j, t in enumerate(ktypes)], axis=1).astype(np.float64) if nk else keys
+        vals = np.ctypeslib.as_array(res.values, shape=(na * n,)).reshape(na, n).copy() if n and na else \
+            np.zeros((na, n))
+        cnts = np.ctypeslib.as_array(res.avg_counts, shape=(na * n,)).reshape(na, n).copy() if n and na else \
+            np.zeros((na, n), dtype=np.int64)
+        stats = (res.num_docs_scanned, res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter,
+                 res.num_total_docs)
+        return keys, vals, cnts, stats
+    finally:
+        o.or_free_result(ctypes.byref(res))
+
+
 def filter_bitmap(schema, seg, q):
     o = lib()
     s = _OrSeg(schema, seg)

@@ -444,6 +444,37 @@ def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, launches, monkey
         t.close()
 
 
+@pytest.mark.parametrize("magnitude", [2 ** 60, 2 ** 44], ids=["past_int64", "past_2^53"])
+def test_long_sum_overflow_guard(oracle, gpu_lib, magnitude):
+    """SUM / AVG over a LONG column whose sum could leave int64 (values near 2^60 over 20k docs) accumulate the
+    values' doubles instead of wrapping; sums between 2^53 and 2^62 stay exact int64.  Pinot sums doubles in doc
+    order (SumAggregationFunction.java:66-73), so both match the oracle within the double-sum tolerance."""
+    rng = np.random.default_rng(magnitude % 1000)
+    schema = [("g", "INT"), ("x", "LONG")]
+    n = 20_000
+    segs = [oracle.make_segment(schema, {"g": rng.integers(0, 5, n),
+                                         "x": rng.integers(magnitude // 2, magnitude, n)}) for _ in range(2)]
+    t, hs = gpu_table(schema, segs)
+    try:
+        for sql in ("SELECT SUM(x), AVG(x), COUNT(*), MAX(x) FROM t GROUP BY g", "SELECT SUM(x), MIN(x) FROM t"):
+            q = parse_query(sql)
+            r = t.execute_groupby(hs, q)
+            o = oracle.run_groupby(schema, segs, q)
+            g = r.as_dict()
+            assert set(g) == set(o.groups)
+            for k, ov in o.groups.items():
+                for (fn, _), x, y in zip(q.aggregations, g[k], ov):
+                    if fn == "AVG":
+                        assert x.count == y.count and x.sum == pytest.approx(y.sum, rel=REL)
+                    elif fn == "SUM":
+                        assert x == pytest.approx(y, rel=REL)
+                        assert abs(x) > 2 ** 53
+                    else:
+                        assert x == y
+    finally:
+        t.close()
+
+
 # ------------------------------------------------------------------------------------------------ aggregation-only
 @pytest.mark.parametrize("case", K.KAT_AGG["cases"], ids=lambda c: "%s_%s" % (c["test"], c["variant"]))
 def test_kat_inter_segment_aggregation(sv, case):
@@ -707,7 +738,32 @@ def test_inverted_index_malformed(gpu_lib):
         offs = np.cumsum([16, len(out_of_range), 0, 0]).astype(">i4").tobytes()
         with pytest.raises(L.PinotGpuError):
             t.attach_inverted_index(h, "a", offs + out_of_range)
+        # a RUN container whose runs hold more values than its declared cardinality (0..3 declared as 2 values)
+        run_bm = (np.array([12347], "<u4").tobytes() + b"\x01" + np.array([0, 1], "<u2").tobytes() +
+                  np.array([1, 0, 3], "<u2").tobytes())
+        offs = np.cumsum([16, len(run_bm), 0, 0]).astype(">i4").tobytes()
+        with pytest.raises(L.PinotGpuError):
+            t.attach_inverted_index(h, "a", offs + run_bm)
         r = t.execute_groupby([h], parse_query("SELECT COUNT(*) FROM t WHERE a IN (1, 2) GROUP BY a"))
         assert {k: v[0] for k, v in r.as_dict().items()} == {(1,): 2, (2,): 1}
+    finally:
+        t.close()
+
+
+def test_long_literals_beyond_double_precision(oracle, gpu_lib):
+    """Dictionary lookups of LONG literals that differ by less than one double ulp (values around 2^60, where
+    interpolation in double precision degenerates) find the exact dictId (BaseImmutableDictionary.insertionIndexOf)."""
+    base = 2 ** 60
+    vals = np.array([base + (i % 7) for i in range(5000)] + [-(2 ** 62), 2 ** 62], dtype=np.int64)
+    schema = [("x", "LONG"), ("g", "INT")]
+    seg = oracle.make_segment(schema, {"x": vals, "g": np.arange(len(vals)) % 3})
+    t, hs = gpu_table(schema, [seg])
+    try:
+        for sql in ("SELECT COUNT(*) FROM t WHERE x = %d GROUP BY g" % (base + 3),
+                    "SELECT COUNT(*) FROM t WHERE x BETWEEN %d AND %d GROUP BY g" % (base + 1, base + 4),
+                    "SELECT COUNT(*) FROM t WHERE x IN (%d, %d, 5) GROUP BY g" % (base + 2, base + 6),
+                    "SELECT COUNT(*) FROM t WHERE x > %d GROUP BY g" % (base + 5)):
+            q = parse_query(sql)
+            assert_same(t.execute_groupby(hs, q), oracle.run_groupby(schema, [seg], q), q, schema)
     finally:
         t.close()

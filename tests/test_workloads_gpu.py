@@ -1,0 +1,142 @@
+"""GPU parity on the benchmarked data: every BASELINE.json configuration (pinot_amd/workloads.py: C1, C2, C3
+AdAnalytics, C4 star-tree, C5 high-cardinality) built by the device generator (pgpu_generate_segment) exactly as
+bench.py builds it, at the bench's segment size (1M docs) and a reduced segment count.
+
+Each test checks, per segment and column, that the device-built dictionary and forward-index bytes equal the
+oracle's generator (or_gen_i64 / or_gen_f64) followed by Pinot segment creation (or_build_column_*: sorted
+dictionary + MSB-first fixed-bit forward index), and that the HIP query result equals the oracle's operator +
+combine over the oracle-built bytes: bit-exact for COUNT / integer SUM / MIN / MAX, 1e-9 relative for the double
+SUM (C2's md).  C4 (star-tree) is checked by the reference's star-tree == scan rule (BaseStarTreeV2Test.java:219-295).
+"""
+import numpy as np
+import pytest
+
+from pinot_amd import _lib as L
+from pinot_amd.executor import GpuTable
+from pinot_amd.query import parse_query
+from pinot_amd.workloads import SEGMENT_DOCS, WORKLOADS
+
+pytestmark = pytest.mark.gpu
+REL = 1e-9
+
+# workload -> segments (1M docs each) in the test
+SIZES = {"c1": 1, "c2": 4, "adanalytics": 8, "adanalytics_inv": 4, "c5": 2, "c4": 3}
+
+
+def _oracle_segments(oracle, w, nseg, docs, table=None, handles=None):
+    """Oracle-built segments from the oracle's generator; when a table is given, also checks that the device-built
+    bytes of every column equal them."""
+    from pinot_amd.segment import SegmentBuffers
+    segs = []
+    for i in range(nseg):
+        cols = {}
+        for (name, typ), g in zip(w.schema, w.gen):
+            vals = oracle.gen_values(g, i * docs, docs)
+            cols[name] = oracle.build_column(L.TYPE_NAMES[typ], vals)
+            if table is not None:
+                card, bits, d, f = table.segment_column_bytes(handles[i], name)
+                c = cols[name]
+                assert (card, bits) == (c.cardinality, c.bits_per_element), (name, i)
+                assert d == c.dict_bytes, "dictionary bytes of %s, segment %d" % (name, i)
+                assert f == c.fwd_bytes, "forward-index bytes of %s, segment %d" % (name, i)
+        segs.append(SegmentBuffers(docs, cols))
+    return segs
+
+
+def _gpu_arrays(table, r, q):
+    """GPU result as (keys [n, k] in value space, values [num_aggs, n] float64, counts of AVG)."""
+    cols = r.gid_columns
+    keys = np.stack([np.asarray(table.dictionary(c))[g] for c, g in zip(q.group_by, cols)], axis=1) if cols else \
+        np.zeros((len(r), 0))
+    vals, cnts = [], []
+    for fn, v, e, c in r._col[2]:
+        vals.append(v if v is not None else e.astype(np.float64))
+        cnts.append(c if c is not None else np.zeros(len(r), dtype=np.int64))
+    return keys, np.array(vals).reshape(len(q.aggregations), len(r)), np.array(cnts).reshape(len(q.aggregations), len(r))
+
+
+def _sorted_by_key(keys, vals, cnts):
+    order = np.lexsort(keys.T[::-1]) if keys.shape[1] else np.arange(len(keys))
+    return keys[order], vals[:, order], cnts[:, order]
+
+
+def assert_same_arrays(table, r, orc, q, schema):
+    types = dict(schema)
+    gk, gv, gc = _sorted_by_key(*_gpu_arrays(table, r, q))
+    ok, ov, oc, _ = orc
+    ok, ov, oc = _sorted_by_key(ok.astype(gk.dtype) if len(ok) else ok.reshape(0, gk.shape[1]), ov, oc)
+    assert gk.shape == ok.shape, (gk.shape, ok.shape)
+    np.testing.assert_array_equal(gk, ok)
+    for a, (fn, col) in enumerate(q.aggregations):
+        fp = col != "*" and types[col] in ("FLOAT", "DOUBLE")
+        if fp and fn in ("SUM", "AVG"):
+            np.testing.assert_allclose(gv[a], ov[a], rtol=REL, atol=1e-6)
+        else:
+            np.testing.assert_array_equal(gv[a], ov[a], err_msg="%s(%s)" % (fn, col))
+        if fn == "AVG":
+            np.testing.assert_array_equal(gc[a], oc[a])
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "adanalytics", "c5"])
+def test_workload_generator_and_query(oracle, gpu_lib, name):
+    w = WORKLOADS[name]()
+    nseg, docs = SIZES[name], SEGMENT_DOCS
+    q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+    t = GpuTable(w.schema)
+    try:
+        hs = [t.generate_segment(w.gen, row0=i * docs, num_docs=docs) for i in range(nseg)]
+        segs = _oracle_segments(oracle, w, nseg, docs, t, hs)
+        r = t.execute_groupby(hs, q)
+        o = oracle.run_groupby_arrays(w.schema, segs, q)
+        assert len(r) == len(o[0]) > 0
+        assert_same_arrays(t, r, o, q, w.schema)
+        st = r.stats
+        assert (st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs) == \
+            (o[3][0], o[3][2], o[3][3])
+    finally:
+        t.close()
+
+
+def test_workload_adanalytics_inverted_index(oracle, gpu_lib):
+    """C3 over the production-style layout of bench.py --workload adanalytics_inv: bitmap inverted indexes on
+    accountId built by the host creator from the device-built forward index; same answer as the oracle's scan."""
+    from bench import attach_inverted_indexes
+    w = WORKLOADS["adanalytics_inv"]()
+    nseg, docs = SIZES["adanalytics_inv"], SEGMENT_DOCS
+    q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+    t = GpuTable(w.schema)
+    try:
+        hs = [t.generate_segment(w.gen, row0=i * docs, num_docs=docs) for i in range(nseg)]
+        attach_inverted_indexes(t, hs, w, docs)
+        segs = _oracle_segments(oracle, w, nseg, docs)
+        r = t.execute_groupby(hs, q)
+        o = oracle.run_groupby_arrays(w.schema, segs, q)
+        assert_same_arrays(t, r, o, q, w.schema)
+        assert r.stats.num_docs_scanned == o[3][0]
+    finally:
+        t.close()
+
+
+def test_workload_c4_star_tree(oracle, gpu_lib):
+    """C4: the star-tree path (per-segment star-trees built by the host builder from the device-built bytes, as
+    bench.py does) gives the oracle's scan answer on the same data, and so does the scan path (useStarTree=false)."""
+    from bench import attach_star_trees
+    w = WORKLOADS["c4"]()
+    nseg, docs = SIZES["c4"], SEGMENT_DOCS
+    q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+    t = GpuTable(w.schema)
+    try:
+        hs = [t.generate_segment(w.gen, row0=i * docs, num_docs=docs) for i in range(nseg)]
+        segs = _oracle_segments(oracle, w, nseg, docs, t, hs)
+        attach_star_trees(t, hs, w, docs)
+        o = oracle.run_groupby_arrays(w.schema, segs, q)
+        r = t.execute_groupby(hs, q)
+        assert_same_arrays(t, r, o, q, w.schema)
+        q.use_star_tree = False
+        rs = t.execute_groupby(hs, q)
+        assert_same_arrays(t, rs, o, q, w.schema)
+        # the scan path reads every doc; the star-tree path reads pre-aggregated documents only
+        assert rs.stats.num_docs_scanned == o[3][0]
+        assert r.stats.num_docs_scanned < rs.stats.num_docs_scanned
+    finally:
+        t.close()

@@ -221,6 +221,20 @@ int pgpu_plan_timing(pgpu_plan plan, double* out3);
  * segment's dictionaries (EmptyFilterOperator, core/plan/FilterPlanNode.java:146-176).  out holds num_segments. */
 int pgpu_plan_scanned_segments(pgpu_plan plan, uint8_t* out);
 
+/* numEntriesScannedInFilter of one segment (ExecutionStatistics, AndDocIdSet.getNumEntriesScannedInFilter,
+ * core/operator/docidsets/AndDocIdSet.java:148-155) from the doc sets of its predicates: `filter` is the query's
+ * postfix program; leaf_types[i] is predicate i's leaf operator in this segment (enum pgpu_leaf_type, the outcome
+ * of FilterOperatorUtils.getLeafFilterOperator, core/operator/filter/FilterOperatorUtils.java:42-82) and
+ * leaf_masks[i] its matching docs (bit d % 32 of word d / 32; may be NULL for EMPTY / ALL leaves).  Pinot's
+ * iterators (AndDocIdSet / OrDocIdSet merging, SVScanDocIdIterator.applyAnd, AndDocIdIterator leap-frog,
+ * OrDocIdIterator) are replayed over the sets.  The plans compute the same statistic on the device; this entry is
+ * the host form (a caller holding the doc sets, tests). */
+enum pgpu_leaf_type { PGPU_LEAF_EMPTY = 0, PGPU_LEAF_MATCH_ALL = 1, PGPU_LEAF_SCAN = 2, PGPU_LEAF_SORTED = 3,
+                      PGPU_LEAF_BITMAP = 4 };
+int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t num_filter_ops, const int32_t* leaf_types,
+                                const uint32_t* const* leaf_masks, int32_t num_leaves, int32_t num_docs,
+                                int64_t* out);
+
 /* ---- results: AggregationGroupByResult (core/query/aggregation/groupby/AggregationGroupByResult.java:31-81) */
 int pgpu_result_num_groups(pgpu_result r, int64_t* n);
 /* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */

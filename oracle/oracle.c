@@ -496,11 +496,15 @@ static inline int pred_apply(const pred_eval* e, int id) {
 /* ======================================================================================= filter operators */
 
 /* Operator tree after FilterPlanNode.constructPhysicalOperator (core/plan/FilterPlanNode.java:146-247) and
- * FilterOperatorUtils.getAnd/OrFilterOperator (:87-135): EMPTY, MATCH_ALL, SCAN leaf, AND, OR, NOT. */
-enum { FN_EMPTY = 0, FN_ALL = 1, FN_SCAN = 2, FN_AND = 3, FN_OR = 4, FN_NOT = 5 };
+ * FilterOperatorUtils (:42-135): EMPTY, MATCH_ALL, leaf operators (scan / sorted-index / bitmap-index), AND, OR,
+ * NOT.  Leaf choice = FilterOperatorUtils.getLeafFilterOperator (:42-82): RANGE on a sorted column ->
+ * SortedIndexBasedFilterOperator, else scan (no range indexes here); EQ / NOT_EQ / IN / NOT_IN on a sorted column
+ * -> sorted, else on a column with an inverted index -> BitmapBasedFilterOperator, else scan.  NOT is not part of
+ * the 0.10 FilterContext; it is modelled as a scan-based iterator over its child (match = child does not match). */
+enum { FN_EMPTY = 0, FN_ALL = 1, FN_SCAN = 2, FN_AND = 3, FN_OR = 4, FN_NOT = 5, FN_SORTED = 6, FN_BITMAP = 7 };
 typedef struct fnode {
   int type;
-  int pred;              /* SCAN: predicate index */
+  int pred;              /* leaves: predicate index */
   int nchild;
   struct fnode** child;
 } fnode;
@@ -512,8 +516,19 @@ static void fn_free(fnode* n) {
   free(n->child); free(n);
 }
 
+/* reorderAndFilterChildOperators priorities (FilterOperatorUtils.java:143-178). */
+static int and_priority(const fnode* n) {
+  switch (n->type) {
+    case FN_SORTED: return 0;
+    case FN_BITMAP: return 1;
+    case FN_AND: return 3;
+    case FN_OR: return 4;
+    default: return 5; /* scan (single-value columns), NOT */
+  }
+}
+
 /* Build from the postfix program, simplifying always-true/false leaves exactly as FilterPlanNode does. */
-static fnode* build_filter_tree(const or_query* q, const pred_eval* evals, char* msg, int ml) {
+static fnode* build_filter_tree(const or_segment* seg, const or_query* q, const pred_eval* evals, char* msg, int ml) {
   if (q->num_filter_ops == 0) return fn_new(FN_ALL);
   fnode** stack = calloc((size_t)q->num_filter_ops + 1, sizeof(fnode*));
   int sp = 0;
@@ -521,10 +536,18 @@ static fnode* build_filter_tree(const or_query* q, const pred_eval* evals, char*
     const or_filter_op* op = &q->filter[i];
     if (op->op == OR_OP_PRED) {
       const pred_eval* e = &evals[op->arg];
+      const or_predicate* pr = &q->predicates[op->arg];
+      const or_column* c = &seg->columns[pr->column];
       fnode* n;
       if (e->always_false) n = fn_new(FN_EMPTY);          /* FilterOperatorUtils.java:44-46 */
       else if (e->always_true) n = fn_new(FN_ALL);        /* :47-48 */
-      else { n = fn_new(FN_SCAN); n->pred = op->arg; }
+      else {
+        int type = FN_SCAN;
+        if (c->is_sorted) type = FN_SORTED;                                    /* :57-58, :73-74 */
+        else if (pr->type != OR_PRED_RANGE && c->has_inverted) type = FN_BITMAP; /* :76-77 */
+        n = fn_new(type);
+        n->pred = op->arg;
+      }
       stack[sp++] = n;
     } else if (op->op == OR_OP_NOT) {
       if (sp < 1) goto bad;
@@ -546,10 +569,10 @@ static fnode* build_filter_tree(const or_query* q, const pred_eval* evals, char*
         fnode* c = kids[j];
         if (result) { fn_free(c); continue; }
         if (is_and) {
-          if (c->type == FN_EMPTY) { result = c; continue; }      /* FilterPlanNode.java:152-155 */
+          if (c->type == FN_EMPTY) { result = c; continue; }      /* getAndFilterOperator :90-95 */
           if (c->type == FN_ALL) { fn_free(c); continue; }
         } else {
-          if (c->type == FN_ALL) { result = c; continue; }        /* :167-170 */
+          if (c->type == FN_ALL) { result = c; continue; }        /* getOrFilterOperator :115-120 */
           if (c->type == FN_EMPTY) { fn_free(c); continue; }
         }
         keep[nk++] = c;
@@ -559,16 +582,12 @@ static fnode* build_filter_tree(const or_query* q, const pred_eval* evals, char*
       else if (nk == 1) { result = keep[0]; free(keep); }
       else {
         result = fn_new(is_and ? FN_AND : FN_OR);
-        if (is_and) {
-          /* reorderAndFilterChildOperators (FilterOperatorUtils.java:143-178): stable sort by priority
-           * AND=3, OR=4, scan=5 (no indexes in this model). */
+        if (is_and) { /* stable sort by priority */
           fnode** sorted = malloc(sizeof(fnode*) * (size_t)nk);
           int ns = 0;
-          for (int pr = 3; pr <= 5; pr++)
-            for (int j = 0; j < nk; j++) {
-              int p = keep[j]->type == FN_AND ? 3 : keep[j]->type == FN_OR ? 4 : 5;
-              if (p == pr) sorted[ns++] = keep[j];
-            }
+          for (int pr = 0; pr <= 5; pr++)
+            for (int j = 0; j < nk; j++)
+              if (and_priority(keep[j]) == pr) sorted[ns++] = keep[j];
           free(keep);
           keep = sorted;
         }
@@ -589,38 +608,11 @@ bad:
   return NULL;
 }
 
-/* ---- DocId iterators: SVScanDocIdIterator (:56-66), AndDocIdIterator (:40-67), OrDocIdIterator (:25-130),
- * MatchAllDocIdIterator.  NOT is evaluated as a scan over its child (not part of the 0.10 FilterContext). */
-typedef struct iter {
-  int type;
-  int next_doc;            /* scan / and / all */
-  int64_t scanned;         /* scan: _numEntriesScanned */
-  const pred_eval* eval;
-  const or_column* col;
-  int num_docs;
-  int n;                   /* children */
-  struct iter** kids;
-  int* next_ids;           /* or: _nextDocIds */
-  int num_not_exhausted;   /* or */
-  int prev_doc;            /* or */
-  const fnode* node;       /* not */
-  const or_segment* seg;
-  const pred_eval* evals;
-  const or_query* q;
-} iter;
-
-static int it_next(iter* it);
-static int it_advance(iter* it, int target);
-
-static inline int scan_match(iter* it, int doc) {
-  return pred_apply(it->eval, fixedbit_read(it->col->fwd, doc, it->col->bits));
-}
-
 static int node_match(const fnode* n, const or_segment* seg, const pred_eval* evals, const or_query* q, int doc) {
   switch (n->type) {
     case FN_EMPTY: return 0;
     case FN_ALL: return 1;
-    case FN_SCAN: {
+    case FN_SCAN: case FN_SORTED: case FN_BITMAP: {
       const or_column* c = &seg->columns[q->predicates[n->pred].column];
       return pred_apply(&evals[n->pred], fixedbit_read(c->fwd, doc, c->bits));
     }
@@ -630,25 +622,69 @@ static int node_match(const fnode* n, const or_segment* seg, const pred_eval* ev
   }
 }
 
+/* ---- DocId iterators (core/operator/dociditerators/, docidsets/):
+ *   IT_SCAN  SVScanDocIdIterator (:56-94): next / advance / applyAnd, counting _numEntriesScanned (NOT: same, over
+ *            the negated child);
+ *   IT_IDX   SortedDocIdIterator / BitmapDocIdIterator / RangelessBitmapDocIdIterator: a docId set, no entries
+ *            scanned (`sorted` tells SortedDocIdIterator apart for AndDocIdSet's classification);
+ *   IT_AND   AndDocIdIterator leap-frog (:40-67);  IT_OR  OrDocIdIterator (:25-130).
+ * Sorted-index and bitmap-index doc sets are built from the forward index (the docs a sorted / inverted index
+ * returns are exactly the predicate's matches) without counting entries. */
+enum { IT_EMPTY = 0, IT_ALL = 1, IT_SCAN = 2, IT_IDX = 3, IT_AND = 4, IT_OR = 5 };
+typedef struct iter {
+  int type;
+  int next_doc;            /* scan / idx / and / all */
+  int64_t scanned;         /* scan: _numEntriesScanned */
+  const fnode* node;       /* scan: the leaf (or NOT) node */
+  uint64_t* bits;          /* idx: docId set */
+  int sorted;              /* idx: a SortedDocIdIterator */
+  int num_docs;
+  int n;                   /* children */
+  struct iter** kids;
+  int* next_ids;           /* or: _nextDocIds */
+  int num_not_exhausted;   /* or */
+  int prev_doc;            /* or */
+  const or_segment* seg;
+  const pred_eval* evals;
+  const or_query* q;
+} iter;
+
+static int it_next(iter* it);
+static int it_advance(iter* it, int target);
+
+static inline int scan_match(iter* it, int doc) {
+  if (it->node->type == FN_NOT) return !node_match(it->node->child[0], it->seg, it->evals, it->q, doc);
+  return node_match(it->node, it->seg, it->evals, it->q, doc);
+}
+
+static int idx_next(iter* it) {
+  int nw = (it->num_docs + 63) / 64;
+  if (it->next_doc >= it->num_docs) return EOF_DOC;
+  int w = it->next_doc >> 6;
+  uint64_t m = it->bits[w] & (~0ull << (it->next_doc & 63));
+  while (!m) {
+    if (++w >= nw) return EOF_DOC;
+    m = it->bits[w];
+  }
+  int d = w * 64 + __builtin_ctzll(m);
+  if (d >= it->num_docs) return EOF_DOC;
+  it->next_doc = d + 1;
+  return d;
+}
+
 static int it_next(iter* it) {
   switch (it->type) {
-    case FN_EMPTY: return EOF_DOC;
-    case FN_ALL: return it->next_doc < it->num_docs ? it->next_doc++ : EOF_DOC;
-    case FN_SCAN: /* SVScanDocIdIterator.next :56-66 */
+    case IT_EMPTY: return EOF_DOC;
+    case IT_ALL: return it->next_doc < it->num_docs ? it->next_doc++ : EOF_DOC;
+    case IT_IDX: return idx_next(it);
+    case IT_SCAN: /* SVScanDocIdIterator.next :56-66 */
       while (it->next_doc < it->num_docs) {
         int d = it->next_doc++;
         it->scanned++;
         if (scan_match(it, d)) return d;
       }
       return EOF_DOC;
-    case FN_NOT:
-      while (it->next_doc < it->num_docs) {
-        int d = it->next_doc++;
-        it->scanned++;
-        if (!node_match(it->node->child[0], it->seg, it->evals, it->q, d)) return d;
-      }
-      return EOF_DOC;
-    case FN_AND: { /* AndDocIdIterator.next :40-67 */
+    case IT_AND: { /* AndDocIdIterator.next :40-67 */
       int max_doc = it->next_doc, max_idx = -1, index = 0;
       while (index < it->n) {
         if (index == max_idx) { index++; continue; }
@@ -661,7 +697,7 @@ static int it_next(iter* it) {
       it->next_doc = max_doc;
       return it->next_doc++;
     }
-    default: { /* FN_OR: OrDocIdIterator.next */
+    default: { /* IT_OR: OrDocIdIterator.next */
       int next = INT32_MAX;
       int exhausted = 0;
       for (int i = 0; i < it->num_not_exhausted; i++) {
@@ -687,10 +723,10 @@ static int it_next(iter* it) {
 
 static int it_advance(iter* it, int target) {
   switch (it->type) {
-    case FN_EMPTY: return EOF_DOC;
-    case FN_ALL: it->next_doc = target; return it_next(it);
-    case FN_SCAN: case FN_NOT: it->next_doc = target; return it_next(it); /* SVScanDocIdIterator.advance :69-72 */
-    case FN_AND: it->next_doc = target; return it_next(it);
+    case IT_EMPTY: return EOF_DOC;
+    case IT_ALL: case IT_IDX: case IT_SCAN: case IT_AND: /* SVScanDocIdIterator.advance :69-72, ... */
+      it->next_doc = target;
+      return it_next(it);
     default: { /* OrDocIdIterator.advance */
       int next = INT32_MAX;
       int exhausted = 0;
@@ -716,41 +752,120 @@ static int it_advance(iter* it, int target) {
 }
 
 typedef struct { iter** all; int n, cap; } iter_pool;
-static iter* it_build(const fnode* n, const or_segment* seg, const pred_eval* evals, const or_query* q,
-                      iter_pool* pool) {
+static iter* it_new(int type, const or_segment* seg, const pred_eval* evals, const or_query* q, iter_pool* pool) {
   iter* it = calloc(1, sizeof(iter));
   if (pool->n == pool->cap) { pool->cap = pool->cap ? pool->cap * 2 : 16; pool->all = realloc(pool->all, sizeof(iter*) * pool->cap); }
   pool->all[pool->n++] = it;
-  it->type = n->type;
+  it->type = type;
   it->num_docs = seg->num_docs;
   it->seg = seg;
   it->evals = evals;
   it->q = q;
-  if (n->type == FN_SCAN) {
-    it->eval = &evals[n->pred];
-    it->col = &seg->columns[q->predicates[n->pred].column];
-  } else if (n->type == FN_NOT) {
-    it->node = n;
-  } else if (n->type == FN_AND || n->type == FN_OR) {
-    it->n = n->nchild;
-    it->kids = calloc((size_t)n->nchild, sizeof(iter*));
-    for (int i = 0; i < n->nchild; i++) it->kids[i] = it_build(n->child[i], seg, evals, q, pool);
-    if (n->type == FN_OR) {
-      it->next_ids = malloc(sizeof(int) * (size_t)n->nchild);
-      for (int i = 0; i < n->nchild; i++) it->next_ids[i] = -1;
-      it->num_not_exhausted = n->nchild;
-      it->prev_doc = -1;
-    }
+  return it;
+}
+static iter* it_new_idx(uint64_t* bits, int sorted, const or_segment* seg, const pred_eval* evals, const or_query* q,
+                        iter_pool* pool) {
+  iter* it = it_new(IT_IDX, seg, evals, q, pool);
+  it->bits = bits;
+  it->sorted = sorted;
+  return it;
+}
+static iter* it_new_multi(int type, iter** kids, int n, const or_segment* seg, const pred_eval* evals,
+                          const or_query* q, iter_pool* pool) {
+  iter* it = it_new(type, seg, evals, q, pool);
+  it->n = n;
+  it->kids = kids;
+  if (type == IT_OR) {
+    it->next_ids = malloc(sizeof(int) * (size_t)(n ? n : 1));
+    for (int i = 0; i < n; i++) it->next_ids[i] = -1;
+    it->num_not_exhausted = n;
+    it->prev_doc = -1;
   }
   return it;
 }
+
+/* FilterBlockDocIdSet.iterator() of node n: AndDocIdSet.iterator (:60-146) / OrDocIdSet.iterator (:57-110) build
+ * their children's iterators first, then merge index-based ones (sorted ranges, bitmaps) into one bitmap; an AND
+ * with index-based and scan-based children runs the scans' applyAnd over it (numEntriesScanned += its size). */
+static iter* it_build(const fnode* n, const or_segment* seg, const pred_eval* evals, const or_query* q,
+                      iter_pool* pool) {
+  const int nd = seg->num_docs, nw = (nd + 63) / 64;
+  switch (n->type) {
+    case FN_EMPTY: return it_new(IT_EMPTY, seg, evals, q, pool);
+    case FN_ALL: return it_new(IT_ALL, seg, evals, q, pool);
+    case FN_SCAN: case FN_NOT: {
+      iter* it = it_new(IT_SCAN, seg, evals, q, pool);
+      it->node = n;
+      return it;
+    }
+    case FN_SORTED: case FN_BITMAP: {
+      uint64_t* bits = calloc((size_t)(nw ? nw : 1), 8);
+      for (int d = 0; d < nd; d++) if (node_match(n, seg, evals, q, d)) bits[d >> 6] |= 1ull << (d & 63);
+      return it_new_idx(bits, n->type == FN_SORTED, seg, evals, q, pool);
+    }
+    default: break;
+  }
+  const int k = n->nchild;
+  iter** kids = calloc((size_t)k, sizeof(iter*));
+  for (int i = 0; i < k; i++) kids[i] = it_build(n->child[i], seg, evals, q, pool);
+  int nsorted = 0, nbitmap = 0, nscan = 0, nrem = 0;
+  for (int i = 0; i < k; i++) {
+    if (kids[i]->type == IT_IDX) { if (kids[i]->sorted) nsorted++; else nbitmap++; }
+    else if (kids[i]->type == IT_SCAN) nscan++;
+    else nrem++;
+  }
+  const int nidx = nsorted + nbitmap;
+  if (n->type == FN_AND) {
+    if (!((nidx > 0 && nscan > 0) || nidx > 1)) return it_new_multi(IT_AND, kids, k, seg, evals, q, pool);
+    uint64_t* bits = malloc(sizeof(uint64_t) * (size_t)(nw ? nw : 1));
+    for (int w = 0; w < nw; w++) bits[w] = ~0ull;
+    for (int i = 0; i < k; i++)
+      if (kids[i]->type == IT_IDX) for (int w = 0; w < nw; w++) bits[w] &= kids[i]->bits[w];
+    for (int i = 0; i < k; i++) { /* ScanBasedDocIdIterator.applyAnd (SVScanDocIdIterator.java:75-94) */
+      iter* sc = kids[i];
+      if (sc->type != IT_SCAN) continue;
+      for (int w = 0; w < nw; w++) {
+        uint64_t m = bits[w];
+        while (m) {
+          int b = __builtin_ctzll(m);
+          m &= m - 1;
+          int d = w * 64 + b;
+          if (d >= nd) { bits[w] &= ~(1ull << b); continue; }
+          sc->scanned++;
+          if (!scan_match(sc, d)) bits[w] &= ~(1ull << b);
+        }
+      }
+    }
+    iter* rangeless = it_new_idx(bits, 0, seg, evals, q, pool);
+    if (nrem == 0) { free(kids); return rangeless; }
+    iter** ks = calloc((size_t)nrem + 1, sizeof(iter*));
+    int j = 0;
+    ks[j++] = rangeless;
+    for (int i = 0; i < k; i++) if (kids[i]->type != IT_IDX && kids[i]->type != IT_SCAN) ks[j++] = kids[i];
+    free(kids);
+    return it_new_multi(IT_AND, ks, j, seg, evals, q, pool);
+  }
+  /* OR */
+  if (nidx <= 1) return it_new_multi(IT_OR, kids, k, seg, evals, q, pool);
+  uint64_t* bits = calloc((size_t)(nw ? nw : 1), 8);
+  for (int i = 0; i < k; i++)
+    if (kids[i]->type == IT_IDX) for (int w = 0; w < nw; w++) bits[w] |= kids[i]->bits[w];
+  iter* merged = it_new_idx(bits, 0, seg, evals, q, pool);
+  if (nidx == k) { free(kids); return merged; }
+  iter** ks = calloc((size_t)(k - nidx) + 1, sizeof(iter*));
+  int j = 0;
+  ks[j++] = merged;
+  for (int i = 0; i < k; i++) if (kids[i]->type != IT_IDX) ks[j++] = kids[i];
+  free(kids);
+  return it_new_multi(IT_OR, ks, j, seg, evals, q, pool);
+}
 static int64_t pool_scanned(iter_pool* p) {
   int64_t s = 0;
-  for (int i = 0; i < p->n; i++) if (p->all[i]->type == FN_SCAN || p->all[i]->type == FN_NOT) s += p->all[i]->scanned;
+  for (int i = 0; i < p->n; i++) if (p->all[i]->type == IT_SCAN) s += p->all[i]->scanned;
   return s;
 }
 static void pool_free(iter_pool* p) {
-  for (int i = 0; i < p->n; i++) { free(p->all[i]->kids); free(p->all[i]->next_ids); free(p->all[i]); }
+  for (int i = 0; i < p->n; i++) { free(p->all[i]->kids); free(p->all[i]->next_ids); free(p->all[i]->bits); free(p->all[i]); }
   free(p->all);
 }
 
@@ -957,7 +1072,7 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
     int st = build_pred_eval(seg, &q->predicates[i], &evals[i], r->msg, sizeof r->msg);
     if (st) { r->status = st; for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return; }
   }
-  fnode* root = build_filter_tree(q, evals, r->msg, sizeof r->msg);
+  fnode* root = build_filter_tree(seg, q, evals, r->msg, sizeof r->msg);
   if (!root) { r->status = -1; for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return; }
   iter_pool pool = {0};
   iter* it = it_build(root, seg, evals, q, &pool);
@@ -1286,7 +1401,7 @@ int or_filter_bitmap(const or_segment* seg, const or_query* q, uint64_t* bits, c
     int st = build_pred_eval(seg, &q->predicates[i], &evals[i], msg, ml);
     if (st) { for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return st; }
   }
-  fnode* root = build_filter_tree(q, evals, msg, ml);
+  fnode* root = build_filter_tree(seg, q, evals, msg, ml);
   if (!root) { for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return -1; }
   memset(bits, 0, sizeof(uint64_t) * (size_t)((seg->num_docs + 63) / 64));
   for (int d = 0; d < seg->num_docs; d++)

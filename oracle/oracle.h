@@ -46,7 +46,10 @@ typedef struct {
   int32_t bits;         /* bitsPerElement = getNumBitsPerValue(cardinality - 1) */
   int32_t entry_width;  /* bytes per dictionary entry: 4 / 8 / numBytesPerValue for strings */
   int32_t padding_byte; /* string dictionary padding byte (0 for segments built since 0.3) */
-  int32_t is_sorted;    /* column.X.isSorted; informational (the forward index here is always fixed-bit) */
+  int32_t is_sorted;    /* column.X.isSorted: predicates run as SortedIndexBasedFilterOperator (the forward index
+                           here is always fixed-bit; the sorted docId ranges are read from it) */
+  int32_t has_inverted; /* a bitmap inverted index is loaded: EQ / NOT_EQ / IN / NOT_IN run as
+                           BitmapBasedFilterOperator (docIds read from the forward index) */
   const uint8_t* dict;  /* BIG_ENDIAN fixed-width sorted values (BaseImmutableDictionary.java:45-60) */
   const uint8_t* fwd;   /* MSB-first packed dictIds (FixedBitSVForwardIndexWriter.java:39-50) */
 } or_column;

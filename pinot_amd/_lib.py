@@ -53,6 +53,10 @@ class PredicateC(ctypes.Structure):
                 ("values", c_char_pp), ("upper_inclusive", c_i32), ("reserved", c_i32)]
 
 
+# pgpu_leaf_type: Pinot's leaf operator of a predicate in one segment (pgpu_filter_entries_scanned)
+LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP = 0, 1, 2, 3, 4
+
+
 class FilterOpC(ctypes.Structure):
     _fields_ = [("op", c_i32), ("arg", c_i32)]
 
@@ -143,6 +147,8 @@ _PROTOS = {
     "pgpu_result_stats": (c_int, [c_voidp, c_i64p]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
+    "pgpu_filter_entries_scanned": (c_int, [ctypes.POINTER(FilterOpC), c_i32, c_i32p, ctypes.POINTER(c_voidp), c_i32,
+                                            c_i32, c_i64p]),
     "pgpu_generate_segment": (c_int, [c_voidp, ctypes.POINTER(GenColumnC), c_i32, c_i64, c_i32, c_i64p]),
     "pgpu_segment_column_info": (c_int, [c_voidp, c_i64, c_int, c_i32p, c_i32p, c_i64p, c_i64p]),
     "pgpu_segment_column_bytes": (c_int, [c_voidp, c_i64, c_int, c_u8p, c_u8p]),

@@ -189,7 +189,6 @@ __device__ __forceinline__ uint64_t slot_init(int kind) {
 }
 
 // Leaf descriptors of the current segment held in registers (reloaded only when the segment changes).
-constexpr int kFastLeaves = 4;
 struct LeafReg {
   const uint32_t* fwd;
   const uint32_t* set;

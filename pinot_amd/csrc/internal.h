@@ -30,7 +30,8 @@ constexpr int kMaxStage = 4;                // distinct filter columns staged in
 constexpr int kQueueCap = 1024;             // matched-doc queue entries per workgroup (LDS)
 constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
-constexpr int kDenseGroupMin = 256;         // matches per wave-tile (of 2048 docs) above which whole groups are decoded
+constexpr int kDenseGroupMin = 256;
+constexpr int kFastLeaves = 4;              // pure-AND programs up to this many leaves keep them in registers         // matches per wave-tile (of 2048 docs) above which whole groups are decoded
 
 // LEAF_DOCRANGE: a predicate on a sorted column (SortedIndexBasedFilterOperator, core/operator/filter/
 // SortedIndexBasedFilterOperator.java:51-125): docIds [lo, lo + span), evaluated without reading any column.
@@ -68,8 +69,11 @@ struct KSegHdr {
   int32_t num_docs;
   int32_t tile_base;  // first tile of this segment in the plan's tile space
   int32_t num_tiles;
-  int32_t pad;
+  int32_t stats;      // numEntriesScannedInFilter counted in the scan kernel (filter_stats.h): STATS_* kind in bits
+                      // 0-1; STATS_CHAIN: bit 4 + k = leaf k (evaluation order) is a scan whose applyAnd input is
+                      // counted; STATS_LEAP2: leaves of scans A / B in bits 8-9 / 10-11
 };
+enum KStats : int32_t { KSTATS_NONE = 0, KSTATS_CHAIN = 1, KSTATS_LEAP2 = 2 };
 
 struct KParams {
   const uint8_t* segs;     // num_segs records of seg_stride bytes
@@ -98,7 +102,18 @@ struct KParams {
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
-  unsigned long long* stats;      // [0] docs matched
+  unsigned long long* stats;      // [0] docs matched, [2] entries scanned in filter (STATS_CHAIN / LEAP2 segments)
+  // STATS_LEAP2 segments: per (tile, wave) the wave's transfer map of AndDocIdIterator over scans A, B (packed:
+  // cost from entry "A scanning" bits 0-23, from "B scanning" bits 24-47, exit states bits 48-49)
+  uint64_t* leap_maps;
+};
+
+// leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to
+// out + out_word + leaf * ceil(numDocs / 32) (STATS_GENERIC segments, replayed on the host).
+struct KMaskJob {
+  int32_t rec;
+  int32_t group0;
+  int64_t out_word;
 };
 
 // ---------------------------------------------------------------------------------------------- star-tree
@@ -220,6 +235,11 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
 // In-place exclusive prefix sum of n u32 (one workgroup; n up to a few 10^4).
 int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
+// Per STATS_LEAP2 record of a launch: composes its (tile, wave) maps in doc order into the segment's count
+// (stats[2] += ...).
+int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint64_t* maps,
+                         unsigned long long* stats, void* stream);
+int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);

@@ -267,6 +267,44 @@ __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, 
   }
 }
 
+// ---------------------------------------------------------------------------------------------- filter stats
+// numEntriesScannedInFilter of STATS_LEAP2 segments (AndDocIdIterator over two SVScanDocIdIterators,
+// AndDocIdIterator.java:40-67): the scan kernel leaves one transfer map per (tile, wave) -- the entries counted
+// and the exit state for each entry state -- and one thread per segment composes them in doc order from the
+// initial state (scan A at doc 0).
+__global__ void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride, int32_t num_segs,
+                                     const uint64_t* __restrict__ maps, unsigned long long* __restrict__ stats) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long total = 0;
+  if (s < num_segs) {
+    const KSegHdr* h = reinterpret_cast<const KSegHdr*>(segs + (int64_t)s * seg_stride);
+    if ((h->stats & 3) == KSTATS_LEAP2) {
+      const uint64_t* m = maps + (int64_t)h->tile_base * (kBlock / 64);
+      const int64_t n = (int64_t)h->num_tiles * (kBlock / 64);
+      uint32_t state = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        const uint64_t w = m[i];
+        total += state ? (w >> 24) & 0xFFFFFFull : w & 0xFFFFFFull;
+        state = (uint32_t)(w >> (48 + state)) & 1u;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
+  if ((threadIdx.x & 63) == 0 && total) atomicAdd(stats + 2, total);
+}
+
+// The leaves' match bitmaps of STATS_GENERIC segments (the replay of filter_stats.cpp runs on the host).
+__global__ __launch_bounds__(kBlock) void leaf_masks_kernel(const KParams p, const KMaskJob* __restrict__ jobs,
+                                                           uint32_t* __restrict__ out) {
+  const KMaskJob J = jobs[blockIdx.x];
+  const SegView S = seg_view(p, J.rec);
+  const int64_t ngroups = ((int64_t)S.hdr->num_docs + 31) >> 5;
+  const int64_t g = (int64_t)J.group0 + threadIdx.x;
+  if (g >= ngroups) return;
+  for (int l = 0; l < p.num_leaves; ++l)
+    out[J.out_word + (int64_t)l * ngroups + g] = leaf_mask(S.leaves[l], S.cols[p.leaf_col[l]], g);
+}
+
 // ---------------------------------------------------------------------------------------------- generator
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -468,6 +506,20 @@ int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream) {
   if (grid > 4096) grid = 4096;
   const size_t lds = (size_t)kMaxStack * kBlock * sizeof(uint32_t);
   hipLaunchKernelGGL(filter_bitmap_kernel, dim3((unsigned)grid), dim3(kBlock), lds, S(stream), q, out_words);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint64_t* maps,
+                         unsigned long long* stats, void* stream) {
+  if (num_segs <= 0) return 0;
+  hipLaunchKernelGGL(leap2_compose_kernel, dim3((num_segs + 255) / 256), dim3(256), 0, S(stream), segs, seg_stride,
+                     num_segs, maps, stats);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream) {
+  if (num_jobs <= 0) return 0;
+  hipLaunchKernelGGL(leaf_masks_kernel, dim3(num_jobs), dim3(kBlock), 0, S(stream), p, jobs, out);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/pinotgpu.h"
+#include "filter_stats.h"
 #include "host_common.h"
 #include "internal.h"
 
@@ -420,7 +421,8 @@ struct Scratch {
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
-  HostPinned stage, starstage, bitstage;
+  DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
+  HostPinned stage, starstage, bitstage, maskstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
   void release() {
@@ -434,6 +436,7 @@ struct Scratch {
     starwork.release();
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
+    leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -700,7 +703,14 @@ struct pgpu_plan_s {
   std::vector<std::shared_ptr<InvIndex>> inv_refs;  // inverted indexes the bit tasks point into (kept alive)
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
-  int64_t scanned_entries_model = 0;      // sum over scanned segments of numDocs x variable leaves
+  int64_t scanned_entries_model = 0;      // numEntriesScannedInFilter of the STATS_CONST segments (host)
+  bool in_kernel_stats = false;           // the scan kernel counts STATS_CHAIN / STATS_LEAP2 segments
+  bool any_leap2 = false;
+  // STATS_GENERIC segments: their filter tree, replayed on the host over the leaves' device bitmaps
+  struct GenericStat { int64_t rec; int32_t num_docs; StatTree tree; int64_t out_word; };
+  std::vector<GenericStat> generic;
+  int64_t generic_words = 0;
+  std::vector<int> leaf_perm;             // evaluation position -> predicate index
   int64_t post_exempt_docs = 0;           // aggregation-only: docs of segments answered from metadata / dictionary
   int segments_matched_filter = 0;
   std::vector<uint8_t> seg_scanned;       // per plan segment: 1 = scanned (filter not folded to empty)
@@ -1454,6 +1464,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<KBitTask> bit_tasks;
     std::vector<KBitBlock> bit_blocks;
     std::vector<std::shared_ptr<InvIndex>> inv_refs;
+    std::vector<pgpu_plan_s::GenericStat> generic;  // rec: chunk-relative record index
+    bool any_leap2 = false;
     int64_t docbit_words = 0;
     std::vector<uint8_t> scanned;
     int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
@@ -1514,9 +1526,43 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
         if (used) continue;
       }
-      for (int l = 0; l < P->num_leaves; ++l)  // sorted columns go through the sorted index: no entries scanned
-        if (tri[l] == T_VAR && !s->cols[q->predicates[l].column].sorted && leaves[l].kind != LEAF_BITMAP)
-          C.entries += s->num_docs;  // index leaves (sorted, inverted) scan no entries
+      // numEntriesScannedInFilter (filter_stats.h): Pinot's leaf operators in this segment, its folded operator
+      // tree, and how the count is taken
+      int32_t rec_stats = KSTATS_NONE;
+      {
+        std::vector<int32_t> lt(P->num_leaves);
+        for (int l = 0; l < P->num_leaves; ++l) {
+          const pgpu_predicate& pr = q->predicates[l];
+          const Column& col = s->cols[pr.column];
+          lt[l] = tri[l] == T_NONE ? SL_EMPTY : tri[l] == T_ALL ? SL_ALL : col.sorted ? SL_SORTED :
+                  (pr.type != PGPU_PRED_RANGE && col.inv) ? SL_BITMAP : SL_SCAN;
+        }
+        StatTree st = build_stat_tree(P->ops, lt);
+        StatsPlan sp = classify_stat_tree(st, s->num_docs);
+        std::vector<int> pos(P->num_leaves);  // predicate index -> evaluation position
+        for (int k = 0; k < P->num_leaves; ++k) pos[perm[k]] = k;
+        if (sp.kind == STATS_CHAIN && P->in_kernel_stats) {
+          // counted in the kernel when its evaluation order is Pinot's: index leaves, then the scans in order
+          int last_idx = -1, prev_scan = -1;
+          bool ok = true;
+          for (int l : sp.index_leaves) last_idx = std::max(last_idx, pos[l]);
+          for (int l : sp.scan_leaves) { ok &= pos[l] > last_idx && pos[l] > prev_scan; prev_scan = pos[l]; }
+          if (ok) {
+            rec_stats = KSTATS_CHAIN;
+            for (int l : sp.scan_leaves) rec_stats |= 1 << (4 + pos[l]);
+          } else {
+            sp.kind = STATS_GENERIC;
+          }
+        } else if (sp.kind == STATS_LEAP2 && P->in_kernel_stats) {
+          rec_stats = KSTATS_LEAP2 | (pos[sp.scan_leaves[0]] << 8) | (pos[sp.scan_leaves[1]] << 10);
+          C.any_leap2 = true;
+        } else if (sp.kind != STATS_CONST) {
+          sp.kind = STATS_GENERIC;
+        }
+        if (sp.kind == STATS_CONST) C.entries += sp.constant;
+        if (sp.kind == STATS_GENERIC)
+          C.generic.push_back({(int64_t)(C.rec.size() / P->seg_stride), s->num_docs, std::move(st), 0});
+      }
       if (C.sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
         std::vector<double> frac(P->num_leaves, 1.0);
         for (int l = 0; l < P->num_leaves; ++l) {
@@ -1540,6 +1586,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       h->num_docs = s->num_docs;
       h->tile_base = (int32_t)C.tiles;  // chunk-relative
       h->num_tiles = (int32_t)((s->num_docs + kTileDocs - 1) / kTileDocs);
+      h->stats = rec_stats;
       KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
       for (int j = 0; j < nqc; ++j) {
         const Column& c = s->cols[P->query_cols[j]];
@@ -1708,6 +1755,13 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     P->bit_tasks.insert(P->bit_tasks.end(), C.bit_tasks.begin(), C.bit_tasks.end());
     P->inv_refs.insert(P->inv_refs.end(), C.inv_refs.begin(), C.inv_refs.end());
+    for (auto& g : C.generic) {
+      g.rec += rec0 / std::max(P->seg_stride, 1);
+      g.out_word = P->generic_words;
+      P->generic_words += (int64_t)P->num_leaves * (((int64_t)g.num_docs + 31) / 32);
+      P->generic.push_back(std::move(g));
+    }
+    P->any_leap2 |= C.any_leap2;
     P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
@@ -1723,6 +1777,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // operator on its own worker thread, BaseCombineOperator.java:85-115).
   const bool part_eligible = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes &&
                              !getenv_flag("PGPU_NO_PARTITION");
+  // CHAIN / LEAP2 statistics need the direct kernel's register fast path (a pure AND of <= kFastLeaves leaves)
+  P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !scan_on && !part_eligible;
+  P->leaf_perm = perm;
   const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
   if (se && !any_star && !any_inv && !scan_on && !part_eligible && stream_chunks > 1) {
     for (Segment* s : P->segs) {
@@ -1863,6 +1920,11 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = sc->stats.as<unsigned long long>();
+  if (P->any_leap2) {  // one map per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
+    TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *
+                             (kBlock / 64) * 8));
+    kp.leap_maps = sc->leap_maps.as<uint64_t>();
+  }
   const int star_blocks = (int)P->star.size() * P->star_chunks;
   if (P->mode == MODE_LDS) {
     TRY(sc->slab.ensure((size_t)std::max(max_chunks * P->grid + star_blocks, 1) * X.words * 8));
@@ -1926,6 +1988,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
   kp.tile_seg = sc->tile_seg.as<int32_t>() + C.tile_begin;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->grid, C.num_tiles));
   if (P->mode == MODE_LDS) kp.slab = X.kp.slab + X.slabs_used * X.words;
+  if (kp.leap_maps) kp.leap_maps += C.tile_begin * (kBlock / 64);
   if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>() + C.tile_begin, stream))
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (c == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
@@ -1973,6 +2036,9 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
+  if (C.num_tiles > 0 && P->any_leap2 && !P->partitioned &&
+      launch_leap2_compose(kp.segs, kp.seg_stride, kp.num_segs, kp.leap_maps, kp.stats, stream))
+    return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (C.num_tiles > 0 && !P->partitioned && P->mode == MODE_LDS) X.slabs_used += grid;
   P->launches_done = c + 1;
   return 0;
@@ -2025,6 +2091,26 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     sp.stats = kp.stats;
     if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
       return fail(PGPU_ERR_DEVICE, "star-tree scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
+  if (!P->generic.empty()) {
+    // STATS_GENERIC segments: the leaves' match bitmaps, read back and replayed on the host at finalize
+    std::vector<KMaskJob> jobs;
+    for (const auto& g : P->generic)
+      for (int64_t g0 = 0; g0 < ((int64_t)g.num_docs + 31) / 32; g0 += kBlock)
+        jobs.push_back(KMaskJob{(int32_t)g.rec, (int32_t)g0, g.out_word});
+    TRY(sc->mask_jobs.ensure(std::max<size_t>(jobs.size(), 1) * sizeof(KMaskJob)));
+    TRY(sc->leaf_masks.ensure((size_t)std::max<int64_t>(P->generic_words, 1) * 4));
+    TRY(sc->maskstage.ensure(std::max<size_t>(jobs.size() * sizeof(KMaskJob), (size_t)P->generic_words * 4) + 16));
+    memcpy(sc->maskstage.p, jobs.data(), jobs.size() * sizeof(KMaskJob));
+    HIP_TRY(hipMemcpyAsync(sc->mask_jobs.p, sc->maskstage.p, jobs.size() * sizeof(KMaskJob), hipMemcpyHostToDevice,
+                           stream));
+    KParams mp = kp;
+    mp.segs = sc->segrec.as<uint8_t>();
+    if (launch_leaf_masks(mp, sc->mask_jobs.as<KMaskJob>(), (int32_t)jobs.size(), sc->leaf_masks.as<uint32_t>(),
+                          stream))
+      return fail(PGPU_ERR_DEVICE, "leaf mask launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipMemcpyAsync(sc->maskstage.p, sc->leaf_masks.p, (size_t)P->generic_words * 4, hipMemcpyDeviceToHost,
+                           stream));
   }
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
   if (P->mode == MODE_LDS) {
@@ -2082,11 +2168,11 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     matched = st[words];
-    star_scanned = st[words + 1];
+    star_scanned = st[words + 1] + st[words + 2];
     for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
     TRY(R->alloc(nk, nslots, n));
     int64_t j = 0;
@@ -2112,12 +2198,12 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
-    star_scanned = st[2];
+    star_scanned = st[2] + st[3];
     TRY(R->alloc(nk, nslots, n));
     if (n > 0) {
       const uint8_t* dev = sc->ckeys.as<uint8_t>();
@@ -2141,12 +2227,12 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
-    star_scanned = st[2];
+    star_scanned = st[2] + st[3];
     if (n > 0) {
       TRY(sc->stage.ensure((size_t)n * rec * 8));
       st = reinterpret_cast<uint64_t*>(sc->stage.p);
@@ -2180,8 +2266,23 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     else
       R->agg_conv[a] = is_int_type(P->table->types[P->agg_col[a]]) ? RCONV_I64 : RCONV_KEY_F64;
   }
+  int64_t generic_entries = 0;
+  if (!P->generic.empty()) {  // the leaves' bitmaps were copied into maskstage by the (synchronised) stream
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(P->scratch->maskstage.p);
+    std::vector<int64_t> part(P->generic.size(), 0);
+    auto replay = [&](int i) {
+      const auto& g = P->generic[i];
+      const int64_t ngroups = ((int64_t)g.num_docs + 31) / 32;
+      std::vector<const uint32_t*> masks(P->num_leaves);
+      for (int k = 0; k < P->num_leaves; ++k) masks[P->leaf_perm[k]] = words + g.out_word + (int64_t)k * ngroups;
+      part[i] = simulate_entries_scanned(g.tree, masks, g.num_docs);
+    };
+    if (P->generic.size() > 4) host_pool().run((int)P->generic.size(), replay);
+    else for (size_t i = 0; i < P->generic.size(); ++i) replay((int)i);
+    for (int64_t v : part) generic_entries += v;
+  }
   R->stats[0] = (int64_t)matched;
-  R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned;
+  R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned + generic_entries;
   R->stats[2] = ((int64_t)matched - P->post_exempt_docs) * P->num_projected;
   R->stats[3] = P->total_docs;
   R->stats[4] = (int64_t)P->segs.size();

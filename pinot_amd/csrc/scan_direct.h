@@ -5,6 +5,39 @@
 
 namespace pgpu {
 
+// numEntriesScannedInFilter of an AND of two scans A, B (AndDocIdIterator.java:40-67 over SVScanDocIdIterators):
+// the iterators hand the scan back and forth, so each doc is scanned once, plus once more when the scanner at that
+// doc matches it (the other iterator then evaluates the same doc).  Scanner state after a doc: B after a doc A
+// matches and B does not, A after a doc B matches, unchanged otherwise.  The lane builds that state for its 32 docs
+// with a 5-step segmented fill (for both possible entry states), the wave composes its 64 lanes in order, and
+// lane 0 stores the wave's map (leap2_compose_kernel chains the maps of a segment).
+__device__ __forceinline__ void leap2_wave_map(uint64_t* __restrict__ maps, int64_t slot, int lane, uint32_t a,
+                                               uint32_t b, uint32_t v) {
+  a &= v;
+  b &= v;
+  const uint32_t e = a | b;
+  uint32_t fill = a & ~b, seen = e;  // state after doc i: B (1) / A (0) where some event at or before i
+#pragma unroll
+  for (int k = 1; k < 32; k <<= 1) {
+    fill |= (fill << k) & ~seen;
+    seen |= seen << k;
+  }
+  const uint32_t before_a = fill << 1;                       // state before each doc, entering in A
+  const uint32_t before_b = ((fill | ~seen) << 1) | 1u;      // ... entering in B
+  const uint32_t nv = __popc(v);
+  uint32_t c0 = nv + __popc((a & ~before_a) | (b & before_a));
+  uint32_t c1 = nv + __popc((a & ~before_b) | (b & before_b));
+  uint32_t ex = e ? ((fill >> 31) & 1u) * 3u : 2u;           // bit s: exit state from entry s
+  for (int off = 1; off < 64; off <<= 1) {                   // ordered composition: left = this lane's range
+    const uint32_t r0 = __shfl_down(c0, off), r1 = __shfl_down(c1, off), re = __shfl_down(ex, off);
+    const uint32_t m0 = ex & 1u, m1 = (ex >> 1) & 1u;
+    const uint32_t n0 = c0 + (m0 ? r1 : r0), n1 = c1 + (m1 ? r1 : r0);
+    const uint32_t ne = ((re >> m0) & 1u) | (((re >> m1) & 1u) << 1);
+    if ((lane & (2 * off - 1)) == 0) { c0 = n0; c1 = n1; ex = ne; }
+  }
+  if (lane == 0) maps[slot] = (uint64_t)c0 | ((uint64_t)c1 << 24) | ((uint64_t)ex << 48);
+}
+
 // ---------------------------------------------------------------------------------------------- K3 fused
 // DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
@@ -35,6 +68,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
   // The tiles in flight on an XCD then come from ~one segment at a time and that segment's dictionaries / LUTs
   // (the targets of the gathers) stay in the XCD's 4 MiB L2.
   unsigned long long matched = 0;
+  uint32_t in_filter = 0;  // STATS_CHAIN entries of this lane (< 2^32: at most 4 leaves x 32 docs x tiles)
   const int64_t T = p.num_tiles;
   int64_t t_begin, t_end, t_step;
   if (gridDim.x >= 64 && (gridDim.x & 7) == 0) {
@@ -53,6 +87,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
     SegView S{};
     int64_t tile_base = 0;
     int nd = 0;
+    int stats = 0;  // the segment's KSegHdr.stats
     // named registers, not an array: a runtime-guarded array of structs lands in scratch
     LeafReg R0{}, R1{}, R2{}, R3{};
     const int nl = p.num_leaves;
@@ -72,6 +107,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
         S = seg_view(p, seg);
         tile_base = S.hdr->tile_base;
         nd = S.hdr->num_docs;
+        stats = S.hdr->stats;
         if (fast) PGPU_LOAD_LEAVES();
       }
       const int64_t group = (t - tile_base) * kBlock + tid;
@@ -79,9 +115,24 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
       const int64_t doc0 = group << 5;
       uint32_t mask = doc0 >= nd ? 0u : (nd - doc0 >= 32 ? ~0u : ((1u << (nd - doc0)) - 1u));
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
-      if (fast) {
+      if (fast && (stats & 3) == KSTATS_LEAP2) {
+        // two scans in leap-frog: both masks are needed for the entry count, no early exit
+        const uint32_t v = mask;
+        const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
+        uint32_t ma = 0, mb = 0;
+        for (int l = 0; l < nl; ++l) {
+          const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
+          const uint32_t m = leaf_mask_reg(r, gclamp);
+          ma = l == la ? m : ma;
+          mb = l == lb ? m : mb;
+          mask &= m;
+        }
+        leap2_wave_map(p.leap_maps, t * (kBlock / 64) + wave, lane, ma, mb, v);
+      } else if (fast) {
         for (int l = 0; l < nl; ++l) {
           if (!__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
+          // applyAnd of a scan after the index leaves (AndDocIdSet.java:124-126): its input docs are its entries
+          if ((stats >> (4 + l)) & 1) in_filter += __popc(mask);
           const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
           mask &= leaf_mask_reg(r, gclamp);
         }
@@ -137,6 +188,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
   // numDocsScanned: wave reduce, one atomic per wave.
   for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
   if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
+  unsigned long long entries = in_filter;
+  for (int off = 32; off > 0; off >>= 1) entries += __shfl_xor(entries, off);
+  if ((tid & 63) == 0 && entries) atomicAdd(p.stats + 2, entries);
 
   if (MODE == MODE_LDS) {
     __syncthreads();

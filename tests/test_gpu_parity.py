@@ -47,8 +47,10 @@ def gpu_table(schema, segments):
 # ------------------------------------------------------------------------------------------------ KATs
 @pytest.fixture(scope="module")
 def sv(oracle, gpu_lib):
-    seg = oracle.make_segment(K.SCHEMA, K.sv_columns())
-    t, hs = gpu_table(K.SCHEMA, [seg])
+    """The KAT segment with the reference's index layout: the oracle reads its fixed-bit view with the sorted
+    flags, the GPU pins column5 / daysSinceEpoch as SortedIndexReaderImpl pairs."""
+    seg = K.kat_segment(oracle)
+    t, hs = gpu_table(K.SCHEMA, [K.kat_segment(oracle, pairs=True)])
     yield seg, t, hs[0]
     t.close()
 
@@ -60,9 +62,7 @@ def test_kat_inner_segment(oracle, sv, case, with_filter):
     q = K.inner_query(case["group_by"], with_filter)
     r = t.execute_groupby([h], q)
     exp = case["filter" if with_filter else "no_filter"]
-    docs, _, post, total = exp["stats"]
-    assert (r.stats.num_docs_scanned, r.stats.num_entries_scanned_post_filter, r.stats.num_total_docs) == \
-        (docs, post, total)
+    assert r.stats.as_tuple() == tuple(exp["stats"])  # numEntriesScannedInFilter 84134 with the filter
     key = K.key_tuple(case["group_by"], exp["key"])
     K.check_inner_values(r.as_dict()[key], exp["values"])
     assert_same(r, oracle.run_groupby(K.SCHEMA, [seg], q, combine=False), q, K.SCHEMA)
@@ -91,8 +91,7 @@ def test_kat_inter_segment(oracle, sv, case):
     handles = [h] * K.KAT["inter_segment_num_segments"]
     q = QueryContext(case["group_by"], [tuple(a) for a in case["aggs"]])
     r = t.execute_groupby(handles, q)
-    assert (r.stats.num_docs_scanned, r.stats.num_entries_scanned_post_filter, r.stats.num_total_docs) == \
-        (case["stats"][0], case["stats"][2], case["stats"][3])
+    assert r.stats.as_tuple() == tuple(case["stats"])
     got = r.as_dict()
     rows = {K.key_tuple(case["group_by"], k): v for k, v in case["rows"]}
     if case["complete"]:
@@ -111,7 +110,7 @@ def test_kat_sql_string_filter(oracle, sv):
     r = t.execute_groupby([h], q)
     exp = K.KAT["inner_segment_group_by"][0]["filter"]
     K.check_inner_values(r.as_dict()[(242920,)], exp["values"])
-    assert r.stats.num_docs_scanned == 6129
+    assert r.stats.as_tuple() == tuple(exp["stats"])
 
 
 def test_bad_literal_is_bad_query(sv):
@@ -203,8 +202,7 @@ def test_random_queries_vs_oracle(oracle, gpu_lib, seed, monkeypatch):
             r = t.execute_groupby(hs, q)
             o = oracle.run_groupby(SCHEMA_R, segs, q, combine=False, max_initial_capacity=10000)
             assert_same(r, o, q, SCHEMA_R)
-            assert r.stats.num_docs_scanned == o.stats[0]
-            assert r.stats.num_total_docs == o.stats[3]
+            assert r.stats.as_tuple() == o.stats, (q.filter, r.stats, o.stats)
     finally:
         t.close()
 
@@ -519,8 +517,7 @@ def test_random_aggregation_only_vs_oracle(oracle, gpu_lib, seed):
                     assert x == pytest.approx(y, rel=REL, abs=1e-6)
                 else:
                     assert x == y, (fn, col, x, y)
-            st = r.stats.as_tuple()
-            assert (st[0], st[2], st[3]) == (o.stats[0], o.stats[2], o.stats[3]), (r.stats, o.stats)
+            assert r.stats.as_tuple() == o.stats, (q.filter, r.stats, o.stats)
     finally:
         t.close()
 
@@ -557,7 +554,10 @@ def _sorted_pair_segment(oracle, schema, cols, sorted_col):
     out = dict(seg.columns)
     out[sorted_col] = ColumnData(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.dict_bytes, pairs,
                                  fwd_format=L.FWD_SORTED_PAIRS, is_sorted=True)
-    return seg, SegmentBuffers(n, out)
+    from dataclasses import replace
+    orc = dict(seg.columns)
+    orc[sorted_col] = replace(c, is_sorted=True)  # the oracle: fixed-bit bytes, SortedIndexBasedFilterOperator leaves
+    return SegmentBuffers(n, orc), SegmentBuffers(n, out)
 
 
 SORTED_QUERIES = [
@@ -586,11 +586,13 @@ def test_sorted_column_docrange_leaves(oracle, gpu_lib, n):
             r = t.execute_groupby(hs, q)
             o = oracle.run_groupby(schema, [seg, seg], q)
             assert_same(r, o, q, schema)
-            assert r.stats.num_docs_scanned == o.stats[0], sql
-        # the sorted leaf scans no entries; the v leaf scans every doc of both segments
+            assert r.stats.as_tuple() == o.stats, (sql, r.stats, o.stats)
+        # the sorted leaf scans no entries; the v leaf's applyAnd scans only the sorted leaf's docs
+        # (AndDocIdSet.java:124-126)
         r = t.execute_groupby(hs, parse_query(SORTED_QUERIES[1]))
-        if n > 1:
-            assert r.stats.num_entries_scanned_in_filter == 2 * n
+        in_range = int(np.count_nonzero((cols["s"] >= 10) & (cols["s"] <= 70)))
+        if n > 1:  # one doc: every leaf folds to match-all or empty (cardinality 1)
+            assert r.stats.num_entries_scanned_in_filter == 2 * in_range
         bm = t.filter_bitmap(hs[0], parse_query(SORTED_QUERIES[2]), n)
         np.testing.assert_array_equal(bm, oracle.filter_bitmap(schema, seg, parse_query(SORTED_QUERIES[2])))
     finally:
@@ -607,8 +609,7 @@ def _fixed_bit_view(seg):
         if c.fwd_format == L.FWD_SORTED_PAIRS:
             pairs = np.frombuffer(c.fwd_bytes, dtype=">i4").reshape(-1, 2).astype(np.int64)
             ids = np.repeat(np.arange(c.cardinality), np.maximum(pairs[:, 1] - pairs[:, 0] + 1, 0))
-            c = replace(c, fwd_bytes=pack_msb_first(ids, c.bits_per_element), fwd_format=L.FWD_FIXED_BIT,
-                        is_sorted=False)
+            c = replace(c, fwd_bytes=pack_msb_first(ids, c.bits_per_element), fwd_format=L.FWD_FIXED_BIT)
         cols[name] = c
     return SegmentBuffers(seg.num_docs, cols)
 
@@ -688,6 +689,8 @@ def test_inverted_index_leaves(oracle, gpu_lib, tmp_path, run_optimize):
     hm = [mixed.pin_segment(s if k != 1 else
                             SegmentBuffers(s.num_docs, {c: replace(d, inv_bytes=None) for c, d in s.columns.items()}))
           for k, s in enumerate(segs)]
+    orc_mixed = [o if k != 1 else SegmentBuffers(o.num_docs, {c: replace(d, inv_bytes=None) for c, d in o.columns.items()})
+                 for k, o in enumerate(orc)]
     plain = GpuTable(schema)  # the same segments without inverted indexes: scan leaves
     hp = [plain.pin_segment(SegmentBuffers(s.num_docs, {c: replace(d, inv_bytes=None) for c, d in s.columns.items()}))
           for s in segs]
@@ -695,11 +698,15 @@ def test_inverted_index_leaves(oracle, gpu_lib, tmp_path, run_optimize):
         for sql in INV_QUERIES:
             q = parse_query(sql)
             r = t.execute_groupby(hs, q)
-            assert_same(r, oracle.run_groupby(schema, orc, q), q, schema)
+            o = oracle.run_groupby(schema, orc, q)
+            assert_same(r, o, q, schema)
+            assert r.stats.as_tuple() == o.stats, (sql, r.stats, o.stats)
             rp = plain.execute_groupby(hp, q)
             assert r.stats.num_docs_scanned == rp.stats.num_docs_scanned, sql
             assert r.stats.num_entries_scanned_in_filter <= rp.stats.num_entries_scanned_in_filter, sql
-            assert_same(mixed.execute_groupby(hm, q), oracle.run_groupby(schema, orc, q), q, schema)
+            rm, om = mixed.execute_groupby(hm, q), oracle.run_groupby(schema, orc_mixed, q)
+            assert_same(rm, om, q, schema)
+            assert rm.stats.as_tuple() == om.stats, (sql, rm.stats, om.stats)
         r = t.execute_groupby(hs, parse_query("SELECT COUNT(*) FROM t WHERE a IN (2, 3) GROUP BY g"))
         assert r.stats.num_entries_scanned_in_filter == 0
         for sql in ("SELECT COUNT(*), SUM(v), MIN(v), MAX(g) FROM t WHERE a = 3",

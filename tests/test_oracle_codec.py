@@ -75,7 +75,7 @@ def test_string_dictionary_padding_lookup(oracle):
         fwd = bytes.fromhex(c["fwd_hex"]) + b"\0" * 8
         assert [o.or_bitset_read_int(fwd, i, 1) for i in range(5)] == expect_fwd
         d = ctypes.create_string_buffer(bytes.fromhex(c["dict_hex"]))
-        col = oracle.OrColumn(L.STRING, 2, 1, c["lengthOfEachEntry"], pad, 0, ctypes.cast(d, ctypes.c_void_p), None)
+        col = oracle.OrColumn(L.STRING, 2, 1, c["lengthOfEachEntry"], pad, 0, 0, ctypes.cast(d, ctypes.c_void_p), None)
         err = ctypes.c_int()
         lynda = o.or_dict_insertion_index_of(ctypes.byref(col), b"lynda", ctypes.byref(err))
         lynda2 = o.or_dict_insertion_index_of(ctypes.byref(col), b"lynda 2.0", ctypes.byref(err))

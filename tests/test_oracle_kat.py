@@ -12,7 +12,7 @@ from pinot_amd.query import QueryContext
 
 @pytest.fixture(scope="module")
 def sv_segment(oracle):
-    return oracle.make_segment(K.SCHEMA, K.sv_columns())
+    return K.kat_segment(oracle)
 
 
 def test_segment_cardinalities(sv_segment):
@@ -32,9 +32,7 @@ def test_inner_segment_group_by(oracle, sv_segment, case, with_filter):
     exp = case["filter" if with_filter else "no_filter"]
     assert r.holder == case["holder"]
     docs, in_filter, post, total = exp["stats"]
-    assert r.stats[0] == docs and r.stats[2] == post and r.stats[3] == total
-    if not with_filter:
-        assert r.stats[1] == in_filter
+    assert r.stats == (docs, in_filter, post, total)
     key = K.key_tuple(case["group_by"], exp["key"])
     assert key in r.groups
     K.check_inner_values(r.groups[key], exp["values"])
@@ -56,7 +54,7 @@ def test_aggregation_only_totals(oracle, sv_segment, with_filter):
 def test_inter_segment_group_by(oracle, sv_segment, case):
     q = QueryContext(case["group_by"], [tuple(a) for a in case["aggs"]])
     r = oracle.run_groupby(K.SCHEMA, [sv_segment] * K.KAT["inter_segment_num_segments"], q, combine=True)
-    assert r.stats[0] == case["stats"][0] and r.stats[2] == case["stats"][2] and r.stats[3] == case["stats"][3]
+    assert r.stats == tuple(case["stats"])
     rows = {K.key_tuple(case["group_by"], k): v for k, v in case["rows"]}
     if case["complete"]:
         assert set(r.groups) == set(rows)
@@ -83,10 +81,7 @@ def test_aggregation_only_inner_segment(oracle, sv_segment, with_filter):
     exp = K.KAT["inner_segment_aggregation_only"]["filter" if with_filter else "no_filter"]
     assert list(r.groups) == [()]
     K.check_inner_values(r.groups[()], exp["values"])
-    docs, in_filter, post, total = exp["stats"]
-    assert (r.stats[0], r.stats[2], r.stats[3]) == (docs, post, total)
-    if not with_filter:
-        assert r.stats[1] == in_filter
+    assert r.stats == tuple(exp["stats"])
 
 
 @pytest.mark.parametrize("case", K.KAT_AGG["cases"], ids=lambda c: "%s_%s" % (c["test"], c["variant"]))

@@ -103,9 +103,9 @@ struct KParams {
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
   unsigned long long* stats;      // [0] docs matched, [2] entries scanned in filter (STATS_CHAIN / LEAP2 segments)
-  // STATS_LEAP2 segments: per (tile, wave) the wave's transfer map of AndDocIdIterator over scans A, B (packed:
-  // cost from entry "A scanning" bits 0-23, from "B scanning" bits 24-47, exit states bits 48-49)
-  uint64_t* leap_maps;
+  // STATS_LEAP2 segments: per (tile, wave) one byte of AndDocIdIterator state over scans A, B: bit 0 = a doc
+  // matches, bit 1 = scanner after the wave's docs (1 = B), bits 2-3 = entry difference at its first match + 1
+  uint8_t* leap_maps;
 };
 
 // leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to
@@ -237,7 +237,7 @@ int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 // Per STATS_LEAP2 record of a launch: composes its (tile, wave) maps in doc order into the segment's count
 // (stats[2] += ...).
-int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint64_t* maps,
+int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint8_t* maps,
                          unsigned long long* stats, void* stream);
 int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,

@@ -269,28 +269,33 @@ __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, 
 
 // ---------------------------------------------------------------------------------------------- filter stats
 // numEntriesScannedInFilter of STATS_LEAP2 segments (AndDocIdIterator over two SVScanDocIdIterators,
-// AndDocIdIterator.java:40-67): the scan kernel leaves one transfer map per (tile, wave) -- the entries counted
-// and the exit state for each entry state -- and one thread per segment composes them in doc order from the
-// initial state (scan A at doc 0).
-__global__ void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride, int32_t num_segs,
-                                     const uint64_t* __restrict__ maps, unsigned long long* __restrict__ stats) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long total = 0;
-  if (s < num_segs) {
-    const KSegHdr* h = reinterpret_cast<const KSegHdr*>(segs + (int64_t)s * seg_stride);
-    if ((h->stats & 3) == KSTATS_LEAP2) {
-      const uint64_t* m = maps + (int64_t)h->tile_base * (kBlock / 64);
-      const int64_t n = (int64_t)h->num_tiles * (kBlock / 64);
-      uint32_t state = 0;
-      for (int64_t i = 0; i < n; ++i) {
-        const uint64_t w = m[i];
-        total += state ? (w >> 24) & 0xFFFFFFull : w & 0xFFFFFFull;
-        state = (uint32_t)(w >> (48 + state)) & 1u;
-      }
-    }
+// AndDocIdIterator.java:40-67): the scan kernel counted every entry assuming each wave-tile is entered with scan A
+// running, and left one byte per (tile, wave) (bit 0: a doc matches, bit 1: scanner after it, bits 2-3: count
+// difference at its first match when entered with B running, + 1).  One wave per segment chains the bytes in doc
+// order from the initial state (scan A at doc 0), 64 at a time: a byte's entry state is the exit of the nearest
+// earlier byte with a match (ballots), or the state carried from the previous 64.
+__global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride,
+                                                           int32_t num_segs, const uint8_t* __restrict__ maps,
+                                                           unsigned long long* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (s >= num_segs) return;  // wave-uniform
+  const KSegHdr* h = reinterpret_cast<const KSegHdr*>(segs + (int64_t)s * seg_stride);
+  if ((h->stats & 3) != KSTATS_LEAP2) return;
+  const uint8_t* m = maps + (int64_t)h->tile_base * (kBlock / 64);
+  const int64_t n = (int64_t)h->num_tiles * (kBlock / 64);
+  long long total = 0;
+  uint32_t carry = 0;  // scanner state entering this batch of 64 (0 = A)
+  for (int64_t base = 0; base < n; base += 64) {
+    const uint32_t w = base + lane < n ? m[base + lane] : 0u;
+    const uint64_t has = __ballot(w & 1u), exb = __ballot((w >> 1) & 1u);
+    const uint64_t below = has & ((1ull << lane) - 1ull);
+    const uint32_t entry = below ? (uint32_t)((exb >> (63 - __builtin_clzll(below))) & 1ull) : carry;
+    if ((w & 1u) && entry) total += (long long)((w >> 2) & 3u) - 1;
+    if (has) carry = (uint32_t)((exb >> (63 - __builtin_clzll(has))) & 1ull);
   }
   for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
-  if ((threadIdx.x & 63) == 0 && total) atomicAdd(stats + 2, total);
+  if (lane == 0 && total) atomicAdd(stats + 2, (unsigned long long)total);
 }
 
 // The leaves' match bitmaps of STATS_GENERIC segments (the replay of filter_stats.cpp runs on the host).
@@ -509,10 +514,10 @@ int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream) {
   return PGPU_HIP_OK(hipGetLastError());
 }
 
-int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint64_t* maps,
+int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint8_t* maps,
                          unsigned long long* stats, void* stream) {
   if (num_segs <= 0) return 0;
-  hipLaunchKernelGGL(leap2_compose_kernel, dim3((num_segs + 255) / 256), dim3(256), 0, S(stream), segs, seg_stride,
+  hipLaunchKernelGGL(leap2_compose_kernel, dim3((num_segs + 3) / 4), dim3(256), 0, S(stream), segs, seg_stride,
                      num_segs, maps, stats);
   return PGPU_HIP_OK(hipGetLastError());
 }

@@ -453,6 +453,7 @@ struct pgpu_table_s {
   std::vector<int32_t> types;
   std::mutex mu;
   std::unordered_map<int64_t, std::unique_ptr<Segment>> segments;
+  std::vector<Segment*> by_handle;  // handle -> segment (handles are dense), nullptr once unpinned
   int64_t next_handle = 1;
   std::vector<Dict> global;
   std::vector<uint64_t> global_version;
@@ -642,6 +643,8 @@ int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
     if (merge_dict(t->global[c], seg->cols[c].dict)) t->global_version[c]++;
   int64_t h = t->next_handle++;
   seg->handle = h;
+  if ((int64_t)t->by_handle.size() <= h) t->by_handle.resize(h + 1, nullptr);
+  t->by_handle[h] = seg.get();
   t->segments[h] = std::move(seg);
   return h;
 }
@@ -706,6 +709,7 @@ struct pgpu_plan_s {
   int64_t scanned_entries_model = 0;      // numEntriesScannedInFilter of the STATS_CONST segments (host)
   bool in_kernel_stats = false;           // the scan kernel counts STATS_CHAIN / STATS_LEAP2 segments
   bool any_leap2 = false;
+  bool leap_reserved = false;             // the scan's LDS holds the LEAP2 bytes (configure); maps allocated
   // STATS_GENERIC segments: their filter tree, replayed on the host over the leaves' device bitmaps
   struct GenericStat { int64_t rec; int32_t num_docs; StatTree tree; int64_t out_word; };
   std::vector<GenericStat> generic;
@@ -1230,6 +1234,44 @@ struct ExecCtx {
   int64_t slabs_used = 0;  // MODE_LDS: slabs written by the scan launches so far (launches pack them back to back)
 };
 
+// numEntriesScannedInFilter method of a segment whose leaves have the Pinot operator kinds `sig` (base-5 digits,
+// predicate 0 first; filter_stats.h): the folded tree, and the scan-kernel record bits of CHAIN / LEAP2.
+struct SegStats {
+  StatTree tree;
+  int kind = STATS_CONST;
+  int64_t const_per_doc = 0;
+  int32_t rec_stats = KSTATS_NONE;
+};
+SegStats classify_segment_stats(const pgpu_plan_s* P, uint64_t sig) {
+  std::vector<int32_t> lt(P->num_leaves);
+  for (int l = P->num_leaves - 1; l >= 0; --l) { lt[l] = (int32_t)(sig % 5); sig /= 5; }
+  SegStats ss;
+  ss.tree = build_stat_tree(P->ops, lt);
+  const StatsPlan sp = classify_stat_tree(ss.tree, 1);
+  ss.kind = sp.kind;
+  ss.const_per_doc = sp.constant;
+  std::vector<int> pos(P->num_leaves);  // predicate index -> evaluation position in the kernel
+  for (int k = 0; k < P->num_leaves; ++k) pos[P->leaf_perm[k]] = k;
+  if (sp.kind == STATS_CHAIN && P->in_kernel_stats) {
+    // counted in the kernel when its evaluation order is Pinot's: index leaves, then the scans in order
+    int last_idx = -1, prev_scan = -1;
+    bool ok = true;
+    for (int l : sp.index_leaves) last_idx = std::max(last_idx, pos[l]);
+    for (int l : sp.scan_leaves) { ok &= pos[l] > last_idx && pos[l] > prev_scan; prev_scan = pos[l]; }
+    if (ok) {
+      ss.rec_stats = KSTATS_CHAIN;
+      for (int l : sp.scan_leaves) ss.rec_stats |= 1 << (4 + pos[l]);
+    } else {
+      ss.kind = STATS_GENERIC;
+    }
+  } else if (sp.kind == STATS_LEAP2 && P->in_kernel_stats) {
+    ss.rec_stats = KSTATS_LEAP2 | (pos[sp.scan_leaves[0]] << 8) | (pos[sp.scan_leaves[1]] << 10);
+  } else if (sp.kind != STATS_CONST) {
+    ss.kind = STATS_GENERIC;
+  }
+  return ss;
+}
+
 // True when an int64 accumulator cannot overflow for SUM / AVG over integer column `col` of these segments.
 bool int_sum_fits(const std::vector<Segment*>& segs, int col) {
   long double bound = 0;
@@ -1266,9 +1308,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::lock_guard<std::mutex> g(t->mu);
     P->segs.reserve(nsegs);
     for (int i = 0; i < nsegs; ++i) {
-      auto it = t->segments.find(handles[i]);
-      if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)handles[i]);
-      P->segs.push_back(it->second.get());
+      const int64_t h = handles[i];
+      Segment* sp = h > 0 && h < (int64_t)t->by_handle.size() ? t->by_handle[h] : nullptr;
+      if (!sp) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+      P->segs.push_back(sp);
     }
   }
   // query columns
@@ -1506,6 +1549,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<Tri> tri(P->num_leaves);
     std::vector<int> ids_scratch;
     std::vector<uint8_t> rec(P->seg_stride);
+    std::unordered_map<uint64_t, SegStats> stat_cache;
     for (size_t i = b; i < e; ++i) {
       Segment* s = P->segs[i];
       for (int l = 0; l < P->num_leaves; ++l) {
@@ -1530,38 +1574,24 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       // tree, and how the count is taken
       int32_t rec_stats = KSTATS_NONE;
       {
-        std::vector<int32_t> lt(P->num_leaves);
+        // the tree depends only on the leaves' operator kinds: classified once per distinct kind vector of the
+        // chunk (no per-segment allocation)
+        uint64_t sig = 0;
         for (int l = 0; l < P->num_leaves; ++l) {
           const pgpu_predicate& pr = q->predicates[l];
           const Column& col = s->cols[pr.column];
-          lt[l] = tri[l] == T_NONE ? SL_EMPTY : tri[l] == T_ALL ? SL_ALL : col.sorted ? SL_SORTED :
-                  (pr.type != PGPU_PRED_RANGE && col.inv) ? SL_BITMAP : SL_SCAN;
+          const int k = tri[l] == T_NONE ? SL_EMPTY : tri[l] == T_ALL ? SL_ALL : col.sorted ? SL_SORTED :
+                        (pr.type != PGPU_PRED_RANGE && col.inv) ? SL_BITMAP : SL_SCAN;
+          sig = sig * 5 + (uint64_t)k;
         }
-        StatTree st = build_stat_tree(P->ops, lt);
-        StatsPlan sp = classify_stat_tree(st, s->num_docs);
-        std::vector<int> pos(P->num_leaves);  // predicate index -> evaluation position
-        for (int k = 0; k < P->num_leaves; ++k) pos[perm[k]] = k;
-        if (sp.kind == STATS_CHAIN && P->in_kernel_stats) {
-          // counted in the kernel when its evaluation order is Pinot's: index leaves, then the scans in order
-          int last_idx = -1, prev_scan = -1;
-          bool ok = true;
-          for (int l : sp.index_leaves) last_idx = std::max(last_idx, pos[l]);
-          for (int l : sp.scan_leaves) { ok &= pos[l] > last_idx && pos[l] > prev_scan; prev_scan = pos[l]; }
-          if (ok) {
-            rec_stats = KSTATS_CHAIN;
-            for (int l : sp.scan_leaves) rec_stats |= 1 << (4 + pos[l]);
-          } else {
-            sp.kind = STATS_GENERIC;
-          }
-        } else if (sp.kind == STATS_LEAP2 && P->in_kernel_stats) {
-          rec_stats = KSTATS_LEAP2 | (pos[sp.scan_leaves[0]] << 8) | (pos[sp.scan_leaves[1]] << 10);
-          C.any_leap2 = true;
-        } else if (sp.kind != STATS_CONST) {
-          sp.kind = STATS_GENERIC;
-        }
-        if (sp.kind == STATS_CONST) C.entries += sp.constant;
-        if (sp.kind == STATS_GENERIC)
-          C.generic.push_back({(int64_t)(C.rec.size() / P->seg_stride), s->num_docs, std::move(st), 0});
+        auto it = stat_cache.find(sig);
+        if (it == stat_cache.end()) it = stat_cache.emplace(sig, classify_segment_stats(P, sig)).first;
+        const SegStats& ss = it->second;
+        rec_stats = ss.rec_stats;
+        C.any_leap2 |= (rec_stats & 3) == KSTATS_LEAP2;
+        if (ss.kind == STATS_CONST) C.entries += ss.const_per_doc * s->num_docs;
+        if (ss.kind == STATS_GENERIC)
+          C.generic.push_back({(int64_t)(C.rec.size() / P->seg_stride), s->num_docs, ss.tree, 0});
       }
       if (C.sel_docs == 0) {  // selectivity estimate from the first scanned segment's translated leaves
         std::vector<double> frac(P->num_leaves, 1.0);
@@ -1676,6 +1706,16 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
     }
     if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
+    if (P->any_leap2 || (se && P->in_kernel_stats)) {
+      P->leap_reserved = true;
+      // STATS_LEAP2 bytes of a workgroup's tiles are buffered in LDS (one per tile and wave) until the end of the
+      // scan: at most kLeapLdsTiles tiles per workgroup (more workgroups than resident ones for huge plans)
+      constexpr int64_t kLeapLdsTiles = 4096;
+      const int64_t need = (tile_base + kLeapLdsTiles - 4) / (kLeapLdsTiles - 3);
+      if (P->grid < need) P->grid = (int)((need + 7) & ~int64_t(7));
+      const int64_t per_wg = (tile_base + P->grid - 1) / std::max(P->grid, 1) + 3;
+      P->lds_bytes += (size_t)((per_wg * (kBlock / 64) + 15) & ~int64_t(15));
+    }
     // Large dense tables: partitioned group-by (partition.h) instead of random global atomics.
     if (P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes && P->star.empty() && tile_base > 0 &&
         P->total_docs < (int64_t)UINT32_MAX && !getenv_flag("PGPU_NO_PARTITION")) {
@@ -1920,10 +1960,10 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = sc->stats.as<unsigned long long>();
-  if (P->any_leap2) {  // one map per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
+  if (P->leap_reserved) {  // one byte per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
     TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *
-                             (kBlock / 64) * 8));
-    kp.leap_maps = sc->leap_maps.as<uint64_t>();
+                             (kBlock / 64)));
+    kp.leap_maps = sc->leap_maps.as<uint8_t>();
   }
   const int star_blocks = (int)P->star.size() * P->star_chunks;
   if (P->mode == MODE_LDS) {
@@ -2036,7 +2076,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
-  if (C.num_tiles > 0 && P->any_leap2 && !P->partitioned &&
+  if (C.num_tiles > 0 && P->any_leap2 && P->leap_reserved && !P->partitioned &&
       launch_leap2_compose(kp.segs, kp.seg_stride, kp.num_segs, kp.leap_maps, kp.stats, stream))
     return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (C.num_tiles > 0 && !P->partitioned && P->mode == MODE_LDS) X.slabs_used += grid;
@@ -2350,6 +2390,7 @@ int pgpu_table_destroy(pgpu_table t) {
   hipStreamSynchronize(t->stream);
   for (auto& kv : t->segments) free_segment(t, kv.second.get());
   t->segments.clear();
+  t->by_handle.clear();
   for (auto& s : t->scratch_pool) if (s) s->release();
   t->gen.pos.release(); t->gen.presence.release(); t->gen.code_to_pos.release(); t->gen.cdf.release();
   t->gen.pos_to_id.release();
@@ -2449,6 +2490,7 @@ int pgpu_unpin_segment(pgpu_table t, int64_t h) {
   if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
   hipStreamSynchronize(t->stream);
   free_segment(t, it->second.get());
+  t->by_handle[h] = nullptr;
   t->segments.erase(it);
   return 0;
 }

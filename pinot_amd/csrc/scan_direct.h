@@ -7,35 +7,42 @@ namespace pgpu {
 
 // numEntriesScannedInFilter of an AND of two scans A, B (AndDocIdIterator.java:40-67 over SVScanDocIdIterators):
 // the iterators hand the scan back and forth, so each doc is scanned once, plus once more when the scanner at that
-// doc matches it (the other iterator then evaluates the same doc).  Scanner state after a doc: B after a doc A
-// matches and B does not, A after a doc B matches, unchanged otherwise.  The lane builds that state for its 32 docs
-// with a 5-step segmented fill (for both possible entry states), the wave composes its 64 lanes in order, and
-// lane 0 stores the wave's map (leap2_compose_kernel chains the maps of a segment).
-__device__ __forceinline__ void leap2_wave_map(uint64_t* __restrict__ maps, int64_t slot, int lane, uint32_t a,
-                                               uint32_t b, uint32_t v) {
+// doc matches it (the other iterator then evaluates the same doc).  Scanner after a doc: B after a doc A matches
+// and B does not, A after a doc B matches, unchanged otherwise -- so only a group's first matching doc depends on
+// the scanner the group is entered with.  Each lane builds the scanner state over its 32 docs (5-step segmented
+// fill), counts its entries with the entry state the wave's ballots give it (the exit of the previous lane with a
+// match), and the wave stores one byte for the rest: whether it has a match, its exit state, and the count
+// difference at its first match between entering in B and in A (leap2_compose_kernel chains the bytes of a
+// segment in doc order).  The byte goes to the workgroup's LDS list (one per tile and wave), stored to global
+// memory once after the tile loop.  Returns the lane's entries (entering the wave in A).
+__device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, int64_t slot, int lane, uint32_t a,
+                                                  uint32_t b, uint32_t v) {
   a &= v;
   b &= v;
   const uint32_t e = a | b;
-  uint32_t fill = a & ~b, seen = e;  // state after doc i: B (1) / A (0) where some event at or before i
+  uint32_t fill = a & ~b, seen = e;  // scanner after doc i: B (1) / A (0), where some doc <= i matches
 #pragma unroll
   for (int k = 1; k < 32; k <<= 1) {
     fill |= (fill << k) & ~seen;
     seen |= seen << k;
   }
-  const uint32_t before_a = fill << 1;                       // state before each doc, entering in A
-  const uint32_t before_b = ((fill | ~seen) << 1) | 1u;      // ... entering in B
-  const uint32_t nv = __popc(v);
-  uint32_t c0 = nv + __popc((a & ~before_a) | (b & before_a));
-  uint32_t c1 = nv + __popc((a & ~before_b) | (b & before_b));
-  uint32_t ex = e ? ((fill >> 31) & 1u) * 3u : 2u;           // bit s: exit state from entry s
-  for (int off = 1; off < 64; off <<= 1) {                   // ordered composition: left = this lane's range
-    const uint32_t r0 = __shfl_down(c0, off), r1 = __shfl_down(c1, off), re = __shfl_down(ex, off);
-    const uint32_t m0 = ex & 1u, m1 = (ex >> 1) & 1u;
-    const uint32_t n0 = c0 + (m0 ? r1 : r0), n1 = c1 + (m1 ? r1 : r0);
-    const uint32_t ne = ((re >> m0) & 1u) | (((re >> m1) & 1u) << 1);
-    if ((lane & (2 * off - 1)) == 0) { c0 = n0; c1 = n1; ex = ne; }
+  const uint32_t before = fill << 1;  // scanner before each doc, entering in A
+  uint32_t c = __popc(v) + __popc((a & ~before) | (b & before));
+  const int f = e ? __builtin_ctz(e) : 0;
+  const int d = e ? (int)((b >> f) & 1u) - (int)((a >> f) & 1u) : 0;  // entering in B instead, at the first match
+  // wave-wide state from ballots only (scalar masks, no lane shuffles, no divergent branch)
+  const uint64_t evm = __ballot(e != 0u), exm = __ballot(e != 0u && (fill >> 31));
+  const uint64_t bfm = __ballot((b >> f) & 1u), afm = __ballot((a >> f) & 1u);
+  const uint64_t below = evm & ((1ull << lane) - 1ull);
+  if (below && ((exm >> (63 - __builtin_clzll(below))) & 1ull)) c += d;
+  uint32_t m = 0;
+  if (evm) {
+    const int first = __builtin_ctzll(evm), last = 63 - __builtin_clzll(evm);
+    const int df = (int)((bfm >> first) & 1ull) - (int)((afm >> first) & 1ull);
+    m = 1u | (uint32_t)(((exm >> last) & 1ull) << 1) | ((uint32_t)(df + 1) << 2);
   }
-  if (lane == 0) maps[slot] = (uint64_t)c0 | ((uint64_t)c1 << 24) | ((uint64_t)ex << 48);
+  if (lane == 0) maps[slot] = (uint8_t)m;  // an LDS slot: global stores inside the tile loop cost the loop registers
+  return c;
 }
 
 // ---------------------------------------------------------------------------------------------- K3 fused
@@ -56,6 +63,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
   uint32_t* wq = stack + (p.pure_and ? 0 : kMaxStack * kBlock) + wave * 2 * kWaveQ;
   uint32_t* wqs = wq + kWaveQ;
   uint32_t qn = 0;  // wave-uniform fill
+  // STATS_LEAP2 bytes of this workgroup's tiles, [tile k of the workgroup][wave], after the match queues
+  uint8_t* lmaps = reinterpret_cast<uint8_t*>(stack + (p.pure_and ? 0 : kMaxStack * kBlock) + (kBlock / 64) * 2 * kWaveQ);
+  int kk = 0;  // tiles of this workgroup so far
 
   if (MODE == MODE_LDS) {
     for (int64_t i = tid; i < table_words; i += kBlock) lds[i] = slot_init(p.slot_kind[i / G]);
@@ -115,27 +125,23 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
       const int64_t doc0 = group << 5;
       uint32_t mask = doc0 >= nd ? 0u : (nd - doc0 >= 32 ? ~0u : ((1u << (nd - doc0)) - 1u));
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
-      if (fast && (stats & 3) == KSTATS_LEAP2) {
-        // two scans in leap-frog: both masks are needed for the entry count, no early exit
+      if (fast) {
+        // STATS_LEAP2 (two scans in leap-frog): both masks are needed for the entry count, no early exit
+        const bool leap = (stats & 3) == KSTATS_LEAP2;
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;
         for (int l = 0; l < nl; ++l) {
+          if (!leap && !__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
+          // applyAnd of a scan after the index leaves (AndDocIdSet.java:124-126): its input docs are its entries
+          if ((stats >> (4 + l)) & 1) in_filter += __popc(mask);
           const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
           const uint32_t m = leaf_mask_reg(r, gclamp);
           ma = l == la ? m : ma;
           mb = l == lb ? m : mb;
           mask &= m;
         }
-        leap2_wave_map(p.leap_maps, t * (kBlock / 64) + wave, lane, ma, mb, v);
-      } else if (fast) {
-        for (int l = 0; l < nl; ++l) {
-          if (!__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
-          // applyAnd of a scan after the index leaves (AndDocIdSet.java:124-126): its input docs are its entries
-          if ((stats >> (4 + l)) & 1) in_filter += __popc(mask);
-          const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
-          mask &= leaf_mask_reg(r, gclamp);
-        }
+        if (leap) in_filter += leap2_entries(lmaps, kk * (kBlock / 64) + wave, lane, ma, mb, v);
       } else {
         mask = eval_filter(p, S, gclamp, mask, stack);
       }
@@ -182,8 +188,12 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
           qn = 0;
         }
       }
+      ++kk;
     }
     if (qn) flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
+    if (p.leap_maps)  // each wave stores its own bytes (tiles of other segments hold don't-care values)
+      for (int k = lane; k < kk; k += 64)
+        p.leap_maps[(t_begin + (int64_t)k * t_step) * (kBlock / 64) + wave] = lmaps[k * (kBlock / 64) + wave];
   }
   // numDocsScanned: wave reduce, one atomic per wave.
   for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);

@@ -219,7 +219,7 @@ def cpu_baseline(table, handles, query, workload, docs, args):
     import _oracle
     from pinot_amd.segment import ColumnData, SegmentBuffers
     types = dict(workload.schema)
-    nsample = args.cpu_sample_segments or workload.cpu_sample_segments
+    nsample = args.cpu_sample_segments or max(workload.cpu_sample_segments, 2 * host_cores())
     sample = handles[:max(1, min(nsample, len(handles)))]
     segs = []
     from pinot_amd import _lib as L
@@ -230,7 +230,7 @@ def cpu_baseline(table, handles, query, workload, docs, args):
             tcode = L.TYPE_NAMES[typ]
             cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
         segs.append(SegmentBuffers(docs, cols))
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_cores()
     _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False)  # warm-up
     reps, elapsed = 0, 0.0
     t0 = time.perf_counter()
@@ -243,8 +243,30 @@ def cpu_baseline(table, handles, query, workload, docs, args):
     rows = reps * len(segs) * docs
     _ = types
     return {"value": rows / elapsed, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": "%d segments x %d rows, %d repetitions, %.1f s, %d worker threads (oracle/oracle.c)" % (
-                len(segs), docs, reps, elapsed, threads)}
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "sample": "%d segments x %d rows, %d repetitions, %.1f s, %d worker threads = every core this process may "
+                      "run on (sched_getaffinity; the machine has %s) (oracle/oracle.c, one task per segment as "
+                      "GroupByCombineOperator%s)" % (len(segs), docs, reps, elapsed, threads, os.cpu_count(),
+                                                     "; scan path: the star-tree operator is not restated in C"
+                                                     if workload.star_tree else "")}
+
+
+def host_cores():
+    """Cores this process may run on (the GPU box grants a share of the machine: os.cpu_count() shows all)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def main():
@@ -319,6 +341,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     probe = table.plan(handles, q)
     nslots, nkeys, kinds = probe.layout()
+    probe_nslots = nslots
     probe.close()
     d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
     # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
@@ -326,6 +349,8 @@ def main():
 
     phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0,
               "decode": 0.0}
+
+    star_work = [0, 0, 0]
 
     def step():
         c0 = time.perf_counter()
@@ -344,7 +369,11 @@ def main():
             res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
         c4 = time.perf_counter()
         tm = plan.timing_us()
-        k_us = (tm[1], max(int(tm[2]), 1))  # scan launches of this query: summed duration, count
+        if w.star_tree and not args.no_star_tree:  # star-tree plans: traversal + pre-aggregated document scan
+            k_us = (tm[3], 1)
+            star_work[:] = plan.star_work()
+        else:
+            k_us = (tm[1], max(int(tm[2]), 1))  # scan launches of this query: summed duration, count
         fc_us, dec_us = plan.finalize_us
         plan.close()
         c5 = time.perf_counter()
@@ -389,7 +418,26 @@ def main():
 
     log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
-    if not args.no_bytes and not w.star_tree:  # scan-path bytes model; star-tree plans: n/a
+    if not args.no_bytes and w.star_tree and not args.no_star_tree and star_work[0] > 0:
+        # star-tree bytes model: nodes x 28 B + star-tree documents read x (bits of the dimensions
+        # they are read for + 8 B per pre-aggregated metric array)
+        preds = []
+        if q.filter is not None:
+            q.filter.postfix(preds, [])
+        dims = sorted(set(q.group_by) | {p.column for p in preds})
+        dim_bits = sum(_col_info(table, int(handles[0]), c)[1] for c in dims)
+        nslots = probe_nslots
+        per_doc = dim_bits / 8.0 + 8.0 * nslots
+        bytes_alg = star_work[1] * 28 + star_work[2] * per_doc
+        achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                    "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
+                    "kernels": "startree_traverse_kernel + startree_scan_kernel",
+                    "star_segments": int(star_work[0]), "star_nodes": int(star_work[1]),
+                    "star_docs_read": int(star_work[2]), "bytes_per_star_doc": per_doc,
+                    "launches_per_query": 1, "kernel_us_per_query": round(kernel_avg_us, 2)}
+    if not args.no_bytes and (not w.star_tree or args.no_star_tree):  # scan-path bytes model
         bytes_alg, matched = compulsory_bytes(table, handles, q, docs, w.inverted_columns)
         bytes_alg /= launches  # equal chunks of statistically identical segments: per-launch share
         achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
@@ -402,7 +450,7 @@ def main():
             roofline["traffic"] = round(pmc["traffic"], 0)
             roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not w.star_tree:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("bytes_alg pass done; CPU baseline")
         cpu = cpu_baseline(table, handles, q, w, docs, args)
 

@@ -214,8 +214,13 @@ int pgpu_plan_create_execute(pgpu_table table, const int64_t* segment_handles, i
                              const pgpu_query* q, void* stream, void* d_table, pgpu_plan* out);
 
 /* Timing of the last execution of this plan (HIP events on the execution stream), microseconds:
- * [0] whole execute, [1] the scan kernel launches (summed), [2] number of scan launches. */
-int pgpu_plan_timing(pgpu_plan plan, double* out3);
+ * [0] whole execute, [1] the scan kernel launches (summed), [2] number of scan launches, [3] the star-tree kernels
+ * (traversal + pre-aggregated document scan; 0 without star-tree segments).  out holds 4 doubles. */
+int pgpu_plan_timing(pgpu_plan plan, double* out4);
+
+/* Star-tree work of the last execution (after finalize): [0] segments answered from their star-tree, [1] their
+ * tree nodes (28 bytes each, OffHeapStarTreeNode), [2] star-tree documents the residual scan read. */
+int pgpu_plan_star_work(pgpu_plan plan, int64_t* out3);
 
 /* Per plan segment (plan order): 1 if the segment is scanned, 0 if its filter folds to always-false against the
  * segment's dictionaries (EmptyFilterOperator, core/plan/FilterPlanNode.java:146-176).  out holds num_segments. */
@@ -234,6 +239,55 @@ enum pgpu_leaf_type { PGPU_LEAF_EMPTY = 0, PGPU_LEAF_MATCH_ALL = 1, PGPU_LEAF_SC
 int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t num_filter_ops, const int32_t* leaf_types,
                                 const uint32_t* const* leaf_masks, int32_t num_leaves, int32_t num_docs,
                                 int64_t* out);
+
+/* ---- after the combine: server trim, server response, broker reduce (the step after the device path) */
+/* ORDER BY expression over the result: a group-by column (index = its position in the GROUP BY) or an aggregation
+ * (index = its position in the query; compared by its final result, as TableResizer's extractors do). */
+enum pgpu_order_kind { PGPU_ORDER_GROUP_BY = 0, PGPU_ORDER_AGGREGATION = 1 };
+typedef struct {
+  int32_t kind;
+  int32_t index;
+  int32_t ascending;
+} pgpu_order_by;
+/* SQL-mode query options of the combine (QueryContext / InstancePlanMakerImplV2.java:64-84). */
+typedef struct {
+  int32_t num_order_by;
+  const pgpu_order_by* order_by;
+  int32_t limit;                       /* LIMIT (SQL default 10) */
+  int32_t min_server_group_trim_size;  /* min.server.group.trim.size (default 5000); <= 0 disables server trim */
+  int32_t group_trim_threshold;        /* groupby.trim.threshold (default 1000000) */
+  int32_t num_select;                  /* broker reduce: the SELECT list in order (kind / index as for ORDER BY; */
+  const pgpu_order_by* select;         /* ascending unused); 0 = every group-by column, then every aggregation */
+} pgpu_sql_trim;
+
+/* The server's SQL-mode combined table (GroupByOrderByCombineOperator.java:82-97 + IndexedTable.finish,
+ * core/data/table/IndexedTable.java:62-89): with ORDER BY the top max(limit * 5, minServerGroupTrimSize) groups in
+ * ORDER BY order; without it `limit` groups (Pinot keeps the first keys its threads insert -- thread-order
+ * dependent; here the smallest composite keys); trim disabled: every group (sorted if ORDER BY).  Ties order by
+ * composite key.  Pinot resizes lossily past groupby.trim.threshold groups; the device combine is exact, so the
+ * result is the exact top records.  `out` is a new result (destroy both). */
+int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* out);
+
+/* PQL-mode trim (AggregationGroupByTrimmingService.trimIntermediateResultsMap, :54-120): per aggregation the rows of
+ * its top max(limit * 5, 5000) groups (MIN: smallest values, the others largest; by final result), applied only past
+ * 4 x that many groups; final_results != 0 gives the broker's trimFinalResults (:126-150): the top `limit`.
+ * rows is [num_aggs][cap] (may be NULL to get counts[num_aggs] only). */
+int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, int64_t* rows, int64_t cap,
+                         int64_t* counts);
+
+/* Server response of a SQL-mode group-by (IntermediateResultsBlock.getResultDataTable, core/operator/blocks/
+ * IntermediateResultsBlock.java:329-345; DataTableBuilder.java:55-103; DataTableImplV3.toBytes :183-290): DataTable V3
+ * bytes with the group-by columns and the aggregations' intermediate results (COUNT LONG, SUM / MIN / MAX DOUBLE,
+ * AVG an AvgPair OBJECT) of every row of `r`, and the block's execution statistics as metadata.  `table` supplies
+ * the group keys' values and column names.  out == NULL: *len = the size needed. */
+int pgpu_result_datatable(pgpu_result r, pgpu_table table, void* out, int64_t cap, int64_t* len);
+
+/* Broker reduce of SQL-mode group-by responses (GroupByDataTableReducer.java:290-330): the servers' DataTable V3
+ * bytes merged by key (AggregationFunction.merge), final results, ORDER BY (ties by key), LIMIT, and summed
+ * statistics, written as the BrokerResponseNative JSON (resultTable + statistics) into json (NUL-terminated;
+ * json == NULL: *len = the length needed without the NUL). */
+int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32_t num_tables,
+                           const pgpu_sql_trim* spec, char* json, int64_t cap, int64_t* len);
 
 /* ---- results: AggregationGroupByResult (core/query/aggregation/groupby/AggregationGroupByResult.java:31-81) */
 int pgpu_result_num_groups(pgpu_result r, int64_t* n);

@@ -57,6 +57,19 @@ class PredicateC(ctypes.Structure):
 LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP = 0, 1, 2, 3, 4
 
 
+ORDER_GROUP_BY, ORDER_AGGREGATION = 0, 1
+
+
+class OrderByC(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("index", ctypes.c_int32), ("ascending", ctypes.c_int32)]
+
+
+class SqlTrimC(ctypes.Structure):
+    _fields_ = [("num_order_by", ctypes.c_int32), ("order_by", ctypes.POINTER(OrderByC)), ("limit", ctypes.c_int32),
+                ("min_server_group_trim_size", ctypes.c_int32), ("group_trim_threshold", ctypes.c_int32),
+                ("num_select", ctypes.c_int32), ("select", ctypes.POINTER(OrderByC))]
+
+
 class FilterOpC(ctypes.Structure):
     _fields_ = [("op", c_i32), ("arg", c_i32)]
 
@@ -127,6 +140,7 @@ _PROTOS = {
     "pgpu_execute_groupby": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp,
                                      ctypes.POINTER(c_voidp)]),
     "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),
+    "pgpu_plan_star_work": (c_int, [c_voidp, c_i64p]),
     "pgpu_plan_scanned_segments": (c_int, [c_voidp, c_u8p]),
     "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_attach_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),
@@ -147,6 +161,11 @@ _PROTOS = {
     "pgpu_result_stats": (c_int, [c_voidp, c_i64p]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
+    "pgpu_result_trim_sql": (c_int, [c_voidp, ctypes.POINTER(SqlTrimC), ctypes.POINTER(c_voidp)]),
+    "pgpu_result_trim_pql": (c_int, [c_voidp, c_i32, c_i32, c_i64p, c_i64, c_i64p]),
+    "pgpu_result_datatable": (c_int, [c_voidp, c_voidp, c_voidp, c_i64, c_i64p]),
+    "pgpu_broker_reduce_sql": (c_int, [ctypes.POINTER(c_voidp), c_i64p, c_i32, ctypes.POINTER(SqlTrimC), c_voidp,
+                                       c_i64, c_i64p]),
     "pgpu_filter_entries_scanned": (c_int, [ctypes.POINTER(FilterOpC), c_i32, c_i32p, ctypes.POINTER(c_voidp), c_i32,
                                             c_i32, c_i64p]),
     "pgpu_generate_segment": (c_int, [c_voidp, ctypes.POINTER(GenColumnC), c_i32, c_i64, c_i32, c_i64p]),

@@ -11,13 +11,13 @@ LIB_PATH = os.path.join(HERE, "libpinotgpu.so")
 # (source, extra flags, object name): the scan kernels are compiled once per accumulator mode so the objects
 # build in parallel.
 SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime"), ("startree.cpp", [], "startree"),
-           ("filter_stats.cpp", [], "filter_stats"),
+           ("filter_stats.cpp", [], "filter_stats"), ("server_response.cpp", [], "server_response"),
            ("k_partition.hip", [], "k_partition")] + \
     [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
     [("k_staged.hip", ["-DPGPU_MODE=%d" % m], "k_staged_%d" % m) for m in range(3)] + \
     [("k_startree.hip", ["-DPGPU_MODE=%d" % m], "k_startree_%d" % m) for m in range(3)]
 HEADERS = ["internal.h", "device.h", "scan_direct.h", "scan_staged.h", "host_common.h", "startree_kernels.h",
-           "partition.h", "filter_stats.h"]
+           "partition.h", "filter_stats.h", "host_result.h"]
 ARCH = os.environ.get("PGPU_OFFLOAD_ARCH", "gfx950")
 
 

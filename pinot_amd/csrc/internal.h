@@ -156,7 +156,8 @@ struct KStarParams {
   uint64_t* table;                        // MODE_GLOBAL / MODE_HASH
   uint64_t* slab;                         // MODE_LDS: this kernel's first slab
   unsigned long long* hash_keys;
-  unsigned long long* stats;              // [0] docs matched, [1] entries scanned in filter
+  unsigned long long* stats;              // [0] docs matched, [1] entries scanned in filter, [3] star-tree
+                                          // documents read (positions of the emitted ranges)
 };
 
 // ---------------------------------------------------------------------------------------------- partitioned

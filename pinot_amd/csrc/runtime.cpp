@@ -32,6 +32,7 @@
 #include "../../include/pinotgpu.h"
 #include "filter_stats.h"
 #include "host_common.h"
+#include "host_result.h"
 #include "internal.h"
 
 using namespace pgpu;
@@ -125,53 +126,6 @@ struct DevBuf {
   }
   template <class T>
   T* as() const { return reinterpret_cast<T*>(p); }
-};
-
-struct HostPinned {
-  void* p = nullptr;
-  size_t cap = 0;
-  int ensure(size_t n) {
-    if (n <= cap) return 0;
-    if (p) hipHostFree(p);
-    p = nullptr;
-    size_t c = std::max<size_t>(n + n / 4, 4096);
-    HIP_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
-    cap = c;
-    return 0;
-  }
-  void release() {
-    if (p) hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
-
-// Pinned host buffers that hold finalized results, reused across queries (a result of ~10M groups is hundreds of
-// MB: pinning it per query would cost more than the scan).  Shared by a table and the results it produced, so a
-// result may outlive its table.
-struct ResultPool {
-  std::mutex mu;
-  std::vector<HostPinned> free;
-  ~ResultPool() {
-    for (auto& h : free) h.release();
-  }
-  HostPinned take() {
-    std::lock_guard<std::mutex> g(mu);
-    if (free.empty()) return HostPinned();
-    HostPinned h = free.back();
-    free.pop_back();
-    return h;
-  }
-  void give(HostPinned h) {
-    if (!h.p) return;
-    std::lock_guard<std::mutex> g(mu);
-    free.push_back(h);
-    if (free.size() > 4) {  // keep the largest few
-      auto it = std::min_element(free.begin(), free.end(), [](const HostPinned& a, const HostPinned& b) { return a.cap < b.cap; });
-      it->release();
-      free.erase(it);
-    }
-  }
 };
 
 // Host worker pool for per-query planning of long segment lists (the per-segment predicate translation that
@@ -465,6 +419,17 @@ struct pgpu_table_s {
   int num_cus = 256;
 };
 
+int pgpu::table_dict_view(pgpu_table t, int col, DictView* out) {
+  if (!t || col < 0 || col >= (int)t->names.size()) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad column %d", col);
+  const Dict& d = t->global[col];
+  out->type = d.type;
+  out->iv = &d.iv;
+  out->dv = &d.dv;
+  out->sv = &d.sv;
+  out->name = t->names[col];
+  return 0;
+}
+
 namespace {
 
 // ------------------------------------------------------------------------------------------------ dictionaries
@@ -755,36 +720,10 @@ struct pgpu_plan_s {
   int star_chunks = 1;
   size_t star_lds_bytes = 0;
   int64_t star_segments = 0;
+  int64_t star_docs_read = 0;                                // star-tree documents K6 read (after finalize)
 };
 
-struct pgpu_result_s {
-  int64_t n = 0;
-  int num_keys = 0;
-  int num_aggs = 0;
-  int num_slots = 0;
-  // Groups in ascending composite-key order, columnar in one pinned buffer: int32 group-by dictIds
-  // [num_keys][n], then (8-aligned) u64 accumulator words [num_slots][n]; slot 0 = COUNT.
-  HostPinned buf;
-  std::shared_ptr<ResultPool> pool;
-  std::vector<int32_t> agg_slot;          // per aggregation: its slot
-  std::vector<uint8_t> agg_conv;          // per aggregation: how the slot word reads (RCONV_*)
-  int64_t stats[6] = {0, 0, 0, 0, 0, 0};
-  ~pgpu_result_s() {
-    if (pool) pool->give(buf);
-    else buf.release();
-  }
-  static size_t slot_offset(int nk, int64_t n) { return ((size_t)nk * n * 4 + 7) & ~size_t(7); }
-  int alloc(int nk, int ns, int64_t rows) {
-    num_keys = nk;
-    num_slots = ns;
-    n = rows;
-    if (pool && !buf.p) buf = pool->take();
-    return buf.ensure(std::max<size_t>(slot_offset(nk, rows) + (size_t)ns * rows * 8, 64));
-  }
-  int32_t* gid(int j) { return reinterpret_cast<int32_t*>(buf.p) + (size_t)j * n; }
-  uint64_t* slot(int s) { return reinterpret_cast<uint64_t*>((uint8_t*)buf.p + slot_offset(num_keys, n)) + (size_t)s * n; }
-};
-enum { RCONV_I64 = 0, RCONV_F64 = 1, RCONV_KEY_F64 = 2 };
+
 
 namespace {
 
@@ -2208,11 +2147,12 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     matched = st[words];
     star_scanned = st[words + 1] + st[words + 2];
+    P->star_docs_read = (int64_t)st[words + 3];
     for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
     TRY(R->alloc(nk, nslots, n));
     int64_t j = 0;
@@ -2238,12 +2178,13 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
+    P->star_docs_read = (int64_t)st[4];
     TRY(R->alloc(nk, nslots, n));
     if (n > 0) {
       const uint8_t* dev = sc->ckeys.as<uint8_t>();
@@ -2267,12 +2208,13 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 24, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
+    P->star_docs_read = (int64_t)st[4];
     if (n > 0) {
       TRY(sc->stage.ensure((size_t)n * rec * 8));
       st = reinterpret_cast<uint64_t*>(sc->stage.p);
@@ -2297,6 +2239,11 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   const int na = (int)P->agg_fn.size();
   R->num_aggs = na;
   R->agg_slot = P->agg_slot;
+  R->key_cols = P->key_cols;
+  R->key_types.clear();
+  for (int c : P->key_cols) R->key_types.push_back(P->table->types[c]);
+  R->agg_fn = P->agg_fn;
+  R->agg_col = P->agg_col;
   R->agg_conv.assign(na, RCONV_I64);
   for (int a = 0; a < na; ++a) {
     const int fn = P->agg_fn[a];
@@ -3014,6 +2961,16 @@ int pgpu_plan_scanned_segments(pgpu_plan P, uint8_t* out) {
   return 0;
 }
 
+int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
+  if (!P || !out3) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  int64_t nodes = 0;
+  for (const KStarSeg& k : P->star) nodes += k.num_nodes;
+  out3[0] = (int64_t)P->star.size();
+  out3[1] = nodes;
+  out3[2] = P->star_docs_read;
+  return 0;
+}
+
 int pgpu_plan_timing(pgpu_plan P, double* out3) {
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   Scratch* sc = P->scratch;
@@ -3026,9 +2983,12 @@ int pgpu_plan_timing(pgpu_plan P, double* out3) {
     HIP_TRY(hipEventElapsedTime(&b, sc->cev[2 * c], sc->cev[2 * c + 1]));
     k += b;
   }
+  float st = 0;
+  if (!P->star.empty()) HIP_TRY(hipEventElapsedTime(&st, sc->ev[1], sc->ev[2]));
   out3[0] = a * 1000.0;
   out3[1] = k * 1000.0;
   out3[2] = P->num_tiles > 0 ? (double)P->launches_done : 0.0;
+  out3[3] = st * 1000.0;
   return 0;
 }
 

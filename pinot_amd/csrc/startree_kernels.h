@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void startree_scan_kernel(const KStarParams p)
   const int nr = S.out[0], rem = S.out[1];
   const int64_t T = S.prefix[nr];
   const int64_t lo = (int64_t)chunk * T / p.chunks_per_seg, hi = (int64_t)(chunk + 1) * T / p.chunks_per_seg;
-  unsigned long long matched = 0, scanned = 0;
+  unsigned long long matched = 0, scanned = 0, read = 0;  // read: star-tree documents of the emitted ranges
   const int nrem = __popc(rem);
   // Each lane walks positions lo + tid + k * 256 in batches of NB, every dependent level (range -> doc ->
   // residual dictIds -> group keys / pre-aggregated values) issued for the whole batch before it is consumed.
@@ -162,6 +162,7 @@ __global__ __launch_bounds__(256) void startree_scan_kernel(const KStarParams p)
         doc[k] = S.ranges[0];
       }
       scanned += ok[k] ? nrem : 0;
+      read += ok[k] ? 1 : 0;
     }
     for (int r = rem; r; r &= r - 1) {
       const int d = __ffs(r) - 1;
@@ -218,10 +219,12 @@ __global__ __launch_bounds__(256) void startree_scan_kernel(const KStarParams p)
   for (int off = 32; off > 0; off >>= 1) {
     matched += __shfl_xor(matched, off);
     scanned += __shfl_xor(scanned, off);
+    read += __shfl_xor(read, off);
   }
   if ((tid & 63) == 0) {
     if (matched) atomicAdd(p.stats, matched);
     if (scanned) atomicAdd(p.stats + 1, scanned);
+    if (read) atomicAdd(p.stats + 3, read);
   }
   if (MODE == MODE_LDS) {
     __syncthreads();

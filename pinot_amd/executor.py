@@ -51,8 +51,10 @@ class GroupByResult:
     """Groups in ascending composite-key order, held columnar (numpy) as the C ABI returns them; the Python form
     ({key tuple: [aggregation results]}) is built on first use of `keys` / `values` / `as_dict()`."""
 
-    def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None):
+    def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None, holder=None, table=None,
+                 query=None):
         self.stats = stats
+        self._holder, self._table, self._query = holder, table, query  # the C result behind the columnar views
         self.exact = exact or {}    # agg index -> np.int64 array of exact integer accumulators
         self._keys, self._values = keys, values
         # columnar: (dicts, [per group-by column: [n] int32 dictIds], per-agg (fn, values f64 | None,
@@ -104,6 +106,61 @@ class GroupByResult:
 
     def __len__(self):
         return self._n
+
+    # ---- after the combine (server_response.cpp)
+    def trim_sql(self, query=None):
+        """The server's SQL-mode combined table (GroupByOrderByCombineOperator + IndexedTable.finish): the top
+        max(limit * 5, minServerGroupTrimSize) groups in ORDER BY order, `limit` groups without ORDER BY, every group
+        when server trim is off (query.min_server_group_trim_size <= 0)."""
+        query = query or self._query
+        keep, spec = query.sql_trim_c()
+        out = ctypes.c_void_p()
+        L.check(self._table.lib.pgpu_result_trim_sql(self._holder.r, ctypes.byref(spec), ctypes.byref(out)))
+        return _decode_result(self._table, query, _ResultHolder(self._table.lib, out))
+
+    def trim_pql(self, limit, final=False):
+        """AggregationGroupByTrimmingService: per aggregation the [(key tuple, value)] of its top groups (MIN
+        ascending, the others descending; final=True: the broker's top `limit`, else the server trim)."""
+        lib, na = self._table.lib, len(self._query.aggregations)
+        counts = np.zeros(max(na, 1), dtype=np.int64)
+        L.check(lib.pgpu_result_trim_pql(self._holder.r, limit, int(final), None, 0, L.ptr(counts, ctypes.c_int64)))
+        cap = int(counts.max()) if na else 0
+        rows = np.zeros(max(na * cap, 1), dtype=np.int64)
+        L.check(lib.pgpu_result_trim_pql(self._holder.r, limit, int(final), L.ptr(rows, ctypes.c_int64), cap,
+                                         L.ptr(counts, ctypes.c_int64)))
+        keys, values = self.keys, self.values
+        out = []
+        for a in range(na):
+            sel = rows[a * cap:a * cap + counts[a]]
+            out.append([(keys[i], values[i][a]) for i in sel.tolist()])
+        return out
+
+    def datatable(self):
+        """The server response bytes (DataTable V3, IntermediateResultsBlock.getResultDataTable) of these rows."""
+        lib = self._table.lib
+        n = ctypes.c_int64()
+        L.check(lib.pgpu_result_datatable(self._holder.r, self._table.handle, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(n.value, 1))
+        L.check(lib.pgpu_result_datatable(self._holder.r, self._table.handle, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+
+def broker_reduce_sql(datatables, query):
+    """GroupByDataTableReducer (SQL): merges the servers' DataTable V3 responses, ORDER BY, LIMIT, final results;
+    returns the BrokerResponseNative as a dict (resultTable + statistics)."""
+    import json
+    lib = L.load()
+    keep, spec = query.sql_trim_c()
+    bufs = [ctypes.create_string_buffer(bytes(b), max(len(b), 1)) for b in datatables]
+    ptrs = (ctypes.c_void_p * max(len(bufs), 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+    lens = np.array([len(b) for b in datatables] or [0], dtype=np.int64)
+    n = ctypes.c_int64()
+    L.check(lib.pgpu_broker_reduce_sql(ptrs, L.ptr(lens, ctypes.c_int64), len(bufs), ctypes.byref(spec), None, 0,
+                                       ctypes.byref(n)))
+    out = ctypes.create_string_buffer(n.value + 1)
+    L.check(lib.pgpu_broker_reduce_sql(ptrs, L.ptr(lens, ctypes.c_int64), len(bufs), ctypes.byref(spec), out,
+                                       n.value + 1, ctypes.byref(n)))
+    return json.loads(out.value.decode("utf-8"))
 
 
 def aggregation_defaults(aggregations):
@@ -408,8 +465,15 @@ class Plan:
         return out[:self.num_segments].astype(bool)
 
     def timing_us(self):
-        out = (ctypes.c_double * 3)()
+        """(execute, scan launches summed, number of scan launches, star-tree kernels) in microseconds."""
+        out = (ctypes.c_double * 4)()
         L.check(self.lib.pgpu_plan_timing(self.handle, out))
+        return out[0], out[1], out[2], out[3]
+
+    def star_work(self):
+        """(star-tree segments, their nodes, star-tree documents read) of the last finalized execution."""
+        out = (ctypes.c_int64 * 3)()
+        L.check(self.lib.pgpu_plan_star_work(self.handle, out))
         return out[0], out[1], out[2]
 
     def finalize(self, stream=None, d_table=None):
@@ -500,4 +564,5 @@ def _decode_result(table, query, holder):
         aggs.append((fn, v, e, c))
     st = np.zeros(6, dtype=np.int64)
     L.check(lib.pgpu_result_stats(r, L.ptr(st, ctypes.c_int64)))
-    return GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n))
+    return GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n), holder=holder,
+                         table=table, query=query)

@@ -20,6 +20,9 @@ UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
 _PRED_CODE = {EQ: L.PRED_EQ, NOT_EQ: L.PRED_NOT_EQ, IN: L.PRED_IN, NOT_IN: L.PRED_NOT_IN, RANGE: L.PRED_RANGE}
 AGG_FUNCTIONS = {"COUNT": L.AGG_COUNT, "SUM": L.AGG_SUM, "MIN": L.AGG_MIN, "MAX": L.AGG_MAX, "AVG": L.AGG_AVG}
 DEFAULT_NUM_GROUPS_LIMIT = 100000  # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT (:70)
+DEFAULT_LIMIT = 10  # QueryContext default LIMIT / TOP
+DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE = 5000  # InstancePlanMakerImplV2.DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE
+DEFAULT_GROUP_TRIM_THRESHOLD = 1000000  # InstancePlanMakerImplV2.DEFAULT_GROUPBY_TRIM_THRESHOLD
 
 
 class Predicate:
@@ -94,12 +97,43 @@ class FilterContext:
 
 class QueryContext:
     def __init__(self, group_by, aggregations, filter=None, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT,
-                 use_star_tree=True):
+                 use_star_tree=True, select=None, order_by=None, limit=DEFAULT_LIMIT,
+                 min_server_group_trim_size=DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE,
+                 group_trim_threshold=DEFAULT_GROUP_TRIM_THRESHOLD):
         self.filter = filter
         self.use_star_tree = use_star_tree  # debug option useStarTree (StarTreeUtils.java:51-59)
         self.group_by = list(group_by)
         self.aggregations = [(fn.upper(), col) for fn, col in aggregations]
         self.num_groups_limit = num_groups_limit
+        # SQL-mode parts (QueryContext.getSelectExpressions / getOrderByExpressions / getLimit): the SELECT list as
+        # ('col', name) / ('agg', FN, col), ORDER BY as [(expr, ascending)], LIMIT; the combine's trim options
+        # (InstancePlanMakerImplV2.java:64-84)
+        self.select = list(select) if select is not None else \
+            [("col", c) for c in self.group_by] + [("agg", fn, col) for fn, col in self.aggregations]
+        self.order_by = list(order_by or [])
+        self.limit = limit
+        self.min_server_group_trim_size = min_server_group_trim_size
+        self.group_trim_threshold = group_trim_threshold
+
+    def expr_ref(self, expr):
+        """(kind, index) of a SELECT / ORDER BY expression over the result: (0, group-by position) or
+        (1, aggregation position)."""
+        if expr[0] == "col":
+            return L.ORDER_GROUP_BY, self.group_by.index(expr[1])
+        return L.ORDER_AGGREGATION, self.aggregations.index((expr[1].upper(), expr[2]))
+
+    def sql_trim_c(self):
+        """The SQL-mode combine / reduce options as pgpu_sql_trim (keepalive, struct)."""
+        ob = (L.OrderByC * max(len(self.order_by), 1))()
+        for i, (e, asc) in enumerate(self.order_by):
+            ob[i].kind, ob[i].index = self.expr_ref(e)
+            ob[i].ascending = int(asc)
+        sel = (L.OrderByC * max(len(self.select), 1))()
+        for i, e in enumerate(self.select):
+            sel[i].kind, sel[i].index = self.expr_ref(e)
+        t = L.SqlTrimC(len(self.order_by), ob, self.limit, self.min_server_group_trim_size, self.group_trim_threshold,
+                       len(self.select), sel)
+        return (ob, sel), t
 
     def columns(self):
         cols = []
@@ -233,22 +267,24 @@ class _Parser:
         self.i += 1
         return tok[1]
 
+    def select_list_item(self):
+        tok = self.peek()
+        if tok[0] == "id" and self.peek(1) == ("op", "("):
+            fn = self.take("id").upper()
+            self.take("op", "(")
+            col = "*" if self.peek() == ("op", "*") else None
+            if col:
+                self.take("op", "*")
+            else:
+                col = self.take("id")
+            self.take("op", ")")
+            return ("agg", fn, col)
+        return ("col", self.take("id"))
+
     def select_list(self):
         items = []
         while True:
-            tok = self.peek()
-            if tok[0] == "id" and self.peek(1) == ("op", "("):
-                fn = self.take("id").upper()
-                self.take("op", "(")
-                col = "*" if self.peek() == ("op", "*") else None
-                if col:
-                    self.take("op", "*")
-                else:
-                    col = self.take("id")
-                self.take("op", ")")
-                items.append(("agg", fn, col))
-            else:
-                items.append(("col", self.take("id")))
+            items.append(self.select_list_item())
             if self.peek() == ("op", ","):
                 self.take("op", ",")
                 continue
@@ -322,7 +358,9 @@ class _Parser:
 
 
 def parse_query(sql, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
-    """Parses `SELECT aggs FROM t [WHERE ...] GROUP BY cols [TOP n | ORDER BY ... | LIMIT n]`."""
+    """Parses `SELECT cols / aggs FROM t [WHERE ...] [GROUP BY cols] [ORDER BY expr [ASC|DESC], ...]
+    [TOP n | LIMIT n]`.  Aggregations that appear only in ORDER BY are computed as well (Pinot's hidden
+    aggregations) but not selected."""
     p = _Parser(sql)
     p.take("id", "SELECT")
     items = p.select_list()
@@ -340,5 +378,25 @@ def parse_query(sql, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
         while p.peek() == ("op", ","):
             p.take("op", ",")
             group_by.append(p.take("id"))
-    aggs = [(fn, col) for kind, *rest in items if kind == "agg" for fn, col in [rest]]
-    return QueryContext(group_by, aggs, flt, num_groups_limit)
+    order_by, limit = [], DEFAULT_LIMIT
+    if p.kw("ORDER"):
+        p.take("id")
+        p.take("id", "BY")
+        while True:
+            e = p.select_list_item()
+            asc = True
+            if p.kw("ASC", "DESC"):
+                asc = p.take("id").upper() == "ASC"
+            order_by.append((e if e[0] == "col" else ("agg", e[1], e[2]), asc))
+            if p.peek() != ("op", ","):
+                break
+            p.take("op", ",")
+    if p.kw("TOP", "LIMIT"):
+        p.take("id")
+        limit = int(p.take("lit"))
+    select = [("col", it[1]) if it[0] == "col" else ("agg", it[1], it[2]) for it in items]
+    aggs = []
+    for e in [x for x in select if x[0] == "agg"] + [e for e, _ in order_by if e[0] == "agg"]:
+        if (e[1], e[2]) not in aggs:
+            aggs.append((e[1], e[2]))
+    return QueryContext(group_by, aggs, flt, num_groups_limit, select=select, order_by=order_by, limit=limit)

@@ -164,6 +164,12 @@ typedef struct {
 /* Query options: debug option useStarTree=false (StarTreeUtils.isStarTreeDisabled, core/startree/StarTreeUtils.java:
  * 51-59) keeps the scan path on segments that carry a star-tree. */
 #define PGPU_OPT_NO_STAR_TREE 1
+/* Group-by combine of SQL mode (queryOptions groupByMode=sql: GroupByOrderByCombineOperator) instead of the default
+ * PQL GroupByCombineOperator: no inter-segment cap of 2 x numGroupsLimit (GroupByCombineOperator.java:61,78-80,138)
+ * and no numGroupsLimitReached flag (GroupByOrderByCombineOperator.java:246).  Either way a segment whose group-key
+ * space exceeds numGroupsLimit keeps its first numGroupsLimit groups in first-seen docId order
+ * (DictionaryBasedGroupKeyGenerator.java:1101-1113), as Pinot's map-based holders do. */
+#define PGPU_OPT_SQL_GROUP_BY 2
 
 /* A query compiled against a list of pinned segments (InstancePlanMakerImplV2.makeInstancePlan +
  * per-segment AggregationGroupByPlanNode: predicate evaluators per segment, group-key layout, accumulators). */
@@ -311,6 +317,9 @@ int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out);
 /* ExecutionStatistics (core/operator/ExecutionStatistics.java:42): numDocsScanned, numEntriesScannedInFilter,
  * numEntriesScannedPostFilter, numTotalDocs, plus [4] numSegmentsProcessed, [5] numSegmentsMatched. */
 int pgpu_result_stats(pgpu_result r, int64_t* out6);
+/* numGroupsLimitReached (GroupByCombineOperator.java:215-219, PQL mode): 1 when the combined groups reach
+ * numGroupsLimit. */
+int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out);
 int pgpu_result_destroy(pgpu_result r);
 
 /* Docid match bitmap of one segment's filter (the FilterOperator's doc set, K2): bit d of 64-bit word d/64.

@@ -1374,6 +1374,9 @@ int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int
     }
   }
   out->num_groups = ng;
+  /* GroupByCombineOperator.mergeResults (:215-219): the merged map holds >= numGroupsLimit groups (PQL combine);
+   * without the combine, a segment's holder reached its bound. */
+  if (q->combine) out->num_groups_limit_reached = q->num_group_by > 0 && ng >= q->num_groups_limit;
   out->key_blob = kb.b;
   out->key_offsets = koff;
   out->values = malloc(sizeof(double) * (size_t)(ng * na + 1));

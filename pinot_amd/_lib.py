@@ -54,6 +54,8 @@ class PredicateC(ctypes.Structure):
 
 
 # pgpu_leaf_type: Pinot's leaf operator of a predicate in one segment (pgpu_filter_entries_scanned)
+OPT_NO_STAR_TREE = 1
+OPT_SQL_GROUP_BY = 2
 LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP = 0, 1, 2, 3, 4
 
 
@@ -159,6 +161,7 @@ _PROTOS = {
     "pgpu_result_avg_counts": (c_int, [c_voidp, c_int, c_i64p]),
     "pgpu_result_values_i64": (c_int, [c_voidp, c_int, c_i64p]),
     "pgpu_result_stats": (c_int, [c_voidp, c_i64p]),
+    "pgpu_result_groups_limit_reached": (c_int, [c_voidp, ctypes.POINTER(ctypes.c_int32)]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
     "pgpu_result_trim_sql": (c_int, [c_voidp, ctypes.POINTER(SqlTrimC), ctypes.POINTER(c_voidp)]),

@@ -13,6 +13,15 @@ namespace pgpu {
 
 #define PGPU_HIP_OK(x) ((x) == hipSuccess ? 0 : -1)
 
+// Reads through the global address space.  Pointers read out of the packed segment / star-tree records are generic
+// to the compiler, which then emits FLAT loads: those also count in lgkmcnt, so every wait for an LDS access (match
+// queues, LDS tables, LUT caches) waits for all outstanding column loads too.  Every pointer passed here points into
+// device memory (hipMalloc), never into LDS.
+template <typename T>
+using gmem = const __attribute__((address_space(1))) T;
+template <typename T>
+__device__ __forceinline__ gmem<T>* gp(const T* p) { return (gmem<T>*)p; }
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // Value of doc `doc` in a packed column (PinotDataBitSet.readInt semantics).  The two-word window never leaves
@@ -21,7 +30,8 @@ __device__ __forceinline__ uint32_t gather_id(const uint32_t* __restrict__ fwd, 
   const uint64_t bit = (uint64_t)doc * (uint64_t)bits;
   const uint64_t wi = bit >> 5;
   const uint32_t sh = (uint32_t)(bit & 31);
-  const uint64_t two = ((uint64_t)bswap32(fwd[wi]) << 32) | (uint64_t)bswap32(fwd[wi + 1]);
+  gmem<uint32_t>* f = gp(fwd);
+  const uint64_t two = ((uint64_t)bswap32(f[wi]) << 32) | (uint64_t)bswap32(f[wi + 1]);
   return (uint32_t)(two >> (64 - sh - bits)) & ((1u << bits) - 1u);
 }
 
@@ -39,10 +49,17 @@ __device__ __forceinline__ uint32_t extract(const uint32_t (&w)[B + 1]) {
   }
 }
 
-template <int B>
+// G: `words` is in global memory (else an LDS stage buffer: the staged kernel).
+template <int B, bool G = true>
 __device__ __forceinline__ void load_group(const uint32_t* __restrict__ words, uint32_t (&w)[B + 1]) {
+  if constexpr (G) {
+    gmem<uint32_t>* g = gp(words);
 #pragma unroll
-  for (int k = 0; k < B; ++k) w[k] = bswap32(words[k]);
+    for (int k = 0; k < B; ++k) w[k] = bswap32(g[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < B; ++k) w[k] = bswap32(words[k]);
+  }
   w[B] = 0;
 }
 
@@ -74,18 +91,19 @@ __device__ __forceinline__ uint32_t eq_all(const uint32_t (&w)[B + 1], uint32_t 
   return m;
 }
 
-template <int B>
+template <int B, bool G>
 __device__ __forceinline__ uint32_t leaf_range_b(const uint32_t* __restrict__ words, uint32_t lo, uint32_t span) {
   uint32_t w[B + 1];
-  load_group<B>(words, w);
+  load_group<B, G>(words, w);
   if (span == 1) return eq_all<B>(w, lo, std::make_integer_sequence<int, 32>{});
   return range_all<B>(w, lo, lo + span, std::make_integer_sequence<int, 32>{});
 }
 
-template <int B>
+template <int B, bool G>
 __device__ __forceinline__ uint32_t leaf_set_b(const uint32_t* __restrict__ words, const uint32_t* __restrict__ set) {
   uint32_t w[B + 1];
-  load_group<B>(words, w);
+  load_group<B, G>(words, w);
+  gmem<uint32_t>* gs = gp(set);
   uint32_t m = 0;
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
@@ -93,13 +111,14 @@ __device__ __forceinline__ uint32_t leaf_set_b(const uint32_t* __restrict__ word
     uint32_t v;
     if (sh + B <= 32) v = (w[wi] >> (32 - sh - B)) & ((1u << B) - 1u);
     else v = ((w[wi] << (sh + B - 32)) | (w[wi + 1] >> (64 - sh - B))) & ((1u << B) - 1u);
-    m |= ((set[v >> 5] >> (v & 31)) & 1u) << i;
+    m |= ((gs[v >> 5] >> (v & 31)) & 1u) << i;
   }
   return m;
 }
 
 // Wave-uniform dispatch on (kind, bits) to the decoder instance; `words` = this lane's 32-doc group (global
-// memory or an LDS stage buffer).
+// memory, G = true, or an LDS stage buffer).
+template <bool G = true>
 __device__ __forceinline__ uint32_t leaf_eval_words(int kind, int negate, uint32_t lo, uint32_t span,
                                                     const uint32_t* set, const uint32_t* words, int bits) {
   if (kind == LEAF_ALL) return ~0u;
@@ -109,7 +128,7 @@ __device__ __forceinline__ uint32_t leaf_eval_words(int kind, int negate, uint32
     switch (bits) {
 #define PGPU_CASE(B) \
   case B:            \
-    m = leaf_range_b<B>(words, lo, span); \
+    m = leaf_range_b<B, G>(words, lo, span); \
     break;
       PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
       PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
@@ -123,7 +142,7 @@ __device__ __forceinline__ uint32_t leaf_eval_words(int kind, int negate, uint32
     switch (bits) {
 #define PGPU_CASE(B) \
   case B:            \
-    m = leaf_set_b<B>(words, set); \
+    m = leaf_set_b<B, G>(words, set); \
     break;
       PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
       PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
@@ -156,7 +175,7 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
     return negate ? ~m : m;
   }
   if (kind == LEAF_BITMAP) {
-    const uint32_t m = set[group];
+    const uint32_t m = gp(set)[group];
     return negate ? ~m : m;
   }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
@@ -357,7 +376,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     }
     int32_t g[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) g[b] = S[b].cols[kc].lut[id[b]];
+    for (int b = 0; b < NB; ++b) g[b] = gp(S[b].cols[kc].lut)[id[b]];
 #pragma unroll
     for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
   }
@@ -387,10 +406,10 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       }
       if (kind == SLOT_SUM_F64) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) dval[b] = S[b].cols[col].dval[id[b]];
+        for (int b = 0; b < NB; ++b) dval[b] = gp(S[b].cols[col].dval)[id[b]];
       } else {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) ikey[b] = S[b].cols[col].dkey[id[b]];
+        for (int b = 0; b < NB; ++b) ikey[b] = gp(S[b].cols[col].dkey)[id[b]];
       }
     }
     if (G == 1) {  // single row: fold the lane's docs, then the wave
@@ -422,7 +441,7 @@ __device__ __forceinline__ void decode_half(const uint32_t (&w)[B + 1], uint32_t
 template <int B, int H>
 __device__ __forceinline__ void decode_group_b(const uint32_t* __restrict__ words, uint32_t (&ids)[16]) {
   uint32_t w[B + 1];
-  load_group<B>(words, w);
+  load_group<B, true>(words, w);
   decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
 }
 
@@ -461,7 +480,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
-    const int32_t* __restrict__ lut = c.lut;
+    gmem<int32_t>* __restrict__ lut = gp(c.lut);
     const int32_t stride = (int32_t)p.key_stride[j];
     int32_t g[16];
 #pragma unroll
@@ -494,7 +513,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     const KCol& c = S.cols[col];
     decode_group<H>(c.fwd, c.bits, group, ids);
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
-      const int64_t* __restrict__ dk = c.dkey;
+      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
       int64_t v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
@@ -516,7 +535,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       }
     }
     if (need_f) {
-      const double* __restrict__ dv = c.dval;
+      gmem<double>* __restrict__ dv = gp(c.dval);
       double v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;

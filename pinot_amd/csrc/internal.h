@@ -130,6 +130,7 @@ struct KStarSeg {
   int32_t pad;
   const uint32_t* dim_fwd[kMaxStarDims];  // star-tree documents' dictIds (MSB-first, padded)
   int32_t dim_bits[kMaxStarDims];
+  int32_t dim_card[kMaxStarDims];         // the segment's dictionary size of each group-by / predicate dim
   const uint32_t* match[kMaxStarDims];    // matching-dictId bitset of each predicate dim
   const int32_t* key_lut[kMaxKeys];       // local -> global dictId of each group-by key
   int32_t key_dim[kMaxKeys];              // dim of each group-by key
@@ -143,8 +144,11 @@ struct KStarSeg {
 
 struct KStarParams {
   const KStarSeg* segs;
-  int32_t num_segs;
-  int32_t chunks_per_seg;
+  int32_t num_segs;                       // <= kStarMaxSegs per launch
+  int32_t range_cache;                    // ranges per segment cached in LDS (0: binary search in global memory)
+  const int64_t* seg_total;               // K5: 32-doc groups of each segment's emitted ranges
+  int32_t num_wgs;                        // K6 workgroups (persistent: each takes a contiguous run of groups)
+  int32_t pad0;
   int32_t num_keys;
   int32_t num_slots;
   int64_t key_stride[kMaxKeys];
@@ -152,7 +156,7 @@ struct KStarParams {
   int32_t slot_kind[kMaxSlots];
   int32_t slot_int[kMaxSlots];            // 1: the slot's column is INT/LONG (MIN/MAX keys are the value)
   int32_t lds_table_words;
-  int32_t pad;
+  int32_t cache_ints;                     // LDS ints for a segment's key LUTs + residual match sets (0: read global)
   uint64_t* table;                        // MODE_GLOBAL / MODE_HASH
   uint64_t* slab;                         // MODE_LDS: this kernel's first slab
   unsigned long long* hash_keys;
@@ -243,7 +247,8 @@ int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_se
 int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream);
-int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream);
+constexpr int kStarMaxSegs = 4096;  // star-tree segments per K6 launch (their group prefix lives in LDS)
+int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.
 int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,

@@ -11,18 +11,18 @@
 namespace pgpu {
 
 int PGPU_CAT(launch_startree_scan_mode, PGPU_MODE)(const KStarParams& p, size_t lds_bytes, void* stream) {
-  const int grid = p.num_segs * p.chunks_per_seg;
-  if (grid <= 0) return 0;
-  hipLaunchKernelGGL(startree_scan_kernel<PGPU_MODE>, dim3(grid), dim3(256), lds_bytes,
+  const int grid = p.num_wgs;
+  if (grid <= 0 || p.num_segs <= 0) return 0;
+  hipLaunchKernelGGL(startree_scan_kernel<PGPU_MODE>, dim3(grid), dim3(StarBlock<PGPU_MODE>::value), lds_bytes,
                      reinterpret_cast<hipStream_t>(stream), p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 #if PGPU_MODE == 0
-int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, void* stream) {
+int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, void* stream) {
   if (num_segs <= 0) return 0;
   hipLaunchKernelGGL(startree_traverse_kernel, dim3(num_segs), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     segs);
+                     segs, seg_total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif

@@ -45,7 +45,7 @@ __device__ __forceinline__ void part_keys(const KParams& p, const SegView& S, in
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
-    const int32_t* __restrict__ lut = c.lut;
+    gmem<int32_t>* __restrict__ lut = gp(c.lut);
     const int32_t stride = (int32_t)p.key_stride[j];
     int32_t g[16];
 #pragma unroll
@@ -79,7 +79,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     decode_group<H>(c.fwd, c.bits, group, ids);
     uint64_t* __restrict__ out = (two ? pp.mid_val : pp.rec_val) + (int64_t)s * pp.rec_cap;
     if (pp.stream_f64[s]) {
-      const double* __restrict__ dv = c.dval;
+      gmem<double>* __restrict__ dv = gp(c.dval);
       double v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;
@@ -87,7 +87,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
       for (int i = 0; i < 16; ++i)
         if ((m >> i) & 1u) out[pos[i]] = (uint64_t)__double_as_longlong(v[i]);
     } else {
-      const int64_t* __restrict__ dk = c.dkey;
+      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
       int64_t v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;

@@ -25,6 +25,7 @@
 #include <unordered_map>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -249,6 +250,7 @@ constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large 
 constexpr int64_t kPartLds = 64 * 1024;              // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
 constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
+constexpr int kDocIdColumn = -2;                     // query column of the virtual $docId (hidden first-doc slot)
 
 bool is_int_type(int t) { return t == PGPU_INT || t == PGPU_LONG; }
 bool is_fp_type(int t) { return t == PGPU_FLOAT || t == PGPU_DOUBLE; }
@@ -417,6 +419,13 @@ struct pgpu_table_s {
   std::shared_ptr<ResultPool> result_pool = std::make_shared<ResultPool>();
   int64_t device_bytes = 0;
   int num_cus = 256;
+  // The virtual $docId column (identity forward index + values, docs [0, docid_n)): the hidden MIN($docId) slot of
+  // the first-seen numGroupsLimit emulation reads it like any other column.
+  uint32_t* d_docid_fwd = nullptr;
+  int64_t* d_docid_key = nullptr;
+  int docid_bits = 0;
+  int64_t docid_n = 0;
+  std::vector<void*> retired;  // replaced $docId buffers (plans built earlier may still point at them)
 };
 
 int pgpu::table_dict_view(pgpu_table t, int col, DictView* out) {
@@ -580,6 +589,39 @@ int ensure_values(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
   return 0;
 }
 
+int64_t padded_fwd_words(int64_t num_docs, int bits);
+
+// Identity forward index of the virtual $docId column over docs [0, n): Pinot's MSB-first fixed-bit layout of the
+// values 0..n-1 (a sorted "dictionary" of docIds), and the values as int64 (the MIN slot's keys).
+int ensure_docid(pgpu_table_s* t, int64_t n, hipStream_t stream) {
+  if (n <= t->docid_n) return 0;
+  int bits = 1;
+  while (bits < 31 && (int64_t(1) << bits) < n) ++bits;
+  const int64_t words = padded_fwd_words(n, bits);
+  std::vector<uint8_t> fwd((size_t)words * 4, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t bit = (uint64_t)i * bits;
+    for (int b = 0; b < bits; ++b)
+      if ((i >> (bits - 1 - b)) & 1) fwd[(bit + b) >> 3] |= (uint8_t)(0x80u >> ((bit + b) & 7));
+  }
+  std::vector<int64_t> key(n);
+  for (int64_t i = 0; i < n; ++i) key[i] = i;
+  if (t->d_docid_fwd) t->retired.push_back(t->d_docid_fwd);
+  if (t->d_docid_key) t->retired.push_back(t->d_docid_key);
+  t->d_docid_fwd = nullptr;
+  t->d_docid_key = nullptr;
+  t->docid_n = 0;
+  HIP_TRY(hipMalloc(&t->d_docid_fwd, fwd.size()));
+  HIP_TRY(hipMalloc(&t->d_docid_key, (size_t)n * 8));
+  HIP_TRY(hipMemcpyAsync(t->d_docid_fwd, fwd.data(), fwd.size(), hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(t->d_docid_key, key.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  t->docid_bits = bits;
+  t->docid_n = n;
+  t->device_bytes += (int64_t)fwd.size() + n * 8;
+  return 0;
+}
+
 void free_segment(pgpu_table_s* t, Segment* s) {
   for (auto& c : s->cols) {
     if (c.d_lut) hipFree(c.d_lut);
@@ -712,13 +754,28 @@ struct pgpu_plan_s {
   // apply and the GPU result is not reported (PGPU_ERR_UNSUPPORTED: the caller runs Pinot's own operator).
   int64_t num_groups_limit = 0;
   bool limit_sensitive = false;
+  // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
+  // another at finalize, their rows truncated / capped and merged on the host.
+  bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
+  bool composite = false;
+  bool pql_cap = false;                   // GroupByCombineOperator's inter-segment cap of 2 x numGroupsLimit
+  struct Part {
+    std::unique_ptr<pgpu_plan_s> plan;
+    std::vector<int32_t> seg_index;       // plan segment positions of the part's segments
+    bool first_seen = false;              // rows in first-seen order (map holder)
+    bool truncate = false;                // keep the first numGroupsLimit groups (segment key space > the limit)
+  };
+  std::vector<Part> parts;
   // star-tree segments (StarTreeFilterOperator + StarTreeGroupByExecutor instead of the scan)
   std::vector<KStarSeg> star;                                // host images; pointers patched at execute
   std::vector<std::tuple<int, int, int64_t>> star_match_fix; // (star seg, dim, word offset in set_words)
   std::vector<int64_t> star_work_off;                        // per star seg: byte offset of its scratch
   int64_t star_work_bytes = 0;
-  int star_chunks = 1;
+  int star_chunks = 1;                    // K6 workgroups per launch batch (persistent)
+  int star_batches = 0;                   // K6 launches (kStarMaxSegs segments each)
+  int32_t star_range_cache = 0;           // ranges per segment K6 stages in LDS
   size_t star_lds_bytes = 0;
+  int32_t star_cache_ints = 0;  // K6 LDS cache of key LUTs + match sets (max over the star-tree segments; 0: off)
   int64_t star_segments = 0;
   int64_t star_docs_read = 0;                                // star-tree documents K6 read (after finalize)
 };
@@ -1078,7 +1135,7 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
                       hipStream_t stream, bool* used) {
   *used = false;
   const StarTreeDev* st = s->star.get();
-  if (!st || st->num_dims > kMaxStarDims || st->num_nodes < 1) return 0;
+  if (!st || st->num_dims > kMaxStarDims || st->num_nodes < 1 || P->first_doc_slot) return 0;
   bool has_avg = false;
   int avg_col = -1;
   for (int i = 0; i < q->num_aggs; ++i) {
@@ -1149,7 +1206,21 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
     TRY(ensure_lut(t, *s, c, stream));
     k.key_lut[j] = s->cols[c].d_lut;
     k.key_dim[j] = st->dim_of(c);
+    k.dim_card[k.key_dim[j]] = s->cols[c].card;
     if (!(k.pred_mask & (1 << k.key_dim[j]))) k.group_mask |= 1 << k.key_dim[j];
+  }
+  for (const auto& comp : comps) {
+    const int col = q->predicates[comp[0]].column;
+    k.dim_card[st->dim_of(col)] = s->cols[col].card;
+  }
+  {  // K6 LDS cache: the key LUTs and the match sets of the predicate dims (a superset of the residual dims)
+    int64_t ints = 0;
+    for (size_t j = 0; j < P->key_cols.size(); ++j) ints += k.dim_card[k.key_dim[j]];
+    for (int d = 0; d < st->num_dims; ++d)
+      if (k.pred_mask & (1 << d)) ints += (k.dim_card[d] + 31) / 32;
+    constexpr int64_t kStarCacheMax = 8192;  // 32 KB
+    if (P->star_cache_ints >= 0)
+      P->star_cache_ints = ints > kStarCacheMax ? -1 : std::max<int32_t>(P->star_cache_ints, (int32_t)ints);
   }
   const int idx = (int)P->star.size();
   for (int d = 0; d < st->num_dims; ++d) {
@@ -1339,6 +1410,11 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     P->agg_slot.push_back(add_slot(kind, a.column));
   }
+  if (P->first_doc_slot) {  // hidden MIN($docId): each group's first matching doc (its IntGroupIdMap id order)
+    P->slot_kind.push_back(SLOT_MIN_KEY);
+    P->slot_tcol.push_back(kDocIdColumn);
+    P->slot_col.push_back(slot_of(kDocIdColumn));
+  }
   if ((int)P->slot_kind.size() > kMaxSlots) return fail(PGPU_ERR_UNSUPPORTED, "too many accumulators");
   if ((int)P->query_cols.size() > kMaxQueryCols) return fail(PGPU_ERR_UNSUPPORTED, "too many columns");
   {  // TransformOperator.getNumColumnsProjected: distinct group-by and aggregation columns
@@ -1349,6 +1425,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   }
 
   P->num_groups_limit = q->num_groups_limit;
+  P->pql_cap = !(q->options & PGPU_OPT_SQL_GROUP_BY);
   if (q->num_groups_limit > 0) {
     for (Segment* s : P->segs) {
       int64_t prod = 1;
@@ -1433,7 +1510,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     // device LUT / value arrays of the referenced columns (built once per segment, rebuilt when the global
     // dictionary grows); done up front so the per-segment translation below only reads segment state
     for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
-    for (size_t k = 1; k < P->slot_kind.size(); ++k) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
+    for (size_t k = 1; k < P->slot_kind.size(); ++k)
+      if (P->slot_tcol[k] != kDocIdColumn) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
+    if (P->first_doc_slot) TRY(ensure_docid(t, s->num_docs, stream));
   }
   // Per-segment translation (PredicateEvaluatorProvider + FilterPlanNode per segment) in contiguous chunks,
   // on the host worker pool for large segment lists; records carry chunk-relative tile / set offsets, fixed up
@@ -1558,6 +1637,14 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       h->stats = rec_stats;
       KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
       for (int j = 0; j < nqc; ++j) {
+        if (P->query_cols[j] == kDocIdColumn) {
+          kc[j].fwd = t->d_docid_fwd;
+          kc[j].lut = nullptr;
+          kc[j].dkey = t->d_docid_key;
+          kc[j].dval = nullptr;
+          kc[j].bits = t->docid_bits;
+          continue;
+        }
         const Column& c = s->cols[P->query_cols[j]];
         kc[j].fwd = c.d_fwd;
         kc[j].lut = c.d_lut;
@@ -1624,8 +1711,22 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     if (tile_base > INT32_MAX) return fail(PGPU_ERR_UNSUPPORTED, "too many tiles in one plan");
     P->star_segments = (int64_t)P->star.size();
     if (!P->star.empty()) {
-      P->star_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, 1024 / (int64_t)P->star.size()));
-      P->star_lds_bytes = P->mode == MODE_LDS ? (size_t)nslots * G * 8 : 0;
+      if (P->star_cache_ints < 0) P->star_cache_ints = 0;  // some segment's LUTs do not fit: global reads
+      int64_t max_nodes = 0;
+      for (const KStarSeg& k : P->star) max_nodes = std::max<int64_t>(max_nodes, k.num_nodes);
+      P->star_range_cache = max_nodes * 16 <= 32 * 1024 ? (int32_t)max_nodes : 0;
+      const int64_t nseg_launch = std::min<int64_t>((int64_t)P->star.size(), kStarMaxSegs);
+      P->star_batches = (int)(((int64_t)P->star.size() + kStarMaxSegs - 1) / kStarMaxSegs);
+      const int64_t rc = P->star_range_cache;
+      const size_t table_bytes = P->mode == MODE_LDS ? (size_t)((nslots * G + 1) & ~int64_t(1)) * 8 : 0;
+      P->star_lds_bytes = table_bytes + (size_t)((nseg_launch + 2) & ~int64_t(1)) * 8 + (size_t)((rc + 2) & ~int64_t(1)) * 8 +
+                          (size_t)((2 * rc + 3) & ~int64_t(3)) * 4 + (size_t)P->star_cache_ints * 4;
+      // K6: persistent workgroups (1024 threads in MODE_LDS, 256 otherwise), one resident wave of them over the
+      // CUs; each flushes its table slab once
+      const int64_t per_cu = P->mode == MODE_LDS ? std::max<int64_t>(1, std::min<int64_t>(2, (160 * 1024) /
+                                                      std::max<size_t>(P->star_lds_bytes, 1))) : 8;
+      static const int64_t want_env = getenv("PGPU_STAR_WGS") ? atol(getenv("PGPU_STAR_WGS")) : 0;  // A/B knob
+      P->star_chunks = (int)(want_env > 0 ? want_env : (int64_t)t->num_cus * per_cu);
     }
     // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
     P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16;
@@ -1904,7 +2005,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
                              (kBlock / 64)));
     kp.leap_maps = sc->leap_maps.as<uint8_t>();
   }
-  const int star_blocks = (int)P->star.size() * P->star_chunks;
+  const int star_blocks = P->star_batches * P->star_chunks;
   if (P->mode == MODE_LDS) {
     TRY(sc->slab.ensure((size_t)std::max(max_chunks * P->grid + star_blocks, 1) * X.words * 8));
     kp.slab = sc->slab.as<uint64_t>();
@@ -2032,7 +2133,8 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   if (nl == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   if (!P->star.empty()) {
     // star-tree segments: K5 traversal then K6 residual scan + aggregation into the same group table
-    TRY(sc->starwork.ensure((size_t)P->star_work_bytes));
+    TRY(sc->starwork.ensure((size_t)P->star_work_bytes + P->star.size() * 8 + 16));
+    int64_t* seg_total = reinterpret_cast<int64_t*>(sc->starwork.as<uint8_t>() + P->star_work_bytes);
     TRY(sc->starrec.ensure(P->star.size() * sizeof(KStarSeg)));
     std::vector<KStarSeg> recs = P->star;
     for (size_t i = 0; i < recs.size(); ++i) {
@@ -2049,27 +2151,34 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     memcpy(sc->starstage.p, recs.data(), recs.size() * sizeof(KStarSeg));
     HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, recs.size() * sizeof(KStarSeg), hipMemcpyHostToDevice,
                            stream));
-    if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), stream))
+    if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), seg_total, stream))
       return fail(PGPU_ERR_DEVICE, "star-tree traversal launch failed: %s", hipGetErrorString(hipGetLastError()));
     KStarParams sp;
     memset(&sp, 0, sizeof sp);
-    sp.segs = sc->starrec.as<KStarSeg>();
-    sp.num_segs = (int)recs.size();
-    sp.chunks_per_seg = P->star_chunks;
+    sp.num_wgs = P->star_chunks;
+    sp.range_cache = P->star_range_cache;
     sp.num_keys = (int)P->key_cols.size();
     for (size_t j = 0; j < P->key_cols.size(); ++j) sp.key_stride[j] = P->key_stride[j];
     sp.num_keys_total = P->num_keys;
     sp.num_slots = nslots;
     for (int sl = 0; sl < nslots; ++sl) {
       sp.slot_kind[sl] = P->slot_kind[sl];
-      sp.slot_int[sl] = sl > 0 && is_int_type(P->table->types[P->slot_tcol[sl]]) ? 1 : 0;
+      sp.slot_int[sl] = sl > 0 && P->slot_tcol[sl] >= 0 && is_int_type(P->table->types[P->slot_tcol[sl]]) ? 1 : 0;
     }
     sp.table = kp.table;
     sp.slab = P->mode == MODE_LDS ? kp.slab + X.slabs_used * words : nullptr;
     sp.hash_keys = kp.hash_keys;
     sp.stats = kp.stats;
-    if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
-      return fail(PGPU_ERR_DEVICE, "star-tree scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+    sp.cache_ints = P->star_cache_ints;
+    for (int b = 0; b < P->star_batches; ++b) {  // kStarMaxSegs segments per launch, slabs back to back
+      const int s0 = b * kStarMaxSegs;
+      sp.segs = sc->starrec.as<KStarSeg>() + s0;
+      sp.num_segs = (int)std::min<int64_t>(kStarMaxSegs, (int64_t)recs.size() - s0);
+      sp.seg_total = seg_total + s0;
+      if (P->mode == MODE_LDS) sp.slab = kp.slab + (X.slabs_used + (int64_t)b * P->star_chunks) * words;
+      if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
+        return fail(PGPU_ERR_DEVICE, "star-tree scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
   }
   if (!P->generic.empty()) {
     // STATS_GENERIC segments: the leaves' match bitmaps, read back and replayed on the host at finalize
@@ -2094,7 +2203,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
   if (P->mode == MODE_LDS) {
     // fold every slab written: the scan launches' (back to back) and the star-tree chunks' after them
-    const int64_t all = X.slabs_used + (int64_t)P->star.size() * P->star_chunks;
+    const int64_t all = X.slabs_used + (int64_t)P->star_batches * P->star_chunks;
     if (all == 0) {
       if (launch_table_init(X.table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
@@ -2232,10 +2341,6 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     }
   }
   const double t_sync2 = trace_on() ? now_us() : 0;
-  if (P->limit_sensitive && n > P->num_groups_limit)
-    return fail(PGPU_ERR_UNSUPPORTED,
-                "numGroupsLimit %lld reached (%lld groups): Pinot truncates per segment in first-seen order",
-                (long long)P->num_groups_limit, (long long)n);
   const int na = (int)P->agg_fn.size();
   R->num_aggs = na;
   R->agg_slot = P->agg_slot;
@@ -2268,6 +2373,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     else for (size_t i = 0; i < P->generic.size(); ++i) replay((int)i);
     for (int64_t v : part) generic_entries += v;
   }
+  // GroupByCombineOperator.mergeResults (:215-219): the merged map holds >= numGroupsLimit groups (PQL mode only)
+  R->groups_limit_reached = P->pql_cap && nk > 0 && P->num_groups_limit > 0 && n >= P->num_groups_limit;
   R->stats[0] = (int64_t)matched;
   R->stats[1] = P->scanned_entries_model + (int64_t)star_scanned + generic_entries;
   R->stats[2] = ((int64_t)matched - P->post_exempt_docs) * P->num_projected;
@@ -2277,6 +2384,191 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   if (trace_on())
     fprintf(stderr, "[pgpu] finalize: launch+sync1 %.1f us, copy+sync2 %.1f us, decode %.1f us (n=%lld)\n",
             t_sync1 - t_start, t_sync2 - t_sync1, now_us() - t_sync2, (long long)n);
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------ numGroupsLimit
+// Pinot's group-key generators admit a segment's groups in first-seen docId order until numGroupsLimit and drop the
+// docs of later groups (DictionaryBasedGroupKeyGenerator.java:97-161 holder choice, IntGroupIdMap :1101-1113 limit;
+// DoubleGroupByResultHolder.java:89-93 ignores INVALID_ID); the PQL combine admits at most 2 x numGroupsLimit
+// groups across segments (GroupByCombineOperator.java:61,78-80,138).  A plan where either can bind is split into
+// parts: every segment whose key space (product of its local cardinalities) exceeds the limit becomes its own part
+// with a hidden MIN($docId) slot -- each group's first matching doc, i.e. its group-id order -- and keeps the
+// `limit` groups seen first; the other segments form one part.  When the 2x cap can bind (PQL mode, sum over
+// segments of min(key space, limit) > 2 x limit) every segment is a part and groups are admitted segment by
+// segment, each segment's groups in its holder's order (ArrayBasedHolder: key order; map holders: first-seen
+// order) -- one of the orders Pinot's combine threads can produce, the one its single-threaded run produces.
+int split_for_groups_limit(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q,
+                           pgpu_plan_s* P, bool* composite) {
+  *composite = false;
+  if (!q || q->num_group_by <= 0 || q->num_groups_limit <= 0 || nsegs <= 0) return 0;
+  const int64_t L = q->num_groups_limit;
+  const int64_t threshold = std::min<int64_t>(10000, L);  // maxInitialResultHolderCapacity (ARRAY holder bound)
+  std::vector<int64_t> prod(nsegs, 1);
+  int64_t global_keys = 1;  // the table-global key space bounds the distinct groups of any segment set
+  {
+    std::lock_guard<std::mutex> g(t->mu);
+    for (int k = 0; k < q->num_group_by; ++k) {
+      const int c = q->group_by[k];
+      if (c < 0 || c >= (int)t->names.size()) return 0;
+      const int64_t card = std::max<int64_t>((int64_t)t->global[c].size(), 1);
+      global_keys = global_keys > INT64_MAX / card ? INT64_MAX : global_keys * card;
+    }
+    for (int i = 0; i < nsegs; ++i) {
+      const int64_t h = handles[i];
+      Segment* sp = h > 0 && h < (int64_t)t->by_handle.size() ? t->by_handle[h] : nullptr;
+      if (!sp) return 0;  // plan_create_impl reports it
+      for (int k = 0; k < q->num_group_by; ++k) {
+        const int c = q->group_by[k];
+        if (c < 0 || c >= (int)t->names.size()) return 0;
+        const int64_t card = std::max<int64_t>(sp->cols[c].card, 1);
+        prod[i] = prod[i] > INT64_MAX / card ? INT64_MAX : prod[i] * card;
+      }
+    }
+  }
+  const bool pql = !(q->options & PGPU_OPT_SQL_GROUP_BY);
+  bool any_sensitive = false;
+  int64_t bound = 0;
+  for (int i = 0; i < nsegs; ++i) {
+    any_sensitive |= prod[i] > L;
+    bound = std::min<int64_t>(INT64_MAX / 2, bound + std::min<int64_t>(prod[i], L));
+  }
+  const bool cap_may_bind = pql && std::min(bound, global_keys) > 2 * L;
+  if (!any_sensitive && !cap_may_bind) return 0;
+  std::vector<int32_t> rest;
+  auto add_part = [&](const std::vector<int32_t>& idx, bool first_seen, bool truncate) -> int {
+    pgpu_plan_s::Part part;
+    part.plan = std::make_unique<pgpu_plan_s>();
+    part.plan->first_doc_slot = first_seen;
+    part.seg_index = idx;
+    part.first_seen = first_seen;
+    part.truncate = truncate;
+    std::vector<int64_t> hs;
+    for (int32_t i : idx) hs.push_back(handles[i]);
+    TRY(plan_create_impl(t, hs.data(), (int32_t)hs.size(), q, part.plan.get()));
+    P->parts.push_back(std::move(part));
+    return 0;
+  };
+  for (int i = 0; i < nsegs; ++i) {
+    if (cap_may_bind) TRY(add_part({i}, prod[i] > threshold, prod[i] > L));
+    else if (prod[i] > L) TRY(add_part({i}, true, true));
+    else rest.push_back(i);
+  }
+  if (!rest.empty()) TRY(add_part(rest, false, false));
+  P->composite = true;
+  P->table = t;
+  P->num_groups_limit = L;
+  P->pql_cap = pql;
+  P->seg_scanned.assign(nsegs, 0);
+  for (const auto& part : P->parts)
+    for (size_t k = 0; k < part.seg_index.size() && k < part.plan->seg_scanned.size(); ++k)
+      P->seg_scanned[part.seg_index[k]] = part.plan->seg_scanned[k];
+  P->executed = false;
+  return 0;
+}
+
+// Executes and finalizes the parts one after another (one part's group table in memory at a time) and merges their
+// rows on the host: first-seen truncation per part, the 2x cap in admission order, AggregationFunction.merge.
+int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
+  pgpu_table_s* t = P->table;
+  const int64_t L = P->num_groups_limit;
+  std::vector<std::unique_ptr<pgpu_result_s>> rs;
+  for (auto& part : P->parts) {
+    pgpu_plan_s* Q = part.plan.get();
+    Q->scratch = acquire_scratch(t);
+    auto Ri = std::make_unique<pgpu_result_s>();
+    int rc = plan_execute_impl(Q, stream, nullptr);
+    if (!rc) rc = plan_finalize_impl(Q, stream, nullptr, 0, Q->num_keys, Ri.get());
+    if (rc) hipStreamSynchronize(stream);
+    release_scratch(t, Q->scratch);
+    Q->scratch = nullptr;
+    TRY(rc);
+    rs.push_back(std::move(Ri));
+  }
+  const pgpu_plan_s* P0 = P->parts[0].plan.get();
+  const int nk = (int)P0->key_cols.size();
+  const int ns = (int)P0->slot_kind.size() - (P0->first_doc_slot ? 1 : 0);
+  std::vector<int32_t> kind(P0->slot_kind.begin(), P0->slot_kind.begin() + ns);
+  for (const auto& part : P->parts)
+    for (int s = 0; s < ns; ++s)
+      if (part.plan->slot_kind[s] == SLOT_SUM_F64) kind[s] = SLOT_SUM_F64;
+  const int64_t cap = P->pql_cap ? std::min<int64_t>(2 * L, INT32_MAX) : INT64_MAX;
+  std::unordered_map<uint64_t, int64_t> index;
+  std::vector<uint64_t> keys, vals;
+  int64_t counter = 0;
+  for (size_t i = 0; i < P->parts.size(); ++i) {
+    const auto& part = P->parts[i];
+    pgpu_result_s* Ri = rs[i].get();
+    const pgpu_plan_s* Q = part.plan.get();
+    std::vector<int64_t> order(Ri->n);
+    std::iota(order.begin(), order.end(), 0);
+    if (part.first_seen) {
+      const uint64_t* fd = Ri->slot(Ri->num_slots - 1);
+      std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return (int64_t)fd[a] < (int64_t)fd[b]; });
+      if (part.truncate && (int64_t)order.size() > L) order.resize(L);
+    }
+    for (int64_t r : order) {
+      uint64_t key = 0;
+      for (int j = 0; j < nk; ++j) key += (uint64_t)Ri->gid(j)[r] * (uint64_t)P0->key_stride[j];
+      auto it = index.find(key);
+      if (it == index.end()) {
+        if (counter++ >= cap) continue;  // _numGroups.getAndIncrement() < _interSegmentNumGroupsLimit
+        index.emplace(key, (int64_t)keys.size());
+        keys.push_back(key);
+        for (int s = 0; s < ns; ++s) {
+          uint64_t w = Ri->slot(s)[r];
+          if (kind[s] == SLOT_SUM_F64 && Q->slot_kind[s] == SLOT_SUM_I64) {
+            const double d = (double)(int64_t)w;
+            memcpy(&w, &d, 8);
+          }
+          vals.push_back(w);
+        }
+        continue;
+      }
+      uint64_t* dst = vals.data() + it->second * ns;
+      for (int s = 0; s < ns; ++s) {
+        const uint64_t w = Ri->slot(s)[r];
+        switch (kind[s]) {
+          case SLOT_COUNT: case SLOT_SUM_I64: dst[s] += w; break;
+          case SLOT_SUM_F64: {
+            double a, b;
+            memcpy(&a, &dst[s], 8);
+            if (Q->slot_kind[s] == SLOT_SUM_I64) b = (double)(int64_t)w;
+            else memcpy(&b, &w, 8);
+            a += b;
+            memcpy(&dst[s], &a, 8);
+            break;
+          }
+          case SLOT_MIN_KEY: if ((int64_t)w < (int64_t)dst[s]) dst[s] = w; break;
+          default: if ((int64_t)w > (int64_t)dst[s]) dst[s] = w; break;
+        }
+      }
+    }
+  }
+  std::vector<int64_t> rows(keys.size());
+  std::iota(rows.begin(), rows.end(), 0);
+  std::sort(rows.begin(), rows.end(), [&](int64_t a, int64_t b) { return keys[a] < keys[b]; });
+  const int64_t n = (int64_t)rows.size();
+  R->pool = t->result_pool;
+  TRY(R->alloc(nk, ns, n));
+  for (int64_t r = 0; r < n; ++r) {
+    decode_keys(P0, R, r, keys[rows[r]]);
+    for (int s = 0; s < ns; ++s) R->slot(s)[r] = vals[rows[r] * ns + s];
+  }
+  const pgpu_result_s* R0 = rs[0].get();
+  R->num_aggs = R0->num_aggs;
+  R->agg_slot = R0->agg_slot;
+  R->key_cols = R0->key_cols;
+  R->key_types = R0->key_types;
+  R->agg_fn = R0->agg_fn;
+  R->agg_col = R0->agg_col;
+  R->agg_conv = R0->agg_conv;
+  for (int a = 0; a < R->num_aggs; ++a)
+    if ((R->agg_fn[a] == PGPU_AGG_SUM || R->agg_fn[a] == PGPU_AGG_AVG) && kind[R->agg_slot[a]] == SLOT_SUM_F64)
+      R->agg_conv[a] = RCONV_F64;
+  for (const auto& Ri : rs)
+    for (int k = 0; k < 6; ++k) R->stats[k] += Ri->stats[k];
+  R->groups_limit_reached = P->pql_cap && n >= L;
   return 0;
 }
 
@@ -2341,6 +2633,9 @@ int pgpu_table_destroy(pgpu_table t) {
   for (auto& s : t->scratch_pool) if (s) s->release();
   t->gen.pos.release(); t->gen.presence.release(); t->gen.code_to_pos.release(); t->gen.cdf.release();
   t->gen.pos_to_id.release();
+  if (t->d_docid_fwd) hipFree(t->d_docid_fwd);
+  if (t->d_docid_key) hipFree(t->d_docid_key);
+  for (void* p : t->retired) hipFree(p);
   hipStreamDestroy(t->stream);
   delete t;
   return 0;
@@ -2691,7 +2986,7 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
       return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree dimension %d forward index too short", k);
     st->dim_cols.push_back(c);
     st->dim_bits.push_back(bits);
-    fwd_words[k] = ((int64_t)d->num_docs * bits + 31) / 32 + kFwdPadWords;
+    fwd_words[k] = ((int64_t)d->num_docs + 31) / 32 * bits + kFwdPadWords;  // whole 32-doc groups (K6 decode)
     bytes += ((fwd_words[k] * 4) + 15) & ~int64_t(15);
   }
   for (int m = 0; m < d->num_metrics; ++m) {
@@ -2864,14 +3159,19 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
-  TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
-  P->scratch = acquire_scratch(t);
+  bool composite = false;
+  TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
+  if (!composite) {
+    TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
+    P->scratch = acquire_scratch(t);
+  }
   *out = P.release();
   return 0;
 }
 
 int pgpu_plan_destroy(pgpu_plan P) {
   if (!P) return 0;
+  for (auto& part : P->parts) release_scratch(P->table, part.plan->scratch);
   release_scratch(P->table, P->scratch);
   delete P;
   return 0;
@@ -2879,6 +3179,7 @@ int pgpu_plan_destroy(pgpu_plan P) {
 
 int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: its parts have their own group tables");
   if (num_slots) *num_slots = (int32_t)P->slot_kind.size();
   if (num_keys) *num_keys = P->hash ? 0 : P->num_keys;
   if (kinds) for (size_t i = 0; i < P->slot_kind.size(); ++i) kinds[i] = P->slot_kind[i];
@@ -2890,6 +3191,14 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
+  bool composite = false;
+  TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
+  if (composite) {  // executed part by part at finalize
+    if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
+    P->executed = true;
+    *out = P.release();
+    return 0;
+  }
   StreamExec se;
   se.stream = stream ? reinterpret_cast<hipStream_t>(stream) : t->stream;
   se.d_table = d_table;
@@ -2913,6 +3222,11 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
 
 int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  if (P->composite) {
+    if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
+    P->executed = true;
+    return 0;
+  }
   if (P->hash && d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
@@ -2924,7 +3238,13 @@ int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_resu
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   auto R = std::make_unique<pgpu_result_s>();
-  TRY(plan_finalize_impl(P, s, d_table, 0, P->num_keys, R.get()));
+  if (P->composite) {
+    if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+    if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
+    TRY(composite_finalize(P, s, R.get()));
+  } else {
+    TRY(plan_finalize_impl(P, s, d_table, 0, P->num_keys, R.get()));
+  }
   *out = R.release();
   return 0;
 }
@@ -2934,7 +3254,7 @@ int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shar
   if (!P || !out || !d_table_shard || key_begin < 0 || key_count < 0 || key_begin + key_count > P->num_keys)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (P->hash) return fail(PGPU_ERR_UNSUPPORTED, "hash-mode group tables are not key-range shardable");
-  if (P->limit_sensitive)
+  if (P->composite)
     return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit below the key space: finalize the whole table");
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
@@ -2973,6 +3293,7 @@ int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
 
 int pgpu_plan_timing(pgpu_plan P, double* out3) {
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: timing is per part");
   Scratch* sc = P->scratch;
   HIP_TRY(hipEventSynchronize(sc->ev[3]));
   float a = 0;
@@ -3051,6 +3372,11 @@ int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
 int pgpu_result_stats(pgpu_result r, int64_t* out6) {
   if (!r || !out6) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   memcpy(out6, r->stats, sizeof r->stats);
+  return 0;
+}
+int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out) {
+  if (!r || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *out = r->groups_limit_reached ? 1 : 0;
   return 0;
 }
 int pgpu_result_destroy(pgpu_result r) {

@@ -93,12 +93,12 @@ __device__ __forceinline__ uint32_t staged_leaf(const StageRegs& R, int sidx, co
     return L.negate ? ~m : m;
   }
   if (L.kind == LEAF_BITMAP) {
-    const uint32_t m = L.set[group];
+    const uint32_t m = gp(L.set)[group];
     return L.negate ? ~m : m;
   }
   const int b = sidx == 0 ? R.b0 : sidx == 1 ? R.b1 : sidx == 2 ? R.b2 : R.b3;
   const int off = sidx == 0 ? 0 : sidx == 1 ? R.o1 : sidx == 2 ? R.o2 : R.o3;
-  return leaf_eval_words(L.kind, L.negate, L.lo, L.span, L.set, sbuf + off + tid * b, b);
+  return leaf_eval_words<false>(L.kind, L.negate, L.lo, L.span, L.set, sbuf + off + tid * b, b);
 }
 
 template <int MODE>
@@ -107,7 +107,7 @@ __device__ __forceinline__ void aggregate_doc(const KParams& p, const SegView& S
   int64_t key = 0;
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
-    key += (int64_t)c.lut[gather_id(c.fwd, c.bits, doc)] * p.key_stride[j];
+    key += (int64_t)gp(c.lut)[gather_id(c.fwd, c.bits, doc)] * p.key_stride[j];
   }
   int64_t idx = key;
   if (MODE == MODE_HASH) idx = hash_slot(p.hash_keys, G, (uint64_t)key);
@@ -118,8 +118,8 @@ __device__ __forceinline__ void aggregate_doc(const KParams& p, const SegView& S
     if (kind != SLOT_COUNT) {
       const KCol& c = S.cols[p.slot_col[s]];
       const uint32_t id = gather_id(c.fwd, c.bits, doc);
-      if (kind == SLOT_SUM_F64) dval = c.dval[id];
-      else ikey = c.dkey[id];
+      if (kind == SLOT_SUM_F64) dval = gp(c.dval)[id];
+      else ikey = gp(c.dkey)[id];
     }
     accumulate<MODE>(tbl, (int64_t)s * G + idx, kind, ikey, dval);
   }

@@ -54,6 +54,7 @@ class GroupByResult:
     def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None, holder=None, table=None,
                  query=None):
         self.stats = stats
+        self.num_groups_limit_reached = False
         self._holder, self._table, self._query = holder, table, query  # the C result behind the columnar views
         self.exact = exact or {}    # agg index -> np.int64 array of exact integer accumulators
         self._keys, self._values = keys, values
@@ -564,5 +565,9 @@ def _decode_result(table, query, holder):
         aggs.append((fn, v, e, c))
     st = np.zeros(6, dtype=np.int64)
     L.check(lib.pgpu_result_stats(r, L.ptr(st, ctypes.c_int64)))
-    return GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n), holder=holder,
-                         table=table, query=query)
+    reached = ctypes.c_int32()
+    L.check(lib.pgpu_result_groups_limit_reached(r, ctypes.byref(reached)))
+    res = GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n), holder=holder,
+                        table=table, query=query)
+    res.num_groups_limit_reached = bool(reached.value)
+    return res

@@ -99,8 +99,10 @@ class QueryContext:
     def __init__(self, group_by, aggregations, filter=None, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT,
                  use_star_tree=True, select=None, order_by=None, limit=DEFAULT_LIMIT,
                  min_server_group_trim_size=DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE,
-                 group_trim_threshold=DEFAULT_GROUP_TRIM_THRESHOLD):
+                 group_trim_threshold=DEFAULT_GROUP_TRIM_THRESHOLD, sql_group_by=False):
         self.filter = filter
+        # queryOptions groupByMode=sql: GroupByOrderByCombineOperator (no 2 x numGroupsLimit inter-segment cap)
+        self.sql_group_by = sql_group_by
         self.use_star_tree = use_star_tree  # debug option useStarTree (StarTreeUtils.java:51-59)
         self.group_by = list(group_by)
         self.aggregations = [(fn.upper(), col) for fn, col in aggregations]
@@ -174,11 +176,15 @@ class QueryContext:
         cache = self.__dict__.get("_c_cache")
         if cache is not None and cache[0] is column_index and cache[1] == self.num_groups_limit:
             q, keep = cache[2], cache[3]
-            q.options = 0 if getattr(self, "use_star_tree", True) else 1
+            q.options = self._options()
             return q, keep
         q, keep = self._build_c(column_index)
         self._c_cache = (column_index, self.num_groups_limit, q, keep)
         return q, keep
+
+    def _options(self):
+        return (0 if getattr(self, "use_star_tree", True) else L.OPT_NO_STAR_TREE) | \
+            (L.OPT_SQL_GROUP_BY if getattr(self, "sql_group_by", False) else 0)
 
     def _build_c(self, column_index):
         keep = []
@@ -217,7 +223,7 @@ class QueryContext:
         q.num_aggs = len(self.aggregations)
         q.aggs = ac
         q.num_groups_limit = self.num_groups_limit
-        q.options = 0 if getattr(self, "use_star_tree", True) else 1  # PGPU_OPT_NO_STAR_TREE
+        q.options = self._options()
         keep += [pc, oc, gb, ac]
         return q, keep
 

@@ -317,15 +317,49 @@ def test_padding_segments_pin_and_query(gpu_lib, tmp_path):
             t.close()
 
 
-def test_num_groups_limit_reached_declines(oracle, sv):
-    """InterSegmentAggregationSingleValueQueriesTest.java:534-545: GROUP BY column1 with numGroupsLimit 1000 makes
-    Pinot drop groups in first-seen order; the GPU path does not report a result that could differ (the caller
-    runs Pinot's operator), and the oracle confirms the limit is reached."""
+@pytest.mark.parametrize("nseg", [1, 4])
+@pytest.mark.parametrize("sql", [False, True], ids=["pql", "sql"])
+@pytest.mark.parametrize("with_filter", [False, True], ids=["no_filter", "filter"])
+def test_num_groups_limit_first_seen(oracle, sv, nseg, sql, with_filter):
+    """InterSegmentAggregationSingleValueQueriesTest.java:534-545: GROUP BY column1 with numGroupsLimit 1000 (and
+    maxInitialResultHolderCapacity 1000).  column1's key space exceeds the limit, so each segment keeps the first
+    1000 groups of its matching docs in docId order (IntGroupIdMap, DictionaryBasedGroupKeyGenerator.java:
+    1101-1113) and drops the docs of later groups; numGroupsLimitReached is set in PQL mode."""
     seg, t, h = sv
-    q = QueryContext(["column1"], [("COUNT", "*")], None, num_groups_limit=1000)
-    assert oracle.run_groupby(K.SCHEMA, [seg], q, max_initial_capacity=1000).limit_reached
-    with pytest.raises(L.UnsupportedQueryError):
-        t.execute_groupby([h], q)
+    flt = K.inner_query(["column1"], True).filter if with_filter else None
+    q = QueryContext(["column1"], [("COUNT", "*"), ("SUM", "column3"), ("MIN", "column6")], flt,
+                     num_groups_limit=1000, sql_group_by=sql)
+    o = oracle.run_groupby(K.SCHEMA, [seg] * nseg, q, combine=not sql, max_initial_capacity=1000)
+    r = t.execute_groupby([h] * nseg, q)
+    assert_same(r, o, q, K.SCHEMA)
+    assert r.stats.as_tuple() == o.stats
+    if not with_filter:
+        assert len(r) == 1000
+    assert r.num_groups_limit_reached == (not sql and len(r) >= 1000)
+    if not sql:
+        assert r.num_groups_limit_reached == o.limit_reached
+
+
+@pytest.mark.parametrize("sql", [False, True], ids=["pql", "sql"])
+def test_num_groups_limit_inter_segment_cap(oracle, sql):
+    """Segments with disjoint keys: each keeps its first 1000 groups; the PQL combine admits 2 x 1000 groups in
+    total (GroupByCombineOperator.java:61,78-80,138) -- segment by segment, as the oracle's single-threaded
+    combine does -- while SQL mode keeps all 3 x 1000."""
+    schema = [("k", "INT"), ("m", "INT")]
+    rng = np.random.default_rng(7)
+    segs = [oracle.make_segment(schema, {"k": (i * 100000 + rng.integers(0, 3000, 6000)).tolist(),
+                                         "m": rng.integers(0, 1000, 6000).tolist()}) for i in range(3)]
+    q = QueryContext(["k"], [("COUNT", "*"), ("SUM", "m"), ("MAX", "m")], None, num_groups_limit=1000,
+                     sql_group_by=sql)
+    o = oracle.run_groupby(schema, segs, q, combine=not sql, max_initial_capacity=1000)
+    t, hs = gpu_table(schema, segs)
+    try:
+        r = t.execute_groupby(hs, q)
+        assert_same(r, o, q, schema)
+        assert len(r) == (3000 if sql else 2000)
+        assert r.stats.as_tuple() == o.stats
+    finally:
+        t.close()
 
 
 def test_num_groups_limit_not_reached_is_exact(oracle, sv):

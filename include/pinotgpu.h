@@ -170,6 +170,9 @@ typedef struct {
  * space exceeds numGroupsLimit keeps its first numGroupsLimit groups in first-seen docId order
  * (DictionaryBasedGroupKeyGenerator.java:1101-1113), as Pinot's map-based holders do. */
 #define PGPU_OPT_SQL_GROUP_BY 2
+/* Compile the plan afresh instead of reusing the table's cached compilation of the same query over the same
+ * segments (the cache is dropped whenever pinned state changes; PGPU_PLAN_CACHE=0 disables it process-wide). */
+#define PGPU_OPT_NO_PLAN_CACHE 4
 
 /* A query compiled against a list of pinned segments (InstancePlanMakerImplV2.makeInstancePlan +
  * per-segment AggregationGroupByPlanNode: predicate evaluators per segment, group-key layout, accumulators). */

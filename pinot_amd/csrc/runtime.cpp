@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <map>
 #include <unordered_map>
 #include <memory>
@@ -426,6 +427,14 @@ struct pgpu_table_s {
   int docid_bits = 0;
   int64_t docid_n = 0;
   std::vector<void*> retired;  // replaced $docId buffers (plans built earlier may still point at them)
+  // Compiled-plan cache (pgpu_plan_create / _create_execute): the host image of a plan -- per-segment records with
+  // the predicate literals translated to dictId ranges / sets, launch configuration, statistics classification --
+  // keyed by the query bytes, the segment list and `version`, which every change of pinned state bumps (pin, unpin,
+  // index attach, dictionary growth).  A repeated query (a dashboard refresh) skips the host translation; the
+  // device work runs in full every time.
+  std::atomic<uint64_t> version{1};
+  std::mutex cache_mu;
+  std::list<std::pair<std::string, std::shared_ptr<pgpu_plan_s>>> plan_cache;  // most recent first
 };
 
 int pgpu::table_dict_view(pgpu_table t, int col, DictView* out) {
@@ -646,6 +655,7 @@ int64_t padded_fwd_words(int64_t num_docs, int bits) {
 
 // Registers a segment whose columns have parsed dictionaries and device forward indexes.
 int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
+  t->version++;
   for (size_t c = 0; c < seg->cols.size(); ++c)
     if (merge_dict(t->global[c], seg->cols[c].dict)) t->global_version[c]++;
   int64_t h = t->next_handle++;
@@ -760,7 +770,7 @@ struct pgpu_plan_s {
   bool composite = false;
   bool pql_cap = false;                   // GroupByCombineOperator's inter-segment cap of 2 x numGroupsLimit
   struct Part {
-    std::unique_ptr<pgpu_plan_s> plan;
+    std::shared_ptr<pgpu_plan_s> plan;
     std::vector<int32_t> seg_index;       // plan segment positions of the part's segments
     bool first_seen = false;              // rows in first-seen order (map holder)
     bool truncate = false;                // keep the first numGroupsLimit groups (segment key space > the limit)
@@ -2438,7 +2448,7 @@ int split_for_groups_limit(pgpu_table_s* t, const int64_t* handles, int32_t nseg
   std::vector<int32_t> rest;
   auto add_part = [&](const std::vector<int32_t>& idx, bool first_seen, bool truncate) -> int {
     pgpu_plan_s::Part part;
-    part.plan = std::make_unique<pgpu_plan_s>();
+    part.plan = std::make_shared<pgpu_plan_s>();
     part.plan->first_doc_slot = first_seen;
     part.seg_index = idx;
     part.first_seen = first_seen;
@@ -2570,6 +2580,72 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
     for (int k = 0; k < 6; ++k) R->stats[k] += Ri->stats[k];
   R->groups_limit_reached = P->pql_cap && n >= L;
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------ plan cache
+constexpr size_t kPlanCacheEntries = 16;
+
+bool plan_cache_enabled(const pgpu_query* q) {
+  static const bool off = getenv("PGPU_PLAN_CACHE") && getenv("PGPU_PLAN_CACHE")[0] == '0';
+  return !off && q && !(q->options & PGPU_OPT_NO_PLAN_CACHE);
+}
+
+// The bytes that determine a compiled plan: table version, segment handles, and every field of the query
+// (predicate literals included).
+std::string plan_cache_key(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q) {
+  std::string k;
+  auto put = [&](const void* p, size_t n) { k.append(reinterpret_cast<const char*>(p), n); };
+  const uint64_t v = t->version.load();
+  put(&v, 8);
+  put(&nsegs, 4);
+  if (nsegs > 0) put(handles, sizeof(int64_t) * (size_t)nsegs);
+  put(&q->num_predicates, 4);
+  for (int i = 0; i < q->num_predicates; ++i) {
+    const pgpu_predicate& pr = q->predicates[i];
+    const int32_t f[5] = {pr.type, pr.column, pr.num_values, pr.lower_inclusive, pr.upper_inclusive};
+    put(f, sizeof f);
+    for (int j = 0; j < pr.num_values; ++j) {
+      const char* sv = pr.values && pr.values[j] ? pr.values[j] : "";
+      const uint32_t n = (uint32_t)strlen(sv);
+      put(&n, 4);
+      put(sv, n);
+    }
+  }
+  put(&q->num_filter_ops, 4);
+  if (q->num_filter_ops > 0) put(q->filter, sizeof(pgpu_filter_op) * (size_t)q->num_filter_ops);
+  put(&q->num_group_by, 4);
+  if (q->num_group_by > 0) put(q->group_by, sizeof(int32_t) * (size_t)q->num_group_by);
+  put(&q->num_aggs, 4);
+  if (q->num_aggs > 0) put(q->aggs, sizeof(pgpu_agg) * (size_t)q->num_aggs);
+  put(&q->num_groups_limit, 4);
+  put(&q->options, 4);
+  return k;
+}
+
+// On a hit, *P becomes a copy of the cached image (not executed, no scratch).
+bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
+  std::lock_guard<std::mutex> g(t->cache_mu);
+  for (auto it = t->plan_cache.begin(); it != t->plan_cache.end(); ++it) {
+    if (it->first != key) continue;
+    *P = *it->second;
+    t->plan_cache.splice(t->plan_cache.begin(), t->plan_cache, it);
+    P->scratch = nullptr;
+    P->executed = false;
+    P->launches_done = 0;
+    P->d_table_used = nullptr;
+    P->last_stream = nullptr;
+    P->star_docs_read = 0;
+    return true;
+  }
+  return false;
+}
+
+void plan_cache_put(pgpu_table_s* t, const std::string& key, const pgpu_plan_s& P) {
+  auto img = std::make_shared<pgpu_plan_s>(P);
+  img->scratch = nullptr;
+  std::lock_guard<std::mutex> g(t->cache_mu);
+  t->plan_cache.emplace_front(key, std::move(img));
+  while (t->plan_cache.size() > kPlanCacheEntries) t->plan_cache.pop_back();
 }
 
 }  // namespace
@@ -2725,6 +2801,7 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
 }
 
 int pgpu_unpin_segment(pgpu_table t, int64_t h) {
+  if (t) t->version++;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   DeviceGuard g(t->device);
   std::lock_guard<std::mutex> lk(t->mu);
@@ -2921,6 +2998,7 @@ int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, in
 }
 
 int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
+  if (t) t->version++;
   if (!t || (!bytes && num_bytes)) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   DeviceGuard g(t->device);
   std::lock_guard<std::mutex> lk(t->mu);
@@ -2961,6 +3039,7 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
 }
 
 int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
+  if (t) t->version++;
   if (!t || !d) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (d->num_dims < 1 || d->num_dims > kMaxStarDims || d->num_nodes < 1 || d->num_docs < 0 || d->num_metrics < 1)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree shape (dims %d, nodes %d, docs %d, metrics %d)",
@@ -3052,6 +3131,7 @@ int64_t pgpu_table_device_bytes(pgpu_table t) { return t ? t->device_bytes : 0; 
 
 int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int64_t* vi, const double* vd,
                                      const uint8_t* blob, const int64_t* offsets) {
+  if (t) t->version++;
   if (!t || col < 0 || col >= (int)t->names.size() || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   Dict d;
   d.type = t->types[col];
@@ -3162,7 +3242,11 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   bool composite = false;
   TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
   if (!composite) {
-    TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
+    const bool cache = plan_cache_enabled(q);
+    if (!cache || !plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get())) {
+      TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
+      if (cache) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
+    }
     P->scratch = acquire_scratch(t);
   }
   *out = P.release();
@@ -3202,8 +3286,14 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   StreamExec se;
   se.stream = stream ? reinterpret_cast<hipStream_t>(stream) : t->stream;
   se.d_table = d_table;
+  const bool cache = plan_cache_enabled(q);
+  const bool hit = cache && plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get());
   P->scratch = acquire_scratch(t);  // before plan_create_impl takes the table lock (acquire_scratch locks it too)
-  int rc = plan_create_impl(t, handles, nsegs, q, P.get(), &se);
+  int rc = 0;
+  if (!hit) {
+    rc = plan_create_impl(t, handles, nsegs, q, P.get(), &se);
+    if (!rc && cache && !P->executed) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
+  }
   if (!rc && !P->executed) {
     if (P->hash && d_table) rc = fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
     else rc = plan_execute_impl(P.get(), se.stream, d_table);

@@ -808,3 +808,26 @@ def test_long_literals_beyond_double_precision(oracle, gpu_lib):
             assert_same(t.execute_groupby(hs, q), oracle.run_groupby(schema, [seg], q), q, schema)
     finally:
         t.close()
+
+
+def test_plan_cache_reuse_and_invalidation(oracle):
+    """A repeated query reuses the table's compiled plan (same result and statistics); growing a group-by
+    column's global dictionary invalidates it (new key layout), and the answer is still the oracle's."""
+    schema = [("d", "INT"), ("f", "INT"), ("m", "INT")]
+    rng = np.random.default_rng(11)
+    segs = [oracle.make_segment(schema, {"d": rng.integers(0, 50, 4000).tolist(), "f": rng.integers(0, 100, 4000).tolist(),
+                                         "m": rng.integers(0, 1000, 4000).tolist()}) for _ in range(3)]
+    q = parse_query("SELECT COUNT(*), SUM(m), MAX(m) FROM t WHERE f < 40 GROUP BY d")
+    o = oracle.run_groupby(schema, segs, q)
+    t, hs = gpu_table(schema, segs)
+    try:
+        r1 = t.execute_groupby(hs, q)
+        r2 = t.execute_groupby(hs, q)
+        assert_same(r1, o, q, schema)
+        assert r1.as_dict() == r2.as_dict() and r1.stats.as_tuple() == r2.stats.as_tuple() == o.stats
+        t.add_dictionary_values("d", [-5, 1000, 2000])  # the key space grows: cached plans are stale
+        r3 = t.execute_groupby(hs, q)
+        assert_same(r3, o, q, schema)
+        assert r3.stats.as_tuple() == o.stats
+    finally:
+        t.close()

@@ -46,7 +46,11 @@ enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE =
  * FixedBitSVForwardIndexReaderV2.java:33-96: MSB-first big-endian bit packing, PinotDataBitSet layout) and
  * SortedIndexReaderImpl (seglocal/segment/index/readers/sorted/SortedIndexReaderImpl.java:37-116: BIG_ENDIAN
  * (startDocId, endDocId) int pairs per dictId). */
-enum pgpu_fwd_format { PGPU_FWD_FIXED_BIT = 0, PGPU_FWD_SORTED_PAIRS = 1 };
+/* Forward-index formats: FixedBitSVForwardIndexReaderV2 bytes; SortedIndexReaderImpl (start, end) pairs; a raw
+ * (no-dictionary) fixed-width column as FixedByteChunkSVForwardIndexWriter writes it with PASS_THROUGH compression,
+ * versions 2 / 3 (BaseChunkSVForwardIndexWriter.java:130-170; FixedByteChunkSVForwardIndexReader.java:30-110) --
+ * cardinality 0, no dictionary; usable as an aggregation operand (SUM / MIN / MAX / AVG). */
+enum pgpu_fwd_format { PGPU_FWD_FIXED_BIT = 0, PGPU_FWD_SORTED_PAIRS = 1, PGPU_FWD_RAW_FIXED = 2 };
 
 int pgpu_abi_version(void);
 /* Copies the calling thread's last error message (NUL-terminated, truncated to len). Returns its full length. */

@@ -173,6 +173,22 @@ static inline int dict_str(const or_column* c, int id, const uint8_t** p) {
 }
 
 /* Dictionary.readDoubleValues -> getDoubleValue per type (IntDictionary.java:62-64 etc.). */
+double or_raw_get_double(const or_column* c, int doc) {
+  const uint8_t* b = c->fwd;
+  const int version = (int)be32(b), num_chunks = (int)be32(b + 4), size = (int)be32(b + 12);
+  int data_header_start = 16;
+  if (version > 1) data_header_start = (int)be32(b + 24);
+  const int entry = version <= 2 ? 4 : 8; /* BaseChunkSVForwardIndexWriter.getHeaderEntryChunkOffsetSize */
+  const uint8_t* v = b + data_header_start + (int64_t)num_chunks * entry + (int64_t)doc * size;
+  const uint64_t hi = be32(v), lo = size == 8 ? be32(v + 4) : 0;
+  switch (c->data_type) {
+    case OR_INT: return (double)(int32_t)hi;
+    case OR_LONG: return (double)(int64_t)((hi << 32) | lo);
+    case OR_FLOAT: { uint32_t u = (uint32_t)hi; float f; memcpy(&f, &u, 4); return (double)f; }
+    default: { uint64_t u = (hi << 32) | lo; double d; memcpy(&d, &u, 8); return d; }
+  }
+}
+
 double or_dict_get_double(const or_column* c, int id) {
   switch (c->data_type) {
     case OR_INT: return (double)dict_int(c, id);
@@ -1183,8 +1199,12 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
         continue;
       }
       const or_column* c = &seg->columns[ag->column];
-      or_read_dict_ids(c->fwd, c->bits, seg->num_docs, docs, pos, mids);   /* DataFetcher.readDoubleValues */
-      for (int d = 0; d < pos; d++) dvals[d] = or_dict_get_double(c, mids[d]);
+      if (c->raw) { /* DataFetcher.readDoubleValues on a raw column: ForwardIndexReader.readValuesSV */
+        for (int d = 0; d < pos; d++) dvals[d] = or_raw_get_double(c, docs[d]);
+      } else {
+        or_read_dict_ids(c->fwd, c->bits, seg->num_docs, docs, pos, mids);   /* DataFetcher.readDoubleValues */
+        for (int d = 0; d < pos; d++) dvals[d] = or_dict_get_double(c, mids[d]);
+      }
       switch (ag->fn) {
         case OR_AGG_SUM: /* SumAggregationFunction.java:66-73 */
           for (int d = 0; d < pos; d++) if (gids[d] != INVALID_ID) h[gids[d]] = h[gids[d]] + dvals[d];
@@ -1212,7 +1232,9 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
     int all_count = 1, all_minmax = 1;
     for (int a = 0; a < q->num_aggs; a++) {
       all_count &= q->aggs[a].fn == OR_AGG_COUNT;
-      all_minmax &= q->aggs[a].fn == OR_AGG_MIN || q->aggs[a].fn == OR_AGG_MAX;
+      /* isFitForDictionaryBasedPlan needs a dictionary (AggregationPlanNode.java:196-213) */
+      all_minmax &= (q->aggs[a].fn == OR_AGG_MIN || q->aggs[a].fn == OR_AGG_MAX) &&
+                    !seg->columns[q->aggs[a].column].raw;
     }
     if (all_count || all_minmax) r->post_filter = 0;
   }

@@ -51,8 +51,14 @@ typedef struct {
   int32_t has_inverted; /* a bitmap inverted index is loaded: EQ / NOT_EQ / IN / NOT_IN run as
                            BitmapBasedFilterOperator (docIds read from the forward index) */
   const uint8_t* dict;  /* BIG_ENDIAN fixed-width sorted values (BaseImmutableDictionary.java:45-60) */
-  const uint8_t* fwd;   /* MSB-first packed dictIds (FixedBitSVForwardIndexWriter.java:39-50) */
+  const uint8_t* fwd;   /* MSB-first packed dictIds (FixedBitSVForwardIndexWriter.java:39-50), or for a raw column the
+                           FixedByteChunkSVForwardIndexWriter bytes (PASS_THROUGH chunks) */
+  int32_t raw;          /* 1: no-dictionary column (cardinality 0), values read by FixedByteChunkSVForwardIndexReader */
 } or_column;
+
+/* FixedByteChunkSVForwardIndexReader.getInt / getLong / getFloat / getDouble on an uncompressed (PASS_THROUGH)
+ * file (BaseChunkSVForwardIndexReader.java:57-98: header, chunk offsets, raw data from rawDataStart). */
+double or_raw_get_double(const or_column* c, int doc);
 
 typedef struct {
   int32_t num_docs;

@@ -30,7 +30,7 @@ PGPU_ERR_NOT_FOUND = -6
 
 INT, LONG, FLOAT, DOUBLE, STRING = 0, 1, 2, 3, 4
 TYPE_NAMES = {"INT": INT, "LONG": LONG, "FLOAT": FLOAT, "DOUBLE": DOUBLE, "STRING": STRING}
-FWD_FIXED_BIT, FWD_SORTED_PAIRS = 0, 1
+FWD_FIXED_BIT, FWD_SORTED_PAIRS, FWD_RAW_FIXED = 0, 1, 2
 PRED_EQ, PRED_NOT_EQ, PRED_IN, PRED_NOT_IN, PRED_RANGE = 0, 1, 2, 3, 4
 OP_PRED, OP_AND, OP_OR, OP_NOT = 0, 1, 2, 3
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4

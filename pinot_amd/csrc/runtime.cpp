@@ -340,6 +340,10 @@ struct Column {
   int64_t* d_key = nullptr;
   double* d_val = nullptr;
   std::shared_ptr<InvIndex> inv;    // bitmap inverted index, if attached
+  // raw (no-dictionary) column: d_key / d_val hold the values per doc (read through the table's identity $docId
+  // forward index), raw_min / raw_max bound integer sums
+  bool raw = false;
+  int64_t raw_min = 0, raw_max = 0;
 };
 
 // A pinned star-tree (pgpu_attach_startree): one device block holding the nodes, the star-tree documents'
@@ -640,7 +644,8 @@ void free_segment(pgpu_table_s* t, Segment* s) {
       t->device_bytes -= c.inv->bytes;
       c.inv.reset();
     }
-    t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) + (c.d_key ? 16 * std::max(c.card, 1) : 0);
+    t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) +
+                       (c.d_key ? 16 * (c.raw ? std::max(s->num_docs, 1) : std::max(c.card, 1)) : 0);
   }
   if (s->d_block) hipFree(s->d_block);
   if (s->star && s->star->d_block) {
@@ -651,6 +656,69 @@ void free_segment(pgpu_table_s* t, Segment* s) {
 
 int64_t padded_fwd_words(int64_t num_docs, int bits) {
   return ((num_docs + kTileDocs - 1) / kTileDocs) * (int64_t)kBlock * bits + kFwdPadWords;
+}
+
+// A raw fixed-width column (FixedByteChunkSVForwardIndexWriter, PASS_THROUGH chunks; BaseChunkSVForwardIndexReader
+// .java:57-98 header): the per-doc values as the aggregation kernels read them -- int64 key (integer value, or the
+// order-preserving key of the double) and double -- for docs [0, num_docs).
+struct RawValues {
+  std::vector<int64_t> key;
+  std::vector<double> val;
+};
+int parse_raw_column(int type, const pgpu_column_buffers& cb, int32_t num_docs, int c, Column* col, RawValues* out) {
+  if (type == PGPU_STRING) return fail(PGPU_ERR_UNSUPPORTED, "column %d: raw STRING columns are not on the GPU path", c);
+  const int64_t n = cb.fwd_len;
+  const uint8_t* b = cb.fwd;
+  if (!b || n < 16) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index too short", c);
+  const int32_t version = (int32_t)rd_be32(b), num_chunks = (int32_t)rd_be32(b + 4);
+  const int32_t per_chunk = (int32_t)rd_be32(b + 8), size = (int32_t)rd_be32(b + 12);
+  if (version != 2 && version != 3)
+    return fail(PGPU_ERR_UNSUPPORTED, "column %d: raw forward index version %d (2 and 3 are read)", c, version);
+  if (n < 28) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index header truncated", c);
+  const int32_t total = (int32_t)rd_be32(b + 16), compression = (int32_t)rd_be32(b + 20);
+  const int32_t header_start = (int32_t)rd_be32(b + 24);
+  if (compression != 0)
+    return fail(PGPU_ERR_UNSUPPORTED, "column %d: compressed raw chunks (type %d): PASS_THROUGH only", c, compression);
+  const int want = (type == PGPU_INT || type == PGPU_FLOAT) ? 4 : 8;
+  if (size != want) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw entry size %d, type needs %d", c, size, want);
+  if (num_chunks < 0 || per_chunk <= 0 || total < num_docs || (int64_t)num_chunks * per_chunk < num_docs)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index covers %d docs, segment has %d", c, total,
+                num_docs);
+  const int64_t data = (int64_t)header_start + (int64_t)num_chunks * (version == 2 ? 4 : 8);
+  if (header_start < 28 || data + (int64_t)num_docs * size > n)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index too short for %d docs", c, num_docs);
+  col->raw = true;
+  col->card = 0;
+  col->bits = 0;
+  col->fwd_bytes = n;
+  out->key.resize(std::max<int32_t>(num_docs, 1));
+  out->val.resize(std::max<int32_t>(num_docs, 1));
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  for (int32_t i = 0; i < num_docs; ++i) {
+    const uint8_t* v = b + data + (int64_t)i * size;
+    switch (type) {
+      case PGPU_INT: { const int64_t x = (int32_t)rd_be32(v); out->key[i] = x; out->val[i] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
+      case PGPU_LONG: { const int64_t x = (int64_t)rd_be64(v); out->key[i] = x; out->val[i] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
+      case PGPU_FLOAT: {
+        const uint32_t u = rd_be32(v);
+        float f;
+        memcpy(&f, &u, 4);
+        out->val[i] = (double)f;
+        out->key[i] = double_key(out->val[i]);
+        break;
+      }
+      default: {
+        const uint64_t u = rd_be64(v);
+        double x;
+        memcpy(&x, &u, 8);
+        out->val[i] = x;
+        out->key[i] = double_key(x);
+      }
+    }
+  }
+  col->raw_min = num_docs > 0 && lo <= hi ? lo : 0;
+  col->raw_max = num_docs > 0 && lo <= hi ? hi : 0;
+  return 0;
 }
 
 // Registers a segment whose columns have parsed dictionaries and device forward indexes.
@@ -1296,9 +1364,12 @@ SegStats classify_segment_stats(const pgpu_plan_s* P, uint64_t sig) {
 bool int_sum_fits(const std::vector<Segment*>& segs, int col) {
   long double bound = 0;
   for (const Segment* s : segs) {
-    const Dict& d = s->cols[col].dict;
-    if (d.iv.empty()) continue;
-    const long double m = std::max(std::fabs((long double)d.iv.front()), std::fabs((long double)d.iv.back()));
+    const Column& c = s->cols[col];
+    const Dict& d = c.dict;
+    if (!c.raw && d.iv.empty()) continue;
+    const long double lo = c.raw ? (long double)c.raw_min : (long double)d.iv.front();
+    const long double hi = c.raw ? (long double)c.raw_max : (long double)d.iv.back();
+    const long double m = std::max(std::fabs(lo), std::fabs(hi));
     bound += m * (long double)s->num_docs;
   }
   return bound < 0x1p62L;
@@ -1352,6 +1423,16 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     if (c < 0 || c >= ncols) return fail(PGPU_ERR_INVALID_ARGUMENT, "group-by %d: bad column %d", i, c);
     P->key_cols.push_back(c);
     slot_of(c);
+  }
+  // raw (no-dictionary) columns are aggregation operands only: a predicate or a group-by on one runs on Pinot's own
+  // raw-value scan (RawValueBasedFilter / NoDictionaryGroupKeyGenerator), not here
+  for (Segment* s : P->segs) {
+    for (int i = 0; i < q->num_predicates; ++i)
+      if (s->cols[q->predicates[i].column].raw)
+        return fail(PGPU_ERR_UNSUPPORTED, "predicate on raw (no-dictionary) column %d", q->predicates[i].column);
+    for (int i = 0; i < q->num_group_by; ++i)
+      if (s->cols[q->group_by[i]].raw)
+        return fail(PGPU_ERR_UNSUPPORTED, "group-by on raw (no-dictionary) column %d", q->group_by[i]);
   }
   // program
   int depth = 0, max_depth = 0;
@@ -1501,7 +1582,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // Aggregation-only over a match-all segment: COUNT-only is answered from metadata, MIN/MAX-only from the
   // dictionaries (AggregationPlanNode.java:165-183) -- same values, numEntriesScannedPostFilter 0
   // (MetadataBasedAggregationOperator.java:89-92, DictionaryBasedAggregationOperator.java:171-173).
-  bool exempt_kind = false;
+  bool exempt_kind = false, minmax_kind = false;
   if (q->num_group_by == 0 && q->num_aggs > 0) {
     bool all_count = true, all_minmax = true;
     for (int i = 0; i < q->num_aggs; ++i) {
@@ -1509,7 +1590,15 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       all_minmax &= q->aggs[i].fn == PGPU_AGG_MIN || q->aggs[i].fn == PGPU_AGG_MAX;
     }
     exempt_kind = all_count || all_minmax;
+    minmax_kind = all_minmax && !all_count;
   }
+  // DictionaryBasedAggregationOperator needs a dictionary on every MIN / MAX column (AggregationPlanNode.java:196-213)
+  auto raw_minmax = [&](const Segment* s) {
+    if (!minmax_kind) return false;
+    for (int i = 0; i < q->num_aggs; ++i)
+      if (q->aggs[i].column >= 0 && s->cols[q->aggs[i].column].raw) return true;
+    return false;
+  };
   std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
   bool any_star = false, any_inv = false;
   mark();
@@ -1592,7 +1681,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       if (whole == T_NONE || s->num_docs == 0) continue;  // EmptyFilterOperator: the segment is not scanned
       C.scanned.back() = 1;
       C.matched++;
-      if (exempt_kind && whole == T_ALL) C.exempt += s->num_docs;
+      if (exempt_kind && whole == T_ALL && !raw_minmax(s)) C.exempt += s->num_docs;
       if (star_allowed && s->star) {  // only on the sequential path (any_star)
         bool used = false;
         TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
@@ -1656,6 +1745,14 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           continue;
         }
         const Column& c = s->cols[P->query_cols[j]];
+        if (c.raw) {  // values per doc, addressed through the identity docId index
+          kc[j].fwd = t->d_docid_fwd;
+          kc[j].lut = nullptr;
+          kc[j].dkey = c.d_key;
+          kc[j].dval = c.d_val;
+          kc[j].bits = t->docid_bits;
+          continue;
+        }
         kc[j].fwd = c.d_fwd;
         kc[j].lut = c.d_lut;
         kc[j].dkey = c.d_key;
@@ -2728,6 +2825,8 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
   seg->cols.resize(d->num_columns);
   int64_t total_words = 0;
   std::vector<std::vector<uint32_t>> sorted_expansion(d->num_columns);
+  std::vector<RawValues> raw_values(d->num_columns);
+  bool any_raw = false;
   for (int c = 0; c < d->num_columns; ++c) {
     const pgpu_column_buffers& cb = d->columns[c];
     Column& col = seg->cols[c];
@@ -2772,6 +2871,10 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
       if (d->num_docs > 0 && prev_end != d->num_docs - 1)
         return fail(PGPU_ERR_INVALID_ARGUMENT, "sorted pairs do not cover every doc");
       for (auto& x : w) x = __builtin_bswap32(x);  // the device reads the forward index as big-endian bytes
+    } else if (cb.fwd_format == PGPU_FWD_RAW_FIXED) {
+      TRY(parse_raw_column(t->types[c], cb, d->num_docs, c, &col, &raw_values[c]));
+      any_raw = true;
+      continue;  // no per-segment forward-index words: the values live in d_key / d_val
     } else {
       return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: bad forward-index format", c);
     }
@@ -2783,6 +2886,15 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
   int64_t off = 0;
   for (int c = 0; c < d->num_columns; ++c) {
     Column& col = seg->cols[c];
+    if (col.raw) {
+      const size_t n = std::max<int32_t>(d->num_docs, 1);
+      HIP_TRY(hipMalloc(&col.d_key, n * 8));
+      HIP_TRY(hipMalloc(&col.d_val, n * 8));
+      t->device_bytes += 16 * (int64_t)n;
+      HIP_TRY(hipMemcpyAsync(col.d_key, raw_values[c].key.data(), n * 8, hipMemcpyHostToDevice, t->stream));
+      HIP_TRY(hipMemcpyAsync(col.d_val, raw_values[c].val.data(), n * 8, hipMemcpyHostToDevice, t->stream));
+      continue;
+    }
     col.d_fwd = reinterpret_cast<uint32_t*>(seg->d_block) + off;
     const pgpu_column_buffers& cb = d->columns[c];
     HIP_TRY(hipMemsetAsync(col.d_fwd, 0, (size_t)col.fwd_words * 4, t->stream));
@@ -2796,6 +2908,7 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
   }
   HIP_TRY(hipStreamSynchronize(t->stream));
   std::lock_guard<std::mutex> lk(t->mu);
+  if (any_raw) TRY(ensure_docid(t, d->num_docs, t->stream));
   *handle = register_segment(t, std::move(seg));
   return 0;
 }

@@ -90,3 +90,39 @@ def load_v1_segment_dir(path):
         cols[name] = ColumnData(dtype, card, bits, width, d, fwd, pad if dtype == L.STRING else 0, fmt,
                                 props.get(p + "isSorted", "false") == "true", inv)
     return SegmentBuffers(num_docs, cols)
+
+
+RAW_DOCS_PER_CHUNK = 1000  # SingleValueFixedByteRawIndexCreator.NUM_DOCS_PER_CHUNK (:36)
+_RAW_FMT = {L.INT: ">i", L.LONG: ">q", L.FLOAT: ">f", L.DOUBLE: ">d"}
+
+
+def raw_forward_index_bytes(data_type, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK):
+    """A no-dictionary fixed-width column as FixedByteChunkSVForwardIndexWriter writes it with PASS_THROUGH chunks
+    (BaseChunkSVForwardIndexWriter.java:130-193): header (version, numChunks, numDocsPerChunk, sizeOfEntry, then for
+    version > 1 totalDocs, compression type 0, dataHeaderStart), the chunk offsets (int for version 2, long for 3),
+    then the chunks, big-endian values back to back."""
+    import struct
+    if version not in (2, 3):
+        raise ValueError("raw forward index version %d (2 or 3)" % version)
+    fmt = _RAW_FMT[data_type]
+    size = struct.calcsize(fmt)
+    n = len(values)
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    entry = 4 if version == 2 else 8
+    header_size = 7 * 4 + num_chunks * entry
+    hdr = struct.pack(">iiiiiii", version, num_chunks, docs_per_chunk, size, n, 0, 7 * 4)
+    offsets, off = [], header_size
+    for c in range(num_chunks):
+        offsets.append(off)
+        off += min(docs_per_chunk, n - c * docs_per_chunk) * size
+    hdr += b"".join(struct.pack(">i" if version == 2 else ">q", o) for o in offsets)
+    cast = float if data_type in (L.FLOAT, L.DOUBLE) else int
+    body = b"".join(struct.pack(fmt, cast(v)) for v in values)
+    return hdr + body
+
+
+def build_raw_column(type_name, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK):
+    """ColumnData of a raw (no-dictionary) INT / LONG / FLOAT / DOUBLE column."""
+    t = L.TYPE_NAMES[type_name] if isinstance(type_name, str) else int(type_name)
+    fwd = raw_forward_index_bytes(t, values, version, docs_per_chunk)
+    return ColumnData(t, 0, 0, 4 if t in (L.INT, L.FLOAT) else 8, b"", fwd, fwd_format=L.FWD_RAW_FIXED)

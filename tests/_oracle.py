@@ -28,7 +28,8 @@ def build_oracle():
 class OrColumn(ctypes.Structure):
     _fields_ = [("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("entry_width", ctypes.c_int32), ("padding_byte", ctypes.c_int32), ("is_sorted", ctypes.c_int32),
-                ("has_inverted", ctypes.c_int32), ("dict", ctypes.c_void_p), ("fwd", ctypes.c_void_p)]
+                ("has_inverted", ctypes.c_int32), ("dict", ctypes.c_void_p), ("fwd", ctypes.c_void_p),
+                ("raw", ctypes.c_int32)]
 
 
 class OrSegment(ctypes.Structure):
@@ -176,7 +177,8 @@ class _OrSeg:
             self.keep += [d, f]
             cols[i] = OrColumn(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.padding_byte,
                                int(c.is_sorted), int(getattr(c, "inv_bytes", None) is not None),
-                               ctypes.cast(d, ctypes.c_void_p), ctypes.cast(f, ctypes.c_void_p))
+                               ctypes.cast(d, ctypes.c_void_p), ctypes.cast(f, ctypes.c_void_p),
+                               int(c.fwd_format == L.FWD_RAW_FIXED))
         self.keep.append(cols)
         self.seg = OrSegment(seg.num_docs, len(schema), cols)
 

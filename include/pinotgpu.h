@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 1
+#define PGPU_ABI_VERSION 2  /* 2: pgpu_query.end_time_ms, PGPU_ERR_TIMEOUT */
 
 /* ---- status codes (BaseCombineOperator.java:101-107 maps failures to ProcessingException; the Java shim maps
  * these codes the same way and keeps Pinot's CPU operator for PGPU_ERR_UNSUPPORTED). */
@@ -38,6 +38,10 @@ extern "C" {
 #define PGPU_ERR_DEVICE (-4)         /* HIP runtime / kernel failure */
 #define PGPU_ERR_OUT_OF_MEMORY (-5)
 #define PGPU_ERR_NOT_FOUND (-6)      /* unknown segment handle / column */
+#define PGPU_ERR_TIMEOUT (-7)        /* the query's end time passed before its device work completed: the combine's
+                                        timeout (BaseCombineOperator.java:193-203 EXECUTION_TIMEOUT_ERROR for
+                                        aggregation-only, GroupByCombineOperator.java:193-203 QUERY_EXECUTION_ERROR
+                                        wrapping a TimeoutException for group-by); no partial result is returned */
 
 /* FieldSpec.DataType subset of dictionary-encoded single-value columns. */
 enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE = 3, PGPU_STRING = 4 };
@@ -163,6 +167,10 @@ typedef struct {
   const pgpu_agg* aggs;
   int32_t num_groups_limit;   /* InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000 (:70); <= 0 = unlimited */
   int32_t options;            /* PGPU_OPT_* bits */
+  int64_t end_time_ms;        /* QueryContext.getEndTimeMs(): absolute deadline in ms since the Unix epoch (the
+                                 broker's arrival time + timeoutMs); 0 = none.  Checked before launch and on the
+                                 device (the persistent scans stop taking tiles past it): PGPU_ERR_TIMEOUT.  Not part
+                                 of the compiled-plan cache key. */
 } pgpu_query;
 
 /* Query options: debug option useStarTree=false (StarTreeUtils.isStarTreeDisabled, core/startree/StarTreeUtils.java:

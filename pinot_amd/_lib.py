@@ -27,6 +27,7 @@ PGPU_ERR_UNSUPPORTED = -3
 PGPU_ERR_DEVICE = -4
 PGPU_ERR_OUT_OF_MEMORY = -5
 PGPU_ERR_NOT_FOUND = -6
+PGPU_ERR_TIMEOUT = -7
 
 INT, LONG, FLOAT, DOUBLE, STRING = 0, 1, 2, 3, 4
 TYPE_NAMES = {"INT": INT, "LONG": LONG, "FLOAT": FLOAT, "DOUBLE": DOUBLE, "STRING": STRING}
@@ -84,7 +85,7 @@ class QueryC(ctypes.Structure):
     _fields_ = [("num_predicates", c_i32), ("num_filter_ops", c_i32), ("predicates", ctypes.POINTER(PredicateC)),
                 ("filter", ctypes.POINTER(FilterOpC)), ("num_group_by", c_i32), ("num_aggs", c_i32),
                 ("group_by", c_i32p), ("aggs", ctypes.POINTER(AggC)), ("num_groups_limit", c_i32),
-                ("options", c_i32)]
+                ("options", c_i32), ("end_time_ms", c_i64)]
 
 
 class GenColumnC(ctypes.Structure):
@@ -112,6 +113,12 @@ class BadQueryRequestException(PinotGpuError):
 
 class UnsupportedQueryError(PinotGpuError):
     """PGPU_ERR_UNSUPPORTED: the query shape is outside the GPU path."""
+
+
+class QueryTimeoutError(PinotGpuError):
+    """PGPU_ERR_TIMEOUT: the query's end time passed (the combine's TimeoutException; Pinot reports
+    QueryException.EXECUTION_TIMEOUT_ERROR_CODE 250 for aggregation-only and QUERY_EXECUTION_ERROR_CODE 200 for
+    group-by, BaseCombineOperator.java:193-203 / GroupByCombineOperator.java:193-203)."""
 
 
 _PROTOS = {
@@ -203,7 +210,7 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.pgpu_abi_version() != 1:
+    if lib.pgpu_abi_version() != 2:
         raise ImportError("libpinotgpu.so ABI mismatch")
     if path is None:
         _lib = lib
@@ -225,6 +232,8 @@ def check(code):
         raise BadQueryRequestException(code, msg)
     if code == PGPU_ERR_UNSUPPORTED:
         raise UnsupportedQueryError(code, msg)
+    if code == PGPU_ERR_TIMEOUT:
+        raise QueryTimeoutError(code, msg)
     raise PinotGpuError(code, msg)
 
 

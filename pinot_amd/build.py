@@ -14,9 +14,8 @@ SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime"), ("sta
            ("filter_stats.cpp", [], "filter_stats"), ("server_response.cpp", [], "server_response"),
            ("k_partition.hip", [], "k_partition")] + \
     [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
-    [("k_staged.hip", ["-DPGPU_MODE=%d" % m], "k_staged_%d" % m) for m in range(3)] + \
     [("k_startree.hip", ["-DPGPU_MODE=%d" % m], "k_startree_%d" % m) for m in range(3)]
-HEADERS = ["internal.h", "device.h", "scan_direct.h", "scan_staged.h", "host_common.h", "startree_kernels.h",
+HEADERS = ["internal.h", "device.h", "scan_direct.h", "host_common.h", "startree_kernels.h",
            "partition.h", "filter_stats.h", "host_result.h"]
 ARCH = os.environ.get("PGPU_OFFLOAD_ARCH", "gfx950")
 
@@ -41,15 +40,17 @@ def is_stale():
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, defines=(), out=None):
     """Compiles the kernels and the host runtime into pinot_amd/libpinotgpu.so (cross-compiles without a GPU).
-    Each source is compiled to an object in parallel, then linked."""
-    if not force and not is_stale():
+    Each source is compiled to an object in parallel, then linked.  `defines` / `out`: an A/B variant of the
+    library (e.g. ("PGPU_MIN_WAVES=1",)) written to `out` instead, loaded with PGPU_LIB=<out>."""
+    lib_path = out or LIB_PATH
+    if not force and not defines and not out and not is_stale():
         return LIB_PATH
     hipcc = _hipcc()
     flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
-             "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
-    objdir = os.path.join(ROOT, "build", "obj")
+             "-Wall", "-Wno-unused-result", "-Wno-unused-value"] + ["-D" + d for d in defines]
+    objdir = os.path.join(ROOT, "build", "obj" if not out else "obj_" + os.path.basename(out).replace(".", "_"))
     os.makedirs(objdir, exist_ok=True)
     procs = []
     objs = []
@@ -68,12 +69,12 @@ def build(force=False, verbose=False):
             errors.append("%s:\n%s" % (src, out[-8000:]))
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
-    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs
     res = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc link failed:\n" + res.stdout[-8000:])
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(lib_path + ".tmp", lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":

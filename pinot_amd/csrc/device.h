@@ -24,6 +24,14 @@ __device__ __forceinline__ gmem<T>* gp(const T* p) { return (gmem<T>*)p; }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// The query's end time (KParams.deadline: a wall_clock64() value, 0 = none) has passed.  wall_clock64 is a scalar
+// read of the constant-rate device clock, so the answer is uniform across a wave.
+__device__ __forceinline__ bool past_deadline(uint64_t deadline) {
+  return deadline != 0 && (uint64_t)wall_clock64() > deadline;
+}
+// stats[5] != 0: some workgroup stopped at the deadline (the group table is partial; the host reports the timeout).
+__device__ __forceinline__ void flag_timeout(unsigned long long* stats) { atomicOr(stats + 5, 1ull); }
+
 // Value of doc `doc` in a packed column (PinotDataBitSet.readInt semantics).  The two-word window never leaves
 // the allocation thanks to the padding words.
 __device__ __forceinline__ uint32_t gather_id(const uint32_t* __restrict__ fwd, int bits, int64_t doc) {
@@ -49,7 +57,7 @@ __device__ __forceinline__ uint32_t extract(const uint32_t (&w)[B + 1]) {
   }
 }
 
-// G: `words` is in global memory (else an LDS stage buffer: the staged kernel).
+// G: `words` is in global memory (else LDS).
 template <int B, bool G = true>
 __device__ __forceinline__ void load_group(const uint32_t* __restrict__ words, uint32_t (&w)[B + 1]) {
   if constexpr (G) {

@@ -26,8 +26,6 @@ constexpr int kMaxKeys = 8;                 // group-by columns handled on the G
 constexpr int kMaxSlots = 24;               // accumulator rows of the group table
 constexpr int kMaxStack = 8;                // filter evaluation stack depth
 constexpr int kFwdPadWords = 4;
-constexpr int kMaxStage = 4;                // distinct filter columns staged into LDS per tile
-constexpr int kQueueCap = 1024;             // matched-doc queue entries per workgroup (LDS)
 constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
 constexpr int kDenseGroupMin = 256;
@@ -94,11 +92,6 @@ struct KParams {
   int32_t num_slots;
   int32_t slot_kind[kMaxSlots];
   int32_t slot_col[kMaxSlots];
-  int32_t num_stage;               // staged (filter) columns: query column slots, LDS-DMA'd per tile
-  int32_t stage_col[kMaxStage];
-  int32_t leaf_stage[kMaxLeaves];  // staged column of each leaf
-  int32_t stage_words;             // words of one stage buffer (max over the plan's segments)
-  int32_t lds_table_words;         // MODE_LDS group table words at the start of LDS
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
@@ -106,6 +99,10 @@ struct KParams {
   // STATS_LEAP2 segments: per (tile, wave) one byte of AndDocIdIterator state over scans A, B: bit 0 = a doc
   // matches, bit 1 = scanner after the wave's docs (1 = B), bits 2-3 = entry difference at its first match + 1
   uint8_t* leap_maps;
+  // QueryContext.getEndTimeMs as a wall_clock64() reading of this device (0 = no deadline): past it the persistent
+  // scans stop taking tiles and set stats[5] (BaseCombineOperator.java:79-132 / GroupByCombineOperator.java:193-203
+  // give up at the same point; the host then reports the timeout instead of a partial result)
+  uint64_t deadline;
 };
 
 // leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to
@@ -161,7 +158,8 @@ struct KStarParams {
   uint64_t* slab;                         // MODE_LDS: this kernel's first slab
   unsigned long long* hash_keys;
   unsigned long long* stats;              // [0] docs matched, [1] entries scanned in filter, [3] star-tree
-                                          // documents read (positions of the emitted ranges)
+                                          // documents read (positions of the emitted ranges), [5] timed out
+  uint64_t deadline;                      // as KParams.deadline
 };
 
 // ---------------------------------------------------------------------------------------------- partitioned
@@ -221,7 +219,6 @@ int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_seg
 int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream);
 // Resident workgroups per CU of the direct kernel instance (< 0: query failed).
 int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes);
-int launch_scan(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream);
 int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int32_t num_slots, int64_t num_keys,
                         int32_t num_blocks, uint64_t* out, void* stream);
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
@@ -254,6 +251,8 @@ int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void*
 int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,
                          const int32_t* code_to_pos, int32_t n_codes, int64_t row0, int32_t num_docs,
                          int32_t* pos_out, uint32_t* presence, void* stream);
+// One wall_clock64() reading into `out` (host-visible memory): deadline calibration.
+int launch_read_clock(uint64_t* out, void* stream);
 int launch_gen_pack(const int32_t* pos, const int32_t* pos_to_id, int32_t num_docs, int32_t bits, uint32_t* fwd_out,
                     void* stream);
 

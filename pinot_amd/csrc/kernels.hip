@@ -82,7 +82,8 @@ struct SlotKinds {
   int32_t k[kMaxSlots];
 };
 // Each block folds 8 table words; the 32 lanes of a word take every 32nd slab and their partials are combined
-// in lane order, so the result is bitwise reproducible run to run.
+// in lane order: the fold itself has a fixed order, but the LDS slabs it reads were summed with atomicAdd(double),
+// so FLOAT/DOUBLE sums vary in their last bits from run to run (integer slots are exact).
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const uint64_t* __restrict__ slab, SlotKinds kinds,
                                                            int64_t num_keys, int32_t num_slots, int32_t num_blocks,
                                                            uint64_t* __restrict__ out) {
@@ -310,6 +311,11 @@ __global__ __launch_bounds__(kBlock) void leaf_masks_kernel(const KParams p, con
     out[J.out_word + (int64_t)l * ngroups + g] = leaf_mask(S.leaves[l], S.cols[p.leaf_col[l]], g);
 }
 
+// One reading of the device's constant-rate wall clock (host calibration of query deadlines).
+__global__ void read_clock_kernel(uint64_t* out) {
+  if (threadIdx.x == 0) out[0] = (uint64_t)wall_clock64();
+}
+
 // ---------------------------------------------------------------------------------------------- generator
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -401,16 +407,13 @@ int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slo
   return PGPU_HIP_OK(hipGetLastError());
 }
 
-// One object per (kernel family, mode): k_direct.hip / k_staged.hip compiled with -DPGPU_MODE=0,1,2.
+// One object per (kernel family, mode): k_direct.hip / k_startree.hip compiled with -DPGPU_MODE=0,1,2.
 int launch_direct_mode0(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
 int launch_direct_mode1(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
 int launch_direct_mode2(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
 int occupancy_direct_mode0(bool dense, size_t lds_bytes);
 int occupancy_direct_mode1(bool dense, size_t lds_bytes);
 int occupancy_direct_mode2(bool dense, size_t lds_bytes);
-int launch_staged_mode0(const KParams& p, int grid, size_t lds_bytes, void* stream);
-int launch_staged_mode1(const KParams& p, int grid, size_t lds_bytes, void* stream);
-int launch_staged_mode2(const KParams& p, int grid, size_t lds_bytes, void* stream);
 
 int launch_startree_scan_mode0(const KStarParams& p, size_t lds_bytes, void* stream);
 int launch_startree_scan_mode1(const KStarParams& p, size_t lds_bytes, void* stream);
@@ -445,14 +448,6 @@ int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_seg
   hipLaunchKernelGGL(expand_tiles_kernel, dim3(num_segs < 4096 ? num_segs : 4096), dim3(128), 0, S(stream), segs,
                      seg_stride, num_segs, tile_seg);
   return PGPU_HIP_OK(hipGetLastError());
-}
-
-int launch_scan(const KParams& p, int mode, int grid, size_t lds_bytes, void* stream) {
-  switch (mode) {
-    case MODE_LDS: return launch_staged_mode0(p, grid, lds_bytes, stream);
-    case MODE_GLOBAL: return launch_staged_mode1(p, grid, lds_bytes, stream);
-    default: return launch_staged_mode2(p, grid, lds_bytes, stream);
-  }
 }
 
 int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
@@ -544,6 +539,11 @@ int launch_gen_pack(const int32_t* pos, const int32_t* pos_to_id, int32_t num_do
   if (ngroups <= 0) return 0;
   hipLaunchKernelGGL(gen_pack_kernel, dim3((unsigned)((ngroups + 255) / 256)), dim3(256), 0, S(stream), pos,
                      pos_to_id, num_docs, bits, fwd_out);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_read_clock(uint64_t* out, void* stream) {
+  hipLaunchKernelGGL(read_clock_kernel, dim3(1), dim3(64), 0, S(stream), out);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

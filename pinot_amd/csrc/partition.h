@@ -116,6 +116,9 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   const int tid = threadIdx.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
   uint32_t* stack = hist + ((pp.num_parts + 3) & ~3);
+  // Deadline: only K8a tests the clock.  K8c must scatter exactly the docs K8a counted (its cursors run inside
+  // K8a's reservations), so it runs in full or -- once K8a flagged the timeout -- not at all, like K8e / K8d.
+  if (SCATTER && p.deadline && p.stats[5]) return;
   if (SCATTER) {
     for (int c = tid; c < pp.num_coarse; c += kBlock)
       hist[c] = pp.part_start[c << pp.cshift] + pp.block_off[(int64_t)blockIdx.x * pp.num_coarse + c];
@@ -131,6 +134,10 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   int64_t tile_base = 0;
   int nd = 0;
   for (int64_t t = t0; t < t1; ++t) {
+    if (!SCATTER && ((t - t0) & 3) == 0 && past_deadline(p.deadline)) {
+      if ((tid & 63) == 0) flag_timeout(p.stats);
+      break;  // per wave: no barrier inside the tile loop
+    }
     const int cur = p.tile_seg[t];
     if (cur != seg) {
       seg = cur;
@@ -176,6 +183,7 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
   const int tid = threadIdx.x;
+  if (pp.base.deadline && pp.base.stats[5]) return;  // K8a timed out: its counts cover only part of the docs
   const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
   const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
   const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
@@ -231,6 +239,7 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const KParams& p = pp.base;
   const int tid = threadIdx.x;
+  if (p.deadline && p.stats[5]) return;
   const int PR = 1 << pp.pshift;
   const int ns = p.num_slots;
   for (int i = tid; i < ns * PR; i += kBlock) lds[i] = slot_init(p.slot_kind[i / PR]);

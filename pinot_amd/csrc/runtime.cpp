@@ -245,8 +245,6 @@ inline double key_double(int64_t k) {
 }
 
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
-constexpr size_t kLdsPerCu = 160 * 1024;
-constexpr size_t kMaxScanLds = 128 * 1024;          // larger staging falls back to the direct-load kernel
 constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
 constexpr int64_t kPartLds = 64 * 1024;              // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
@@ -439,6 +437,16 @@ struct pgpu_table_s {
   std::atomic<uint64_t> version{1};
   std::mutex cache_mu;
   std::list<std::pair<std::string, std::shared_ptr<pgpu_plan_s>>> plan_cache;  // most recent first
+  // Query deadlines on the device (pgpu_query.end_time_ms): one reading `clock_ticks` of the device's constant-rate
+  // wall clock, taken no earlier than host epoch time `clock_host_us`, maps epoch time to clock ticks; refreshed
+  // every 10 s (calibrate_clock).
+  std::mutex clock_mu;
+  hipStream_t clock_stream = nullptr;
+  uint64_t* clock_pinned = nullptr;
+  double clock_rate_khz = 0;
+  double clock_host_us = 0;
+  uint64_t clock_ticks = 0;
+  double clock_steady_us = -1;
 };
 
 int pgpu::table_dict_view(pgpu_table t, int col, DictView* out) {
@@ -805,7 +813,6 @@ struct pgpu_plan_s {
   std::vector<uint8_t> seg_scanned;       // per plan segment: 1 = scanned (filter not folded to empty)
   int grid = 0;
   size_t lds_bytes = 0;
-  bool staged = false;                    // LDS-DMA scan kernel (else the direct-load kernel)
   bool dense = false;                     // direct kernel instance with whole-group decode (dense tiles)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
   std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
@@ -817,10 +824,6 @@ struct pgpu_plan_s {
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
   double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
   int64_t sel_docs = 0;
-  std::vector<int32_t> stage_slot;        // query column slot of each staged filter column
-  std::vector<int32_t> leaf_stage;        // staged column of each leaf
-  int64_t stage_words = 0;                // one stage buffer (max over segments)
-  int lds_table_words = 0;
   Scratch* scratch = nullptr;
   hipStream_t last_stream = nullptr;
   bool executed = false;
@@ -832,6 +835,9 @@ struct pgpu_plan_s {
   // apply and the GPU result is not reported (PGPU_ERR_UNSUPPORTED: the caller runs Pinot's own operator).
   int64_t num_groups_limit = 0;
   bool limit_sensitive = false;
+  // pgpu_query.end_time_ms (QueryContext.getEndTimeMs) of the query being run: set per query, not cached
+  int64_t end_time_ms = 0;
+  int64_t exec_start_ms = 0;
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -1392,6 +1398,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   if (q->num_predicates > kMaxLeaves) return fail(PGPU_ERR_UNSUPPORTED, "more than %d predicates", kMaxLeaves);
   if (q->num_filter_ops > kMaxOps) return fail(PGPU_ERR_UNSUPPORTED, "filter program longer than %d", kMaxOps);
   P->table = t;
+  P->end_time_ms = q->end_time_ms;
   double tr[8] = {0};
   int ntr = 0;
   auto mark = [&] { if (trace_on() && ntr < 8) tr[ntr++] = now_us(); };
@@ -1575,7 +1582,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   std::vector<ParsedPred> parsed(P->num_leaves);
   for (int l = 0; l < P->num_leaves; ++l)
     TRY(parse_predicate(t->types[q->predicates[l].column], q->predicates[l], &parsed[l]));
-  static const bool scan_on = getenv("PGPU_SCAN") && getenv("PGPU_SCAN")[0] == '1';  // staged A/B kernel
   std::vector<std::vector<int>> star_comps;
   const bool star_allowed = q->num_group_by > 0 && !(q->options & PGPU_OPT_NO_STAR_TREE) &&
                             star_composites(P->ops, q, &star_comps);
@@ -1893,37 +1899,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
       }
     }
-    // LDS-DMA staging of the filter columns (the scan kernel) when the double buffer fits beside the table.
-    for (int l = 0; l < P->num_leaves; ++l) {
-      int sidx = -1;
-      for (size_t k = 0; k < P->stage_slot.size(); ++k)
-        if (P->stage_slot[k] == P->leaf_slot[l]) sidx = (int)k;
-      if (sidx < 0) {
-        P->stage_slot.push_back(P->leaf_slot[l]);
-        sidx = (int)P->stage_slot.size() - 1;
-      }
-      P->leaf_stage.push_back(sidx);
-    }
-    // The LDS-DMA staged kernel is kept as an A/B alternative (PGPU_SCAN=1); the direct-load kernel measured faster
-    // on MI355X (profiles/r01_ab_scan*.log).
-    if ((int)P->stage_slot.size() <= kMaxStage && scan_on) {
-      const bool pure_and = P->pure_and && P->num_leaves <= 4;  // the staged fast path holds at most 4 leaves in registers
-      for (Segment* s : P->segs) {
-        int64_t bits = 0;
-        for (int slot : P->stage_slot) bits += s->cols[P->query_cols[slot]].bits;
-        P->stage_words = std::max<int64_t>(P->stage_words, bits * kBlock);
-      }
-      P->lds_table_words = P->mode == MODE_LDS ? (int)((nslots * G + 1) & ~int64_t(1)) : 0;
-      const size_t lds = (size_t)P->lds_table_words * 8 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + 16 +
-                         (size_t)kQueueCap * 8 + (size_t)P->stage_words * 2 * 4;
-      if (lds <= kMaxScanLds) {
-        P->staged = true;
-        P->pure_and = pure_and;
-        P->lds_bytes = lds;
-        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, kLdsPerCu / lds));
-        P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
-      }
-    }
     return 0;
   };
   // Appends a planned chunk to the plan; tile_shift is added to its records' chunk-relative tile_base (0 keeps
@@ -1965,10 +1940,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   const bool part_eligible = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes &&
                              !getenv_flag("PGPU_NO_PARTITION");
   // CHAIN / LEAP2 statistics need the direct kernel's register fast path (a pure AND of <= kFastLeaves leaves)
-  P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !scan_on && !part_eligible;
+  P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !part_eligible;
   P->leaf_perm = perm;
   const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
-  if (se && !any_star && !any_inv && !scan_on && !part_eligible && stream_chunks > 1) {
+  if (se && !any_star && !any_inv && !part_eligible && stream_chunks > 1) {
     for (Segment* s : P->segs) {
       P->tile_bound += (s->num_docs + kTileDocs - 1) / kTileDocs;
       for (int l = 0; l < P->num_leaves; ++l) {
@@ -2039,11 +2014,69 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   return 0;
 }
 
+// ---- query deadlines (BaseCombineOperator.java:79-132: the combine waits until QueryContext.getEndTimeMs and then
+// returns a timeout block; GroupByCombineOperator.java:193-203 for group-by).  The persistent scans compare the
+// device wall clock against the deadline converted to clock ticks and stop taking tiles past it.
+double epoch_us() {
+  return (double)std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+// Device clock ticks at host epoch time end_ms, never earlier than the true reading (the calibration pairs a clock
+// value with a host time taken before the kernel that read it, so queueing delay only makes deadlines later).
+int deadline_ticks(pgpu_table_s* t, int64_t end_ms, uint64_t* out) {
+  std::lock_guard<std::mutex> g(t->clock_mu);
+  if (!t->clock_stream) {
+    int khz = 0;
+    HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device));
+    if (khz <= 0) return fail(PGPU_ERR_DEVICE, "device wall clock rate unavailable");
+    t->clock_rate_khz = khz;
+    HIP_TRY(hipStreamCreateWithFlags(&t->clock_stream, hipStreamNonBlocking));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&t->clock_pinned), 64, hipHostMallocDefault));
+  }
+  const double steady = now_us();
+  if (t->clock_steady_us < 0 || steady - t->clock_steady_us > 10e6) {
+    double best = 1e300;
+    for (int i = 0; i < 3 && best > 200.0; ++i) {  // the tightest of up to 3 readings
+      const double h0 = epoch_us();
+      if (launch_read_clock(t->clock_pinned, t->clock_stream))
+        return fail(PGPU_ERR_DEVICE, "clock read launch failed: %s", hipGetErrorString(hipGetLastError()));
+      HIP_TRY(hipStreamSynchronize(t->clock_stream));
+      const double h1 = epoch_us();
+      if (h1 - h0 < best) {
+        best = h1 - h0;
+        t->clock_host_us = h0;
+        t->clock_ticks = *reinterpret_cast<volatile uint64_t*>(t->clock_pinned);
+      }
+    }
+    t->clock_steady_us = steady;
+  }
+  const double dt_us = (double)end_ms * 1000.0 - t->clock_host_us;
+  *out = t->clock_ticks + (dt_us > 0 ? (uint64_t)(dt_us * t->clock_rate_khz / 1000.0) : 0);
+  if (*out == 0) *out = 1;
+  return 0;
+}
+
+// The combine's timeout: aggregation-only plans report BaseCombineOperator's EXECUTION_TIMEOUT_ERROR (250),
+// group-by plans GroupByCombineOperator's QUERY_EXECUTION_ERROR (200) wrapping a TimeoutException.
+int timeout_fail(const pgpu_plan_s* P) {
+  if (P->key_cols.empty())
+    return fail(PGPU_ERR_TIMEOUT, "QueryException 250 (EXECUTION_TIMEOUT_ERROR): Timed out while polling results block");
+  return fail(PGPU_ERR_TIMEOUT, "QueryException 200 (QUERY_EXECUTION_ERROR): Timed out while combining group-by results "
+              "after %lldms", (long long)(P->end_time_ms - P->exec_start_ms));
+}
+
 // ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
 // (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X) {
   X.t_start = trace_on() ? now_us() : 0;
+  uint64_t deadline = 0;
+  if (P->end_time_ms > 0) {  // past the end time already: nothing is launched
+    P->exec_start_ms = (int64_t)(epoch_us() / 1000.0);
+    if (P->exec_start_ms >= P->end_time_ms) return timeout_fail(P);
+    TRY(deadline_ticks(P->table, P->end_time_ms, &deadline));
+  }
   Scratch* sc = P->scratch;
   X.nslots = (int)P->slot_kind.size();
   const int nslots = X.nslots;
@@ -2089,6 +2122,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   P->d_table_used = table;
   KParams& kp = X.kp;
   memset(&kp, 0, sizeof kp);
+  kp.deadline = deadline;
   kp.seg_stride = P->seg_stride;
   kp.num_cols = (int)P->query_cols.size();
   kp.num_ops = (int)P->ops.size();
@@ -2127,11 +2161,6 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     kp.table = table;
   }
   TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
-  kp.num_stage = (int)P->stage_slot.size();
-  for (size_t k = 0; k < P->stage_slot.size() && k < (size_t)kMaxStage; ++k) kp.stage_col[k] = P->stage_slot[k];
-  for (size_t l = 0; l < P->leaf_stage.size(); ++l) kp.leaf_stage[l] = P->leaf_stage[l];
-  kp.stage_words = (int32_t)P->stage_words;
-  kp.lds_table_words = P->lds_table_words;
   P->launches_done = 0;
   return 0;
 }
@@ -2218,8 +2247,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
-    const int rc = P->staged ? launch_scan(kp, P->mode, grid, P->lds_bytes, stream)
-                             : launch_filter_groupby(kp, P->mode, P->dense, grid, P->lds_bytes, stream);
+    const int rc = launch_filter_groupby(kp, P->mode, P->dense, grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
@@ -2276,6 +2304,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     sp.slab = P->mode == MODE_LDS ? kp.slab + X.slabs_used * words : nullptr;
     sp.hash_keys = kp.hash_keys;
     sp.stats = kp.stats;
+    sp.deadline = kp.deadline;
     sp.cache_ints = P->star_cache_ints;
     for (int b = 0; b < P->star_batches; ++b) {  // kStarMaxSegs segments per launch, slabs back to back
       const int s0 = b * kStarMaxSegs;
@@ -2363,9 +2392,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
+    if (st[words + 5]) return timeout_fail(P);
     matched = st[words];
     star_scanned = st[words + 1] + st[words + 2];
     P->star_docs_read = (int64_t)st[words + 3];
@@ -2394,9 +2424,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
+    if (st[6]) return timeout_fail(P);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
@@ -2424,9 +2455,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 32, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     t_sync1 = trace_on() ? now_us() : 0;
+    if (st[6]) return timeout_fail(P);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
@@ -2809,6 +2841,8 @@ int pgpu_table_destroy(pgpu_table t) {
   if (t->d_docid_fwd) hipFree(t->d_docid_fwd);
   if (t->d_docid_key) hipFree(t->d_docid_key);
   for (void* p : t->retired) hipFree(p);
+  if (t->clock_stream) hipStreamDestroy(t->clock_stream);
+  if (t->clock_pinned) hipHostFree(t->clock_pinned);
   hipStreamDestroy(t->stream);
   delete t;
   return 0;
@@ -3360,6 +3394,7 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
       TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
       if (cache) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
     }
+    P->end_time_ms = q->end_time_ms;
     P->scratch = acquire_scratch(t);
   }
   *out = P.release();
@@ -3401,6 +3436,7 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   se.d_table = d_table;
   const bool cache = plan_cache_enabled(q);
   const bool hit = cache && plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get());
+  P->end_time_ms = q->end_time_ms;
   P->scratch = acquire_scratch(t);  // before plan_create_impl takes the table lock (acquire_scratch locks it too)
   int rc = 0;
   if (!hit) {

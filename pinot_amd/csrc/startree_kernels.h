@@ -302,6 +302,10 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
   for (; seg < p.num_segs && segpre[seg] < ghi; ++seg) {
     const int64_t lo = max(glo, segpre[seg]) - segpre[seg], hi = min(ghi, segpre[seg + 1]) - segpre[seg];
     if (lo >= hi) continue;  // workgroup-uniform
+    if (p.deadline && __syncthreads_or(past_deadline(p.deadline))) {  // uniform: the segment loop has barriers
+      if (tid == 0) flag_timeout(p.stats);
+      break;
+    }
     const KStarSeg& S = p.segs[seg];
     const int nr = S.out[0], rem = S.out[1];
     const bool ranges_lds = nr <= p.range_cache;
@@ -352,6 +356,10 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
       next = a + 1 < nr ? pre(a + 1) : INT64_MAX;
     }
     for (int64_t base = lo; base < hi; base += BLOCK) {
+      if ((((base - lo) / BLOCK) & 15) == 15 && past_deadline(p.deadline)) {
+        if ((tid & 63) == 0) flag_timeout(p.stats);
+        break;  // per wave: no barrier inside this loop
+      }
       const int64_t pos = base + tid;
       uint32_t mask = 0;
       int64_t g = 0;

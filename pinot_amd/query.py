@@ -12,6 +12,7 @@ per column type by the dictionary lookup, exactly as PredicateUtils.getStoredVal
 """
 import ctypes
 import re
+import time
 
 from . import _lib as L
 
@@ -116,6 +117,14 @@ class QueryContext:
         self.limit = limit
         self.min_server_group_trim_size = min_server_group_trim_size
         self.group_trim_threshold = group_trim_threshold
+        # QueryContext.getEndTimeMs: absolute deadline (ms since the epoch), 0 = none (set_timeout)
+        self.end_time_ms = 0
+
+    def set_timeout(self, timeout_ms):
+        """End time = now + timeout_ms (the broker's arrival time + queryOptions timeoutMs,
+        QueryContext.setEndTimeMs); None clears it.  Past it the GPU path raises QueryTimeoutError."""
+        self.end_time_ms = 0 if timeout_ms is None else int(time.time() * 1000) + int(timeout_ms)
+        return self
 
     def expr_ref(self, expr):
         """(kind, index) of a SELECT / ORDER BY expression over the result: (0, group-by position) or
@@ -177,6 +186,7 @@ class QueryContext:
         if cache is not None and cache[0] is column_index and cache[1] == self.num_groups_limit:
             q, keep = cache[2], cache[3]
             q.options = self._options()
+            q.end_time_ms = getattr(self, "end_time_ms", 0)
             return q, keep
         q, keep = self._build_c(column_index)
         self._c_cache = (column_index, self.num_groups_limit, q, keep)
@@ -224,6 +234,7 @@ class QueryContext:
         q.aggs = ac
         q.num_groups_limit = self.num_groups_limit
         q.options = self._options()
+        q.end_time_ms = getattr(self, "end_time_ms", 0)
         keep += [pc, oc, gb, ac]
         return q, keep
 

@@ -1,0 +1,102 @@
+"""Query deadlines on the GPU path (QueryContext.getEndTimeMs): the combine gives up at the end time and reports a
+timeout instead of a result (BaseCombineOperator.java:193-203 for aggregation-only, GroupByCombineOperator.java:
+193-203 for group-by).  Here: a deadline already past launches nothing; a deadline that passes while the persistent
+scan runs stops it early (the call returns well before the scan would have finished); a generous deadline changes
+nothing; the table stays usable after a timeout."""
+import time
+
+import pytest
+
+from pinot_amd import _lib as L
+from pinot_amd.executor import GpuTable
+from pinot_amd.query import FilterContext, Predicate, QueryContext
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = [("a", "INT"), ("b", "INT"), ("m", "INT"), ("c", "INT")]
+GEN = [{"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 100_000},
+       {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 100_000},
+       {"kind": "UNIFORM", "column_index": 2, "lo": 0, "hi": 1000},
+       {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 100}]
+DOCS = 1_000_000
+
+
+@pytest.fixture(scope="module")
+def table():
+    t = GpuTable(SCHEMA, device=0)
+    handles = [t.generate_segment(GEN, row0=i * DOCS, num_docs=DOCS) for i in range(48)]
+    yield t, handles
+    t.close()
+
+
+def _agg_query():
+    return QueryContext([], [("COUNT", "*"), ("SUM", "m"), ("MAX", "a")],
+                        filter=FilterContext.pred(Predicate.range("b", "1000", "89999")))
+
+
+def _hash_query():
+    # GROUP BY a, b: 10^10 keys -> the open-addressing hash table, one global atomic per doc (a slow scan)
+    return QueryContext(["a", "b"], [("COUNT", "*"), ("SUM", "m")], num_groups_limit=0)
+
+
+def test_deadline_already_past(table):
+    t, handles = table
+    q = _agg_query()
+    q.end_time_ms = int(time.time() * 1000) - 5
+    with pytest.raises(L.QueryTimeoutError) as e:
+        t.execute_groupby(handles, q)
+    assert "250" in e.value.message and "Timed out while polling results block" in e.value.message
+    g = QueryContext(["m"], [("COUNT", "*")])
+    g.end_time_ms = int(time.time() * 1000) - 5
+    with pytest.raises(L.QueryTimeoutError) as e:
+        t.execute_groupby(handles, g)
+    assert "Timed out while combining group-by results" in e.value.message
+
+
+def test_generous_deadline_same_result(table):
+    t, handles = table
+    base = t.execute_aggregation(handles, _agg_query())
+    q = _agg_query().set_timeout(60_000)
+    got = t.execute_aggregation(handles, q)
+    assert got.values == base.values
+    assert got.stats.as_tuple() == base.stats.as_tuple()
+    assert base.stats.num_docs_scanned > 0
+
+
+def test_deadline_stops_running_scan(table):
+    t, handles = table
+    q = _hash_query()
+    with t.plan(handles, q) as p:  # device time of the whole scan, no finalize (tens of millions of groups)
+        p.execute()
+        full_us = p.timing_us()[1]
+    if full_us < 20_000:
+        pytest.skip("scan too short (%.0f us) to cut on this device" % full_us)
+    budget_ms = max(2, int(full_us / 1000 / 10))
+    q.set_timeout(budget_ms)
+    t0 = time.perf_counter()
+    with pytest.raises(L.QueryTimeoutError):
+        with t.plan(handles, q) as p:
+            p.execute()
+            p.finalize()
+    elapsed_ms = (time.perf_counter() - t0) * 1000
+    # stopped within the budget plus one 8-tile step and the plan / sync overheads, far before the full scan
+    assert elapsed_ms < budget_ms + 0.5 * full_us / 1000, (elapsed_ms, budget_ms, full_us)
+    # the table and its scratch stay usable
+    after = t.execute_aggregation(handles, _agg_query())
+    assert after.values == t.execute_aggregation(handles, _agg_query()).values
+
+
+def test_deadline_partitioned_and_streamed(table):
+    t, handles = table
+    # GROUP BY a, c: 10^7 keys x 2 slots = a 160 MB dense table -> the partitioned group-by (K8a..K8d)
+    q = QueryContext(["a", "c"], [("COUNT", "*"), ("SUM", "m")], num_groups_limit=0,
+                     filter=FilterContext.pred(Predicate.range("m", "0", "499")))
+    q.end_time_ms = int(time.time() * 1000) - 1
+    with pytest.raises(L.QueryTimeoutError):
+        t.execute_groupby(handles, q)
+    with pytest.raises(L.QueryTimeoutError):
+        with t.plan_execute(handles, q) as p:
+            p.finalize()
+    q.end_time_ms = 0
+    r = t.execute_groupby(handles[:2], q)
+    assert len(r) > 0

@@ -407,8 +407,23 @@ int pgpu_startree_build(const pgpu_segment_desc* segment, const int32_t* column_
                         int32_t num_dims, const int32_t* skip_star_dims, int32_t num_skip, const pgpu_agg* pairs,
                         int32_t num_pairs, int32_t max_leaf_records, pgpu_startree* out);
 int pgpu_startree_get_desc(pgpu_startree st, pgpu_startree_desc* out);
+/* Star-tree `star_tree_id` of a segment from Pinot's own files, as StarTreeLoaderUtils.loadStarTreeV2 reads them
+ * (seglocal/startree/v2/store/StarTreeLoaderUtils.java:57-107): `index` is the segment's star_tree_index file (v1;
+ * in a v3 segment the star-tree buffer of columns.psf), `index_map` the text of star_tree_index_map
+ * (StarTreeIndexMapUtils.java:150-190: "<id>.<column>.<STAR_TREE|FORWARD_INDEX>.<OFFSET|SIZE> = n").  The
+ * OffHeapStarTree buffer is validated as its constructor does (magic 0xBADDA55B00DAD00D, version 1, header length,
+ * buffer size; OffHeapStarTree.java:45-80); its dimension names (the split order) are matched against
+ * column_names (the table's columns); dimension forward indexes are FixedBitSVForwardIndexReaderV2 bytes with the
+ * segment column's bits_per_element[column]; each "<fn>__<col>" pair's raw PASS_THROUGH chunk forward index
+ * (versions 2 / 3) is decoded -- COUNT as LONG, SUM / MIN / MAX as DOUBLE (FixedByteChunkSVForwardIndexReader),
+ * AVG as AvgPair bytes (VarByteChunkSVForwardIndexReader) -- and pairs of other functions are skipped.  num_docs is
+ * the star-tree's total docs (metadata startree.v2.<id>.total.docs).  Pure host code; attach the result with
+ * pgpu_startree_get_desc + pgpu_attach_startree, release it with pgpu_startree_destroy. */
+int pgpu_startree_load(const void* index, int64_t index_len, const char* index_map, int64_t index_map_len,
+                       int32_t star_tree_id, int32_t num_docs, int32_t num_columns, const char* const* column_names,
+                       const int32_t* bits_per_element, pgpu_startree* out);
 /* Number of star-tree records that come straight from the segment (sorted + aggregated rows), before the star-node
- * and aggregated documents. */
+ * and aggregated documents (-1 for star-trees read by pgpu_startree_load: the files do not record it). */
 int pgpu_startree_num_raw_records(pgpu_startree st, int32_t* n);
 int pgpu_startree_destroy(pgpu_startree st);
 

@@ -156,6 +156,8 @@ _PROTOS = {
     "pgpu_build_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32, c_voidp, c_i64, c_i64p]),
     "pgpu_startree_build": (c_int, [ctypes.POINTER(SegmentDesc), c_i32p, c_i32p, c_i32, c_i32p, c_i32,
                                     ctypes.POINTER(AggC), c_i32, c_i32, ctypes.POINTER(c_voidp)]),
+    "pgpu_startree_load": (c_int, [c_voidp, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32, c_char_pp, c_i32p,
+                                   ctypes.POINTER(c_voidp)]),
     "pgpu_startree_get_desc": (c_int, [c_voidp, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_startree_num_raw_records": (c_int, [c_voidp, c_i32p]),
     "pgpu_startree_destroy": (c_int, [c_voidp]),

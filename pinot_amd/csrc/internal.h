@@ -215,7 +215,10 @@ int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, i
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
 int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                       unsigned long long* hash_keys, void* stream);
-int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg, void* stream);
+// Also the deadline gate of the scan launch that follows it: sets stats[5] when `deadline` (wall_clock64 ticks,
+// 0 = none) has passed.
+int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg,
+                        uint64_t deadline, unsigned long long* stats, void* stream);
 int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream);
 // Resident workgroups per CU of the direct kernel instance (< 0: query failed).
 int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes);
@@ -245,7 +248,8 @@ int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, 
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream);
 constexpr int kStarMaxSegs = 4096;  // star-tree segments per K6 launch (their group prefix lives in LDS)
-int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, void* stream);
+int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, uint64_t deadline,
+                             unsigned long long* stats, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);
 // Synthetic generator (bench): positions of generated values in the sorted domain + presence bitmap, then pack.
 int launch_gen_positions(int32_t kind, uint64_t seed, int64_t lo, int64_t span, const double* cdf,

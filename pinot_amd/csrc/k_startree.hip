@@ -19,10 +19,11 @@ int PGPU_CAT(launch_startree_scan_mode, PGPU_MODE)(const KStarParams& p, size_t 
 }
 
 #if PGPU_MODE == 0
-int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, void* stream) {
+int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, uint64_t deadline,
+                             unsigned long long* stats, void* stream) {
   if (num_segs <= 0) return 0;
   hipLaunchKernelGGL(startree_traverse_kernel, dim3(num_segs), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     segs, seg_total);
+                     segs, seg_total, deadline, stats);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif

@@ -68,9 +68,12 @@ __global__ void __launch_bounds__(256) inv_materialize_kernel(const KBitBlock* _
   }
 }
 
-// tile -> segment map of a plan (one workgroup per segment record).
+// tile -> segment map of a plan (one workgroup per segment record); also the deadline gate of the scan launch
+// that follows (the scan kernels read stats[5] instead of the clock).
 __global__ void expand_tiles_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride, int32_t num_segs,
-                                    int32_t* __restrict__ tile_seg) {
+                                    int32_t* __restrict__ tile_seg, uint64_t deadline,
+                                    unsigned long long* __restrict__ stats) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && past_deadline(deadline)) flag_timeout(stats);
   for (int s = blockIdx.x; s < num_segs; s += gridDim.x) {
     const KSegHdr* h = reinterpret_cast<const KSegHdr*>(segs + (int64_t)s * seg_stride);
     for (int i = threadIdx.x; i < h->num_tiles; i += blockDim.x) tile_seg[h->tile_base + i] = s;
@@ -443,10 +446,11 @@ int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes) {
   }
 }
 
-int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg, void* stream) {
+int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg,
+                        uint64_t deadline, unsigned long long* stats, void* stream) {
   if (num_segs <= 0) return 0;
   hipLaunchKernelGGL(expand_tiles_kernel, dim3(num_segs < 4096 ? num_segs : 4096), dim3(128), 0, S(stream), segs,
-                     seg_stride, num_segs, tile_seg);
+                     seg_stride, num_segs, tile_seg, deadline, stats);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

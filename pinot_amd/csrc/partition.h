@@ -116,9 +116,10 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   const int tid = threadIdx.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
   uint32_t* stack = hist + ((pp.num_parts + 3) & ~3);
-  // Deadline: only K8a tests the clock.  K8c must scatter exactly the docs K8a counted (its cursors run inside
-  // K8a's reservations), so it runs in full or -- once K8a flagged the timeout -- not at all, like K8e / K8d.
-  if (SCATTER && p.deadline && p.stats[5]) return;
+  // Deadline: the flag expand_tiles_kernel set when the query's end time had passed before this launch.  Every
+  // pass reads it at its start and it cannot change while they run, so K8c scatters exactly the docs K8a counted
+  // (its cursors run inside K8a's reservations) or nothing, like K8e / K8d.
+  if (p.deadline && p.stats[5]) return;
   if (SCATTER) {
     for (int c = tid; c < pp.num_coarse; c += kBlock)
       hist[c] = pp.part_start[c << pp.cshift] + pp.block_off[(int64_t)blockIdx.x * pp.num_coarse + c];
@@ -134,10 +135,6 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   int64_t tile_base = 0;
   int nd = 0;
   for (int64_t t = t0; t < t1; ++t) {
-    if (!SCATTER && ((t - t0) & 3) == 0 && past_deadline(p.deadline)) {
-      if ((tid & 63) == 0) flag_timeout(p.stats);
-      break;  // per wave: no barrier inside the tile loop
-    }
     const int cur = p.tile_seg[t];
     if (cur != seg) {
       seg = cur;

@@ -384,7 +384,13 @@ struct Scratch {
   HostPinned stage, starstage, bitstage, maskstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
+  // A query that timed out returns while its device work may still run (wait_plan): the scratch goes back to the
+  // pool marked abandoned and is not handed out again before `busy` (recorded after that work) has completed.
+  hipEvent_t busy = nullptr;
+  bool abandoned = false;
   void release() {
+    if (busy) { hipEventDestroy(busy); busy = nullptr; }
+    abandoned = false;
     for (auto& e : cev) if (e) hipEventDestroy(e);
     cev.clear();
     docbits.release(); bittasks.release(); bitblocks.release();
@@ -871,9 +877,10 @@ namespace {
 Scratch* acquire_scratch(pgpu_table_s* t) {
   std::lock_guard<std::mutex> g(t->mu);
   for (auto& s : t->scratch_pool)
-    if (s) {
+    if (s && (!s->abandoned || hipEventQuery(s->busy) != hipErrorNotReady)) {
       Scratch* r = s.release();
       s.reset();
+      r->abandoned = false;
       return r;
     }
   return new Scratch();
@@ -2066,6 +2073,39 @@ int timeout_fail(const pgpu_plan_s* P) {
               "after %lldms", (long long)(P->end_time_ms - P->exec_start_ms));
 }
 
+// Leaves the plan's scratch to the device work still queued on `stream` (see Scratch::busy).
+int abandon_scratch(Scratch* sc, hipStream_t stream) {
+  if (!sc) return 0;
+  if (!sc->busy) HIP_TRY(hipEventCreateWithFlags(&sc->busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(sc->busy, stream));
+  sc->abandoned = true;
+  return 0;
+}
+
+// Waits for the plan's work on `stream`.  With an end time the wait gives up at it, as the combine's
+// _blockingQueue.poll(endTimeMs - now) / _operatorLatch.await(timeoutMs) do (BaseCombineOperator.java:193-203,
+// GroupByCombineOperator.java:193-203): the query returns PGPU_ERR_TIMEOUT at its deadline and the device work
+// left running keeps its scratch out of the pool until it completes.
+int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
+  if (P->end_time_ms <= 0 || !P->scratch) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    return 0;
+  }
+  Scratch* sc = P->scratch;
+  if (!sc->busy) HIP_TRY(hipEventCreateWithFlags(&sc->busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(sc->busy, stream));
+  for (int spin = 0;; ++spin) {
+    const hipError_t e = hipEventQuery(sc->busy);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) return fail(PGPU_ERR_DEVICE, "query wait failed: %s", hipGetErrorString(e));
+    if (epoch_us() >= (double)P->end_time_ms * 1000.0) {
+      sc->abandoned = true;
+      return timeout_fail(P);
+    }
+    if (spin >= 32) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 // ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
 // (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
@@ -2205,7 +2245,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->grid, C.num_tiles));
   if (P->mode == MODE_LDS) kp.slab = X.kp.slab + X.slabs_used * X.words;
   if (kp.leap_maps) kp.leap_maps += C.tile_begin * (kBlock / 64);
-  if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>() + C.tile_begin, stream))
+  if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>() + C.tile_begin,
+                                              kp.deadline, kp.stats, stream))
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (c == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   HIP_TRY(hipEventRecord(sc->cev[2 * c], stream));
@@ -2286,7 +2327,8 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     memcpy(sc->starstage.p, recs.data(), recs.size() * sizeof(KStarSeg));
     HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, recs.size() * sizeof(KStarSeg), hipMemcpyHostToDevice,
                            stream));
-    if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), seg_total, stream))
+    if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), seg_total, kp.deadline, kp.stats,
+                                 stream))
       return fail(PGPU_ERR_DEVICE, "star-tree traversal launch failed: %s", hipGetErrorString(hipGetLastError()));
     KStarParams sp;
     memset(&sp, 0, sizeof sp);
@@ -2393,7 +2435,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[words + 5]) return timeout_fail(P);
     matched = st[words];
@@ -2425,7 +2467,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
@@ -2456,7 +2498,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
@@ -2618,7 +2660,7 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
     auto Ri = std::make_unique<pgpu_result_s>();
     int rc = plan_execute_impl(Q, stream, nullptr);
     if (!rc) rc = plan_finalize_impl(Q, stream, nullptr, 0, Q->num_keys, Ri.get());
-    if (rc) hipStreamSynchronize(stream);
+    if (rc && !Q->scratch->abandoned) hipStreamSynchronize(stream);
     release_scratch(t, Q->scratch);
     Q->scratch = nullptr;
     TRY(rc);
@@ -3185,6 +3227,61 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+// The device traversal (K5) and residual scan (K6) index node, child, document and dictionary arrays with the
+// star-tree's own numbers, so a tree read from files is checked here as OffHeapStarTree + StarTreeBuilderUtils
+// guarantee it (BFS order, children contiguous and sorted by value, documents and dictIds in range) instead of
+// being read out of bounds on the device.
+int validate_startree(const pgpu_startree_desc* d, const std::vector<int32_t>& dim_card,
+                      const std::vector<int32_t>& dim_bits) {
+  const int N = d->num_nodes, D = d->num_dims, docs = d->num_docs;
+  auto f = [&](int i, int k) {
+    int32_t v;
+    memcpy(&v, d->nodes + (size_t)i * 28 + (size_t)k * 4, 4);  // little-endian records, as the file holds them
+    return v;
+  };
+  int next_child = 1;
+  for (int i = 0; i < N; ++i) {
+    const int dim = f(i, 0), val = f(i, 1), sd = f(i, 2), ed = f(i, 3), ad = f(i, 4), fc = f(i, 5), lc = f(i, 6);
+    if (i == 0 ? dim != -1 : (dim < 0 || dim >= D))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: dimension id %d", i, dim);
+    if (i > 0 && (val < -1 || val >= dim_card[dim]))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: dimension value %d", i, val);
+    // start / end stay StarTreeNode.ALL (-1) where the builder never sets them (the root: TreeNode defaults)
+    if (!(sd == -1 && ed == -1) && (sd < 0 || sd > ed || ed > docs) || ad < 0 || ad >= docs)
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: documents [%d, %d) / %d of %d", i, sd, ed, ad, docs);
+    if ((fc < 0) != (lc < 0)) return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: child range", i);
+    if (fc < 0) continue;
+    if (fc != next_child || lc < fc || lc >= N || fc <= i)
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: children [%d, %d] out of BFS order", i, fc, lc);
+    const int cd = f(fc, 0);
+    for (int c = fc; c <= lc; ++c)
+      if (f(c, 0) != cd || cd <= dim)
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: child %d dimension %d", i, c, f(c, 0));
+    next_child = lc + 1;
+  }
+  if (next_child != N) return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree: %d nodes unreachable", N - next_child);
+  for (int k = 0; k < D; ++k) {  // every document's dictId within the segment dictionary (PinotDataBitSet.readInt)
+    const uint8_t* b = d->dim_fwd[k];
+    const int bits = dim_bits[k];
+    for (int64_t i = 0; i < docs; ++i) {
+      const int64_t bit = i * bits;
+      uint64_t w = 0;
+      for (int j = 0; j < 5 && (bit >> 3) + j < d->dim_fwd_len[k]; ++j) w |= (uint64_t)b[(bit >> 3) + j] << (32 - 8 * j);
+      const uint32_t v = (uint32_t)((w >> (40 - (bit & 7) - bits)) & ((1ull << bits) - 1));
+      if ((int64_t)v >= dim_card[k])
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree dimension %d: document %lld has dictId %u of %d", k,
+                    (long long)i, v, dim_card[k]);
+    }
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
   if (t) t->version++;
   if (!t || !d) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
@@ -3214,6 +3311,11 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
     st->dim_bits.push_back(bits);
     fwd_words[k] = ((int64_t)d->num_docs + 31) / 32 * bits + kFwdPadWords;  // whole 32-doc groups (K6 decode)
     bytes += ((fwd_words[k] * 4) + 15) & ~int64_t(15);
+  }
+  {
+    std::vector<int32_t> card;
+    for (int c : st->dim_cols) card.push_back(std::max(seg.cols[c].card, 1));
+    TRY(validate_startree(d, card, st->dim_bits));
   }
   for (int m = 0; m < d->num_metrics; ++m) {
     const pgpu_agg a = d->metrics[m];
@@ -3449,7 +3551,9 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   }
   if (rc) {
     if (P->scratch) {
-      hipStreamSynchronize(se.stream);  // no launch of this plan may still use its scratch
+      // no launch of this plan may still use its scratch: wait, or (timeout) leave it to the queued work
+      if (rc == PGPU_ERR_TIMEOUT) abandon_scratch(P->scratch, se.stream);
+      else hipStreamSynchronize(se.stream);
       release_scratch(t, P->scratch);
       P->scratch = nullptr;
     }

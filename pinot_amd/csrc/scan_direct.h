@@ -51,10 +51,7 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
 template <int MODE, bool DENSE>
 #ifndef PGPU_MIN_WAVES
-#define PGPU_MIN_WAVES 4  // the sparse instance at 4 waves/SIMD (<= 128 VGPRs)
-#endif
-#ifndef PGPU_SCAN_DEADLINE
-#define PGPU_SCAN_DEADLINE 1
+#define PGPU_MIN_WAVES 1
 #endif
 __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -69,7 +66,11 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
   // STATS_LEAP2 bytes of this workgroup's tiles, [tile k of the workgroup][wave], after the match queues
   uint8_t* lmaps = reinterpret_cast<uint8_t*>(stack + (p.pure_and ? 0 : kMaxStack * kBlock) + (kBlock / 64) * 2 * kWaveQ);
   int kk = 0;  // tiles of this workgroup so far
-  bool timed_out = false;
+  // The query's end time had passed when the launch came up (expand_tiles_kernel, run just before on the stream,
+  // read the device clock and set stats[5]): take no tile.  No clock read in this kernel -- even one outside the
+  // tile loop changes the sparse instance's register allocation (108 -> 134 VGPRs, one wave less per SIMD; an
+  // in-loop check cost 18% on C3, measured).  A scan already running is abandoned by the host (wait_plan).
+  if (p.deadline && p.stats[5]) return;
 
   if (MODE == MODE_LDS) {
     for (int64_t i = tid; i < table_words; i += kBlock) lds[i] = slot_init(p.slot_kind[i / G]);
@@ -193,14 +194,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
         }
       }
       ++kk;
-      // deadline, every 8th tile: finish this tile, take no more.  The clock read constrains the scheduler: the
-      // sparse instance needs __launch_bounds__ min-waves 4 to stay within 128 VGPRs with it.
-      if (PGPU_SCAN_DEADLINE && (kk & 7) == 0 && past_deadline(p.deadline)) {
-        timed_out = true;
-        t_end = t + 1;
-      }
     }
-    if (timed_out && lane == 0) flag_timeout(p.stats);
     if (qn) flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
     if (p.leap_maps)  // each wave stores its own bytes (tiles of other segments hold don't-care values)
       for (int k = lane; k < kk; k += 64)

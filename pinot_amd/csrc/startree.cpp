@@ -12,9 +12,11 @@
 // insertion order), which fixes the star-tree document order exactly as the reference builder lays it out.
 // Pure host code: no HIP call (the CPU tests build star-trees without a GPU).
 #include <algorithm>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -277,7 +279,272 @@ struct pgpu_startree_s {
   int32_t num_raw_records = 0;                // star-tree records before star-node / aggregated documents
 };
 
+// ---------------------------------------------------------------------------------------- Pinot's star-tree files
+// The star_tree_index file of a segment (StarTreeIndexCombiner.java:55-76: per star-tree the OffHeapStarTree buffer,
+// then each split-order dimension's forward index, then each function-column pair's raw forward index) and its
+// star_tree_index_map properties (StarTreeIndexMapUtils.java:150-190), read as StarTreeLoaderUtils.loadStarTreeV2
+// does (seglocal/startree/v2/store/StarTreeLoaderUtils.java:57-107).
+namespace {
+
+inline uint32_t rd_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+inline uint64_t rd_le64(const uint8_t* p) { return (uint64_t)rd_le32(p) | ((uint64_t)rd_le32(p + 4) << 32); }
+
+struct Span {
+  int64_t off = -1, size = -1;
+};
+
+std::string trim(const std::string& x) {
+  size_t a = 0, b = x.size();
+  while (a < b && (x[a] == ' ' || x[a] == '\t' || x[a] == '\r')) ++a;
+  while (b > a && (x[b - 1] == ' ' || x[b - 1] == '\t' || x[b - 1] == '\r')) --b;
+  return x.substr(a, b - a);
+}
+
+// "<id>.<column>.<STAR_TREE|FORWARD_INDEX>.<OFFSET|SIZE> = <value>" lines of star-tree `id`; the column may hold
+// '.' (StarTreeIndexMapUtils.loadFromFile joins the middle tokens).  Forward indexes come back in file order.
+int parse_index_map(const char* text, int64_t len, int id, Span* tree, std::vector<std::pair<std::string, Span>>* fwd) {
+  std::vector<std::pair<std::string, Span>> cols;
+  const std::string all(text, (size_t)len);
+  size_t pos = 0;
+  while (pos < all.size()) {
+    size_t nl = all.find('\n', pos);
+    if (nl == std::string::npos) nl = all.size();
+    const std::string line = trim(all.substr(pos, nl - pos));
+    pos = nl + 1;
+    if (line.empty() || line[0] == '#' || line[0] == '!') continue;
+    const size_t eq = line.find_first_of("=:");
+    if (eq == std::string::npos) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: bad line '%s'", line.c_str());
+    const std::string key = trim(line.substr(0, eq)), val = trim(line.substr(eq + 1));
+    const size_t d1 = key.find('.'), d3 = key.rfind('.');
+    const size_t d2 = d3 == std::string::npos || d3 == 0 ? std::string::npos : key.rfind('.', d3 - 1);
+    if (d1 == std::string::npos || d2 == std::string::npos || d2 <= d1)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: bad key '%s'", key.c_str());
+    char* end = nullptr;
+    const long tid = strtol(key.c_str(), &end, 10);
+    if (end != key.c_str() + d1) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: bad id in '%s'", key.c_str());
+    if (tid != id) continue;
+    const std::string column = key.substr(d1 + 1, d2 - d1 - 1), type = key.substr(d2 + 1, d3 - d2 - 1);
+    const std::string suffix = key.substr(d3 + 1);
+    errno = 0;
+    const long long v = strtoll(val.c_str(), &end, 10);
+    if (errno || end == val.c_str() || *end || v < 0)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: bad value of '%s'", key.c_str());
+    Span* sp;
+    if (type == "STAR_TREE") {
+      sp = tree;
+    } else if (type == "FORWARD_INDEX") {
+      auto it = std::find_if(cols.begin(), cols.end(), [&](const std::pair<std::string, Span>& e) { return e.first == column; });
+      if (it == cols.end()) {
+        cols.emplace_back(column, Span());
+        it = cols.end() - 1;
+      }
+      sp = &it->second;
+    } else {
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: index type '%s'", type.c_str());
+    }
+    if (suffix == "OFFSET") sp->off = v;
+    else if (suffix == "SIZE") sp->size = v;
+    else return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree index map: suffix '%s'", suffix.c_str());
+  }
+  std::sort(cols.begin(), cols.end(), [](const std::pair<std::string, Span>& a, const std::pair<std::string, Span>& b) {
+    return a.second.off < b.second.off;
+  });
+  *fwd = std::move(cols);
+  return PGPU_OK;
+}
+
+// Header of the chunk forward index (BaseChunkSVForwardIndexReader.java:56-100, versions 2 / 3, PASS_THROUGH):
+// returns the start of the chunk-offset table's end (the data) and the entry size / docs per chunk.
+struct ChunkHeader {
+  int32_t version, num_chunks, per_chunk, entry, total, compression, header_start;
+};
+int read_chunk_header(const uint8_t* b, int64_t n, const std::string& name, ChunkHeader* h) {
+  if (n < 28) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: forward index too short", name.c_str());
+  h->version = (int32_t)rd_be32(b);
+  h->num_chunks = (int32_t)rd_be32(b + 4);
+  h->per_chunk = (int32_t)rd_be32(b + 8);
+  h->entry = (int32_t)rd_be32(b + 12);
+  h->total = (int32_t)rd_be32(b + 16);
+  h->compression = (int32_t)rd_be32(b + 20);
+  h->header_start = (int32_t)rd_be32(b + 24);
+  if (h->version != 2 && h->version != 3)
+    return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree metric %s: raw forward index version %d", name.c_str(), h->version);
+  if (h->compression != 0)
+    return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree metric %s: compressed chunks (type %d)", name.c_str(), h->compression);
+  if (h->num_chunks < 0 || h->per_chunk <= 0 || h->header_start < 28 ||
+      h->header_start + (int64_t)h->num_chunks * (h->version == 2 ? 4 : 8) > n)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: bad raw forward index header", name.c_str());
+  return PGPU_OK;
+}
+
+int64_t chunk_position(const uint8_t* b, const ChunkHeader& h, int c) {
+  const uint8_t* e = b + h.header_start + (int64_t)c * (h.version == 2 ? 4 : 8);
+  return h.version == 2 ? (int64_t)(int32_t)rd_be32(e) : (int64_t)rd_be64(e);
+}
+
+// FixedByteChunkSVForwardIndexReader over PASS_THROUGH chunks: value i at data + i * entry (:30-110).
+int read_fixed_metric(const uint8_t* b, int64_t n, int32_t num_docs, int32_t entry, const std::string& name,
+                      std::vector<uint64_t>* out) {
+  ChunkHeader h;
+  if (int rc = read_chunk_header(b, n, name, &h)) return rc;
+  if (h.entry != entry)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: entry size %d, expected %d", name.c_str(), h.entry, entry);
+  const int64_t data = h.header_start + (int64_t)h.num_chunks * (h.version == 2 ? 4 : 8);
+  if (h.total < num_docs || (int64_t)h.num_chunks * h.per_chunk < num_docs || data + (int64_t)num_docs * entry > n)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: covers fewer than %d documents", name.c_str(), num_docs);
+  out->resize(num_docs);
+  for (int32_t i = 0; i < num_docs; ++i) (*out)[i] = rd_be64(b + data + (int64_t)i * 8);
+  return PGPU_OK;
+}
+
+// VarByteChunkSVForwardIndexReader over PASS_THROUGH chunks (:104-190): per chunk numDocsPerChunk int offsets of
+// its rows, then the bytes; AVG's values are AvgPair.toBytes (double sum, long count; AvgPair.java:53-68).
+int read_avg_metric(const uint8_t* b, int64_t n, int32_t num_docs, const std::string& name, std::vector<double>* sum,
+                    std::vector<int64_t>* cnt) {
+  ChunkHeader h;
+  if (int rc = read_chunk_header(b, n, name, &h)) return rc;
+  if ((int64_t)h.num_chunks * h.per_chunk < num_docs)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: covers fewer than %d documents", name.c_str(), num_docs);
+  sum->resize(num_docs);
+  cnt->resize(num_docs);
+  for (int32_t i = 0; i < num_docs; ++i) {
+    const int c = i / h.per_chunk, r = i % h.per_chunk;
+    const int64_t cs = chunk_position(b, h, c);
+    if (cs < 0 || cs + (int64_t)(r + 1) * 4 > n) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: chunk overrun", name.c_str());
+    const int64_t vs = cs + (int32_t)rd_be32(b + cs + (int64_t)r * 4);
+    if (vs < cs || vs + 16 > n)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric %s: value of document %d out of range", name.c_str(), i);
+    const uint64_t u = rd_be64(b + vs);
+    double d;
+    memcpy(&d, &u, 8);
+    (*sum)[i] = d;
+    (*cnt)[i] = (int64_t)rd_be64(b + vs + 8);
+  }
+  return PGPU_OK;
+}
+
+}  // namespace
+
 extern "C" {
+
+int pgpu_startree_load(const void* index, int64_t index_len, const char* index_map, int64_t index_map_len,
+                       int32_t star_tree_id, int32_t num_docs, int32_t num_columns, const char* const* column_names,
+                       const int32_t* bits_per_element, pgpu_startree* out) {
+  if (!index || index_len < 0 || !index_map || index_map_len < 0 || num_docs < 0 || num_columns < 1 || !column_names ||
+      !bits_per_element || !out)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree load arguments");
+  const uint8_t* base = static_cast<const uint8_t*>(index);
+  Span tree;
+  std::vector<std::pair<std::string, Span>> fwd;
+  if (int rc = parse_index_map(index_map, index_map_len, star_tree_id, &tree, &fwd)) return rc;
+  auto in_file = [&](const Span& sp) { return sp.off >= 0 && sp.size >= 0 && sp.off + sp.size <= index_len; };
+  if (!in_file(tree))
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree %d: no STAR_TREE entry inside the index file", star_tree_id);
+  // OffHeapStarTree header, little-endian (OffHeapStarTree.java:45-80; StarTreeBuilderUtils.java:118-171)
+  const uint8_t* tb = base + tree.off;
+  const int64_t tn = tree.size;
+  if (tn < 24 || rd_le64(tb) != 0xBADDA55B00DAD00DULL)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "Invalid magic marker in star-tree data buffer");
+  if (rd_le32(tb + 8) != 1) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "Invalid version in star-tree data buffer");
+  const int64_t root = (int32_t)rd_le32(tb + 12);
+  const int32_t nd = (int32_t)rd_le32(tb + 16);
+  if (nd < 1 || nd > 16) return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree with %d dimensions (1..16)", nd);
+  int64_t off = 20;
+  std::vector<std::string> dims(nd);
+  std::vector<int> seen(nd, 0);
+  for (int i = 0; i < nd; ++i) {
+    if (off + 8 > tn) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree header truncated");
+    const int32_t id = (int32_t)rd_le32(tb + off), nb = (int32_t)rd_le32(tb + off + 4);
+    off += 8;
+    if (id < 0 || id >= nd || seen[id] || nb < 0 || off + nb > tn)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree header: bad dimension entry %d", i);
+    seen[id] = 1;
+    dims[id].assign(reinterpret_cast<const char*>(tb + off), (size_t)nb);
+    off += nb;
+  }
+  if (off + 4 > tn) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree header truncated");
+  const int32_t num_nodes = (int32_t)rd_le32(tb + off);
+  off += 4;
+  if (off != root) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "Error loading star-tree, header length mis-match");
+  if (num_nodes < 1 || off + (int64_t)num_nodes * 28 != tn)
+    return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "Error loading star-tree, buffer size mis-match");
+  auto st = std::make_unique<pgpu_startree_s>();
+  st->num_docs = num_docs;
+  st->nodes.assign(tb + off, tb + tn);
+  // dimensions: split order = header order; forward indexes BIG_ENDIAN fixed-bit with the segment column's bits
+  for (int i = 0; i < nd; ++i) {
+    int col = -1;
+    for (int c = 0; c < num_columns; ++c)
+      if (column_names[c] && dims[i] == column_names[c]) col = c;
+    if (col < 0) return pgpu::host_fail(PGPU_ERR_NOT_FOUND, "star-tree dimension '%s' is not a table column", dims[i].c_str());
+    auto it = std::find_if(fwd.begin(), fwd.end(), [&](const std::pair<std::string, Span>& e) { return e.first == dims[i]; });
+    if (it == fwd.end() || !in_file(it->second))
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree dimension '%s': no forward index", dims[i].c_str());
+    const int bits = bits_per_element[col];
+    const int64_t need = ((int64_t)num_docs * bits + 7) / 8;
+    if (bits < 1 || bits > 31 || it->second.size < need)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree dimension '%s': forward index too short", dims[i].c_str());
+    std::vector<uint8_t> buf(base + it->second.off, base + it->second.off + need);
+    buf.resize(need + 16, 0);
+    st->dim_columns.push_back(col);
+    st->dim_bits.push_back(bits);
+    st->dim_fwd_len.push_back(need);
+    st->dim_fwd.push_back(std::move(buf));
+  }
+  // function-column pairs "<fn>__<col>" (AggregationFunctionColumnPair.java:50-66); value types per
+  // ValueAggregatorFactory.getAggregatedValueType: COUNT LONG, SUM / MIN / MAX DOUBLE, AVG BYTES (AvgPair)
+  for (const auto& e : fwd) {
+    if (std::find(dims.begin(), dims.end(), e.first) != dims.end()) continue;
+    const size_t sep = e.first.find("__");
+    if (sep == std::string::npos) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric '%s'", e.first.c_str());
+    const std::string fn = e.first.substr(0, sep), colname = e.first.substr(sep + 2);
+    int f = -1;
+    if (fn == "count") f = PGPU_AGG_COUNT;
+    else if (fn == "sum") f = PGPU_AGG_SUM;
+    else if (fn == "min") f = PGPU_AGG_MIN;
+    else if (fn == "max") f = PGPU_AGG_MAX;
+    else if (fn == "avg") f = PGPU_AGG_AVG;
+    if (f < 0) continue;  // pairs of other functions (distinctCountHLL, percentileEst, ...): never fit a GPU query
+    int col = -1;
+    if (f != PGPU_AGG_COUNT) {
+      for (int c = 0; c < num_columns; ++c)
+        if (column_names[c] && colname == column_names[c]) col = c;
+      if (col < 0) return pgpu::host_fail(PGPU_ERR_NOT_FOUND, "star-tree metric '%s': no such column", e.first.c_str());
+    }
+    if (!in_file(e.second)) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree metric '%s' outside the file", e.first.c_str());
+    const uint8_t* mb = base + e.second.off;
+    std::vector<double> mf;
+    std::vector<int64_t> mc;
+    if (f == PGPU_AGG_AVG) {
+      if (int rc = read_avg_metric(mb, e.second.size, num_docs, e.first, &mf, &mc)) return rc;
+    } else {
+      std::vector<uint64_t> w;
+      if (int rc = read_fixed_metric(mb, e.second.size, num_docs, 8, e.first, &w)) return rc;
+      if (f == PGPU_AGG_COUNT) {
+        mc.resize(num_docs);
+        for (int32_t i = 0; i < num_docs; ++i) mc[i] = (int64_t)w[i];
+      } else {
+        mf.resize(num_docs);
+        for (int32_t i = 0; i < num_docs; ++i) memcpy(&mf[i], &w[i], 8);
+      }
+    }
+    st->metrics.push_back(pgpu_agg{f, col});
+    st->mf.push_back(std::move(mf));
+    st->mc.push_back(std::move(mc));
+  }
+  if (st->metrics.empty())
+    return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree %d has no COUNT / SUM / MIN / MAX / AVG pair", star_tree_id);
+  for (auto& v : st->dim_fwd) st->fwd_ptrs.push_back(v.data());
+  for (size_t m = 0; m < st->metrics.size(); ++m) {
+    st->f_ptrs.push_back(st->mf[m].empty() ? nullptr : st->mf[m].data());
+    st->c_ptrs.push_back(st->mc[m].empty() ? nullptr : st->mc[m].data());
+  }
+  st->num_raw_records = -1;  // not recorded in the files
+  *out = st.release();
+  return PGPU_OK;
+}
 
 int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_types, const int32_t* split_order,
                         int32_t num_dims, const int32_t* skip_star_dims, int32_t num_skip, const pgpu_agg* pairs,

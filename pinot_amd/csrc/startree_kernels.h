@@ -25,7 +25,9 @@ __device__ __forceinline__ int64_t double_key_dev(double d) {  // order-preservi
 
 #if PGPU_MODE == 0  // one definition: the mode-0 object
 __global__ __launch_bounds__(256) void startree_traverse_kernel(const KStarSeg* __restrict__ segs,
-                                                                int64_t* __restrict__ seg_total) {
+                                                                int64_t* __restrict__ seg_total, uint64_t deadline,
+                                                                unsigned long long* __restrict__ stats) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && past_deadline(deadline)) flag_timeout(stats);  // read by K6
   const KStarSeg& S = segs[blockIdx.x];
   __shared__ int cur_n, next_n, nr, rem;
   const int tid = threadIdx.x;
@@ -251,6 +253,7 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   __shared__ int64_t wsum[BLOCK / 64];
   const int tid = threadIdx.x;
+  if (p.deadline && p.stats[5]) return;  // end time passed before the traversal ran (K5 set the flag)
   const int64_t G = p.num_keys_total;
   const int64_t words = MODE == MODE_LDS ? (int64_t)p.num_slots * G : 0;
   if (MODE == MODE_LDS)
@@ -302,10 +305,6 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
   for (; seg < p.num_segs && segpre[seg] < ghi; ++seg) {
     const int64_t lo = max(glo, segpre[seg]) - segpre[seg], hi = min(ghi, segpre[seg + 1]) - segpre[seg];
     if (lo >= hi) continue;  // workgroup-uniform
-    if (p.deadline && __syncthreads_or(past_deadline(p.deadline))) {  // uniform: the segment loop has barriers
-      if (tid == 0) flag_timeout(p.stats);
-      break;
-    }
     const KStarSeg& S = p.segs[seg];
     const int nr = S.out[0], rem = S.out[1];
     const bool ranges_lds = nr <= p.range_cache;
@@ -356,10 +355,6 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
       next = a + 1 < nr ? pre(a + 1) : INT64_MAX;
     }
     for (int64_t base = lo; base < hi; base += BLOCK) {
-      if ((((base - lo) / BLOCK) & 15) == 15 && past_deadline(p.deadline)) {
-        if ((tid & 63) == 0) flag_timeout(p.stats);
-        break;  // per wave: no barrier inside this loop
-      }
       const int64_t pos = base + tid;
       uint32_t mask = 0;
       int64_t g = 0;

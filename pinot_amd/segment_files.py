@@ -18,6 +18,7 @@
 Host code only; the bytes it yields are what `GpuTable.pin_segment` copies into HBM verbatim.
 """
 import os
+import shutil
 import struct
 
 import numpy as np
@@ -268,6 +269,9 @@ def convert_v1_to_v3(path):
                 offset += len(c.inv_bytes) + len(marker)
     with open(os.path.join(v3, INDEX_MAP_FILE_NAME), "w") as f:
         f.write("\n".join(index_map) + "\n")
+    for star in ("star_tree_index", "star_tree_index_map"):  # copyStarTreeV2 (SegmentV1V2ToV3FormatConverter:182-190)
+        if os.path.exists(os.path.join(path, star)):
+            shutil.copyfile(os.path.join(path, star), os.path.join(v3, star))
     with open(os.path.join(path, METADATA_FILE_NAME)) as f:
         meta = [ln for ln in f.read().splitlines() if not ln.startswith("segment.index.version")]
     with open(os.path.join(v3, METADATA_FILE_NAME), "w") as f:

@@ -90,3 +90,51 @@ def test_startree_empty_match(oracle, c4_gpu):
     q = parse_query("SELECT COUNT(*) FROM t WHERE d3 = 2 AND d3 = 3 GROUP BY d1", num_groups_limit=10 ** 9)
     got = t.execute_groupby(hs, q)
     assert len(got) == 0 and got.stats.num_docs_scanned == 0
+
+
+def test_startree_from_pinot_files(oracle, c4_gpu, tmp_path):
+    """A segment directory with Pinot's star-tree files (v1 -> v3), pinned and its star-tree loaded from the files
+    alone (pgpu_startree_load + pgpu_attach_startree): same answers as the oracle's scan of the raw segment."""
+    from pinot_amd import segment_files as SF
+    from pinot_amd.startree import load_star_trees, write_star_tree_files
+    segs, stars, _, _ = c4_gpu
+    rng = np.random.default_rng(77)
+    cols = SC.c4_columns(rng, 33333, cards=(40, 15, 8, 6))
+    path = str(tmp_path / "seg")
+    seg = SF.write_v1_segment_dir(path, SC.C4_SCHEMA, cols)
+    bits = {n: seg.columns[n].bits_per_element for n, _ in SC.C4_SCHEMA}
+    write_star_tree_files(path, [StarTree.build(SC.C4_SCHEMA, seg, SC.C4_SPLIT, SC.C4_PAIRS, max_leaf_records=250)],
+                          bits, 250)
+    v3 = SF.convert_v1_to_v3(path)
+    loaded = SF.load_segment_dir(path)
+    trees = load_star_trees(v3, SC.C4_SCHEMA, bits)
+    t = GpuTable(SC.C4_SCHEMA)
+    try:
+        h = t.pin_segment(loaded)
+        t.attach_startree(h, trees[0])
+        for sql in SC.C4_QUERIES:
+            q = parse_query(sql, num_groups_limit=10 ** 9)
+            got = t.execute_groupby([h], q)
+            _check(got, oracle.run_groupby(SC.C4_SCHEMA, [loaded], q).groups, q)
+    finally:
+        t.close()
+
+
+def test_startree_malformed_nodes_rejected(c4_gpu):
+    """The attach validates the node array and the documents' dictIds before anything reaches the device."""
+    import ctypes
+    from pinot_amd import _lib as L
+    segs, stars, t, hs = c4_gpu
+    a = stars[0].arrays()
+    for field, value in ((5, 10 ** 6), (0, 99), (3, a["num_docs"] + 5), (4, -1)):
+        d = stars[0].desc()
+        nodes = a["nodes"].copy()
+        nodes[min(1, len(nodes) - 1), field] = value
+        buf = np.ascontiguousarray(nodes, dtype="<i4")
+        d.nodes = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        with pytest.raises(L.PinotGpuError) as e:
+            L.check(t.lib.pgpu_attach_startree(t.handle, hs[0], ctypes.byref(d)))
+        assert e.value.code == L.PGPU_ERR_INVALID_ARGUMENT
+    # the segment's original star-tree is still attached and answers
+    q = parse_query(SC.C4_QUERIES[0], num_groups_limit=10 ** 9)
+    assert len(t.execute_groupby(hs[:1], q)) > 0

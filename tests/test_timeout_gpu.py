@@ -25,7 +25,7 @@ DOCS = 1_000_000
 @pytest.fixture(scope="module")
 def table():
     t = GpuTable(SCHEMA, device=0)
-    handles = [t.generate_segment(GEN, row0=i * DOCS, num_docs=DOCS) for i in range(48)]
+    handles = [t.generate_segment(GEN, row0=i * DOCS, num_docs=DOCS) for i in range(96)]
     yield t, handles
     t.close()
 
@@ -70,9 +70,8 @@ def test_deadline_stops_running_scan(table):
     with t.plan(handles, q) as p:  # device time of the whole scan, no finalize (tens of millions of groups)
         p.execute()
         full_us = p.timing_us()[1]
-    if full_us < 20_000:
-        pytest.skip("scan too short (%.0f us) to cut on this device" % full_us)
-    budget_ms = max(2, int(full_us / 1000 / 10))
+    assert full_us > 4_000, "the hash-table scan of %d docs took only %.0f us" % (len(handles) * DOCS, full_us)
+    budget_ms = max(1, int(full_us / 1000 / 8))
     q.set_timeout(budget_ms)
     t0 = time.perf_counter()
     with pytest.raises(L.QueryTimeoutError):
@@ -81,7 +80,7 @@ def test_deadline_stops_running_scan(table):
             p.finalize()
     elapsed_ms = (time.perf_counter() - t0) * 1000
     # returned at the deadline (plus planning and the wait's polling), far before the full scan
-    assert elapsed_ms < budget_ms + 0.5 * full_us / 1000, (elapsed_ms, budget_ms, full_us)
+    assert elapsed_ms < budget_ms + 0.6 * full_us / 1000, (elapsed_ms, budget_ms, full_us)
     # the table stays usable: the next queries queue behind the abandoned scan on a fresh scratch
     after = t.execute_aggregation(handles, _agg_query())
     assert after.values == t.execute_aggregation(handles, _agg_query()).values

@@ -338,7 +338,12 @@ def main():
         union_dictionaries(table, q.group_by)
     handles = np.array(handles, dtype=np.int64)
 
+    # A real stream for the whole step: the default stream's handle is 0, which the C ABI reads as "the table's own
+    # (non-blocking) stream" -- the collectives (RCCL, or gloo's staged copies) on torch's current stream would then
+    # not be ordered after the scan kernels writing d_table.
+    torch.cuda.set_stream(torch.cuda.Stream())
     stream = torch.cuda.current_stream().cuda_stream
+    assert stream != 0
     probe = table.plan(handles, q)
     nslots, nkeys, kinds = probe.layout()
     probe_nslots = nslots

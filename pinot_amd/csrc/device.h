@@ -384,7 +384,10 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     }
     int32_t g[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) g[b] = gp(S[b].cols[kc].lut)[id[b]];
+    for (int b = 0; b < NB; ++b) {  // the lanes' docs may come from different segments: per-lane select
+      const KCol& c = S[b].cols[kc];
+      g[b] = c.lut ? gp(c.lut)[id[b]] : (int32_t)id[b] + c.lut_off;
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
   }
@@ -417,7 +420,10 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
         for (int b = 0; b < NB; ++b) dval[b] = gp(S[b].cols[col].dval)[id[b]];
       } else {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) ikey[b] = gp(S[b].cols[col].dkey)[id[b]];
+        for (int b = 0; b < NB; ++b) {
+          const KCol& c = S[b].cols[col];
+          ikey[b] = c.dkey ? gp(c.dkey)[id[b]] : c.key_base + (int64_t)id[b];
+        }
       }
     }
     if (G == 1) {  // single row: fold the lane's docs, then the wave
@@ -488,13 +494,18 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
-    gmem<int32_t>* __restrict__ lut = gp(c.lut);
     const int32_t stride = (int32_t)p.key_stride[j];
-    int32_t g[16];
+    if (c.lut) {  // segment-uniform: the whole wave reads one segment here
+      gmem<int32_t>* __restrict__ lut = gp(c.lut);
+      int32_t g[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
+      for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
+      for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) key[i] += ((int32_t)ids[i] + c.lut_off) * stride;
+    }
   }
   // Slots in runs of one column (SUM/MIN/MAX of a column share the decode and the dictionary lookups).
   for (int s = 0; s < p.num_slots;) {
@@ -521,10 +532,15 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     const KCol& c = S.cols[col];
     decode_group<H>(c.fwd, c.bits, group, ids);
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
-      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
       int64_t v[16];
+      if (c.dkey) {
+        gmem<int64_t>* __restrict__ dk = gp(c.dkey);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+        for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? c.key_base + (int64_t)ids[i] : 0;
+      }
       for (int r = s; r < e; ++r) {
         const int kr = p.slot_kind[r];
         if (kr == SLOT_SUM_F64) continue;

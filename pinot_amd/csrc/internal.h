@@ -51,14 +51,18 @@ struct KLeaf {
   const uint32_t* set;
 };
 
-// One query column of one segment.
+// One query column of one segment.  Dictionaries of consecutive values need no lookup: `lut` null = the segment's
+// dictionary is a contiguous run of the table-global one (global dictId = dictId + lut_off); `dkey` null = an
+// INT / LONG dictionary of consecutive values (value = key_base + dictId).  Typical of bounded integer columns
+// (C1, C2, C5's metrics and keys), it saves a dependent gather per matched doc.
 struct KCol {
   const uint32_t* fwd;
   const int32_t* lut;
   const int64_t* dkey;
   const double* dval;
+  int64_t key_base;
   int32_t bits;
-  int32_t pad;
+  int32_t lut_off;
 };
 
 // Per-plan, per-segment record (uploaded once per plan): a KSegHdr followed by num_cols KCol and num_leaves

@@ -45,13 +45,18 @@ __device__ __forceinline__ void part_keys(const KParams& p, const SegView& S, in
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
-    gmem<int32_t>* __restrict__ lut = gp(c.lut);
     const int32_t stride = (int32_t)p.key_stride[j];
-    int32_t g[16];
+    if (c.lut) {
+      gmem<int32_t>* __restrict__ lut = gp(c.lut);
+      int32_t g[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
+      for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
+      for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
+    } else {  // contiguous run of the global dictionary: no lookup
+#pragma unroll
+      for (int i = 0; i < 16; ++i) key[i] += ((int32_t)ids[i] + c.lut_off) * stride;
+    }
   }
 }
 
@@ -87,10 +92,15 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
       for (int i = 0; i < 16; ++i)
         if ((m >> i) & 1u) out[pos[i]] = (uint64_t)__double_as_longlong(v[i]);
     } else {
-      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
       int64_t v[16];
+      if (c.dkey) {
+        gmem<int64_t>* __restrict__ dk = gp(c.dkey);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+        for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? c.key_base + (int64_t)ids[i] : 0;
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         if ((m >> i) & 1u) out[pos[i]] = (uint64_t)v[i];

@@ -335,8 +335,11 @@ struct Column {
   // lazily built device arrays
   int32_t* d_lut = nullptr;
   uint64_t lut_version = ~0ull;
+  int32_t lut_off = -1;             // >= 0: the LUT is lut[i] = lut_off + i (KCol.lut_off)
   int64_t* d_key = nullptr;
   double* d_val = nullptr;
+  bool key_affine = false;          // INT / LONG dictionary of consecutive values: d_key[i] = key_base + i
+  int64_t key_base = 0;
   std::shared_ptr<InvIndex> inv;    // bitmap inverted index, if attached
   // raw (no-dictionary) column: d_key / d_val hold the values per doc (read through the table's identity $docId
   // forward index), raw_min / raw_max bound integer sums
@@ -588,6 +591,8 @@ int ensure_lut(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
   HIP_TRY(hipMemcpyAsync(c.d_lut, lut.data(), sizeof(int32_t) * lut.size(), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   c.lut_version = t->global_version[col];
+  // strictly increasing (both dictionaries sorted), so the ends decide whether it is a contiguous run
+  c.lut_off = c.card > 0 && lut[c.card - 1] - lut[0] == c.card - 1 ? lut[0] : -1;
   return 0;
 }
 
@@ -613,6 +618,11 @@ int ensure_values(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
   HIP_TRY(hipMemcpyAsync(c.d_key, key.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(c.d_val, val.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  if (is_int_type(c.dict.type) && c.card > 0) {  // sorted distinct integers: consecutive iff the ends span card
+    const __int128 span = (__int128)c.dict.iv[c.card - 1] - (__int128)c.dict.iv[0];
+    c.key_affine = span == (__int128)(c.card - 1);
+    c.key_base = c.dict.iv[0];
+  }
   return 0;
 }
 
@@ -1393,6 +1403,12 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C);
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 
+// A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
+bool dict_gathers_forced() {
+  static const bool on = getenv("PGPU_DICT_GATHERS") && getenv("PGPU_DICT_GATHERS")[0] == '1';
+  return on;
+}
+
 int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P,
                      const StreamExec* se = nullptr) {
   if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
@@ -1767,8 +1783,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           continue;
         }
         kc[j].fwd = c.d_fwd;
-        kc[j].lut = c.d_lut;
-        kc[j].dkey = c.d_key;
+        kc[j].lut = c.lut_off >= 0 && !dict_gathers_forced() ? nullptr : c.d_lut;
+        kc[j].lut_off = c.lut_off;
+        kc[j].dkey = c.key_affine && !dict_gathers_forced() ? nullptr : c.d_key;
+        kc[j].key_base = c.key_base;
         kc[j].dval = c.d_val;
         kc[j].bits = c.bits;
       }

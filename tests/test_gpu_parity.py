@@ -427,6 +427,7 @@ def test_finalize_key_range_shards(oracle, gpu_lib):
     t, hs = gpu_table(schema, [seg])
     try:
         q = parse_query("SELECT COUNT(*), SUM(m) FROM t WHERE m < 900 GROUP BY a, b", num_groups_limit=10 ** 6)
+        torch.cuda.set_stream(torch.cuda.Stream())  # a real stream (handle 0 is the table's own to the C ABI)
         stream = torch.cuda.current_stream().cuda_stream
         with t.plan(hs, q) as plan:
             nslots, nkeys, kinds = plan.layout()

@@ -5,9 +5,11 @@ their group-by dictionaries (one key space), plan + execute streams into a calle
 range (large ones, then pgpu_plan_finalize_range per rank), and the merged answer must equal the oracle over the
 union of all segments (GroupByCombineOperator semantics, core/operator/combine/GroupByCombineOperator.java:113-160).
 This is bench.py's step for --gpus N."""
+import datetime
 import json
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -39,7 +41,8 @@ def _segment_columns(seg_index):
 def _worker(rank, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    # a rank that fails must not leave the other waiting in a collective forever
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=60))
     try:
         import _oracle
         from pinot_amd.executor import GpuTable
@@ -48,7 +51,11 @@ def _worker(rank, port, out_dir):
         mine = [rank * SEGS_PER_RANK + i for i in range(SEGS_PER_RANK)]
         handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(s))) for s in mine]
         union_dictionaries(table, ["d", "e"])
+        # a real stream: handle 0 (the default stream) means "the table's own stream" to the C ABI, and the
+        # collectives' copies on torch's stream would not wait for the scan
+        torch.cuda.set_stream(torch.cuda.Stream())
         stream = torch.cuda.current_stream().cuda_stream
+        assert stream != 0
         for name, sql, shard in (("small", SMALL, False), ("large", LARGE, True)):
             q = parse_query(sql, num_groups_limit=10 ** 9)
             probe = table.plan(handles, q)
@@ -84,9 +91,20 @@ def _load(path):
         return {tuple(k): v for k, v in json.load(f)}
 
 
-@pytest.mark.timeout(300)
+def _run_ranks(tmp_path, limit_s=100):
+    ctx = mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=False)
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > limit_s:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail("ranks did not finish within %d s" % limit_s)
+
+
+@pytest.mark.timeout(150)
 def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path):
-    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    _run_ranks(tmp_path)
     segs = [oracle.make_segment(SCHEMA, _segment_columns(s)) for s in range(WORLD * SEGS_PER_RANK)]
     for name, sql, shard in (("small", SMALL, False), ("large", LARGE, True)):
         q = parse_query(sql, num_groups_limit=10 ** 9)
@@ -97,9 +115,10 @@ def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path):
             got = dict(parts[0])
             got.update(parts[1])
         else:  # all-reduce: both ranks hold the whole answer
-            assert parts[0] == parts[1]
+            assert parts[0] == parts[1], "all-reduce left the ranks with different answers"
             got = parts[0]
-        assert set(got) == set(exp), name
+        missing, extra = set(exp) - set(got), set(got) - set(exp)
+        assert not missing and not extra, (name, len(missing), len(extra), sorted(missing)[:5], sorted(extra)[:5])
         for key, vals in exp.items():
             for (fn, col), x, y in zip(q.aggregations, got[key], vals):
                 if col == "md":

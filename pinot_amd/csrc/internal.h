@@ -252,6 +252,7 @@ int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, 
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream);
 constexpr int kStarMaxSegs = 4096;  // star-tree segments per K6 launch (their group prefix lives in LDS)
+int launch_deadline_gate(uint64_t deadline, unsigned long long* stats, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, uint64_t deadline,
                              unsigned long long* stats, void* stream);
 int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void* stream);

@@ -80,6 +80,11 @@ __global__ void expand_tiles_kernel(const uint8_t* __restrict__ segs, int32_t se
   }
 }
 
+// The deadline gate alone (launches from a cached plan's device image, whose tile map needs no expansion).
+__global__ void deadline_gate_kernel(uint64_t deadline, unsigned long long* __restrict__ stats) {
+  if (threadIdx.x == 0 && past_deadline(deadline)) flag_timeout(stats);
+}
+
 // Deterministic fold of the per-workgroup slabs in workgroup order.
 struct SlotKinds {
   int32_t k[kMaxSlots];
@@ -451,6 +456,11 @@ int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_seg
   if (num_segs <= 0) return 0;
   hipLaunchKernelGGL(expand_tiles_kernel, dim3(num_segs < 4096 ? num_segs : 4096), dim3(128), 0, S(stream), segs,
                      seg_stride, num_segs, tile_seg, deadline, stats);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_deadline_gate(uint64_t deadline, unsigned long long* stats, void* stream) {
+  hipLaunchKernelGGL(deadline_gate_kernel, dim3(1), dim3(64), 0, S(stream), deadline, stats);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

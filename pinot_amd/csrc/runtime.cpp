@@ -378,6 +378,23 @@ struct Segment {
   std::unique_ptr<StarTreeDev> star;
 };
 
+// Device copy of a cached plan's launch inputs: the per-segment records (SET pointers patched to its own bitset
+// words) and the tile -> record map.  A repeated query (a cache hit) launches straight from it -- no record upload,
+// no tile expansion -- so its GPU timeline starts with the scan.  The first execution of the cached plan builds it
+// on its stream and records `built`; later executions (any stream) wait on that event.
+struct DeviceImage {
+  std::mutex mu;
+  bool uploaded = false;
+  hipEvent_t built = nullptr;
+  DevBuf segrec, sets, tile_seg;
+  ~DeviceImage() {
+    if (built) hipEventDestroy(built);
+    segrec.release();
+    sets.release();
+    tile_seg.release();
+  }
+};
+
 struct Scratch {
   DevBuf docbits, bittasks, bitblocks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
@@ -391,6 +408,7 @@ struct Scratch {
   // pool marked abandoned and is not handed out again before `busy` (recorded after that work) has completed.
   hipEvent_t busy = nullptr;
   bool abandoned = false;
+  std::shared_ptr<DeviceImage> image;  // the plan image the last execution read (kept while it may still run)
   void release() {
     if (busy) { hipEventDestroy(busy); busy = nullptr; }
     abandoned = false;
@@ -813,6 +831,7 @@ struct pgpu_plan_s {
   std::vector<KBitTask> bit_tasks;        // containers ORed into the docbits by inv_materialize_kernel
   std::vector<KBitBlock> bit_blocks;      // every 65536-doc block of the docbits, with its tasks
   std::vector<std::shared_ptr<InvIndex>> inv_refs;  // inverted indexes the bit tasks point into (kept alive)
+  std::shared_ptr<DeviceImage> image;     // cached plans: device-resident records / tile map (one-launch plans)
   int64_t num_tiles = 0;
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // numEntriesScannedInFilter of the STATS_CONST segments (host)
@@ -1338,6 +1357,11 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
 
 struct ExecCtx {
   KParams kp;
+  // where this execution's records, bitsets and tile map live: the scratch, or the cached plan's DeviceImage
+  uint8_t* segrec = nullptr;
+  uint32_t* sets = nullptr;
+  int32_t* tile_seg = nullptr;
+  bool from_image = false;
   uint64_t* table = nullptr;
   int64_t words = 0;
   int nslots = 0;
@@ -1399,7 +1423,7 @@ bool int_sum_fits(const std::vector<Segment*>& segs, int col) {
 }
 
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X);
-int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C);
+int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, const LaunchChunk& C);
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 
@@ -2001,7 +2025,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         TRY(configure(P->tile_bound));
         TRY(exec_prologue(P, se->stream, se->d_table, stream_chunks, X));
       }
-      TRY(exec_upload_chunk(P, se->stream, L));
+      TRY(exec_upload_chunk(P, se->stream, X, L));
       TRY(exec_launch_chunk(P, se->stream, X, L, c));
     }
     mark();
@@ -2154,6 +2178,45 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
   TRY(sc->stats.ensure(64));
   HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
+  X.segrec = sc->segrec.as<uint8_t>();
+  X.sets = sc->sets.as<uint32_t>();
+  TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
+  X.tile_seg = sc->tile_seg.as<int32_t>();
+  X.from_image = P->image && P->chunks.size() == 1 && P->docbit_words == 0 && !P->set_words_bound && !P->tile_bound;
+  sc->image = X.from_image ? P->image : nullptr;
+  if (X.from_image) {  // build the cached plan's device image once; later executions wait for it
+    DeviceImage& im = *P->image;
+    std::lock_guard<std::mutex> g(im.mu);
+    if (!im.uploaded) {
+      const size_t rn = P->segrec.size(), sn = P->set_words.size() * 4;
+      TRY(im.segrec.ensure(std::max<size_t>(rn, 16)));
+      TRY(im.sets.ensure(std::max<size_t>(sn, 16)));
+      TRY(im.tile_seg.ensure((size_t)std::max<int64_t>(P->num_tiles, 1) * 4));
+      if (!im.built) HIP_TRY(hipEventCreateWithFlags(&im.built, hipEventDisableTiming));
+      uint8_t* stage = reinterpret_cast<uint8_t*>(sc->stage.p);
+      if (rn) memcpy(stage, P->segrec.data(), rn);
+      for (const auto& f : P->set_fix) {
+        const uint32_t* ptr = im.sets.as<uint32_t>() + f.second;
+        memcpy(stage + f.first, &ptr, sizeof ptr);
+      }
+      if (sn) memcpy(stage + rn, P->set_words.data(), sn);
+      if (rn) HIP_TRY(hipMemcpyAsync(im.segrec.p, stage, rn, hipMemcpyHostToDevice, stream));
+      if (sn) HIP_TRY(hipMemcpyAsync(im.sets.p, stage + rn, sn, hipMemcpyHostToDevice, stream));
+      // the plan's scan records (segments its filter prunes or its star-trees answer have none)
+      const int32_t nrec = P->seg_stride > 0 ? (int32_t)(P->segrec.size() / P->seg_stride) : 0;
+      if (nrec > 0 &&
+          launch_expand_tiles(im.segrec.as<uint8_t>(), P->seg_stride, nrec, im.tile_seg.as<int32_t>(), 0,
+                              sc->stats.as<unsigned long long>(), stream))
+        return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
+      HIP_TRY(hipEventRecord(im.built, stream));
+      im.uploaded = true;
+    } else {
+      HIP_TRY(hipStreamWaitEvent(stream, im.built, 0));
+    }
+    X.segrec = im.segrec.as<uint8_t>();
+    X.sets = im.sets.as<uint32_t>();
+    X.tile_seg = im.tile_seg.as<int32_t>();
+  }
   if (P->docbit_words > 0) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
     TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
     TRY(sc->bittasks.ensure(std::max<size_t>(P->bit_tasks.size(), 1) * sizeof(KBitTask)));
@@ -2218,13 +2281,13 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
       return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
     kp.table = table;
   }
-  TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
   P->launches_done = 0;
   return 0;
 }
 
 // Uploads chunk c's records (SET pointers patched to the device bitsets) and its bitset words.
-int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C) {
+int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, const LaunchChunk& C) {
+  if (X.from_image) return 0;  // the cached plan's device image holds the records
   Scratch* sc = P->scratch;
   uint8_t* stage = reinterpret_cast<uint8_t*>(sc->stage.p);
   const size_t r0 = (size_t)C.rec_begin * P->seg_stride, rn = (size_t)C.num_recs * P->seg_stride;
@@ -2256,16 +2319,20 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const LaunchChunk& C) 
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c) {
   Scratch* sc = P->scratch;
   KParams kp = X.kp;
-  kp.segs = sc->segrec.as<uint8_t>() + (size_t)C.rec_begin * P->seg_stride;
+  kp.segs = X.segrec + (size_t)C.rec_begin * P->seg_stride;
   kp.num_segs = (int)C.num_recs;
   kp.num_tiles = (int32_t)C.num_tiles;
-  kp.tile_seg = sc->tile_seg.as<int32_t>() + C.tile_begin;
+  kp.tile_seg = X.tile_seg + C.tile_begin;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->grid, C.num_tiles));
   if (P->mode == MODE_LDS) kp.slab = X.kp.slab + X.slabs_used * X.words;
   if (kp.leap_maps) kp.leap_maps += C.tile_begin * (kBlock / 64);
-  if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, sc->tile_seg.as<int32_t>() + C.tile_begin,
-                                              kp.deadline, kp.stats, stream))
+  if (X.from_image) {  // the tile map is in the image; only the deadline gate remains (and only with a deadline)
+    if (C.num_tiles > 0 && kp.deadline && launch_deadline_gate(kp.deadline, kp.stats, stream))
+      return fail(PGPU_ERR_DEVICE, "gate launch failed: %s", hipGetErrorString(hipGetLastError()));
+  } else if (C.num_recs > 0 && launch_expand_tiles(kp.segs, kp.seg_stride, kp.num_segs, X.tile_seg + C.tile_begin,
+                                                   kp.deadline, kp.stats, stream)) {
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (c == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   HIP_TRY(hipEventRecord(sc->cev[2 * c], stream));
   if (C.num_tiles > 0 && P->partitioned) {
@@ -2340,7 +2407,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
       recs[i].out = recs[i].frontier + 6 * nn;
     }
     for (auto& f : P->star_match_fix)
-      recs[std::get<0>(f)].match[std::get<1>(f)] = sc->sets.as<uint32_t>() + std::get<2>(f);
+      recs[std::get<0>(f)].match[std::get<1>(f)] = X.sets + std::get<2>(f);
     TRY(sc->starstage.ensure(recs.size() * sizeof(KStarSeg)));
     memcpy(sc->starstage.p, recs.data(), recs.size() * sizeof(KStarSeg));
     HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, recs.size() * sizeof(KStarSeg), hipMemcpyHostToDevice,
@@ -2389,7 +2456,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     HIP_TRY(hipMemcpyAsync(sc->mask_jobs.p, sc->maskstage.p, jobs.size() * sizeof(KMaskJob), hipMemcpyHostToDevice,
                            stream));
     KParams mp = kp;
-    mp.segs = sc->segrec.as<uint8_t>();
+    mp.segs = X.segrec;
     if (launch_leaf_masks(mp, sc->mask_jobs.as<KMaskJob>(), (int32_t)jobs.size(), sc->leaf_masks.as<uint32_t>(),
                           stream))
       return fail(PGPU_ERR_DEVICE, "leaf mask launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -2419,7 +2486,7 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
   ExecCtx X;
   TRY(exec_prologue(P, stream, d_table, std::max(nl, 1), X));
   for (int c = 0; c < nl; ++c) {
-    TRY(exec_upload_chunk(P, stream, P->chunks[c]));
+    TRY(exec_upload_chunk(P, stream, X, P->chunks[c]));
     TRY(exec_launch_chunk(P, stream, X, P->chunks[c], c));
   }
   return exec_epilogue(P, stream, X);
@@ -2829,7 +2896,9 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
   return false;
 }
 
-void plan_cache_put(pgpu_table_s* t, const std::string& key, const pgpu_plan_s& P) {
+void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
+  if (P.chunks.size() == 1 && P.docbit_words == 0 && !P.set_words_bound && !P.tile_bound)
+    P.image = std::make_shared<DeviceImage>();  // built by the first execution, shared by every later hit
   auto img = std::make_shared<pgpu_plan_s>(P);
   img->scratch = nullptr;
   std::lock_guard<std::mutex> g(t->cache_mu);
@@ -3268,7 +3337,7 @@ int validate_startree(const pgpu_startree_desc* d, const std::vector<int32_t>& d
     if (i > 0 && (val < -1 || val >= dim_card[dim]))
       return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: dimension value %d", i, val);
     // start / end stay StarTreeNode.ALL (-1) where the builder never sets them (the root: TreeNode defaults)
-    if (!(sd == -1 && ed == -1) && (sd < 0 || sd > ed || ed > docs) || ad < 0 || ad >= docs)
+    if ((!(sd == -1 && ed == -1) && (sd < 0 || sd > ed || ed > docs)) || ad < 0 || ad >= docs)
       return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: documents [%d, %d) / %d of %d", i, sd, ed, ad, docs);
     if ((fc < 0) != (lc < 0)) return fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree node %d: child range", i);
     if (fc < 0) continue;

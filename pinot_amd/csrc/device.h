@@ -374,6 +374,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
   int64_t key[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) key[b] = 0;
+  int st = 0;  // MODE_HASH key stages (key spaces beyond 64 bits)
   for (int j = 0; j < p.num_keys; ++j) {
     const int kc = p.key_col[j];
     uint32_t id[NB];
@@ -390,6 +391,14 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
+    if (MODE == MODE_HASH && st < p.num_stages && j + 1 == p.stage_end[st]) {  // wave-uniform
+      // the group's key -> its slot in stage table st (a dense id), the base of the next group's key
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        key[b] = ok[b] ? hash_slot(p.stage_keys + p.stage_off[st], p.stage_cap[st], (uint64_t)key[b]) * p.stage_mult[st]
+                       : 0;
+      ++st;
+    }
   }
   int64_t idx[NB];
 #pragma unroll

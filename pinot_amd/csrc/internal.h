@@ -22,7 +22,7 @@ constexpr int kTileDocs = kBlock * kDocsPerLane;  // 8192 docs per tile
 constexpr int kMaxQueryCols = 16;           // distinct columns referenced by one query
 constexpr int kMaxLeaves = 16;              // predicate leaves
 constexpr int kMaxOps = 48;                 // postfix filter program length
-constexpr int kMaxKeys = 8;                 // group-by columns handled on the GPU
+constexpr int kMaxKeys = 16;                // group-by columns handled on the GPU
 constexpr int kMaxSlots = 24;               // accumulator rows of the group table
 constexpr int kMaxStack = 8;                // filter evaluation stack depth
 constexpr int kFwdPadWords = 4;
@@ -99,6 +99,16 @@ struct KParams {
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0
+  // Key spaces beyond 64 bits (ArrayMapBasedHolder): the key columns split into consecutive groups; the key of group
+  // s (previous group's slot x stage_mult[s - 1] + the mixed-radix key of its columns, which end at stage_end[s]) is
+  // mapped to its slot in hash table s (stage_cap[s] slots at stage_keys + stage_off[s]); the last group's key is the
+  // group key of the plan's own hash table.  num_stages = 0: one mixed-radix key over all columns.
+  int32_t num_stages;
+  int32_t stage_end[kMaxKeys];
+  int64_t stage_cap[kMaxKeys];
+  int64_t stage_off[kMaxKeys];
+  int64_t stage_mult[kMaxKeys];
+  unsigned long long* stage_keys;
   unsigned long long* stats;      // [0] docs matched, [2] entries scanned in filter (STATS_CHAIN / LEAP2 segments)
   // STATS_LEAP2 segments: per (tile, wave) one byte of AndDocIdIterator state over scans A, B: bit 0 = a doc
   // matches, bit 1 = scanner after the wave's docs (1 = B), bits 2-3 = entry difference at its first match + 1

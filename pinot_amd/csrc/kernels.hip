@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, 
 // AndDocIdIterator.java:40-67): the scan kernel counted every entry assuming each wave-tile is entered with scan A
 // running, and left one byte per (tile, wave) (bit 0: a doc matches, bit 1: scanner after it, bits 2-3: count
 // difference at its first match when entered with B running, + 1).  One wave per segment chains the bytes in doc
-// order from the initial state (scan A at doc 0), 64 at a time: a byte's entry state is the exit of the nearest
+// order from the initial state (scan A at doc 0), 512 at a time (8 per lane): a byte's entry state is the exit of the nearest
 // earlier byte with a match (ballots), or the state carried from the previous 64.
 __global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride,
                                                            int32_t num_segs, const uint8_t* __restrict__ maps,
@@ -294,14 +294,36 @@ __global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __res
   const uint8_t* m = maps + (int64_t)h->tile_base * (kBlock / 64);
   const int64_t n = (int64_t)h->num_tiles * (kBlock / 64);
   long long total = 0;
-  uint32_t carry = 0;  // scanner state entering this batch of 64 (0 = A)
-  for (int64_t base = 0; base < n; base += 64) {
-    const uint32_t w = base + lane < n ? m[base + lane] : 0u;
-    const uint64_t has = __ballot(w & 1u), exb = __ballot((w >> 1) & 1u);
-    const uint64_t below = has & ((1ull << lane) - 1ull);
-    const uint32_t entry = below ? (uint32_t)((exb >> (63 - __builtin_clzll(below))) & 1ull) : carry;
-    if ((w & 1u) && entry) total += (long long)((w >> 2) & 3u) - 1;
-    if (has) carry = (uint32_t)((exb >> (63 - __builtin_clzll(has))) & 1ull);
+  uint32_t carry = 0;  // scanner state entering this batch (0 = A)
+  // 512 bytes per step (a 1M-doc segment's 492 in one): lane l holds bytes [8l, 8l + 8), all loads in flight
+  // together, folded in the lane, then one ballot pass hands each lane the state entering its first match.
+  for (int64_t base = 0; base < n; base += 512) {
+    uint32_t b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = base + 8 * lane + k;
+      b[k] = i < n ? m[i] : 0u;
+    }
+    long long t = 0;
+    int first_diff = 0;
+    bool has = false;
+    uint32_t st = 0;  // exit state of the lane's latest matching byte
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (b[k] & 1u) {
+        const int d = (int)((b[k] >> 2) & 3u) - 1;
+        if (has) t += st ? d : 0;
+        else first_diff = d;
+        st = (b[k] >> 1) & 1u;
+        has = true;
+      }
+    }
+    const uint64_t hasm = __ballot(has), exm = __ballot(has && st);
+    const uint64_t below = hasm & ((1ull << lane) - 1ull);
+    const uint32_t entry = below ? (uint32_t)((exm >> (63 - __builtin_clzll(below))) & 1ull) : carry;
+    if (has && entry) t += first_diff;
+    total += t;
+    if (hasm) carry = (uint32_t)((exm >> (63 - __builtin_clzll(hasm))) & 1ull);
   }
   for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
   if (lane == 0 && total) atomicAdd(stats + 2, (unsigned long long)total);

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -399,6 +400,7 @@ struct Scratch {
   DevBuf docbits, bittasks, bitblocks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
+  DevBuf stage_keys;  // ARRAY_MAP key spaces: the prefix hash table
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
   HostPinned stage, starstage, bitstage, maskstage;
@@ -420,7 +422,7 @@ struct Scratch {
     starstage.release();
     bitstage.release();
     starwork.release();
-    part_start.release(); block_off.release(); rec_key.release(); rec_val.release();
+    part_start.release(); block_off.release(); rec_key.release(); rec_val.release(); stage_keys.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
@@ -873,6 +875,11 @@ struct pgpu_plan_s {
   // pgpu_query.end_time_ms (QueryContext.getEndTimeMs) of the query being run: set per query, not cached
   int64_t end_time_ms = 0;
   int64_t exec_start_ms = 0;
+  // key spaces beyond 64 bits (KParams.num_stages): per stage its end column, table slots, the next group's key
+  // space; stage_space holds every group's key space (the last group's too)
+  std::vector<int32_t> stage_end;
+  std::vector<int64_t> stage_cap, stage_mult, stage_space;
+  unsigned long long* d_stats = nullptr;  // statistics words of the last execution (scratch)
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -1591,7 +1598,43 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     if (!overflow && G > INT64_MAX / card) overflow = true;
     else if (!overflow) G *= card;
   }
-  if (overflow) return fail(PGPU_ERR_UNSUPPORTED, "group key space exceeds 64 bits (ARRAY_MAP holder)");
+  if (overflow) {
+    // ArrayMapBasedHolder (DictionaryBasedGroupKeyGenerator.java:127-137: the cardinality product overflows a long).
+    // The key columns split into consecutive groups whose keys fit 62 bits: group s's key (the previous group's slot x
+    // its own key space + the mixed-radix key of its columns) is mapped on the device to its slot in hash table s --
+    // a dense id below 2^31 -- and the last group's key is the group key of the plan's hash table.  Exact, like the
+    // IntArray map it replaces; the tables are decoded back to dictIds at finalize.
+    const int nk = (int)P->key_cols.size();
+    constexpr int64_t kLim = INT64_C(1) << 62;
+    int64_t docs = 0;
+    for (Segment* s : P->segs) docs += s->num_docs;
+    std::vector<int> ends;
+    std::vector<int64_t> spaces, caps;
+    int64_t capp = 1;  // slots of the previous group's table (1: none)
+    for (int j = 0; j < nk;) {
+      int64_t l = 1;
+      int k = j;
+      while (k < nk && l <= kLim / capp / P->key_card[k]) l *= P->key_card[k++];
+      if (k == j) return fail(PGPU_ERR_UNSUPPORTED, "group key space beyond the staged ARRAY_MAP keys");
+      for (int i = j; i < k; ++i)  // strides restart within each group
+        P->key_stride[i] = i == j ? 1 : P->key_stride[i - 1] * P->key_card[i - 1];
+      ends.push_back(k);
+      spaces.push_back(l);
+      if (k == nk) break;
+      const int64_t want = std::max<int64_t>(2 * std::min<int64_t>(capp * l, std::max<int64_t>(docs, 1)), 1024);
+      int64_t cap = 1;
+      while (cap < want) cap <<= 1;
+      if (cap > (INT64_C(1) << 31)) return fail(PGPU_ERR_UNSUPPORTED, "ARRAY_MAP key stage beyond 2^31 slots");
+      caps.push_back(cap);
+      capp = cap;
+      j = k;
+    }
+    P->stage_end.assign(ends.begin(), ends.end() - 1);
+    P->stage_cap = caps;
+    P->stage_space = spaces;  // per group (the last one included)
+    P->stage_mult.assign(spaces.begin() + 1, spaces.end());
+    G = INT64_C(1) << 40;  // beyond every dense table: the hash table below (no overflow in the sizing products)
+  }
   const int nslots = (int)P->slot_kind.size();
   constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
   // LDS-privatised tables up to 112 KB (one workgroup per CU at the top end): measured on MI355X, an 80 KB table
@@ -1630,7 +1673,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   for (int l = 0; l < P->num_leaves; ++l)
     TRY(parse_predicate(t->types[q->predicates[l].column], q->predicates[l], &parsed[l]));
   std::vector<std::vector<int>> star_comps;
-  const bool star_allowed = q->num_group_by > 0 && !(q->options & PGPU_OPT_NO_STAR_TREE) &&
+  const bool star_allowed = q->num_group_by > 0 && !(q->options & PGPU_OPT_NO_STAR_TREE) && P->stage_end.empty() &&
                             star_composites(P->ops, q, &star_comps);
   // Aggregation-only over a match-all segment: COUNT-only is answered from metadata, MIN/MAX-only from the
   // dictionaries (AggregationPlanNode.java:165-183) -- same values, numEntriesScannedPostFilter 0
@@ -2176,8 +2219,18 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   TRY(sc->segrec.ensure(std::max<size_t>(rec_cap, 16)));
   TRY(sc->stage.ensure(std::max<size_t>(rec_cap + (size_t)std::max<int64_t>(P->set_words_bound,
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
-  TRY(sc->stats.ensure(64));
-  HIP_TRY(hipMemsetAsync(sc->stats.p, 0, 64, stream));
+  // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag): right after the group table when
+  // the table is internal, so finalize reads both with one copy
+  unsigned long long* stats;
+  if (!d_table) {
+    TRY(sc->table.ensure((size_t)X.words * 8 + 64));
+    stats = reinterpret_cast<unsigned long long*>(sc->table.as<uint8_t>() + (size_t)X.words * 8);
+  } else {
+    TRY(sc->stats.ensure(64));
+    stats = sc->stats.as<unsigned long long>();
+  }
+  P->d_stats = stats;
+  HIP_TRY(hipMemsetAsync(stats, 0, 64, stream));
   X.segrec = sc->segrec.as<uint8_t>();
   X.sets = sc->sets.as<uint32_t>();
   TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
@@ -2206,7 +2259,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
       const int32_t nrec = P->seg_stride > 0 ? (int32_t)(P->segrec.size() / P->seg_stride) : 0;
       if (nrec > 0 &&
           launch_expand_tiles(im.segrec.as<uint8_t>(), P->seg_stride, nrec, im.tile_seg.as<int32_t>(), 0,
-                              sc->stats.as<unsigned long long>(), stream))
+                              stats, stream))
         return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
       HIP_TRY(hipEventRecord(im.built, stream));
       im.uploaded = true;
@@ -2234,11 +2287,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
       return fail(PGPU_ERR_DEVICE, "inverted-index materialise launch failed: %s",
                   hipGetErrorString(hipGetLastError()));
   }
-  uint64_t* table = reinterpret_cast<uint64_t*>(d_table);
-  if (!table) {
-    TRY(sc->table.ensure((size_t)X.words * 8));
-    table = sc->table.as<uint64_t>();
-  }
+  uint64_t* table = d_table ? reinterpret_cast<uint64_t*>(d_table) : sc->table.as<uint64_t>();
   X.table = table;
   P->d_table_used = table;
   KParams& kp = X.kp;
@@ -2261,7 +2310,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_keys_total = P->num_keys;
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
-  kp.stats = sc->stats.as<unsigned long long>();
+  kp.stats = stats;
   if (P->leap_reserved) {  // one byte per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
     TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *
                              (kBlock / 64)));
@@ -2275,6 +2324,20 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     if (P->mode == MODE_HASH) {
       TRY(sc->hash_keys.ensure((size_t)P->num_keys * 8));
       kp.hash_keys = sc->hash_keys.as<unsigned long long>();
+      if (!P->stage_end.empty()) {
+        int64_t total = 0;
+        kp.num_stages = (int)P->stage_end.size();
+        for (int s = 0; s < kp.num_stages; ++s) {
+          kp.stage_end[s] = P->stage_end[s];
+          kp.stage_cap[s] = P->stage_cap[s];
+          kp.stage_mult[s] = P->stage_mult[s];
+          kp.stage_off[s] = total;
+          total += P->stage_cap[s];
+        }
+        TRY(sc->stage_keys.ensure((size_t)total * 8));
+        HIP_TRY(hipMemsetAsync(sc->stage_keys.p, 0xFF, (size_t)total * 8, stream));  // every slot empty (~0)
+        kp.stage_keys = sc->stage_keys.as<unsigned long long>();
+      }
     }
     if (!P->partitioned &&  // the partitioned path stores every table word itself
         launch_table_init(table, P->slot_kind.data(), nslots, P->num_keys, kp.hash_keys, stream))
@@ -2518,8 +2581,12 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     // small dense table: one copy (table + stats) and one sync, compacted on the host in key order
     TRY(sc->stage.ensure((size_t)words * 8 + 64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
-    HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + words, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
+    if (reinterpret_cast<const uint8_t*>(P->d_stats) == reinterpret_cast<const uint8_t*>(table) + words * 8) {
+      HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 48, hipMemcpyDeviceToHost, stream));  // table + stats
+    } else {
+      HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipMemcpyAsync(st + words, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+    }
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[words + 5]) return timeout_fail(P);
@@ -2551,7 +2618,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
@@ -2582,7 +2649,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->stage.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st + 1, sc->stats.p, 48, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
@@ -2596,13 +2663,36 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       HIP_TRY(hipMemcpyAsync(st, sc->ckeys.p, (size_t)n * rec * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
     }
+    std::vector<uint64_t> stages;  // ARRAY_MAP: the stage tables (slot -> that group's key), back to back
+    std::vector<int64_t> stage_off;
+    if (!P->stage_end.empty() && n > 0) {
+      int64_t total = 0;
+      for (int64_t c : P->stage_cap) { stage_off.push_back(total); total += c; }
+      stages.resize((size_t)total);
+      HIP_TRY(hipMemcpyAsync(stages.data(), sc->stage_keys.p, (size_t)total * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+    }
     std::vector<int64_t> order(n);
     for (int64_t i = 0; i < n; ++i) order[i] = i;
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return st[a * rec] < st[b * rec]; });
     TRY(R->alloc(nk, nslots, n));
     for (int64_t r = 0; r < n; ++r) {
       const uint64_t* e = st + order[r] * rec;
-      decode_keys(P, R, r, e[0]);
+      if (!P->stage_end.empty()) {  // last group first: its key's slot part names the previous group's key
+        uint64_t cur = e[0];
+        for (int g = (int)P->stage_space.size() - 1; g >= 0; --g) {
+          const uint64_t local = cur % (uint64_t)P->stage_space[g], slot = cur / (uint64_t)P->stage_space[g];
+          const int j0 = g == 0 ? 0 : P->stage_end[g - 1], j1 = g < (int)P->stage_end.size() ? P->stage_end[g] : nk;
+          for (int j = j0; j < j1; ++j)
+            R->gid(j)[r] = (int32_t)((local / (uint64_t)P->key_stride[j]) % (uint64_t)P->key_card[j]);
+          if (g > 0) {
+            if (slot >= (uint64_t)P->stage_cap[g - 1]) return fail(PGPU_ERR_DEVICE, "ARRAY_MAP stage slot out of range");
+            cur = stages[(size_t)(stage_off[g - 1] + (int64_t)slot)];
+          }
+        }
+      } else {
+        decode_keys(P, R, r, e[0]);
+      }
       for (int s = 0; s < nslots; ++s) R->slot(s)[r] = e[1 + s];
     }
   }
@@ -2759,8 +2849,19 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
     for (int s = 0; s < ns; ++s)
       if (part.plan->slot_kind[s] == SLOT_SUM_F64) kind[s] = SLOT_SUM_F64;
   const int64_t cap = P->pql_cap ? std::min<int64_t>(2 * L, INT32_MAX) : INT64_MAX;
-  std::unordered_map<uint64_t, int64_t> index;
-  std::vector<uint64_t> keys, vals;
+  // a group's key: the mixed-radix key, or for ARRAY_MAP plans (prefix key, rest key) -- never a slot number, which
+  // is local to one part's tables
+  using Key = std::array<int32_t, kMaxKeys>;  // the group-by dictIds (slot numbers are local to one part's tables)
+  struct KeyHash {
+    size_t operator()(const Key& k) const {
+      uint64_t h = 0;
+      for (int32_t v : k) h = (h ^ (uint32_t)v) * 0x9E3779B97F4A7C15ull;
+      return (size_t)(h ^ (h >> 29));
+    }
+  };
+  std::unordered_map<Key, int64_t, KeyHash> index;
+  std::vector<Key> keys;
+  std::vector<uint64_t> vals;
   int64_t counter = 0;
   for (size_t i = 0; i < P->parts.size(); ++i) {
     const auto& part = P->parts[i];
@@ -2774,8 +2875,8 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
       if (part.truncate && (int64_t)order.size() > L) order.resize(L);
     }
     for (int64_t r : order) {
-      uint64_t key = 0;
-      for (int j = 0; j < nk; ++j) key += (uint64_t)Ri->gid(j)[r] * (uint64_t)P0->key_stride[j];
+      Key key{};
+      for (int j = 0; j < nk; ++j) key[j] = Ri->gid(j)[r];
       auto it = index.find(key);
       if (it == index.end()) {
         if (counter++ >= cap) continue;  // _numGroups.getAndIncrement() < _interSegmentNumGroupsLimit
@@ -2813,12 +2914,18 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
   }
   std::vector<int64_t> rows(keys.size());
   std::iota(rows.begin(), rows.end(), 0);
-  std::sort(rows.begin(), rows.end(), [&](int64_t a, int64_t b) { return keys[a] < keys[b]; });
+  // ascending mixed-radix key order: the last group-by column is the most significant
+  std::sort(rows.begin(), rows.end(), [&](int64_t a, int64_t b) {
+    for (int j = nk - 1; j >= 0; --j)
+      if (keys[a][j] != keys[b][j]) return keys[a][j] < keys[b][j];
+    return false;
+  });
   const int64_t n = (int64_t)rows.size();
   R->pool = t->result_pool;
   TRY(R->alloc(nk, ns, n));
   for (int64_t r = 0; r < n; ++r) {
-    decode_keys(P0, R, r, keys[rows[r]]);
+    const Key& k = keys[rows[r]];
+    for (int j = 0; j < nk; ++j) R->gid(j)[r] = k[j];
     for (int s = 0; s < ns; ++s) R->slot(s)[r] = vals[rows[r] * ns + s];
   }
   const pgpu_result_s* R0 = rs[0].get();

@@ -68,13 +68,37 @@ def test_kat_inner_segment(oracle, sv, case, with_filter):
     assert_same(r, oracle.run_groupby(K.SCHEMA, [seg], q, combine=False), q, K.SCHEMA)
 
 
-def test_kat_array_map_shape_is_unsupported(sv):
-    """VERY_LARGE_GROUP_BY overflows a 64-bit composite key (Pinot's ARRAY_MAP holder): the GPU path declines
-    and the caller keeps Pinot's operator."""
+@pytest.mark.parametrize("with_filter", [False, True], ids=["no_filter", "filter"])
+def test_kat_array_map_holder(oracle, sv, with_filter):
+    """VERY_LARGE_GROUP_BY (InnerSegmentAggregationSingleValueQueriesTest.java:194-219): 9 group-by columns whose
+    cardinality product overflows a long -- Pinot's ArrayMapBasedHolder.  The GPU maps consecutive column groups to
+    dense slot ids through hash-table stages (KParams.num_stages) and must give the KAT's statistics and values and
+    the oracle's every group."""
     seg, t, h = sv
     case = K.KAT["inner_segment_group_by"][3]
-    with pytest.raises(L.UnsupportedQueryError):
-        t.execute_groupby([h], K.inner_query(case["group_by"], False))
+    q = K.inner_query(case["group_by"], with_filter)
+    q.num_groups_limit = 10 ** 9
+    r = t.execute_groupby([h], q)
+    exp = case["filter" if with_filter else "no_filter"]
+    assert r.stats.as_tuple() == tuple(exp["stats"])
+    key = K.key_tuple(case["group_by"], exp["key"])
+    K.check_inner_values(r.as_dict()[key], exp["values"])
+    assert_same(r, oracle.run_groupby(K.SCHEMA, [seg], q, combine=False), q, K.SCHEMA)
+
+
+def test_array_map_with_groups_limit(oracle, sv):
+    """The ARRAY_MAP shape under the default numGroupsLimit (100000 > 30000 docs: nothing truncated) and a binding
+    limit (first-seen truncation of the map holder, DictionaryBasedGroupKeyGenerator.java:1101-1113)."""
+    seg, t, h = sv
+    case = K.KAT["inner_segment_group_by"][3]
+    for limit in (100_000, 1000):
+        q = K.inner_query(case["group_by"], False)
+        q.num_groups_limit = limit
+        r = t.execute_groupby([h], q)
+        o = oracle.run_groupby(K.SCHEMA, [seg], q, combine=False, max_initial_capacity=min(limit, 10_000))
+        assert_same(r, o, q, K.SCHEMA)
+        if limit < 26_993:  # the segment holds 26993 distinct 9-column groups
+            assert len(r) == limit
 
 
 @pytest.mark.parametrize("with_filter", [False, True])

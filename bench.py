@@ -117,14 +117,18 @@ CALIB_SQL = {
     "c2": "SELECT COUNT(*) FROM t WHERE f = 1 AND f = 2 GROUP BY d",
     "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
 }
-SCAN_KERNELS = ("filter_groupby_kernel", "scan_kernel")
+SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel", "part_aggregate_kernel")
+# the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch)
+LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false>")
 
 
 def _fetch_per_launch(csv_path):
+    """FETCH_SIZE of one scan launch: every kernel of the launch's pipeline summed, averaged over the launches."""
     import csv
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(csv_path))
-            if r["Counter_Name"] == "FETCH_SIZE" and any(k in r["Kernel_Name"] for k in SCAN_KERNELS)]
-    return sum(vals) / len(vals) * 1024.0 if vals else None
+    rows = [r for r in csv.DictReader(open(csv_path)) if r["Counter_Name"] == "FETCH_SIZE"]
+    total = sum(float(r["Counter_Value"]) for r in rows if any(k in r["Kernel_Name"] for k in SCAN_KERNELS))
+    launches = sum(1 for r in rows if any(k in r["Kernel_Name"] for k in LAUNCH_KERNELS))
+    return total / launches * 1024.0 if launches else None
 
 
 def pmc_traffic(args):

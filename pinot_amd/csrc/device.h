@@ -62,6 +62,8 @@ template <int B, bool G = true>
 __device__ __forceinline__ void load_group(const uint32_t* __restrict__ words, uint32_t (&w)[B + 1]) {
   if constexpr (G) {
     gmem<uint32_t>* g = gp(words);
+    // plain loads: word k of every lane is B words apart, so a line is finished by the next instructions; measured
+    // on MI355X, non-temporal loads here cost C3 44% (775 -> 1115 us) and C2 2% (the L2 must keep the lines)
 #pragma unroll
     for (int k = 0; k < B; ++k) w[k] = bswap32(g[k]);
   } else {

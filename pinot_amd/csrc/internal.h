@@ -196,12 +196,19 @@ struct KPartParams {
   int32_t cshift;                   // 0: single level (K8c writes the final layout)
   int32_t num_coarse;               // ceil(num_parts / 2^cshift)
   int32_t chunks_per_coarse;        // K8e workgroups per coarse run
-  int32_t pad;
+  int32_t split_batch;              // K8e records sorted in LDS per batch (multiple of kBlock)
   uint32_t* coarse_fill;            // [num_coarse] K8a reservation counters
   uint32_t* fine_fill;              // [num_parts] K8e reservation counters
   uint32_t* mid_key;                // [rec_cap] coarse layout: key within its coarse range
   uint64_t* mid_val;                // [num_streams][rec_cap]
 };
+
+// K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).
+constexpr int kSplitBatch = 2048;
+// LDS bytes of part_split_kernel: 2^cshift partitions per coarse run, `streams` value streams, `batch` records.
+constexpr size_t part_split_lds(int cshift, int streams, int batch) {
+  return (size_t)3 * ((size_t)1 << cshift) * 4 + 8 + (size_t)streams * batch * 8 + (size_t)batch * (4 + 2) + 16;
+}
 
 // ---------------------------------------------------------------------------------------------- inverted index
 // One Roaring container of a pinned inverted index ORed into a query's docId bitmap.  Containers are kept on the
@@ -256,6 +263,10 @@ int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 // Per STATS_LEAP2 record of a launch: composes its (tile, wave) maps in doc order into the segment's count
 // (stats[2] += ...).
+// reduce_slabs + leap2_compose of a one-launch plan as one launch.
+int launch_epilogue(const uint64_t* slab, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
+                    int32_t num_blocks, uint64_t* out, const uint8_t* segs, int32_t seg_stride, int32_t num_segs,
+                    const uint8_t* maps, unsigned long long* stats, void* stream);
 int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint8_t* maps,
                          unsigned long long* stats, void* stream);
 int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);

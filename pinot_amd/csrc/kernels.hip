@@ -92,13 +92,13 @@ struct SlotKinds {
 // Each block folds 8 table words; the 32 lanes of a word take every 32nd slab and their partials are combined
 // in lane order: the fold itself has a fixed order, but the LDS slabs it reads were summed with atomicAdd(double),
 // so FLOAT/DOUBLE sums vary in their last bits from run to run (integer slots are exact).
-__global__ __launch_bounds__(256) void reduce_slabs_kernel(const uint64_t* __restrict__ slab, SlotKinds kinds,
-                                                           int64_t num_keys, int32_t num_slots, int32_t num_blocks,
-                                                           uint64_t* __restrict__ out) {
+__device__ __forceinline__ void reduce_slabs_block(int64_t blk, const uint64_t* __restrict__ slab,
+                                                   const SlotKinds& kinds, int64_t num_keys, int32_t num_slots,
+                                                   int32_t num_blocks, uint64_t* __restrict__ out) {
   __shared__ uint64_t part[256];
   const int64_t words = (int64_t)num_slots * num_keys;
   const int j = threadIdx.x & 31;
-  const int64_t i = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int64_t i = blk * 8 + (threadIdx.x >> 5);
   const int kind = i < words ? kinds.k[i / num_keys] : SLOT_COUNT;
   uint64_t acc;
   if (kind == SLOT_SUM_F64) {
@@ -144,6 +144,12 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const uint64_t* __res
       out[i] = a;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const uint64_t* __restrict__ slab, SlotKinds kinds,
+                                                           int64_t num_keys, int32_t num_slots, int32_t num_blocks,
+                                                           uint64_t* __restrict__ out) {
+  reduce_slabs_block(blockIdx.x, slab, kinds, num_keys, num_slots, num_blocks, out);
 }
 
 __global__ void table_init_kernel(uint64_t* __restrict__ table, SlotKinds kinds, int32_t num_slots, int64_t num_keys,
@@ -283,11 +289,11 @@ __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, 
 // difference at its first match when entered with B running, + 1).  One wave per segment chains the bytes in doc
 // order from the initial state (scan A at doc 0), 512 at a time (8 per lane): a byte's entry state is the exit of the nearest
 // earlier byte with a match (ballots), or the state carried from the previous 64.
-__global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride,
-                                                           int32_t num_segs, const uint8_t* __restrict__ maps,
-                                                           unsigned long long* __restrict__ stats) {
+__device__ __forceinline__ void leap2_compose_block(int blk, const uint8_t* __restrict__ segs, int32_t seg_stride,
+                                                    int32_t num_segs, const uint8_t* __restrict__ maps,
+                                                    unsigned long long* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
-  const int s = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int s = blk * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (s >= num_segs) return;  // wave-uniform
   const KSegHdr* h = reinterpret_cast<const KSegHdr*>(segs + (int64_t)s * seg_stride);
   if ((h->stats & 3) != KSTATS_LEAP2) return;
@@ -327,6 +333,26 @@ __global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __res
   }
   for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
   if (lane == 0 && total) atomicAdd(stats + 2, (unsigned long long)total);
+}
+
+__global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __restrict__ segs, int32_t seg_stride,
+                                                           int32_t num_segs, const uint8_t* __restrict__ maps,
+                                                           unsigned long long* __restrict__ stats) {
+  leap2_compose_block(blockIdx.x, segs, seg_stride, num_segs, maps, stats);
+}
+
+// The epilogue of a one-launch LDS-table plan in one launch: the slab fold's blocks, then the leap-frog statistics'
+// blocks (independent work; one launch gap and one kernel tail less per query).
+__global__ __launch_bounds__(256) void epilogue_kernel(const uint64_t* __restrict__ slab, SlotKinds kinds,
+                                                       int64_t num_keys, int32_t num_slots, int32_t num_blocks,
+                                                       uint64_t* __restrict__ out, int32_t reduce_blocks,
+                                                       const uint8_t* __restrict__ segs, int32_t seg_stride,
+                                                       int32_t num_segs, const uint8_t* __restrict__ maps,
+                                                       unsigned long long* __restrict__ stats) {
+  if ((int)blockIdx.x < reduce_blocks)  // block-uniform
+    reduce_slabs_block(blockIdx.x, slab, kinds, num_keys, num_slots, num_blocks, out);
+  else
+    leap2_compose_block((int)blockIdx.x - reduce_blocks, segs, seg_stride, num_segs, maps, stats);
 }
 
 // The leaves' match bitmaps of STATS_GENERIC segments (the replay of filter_stats.cpp runs on the host).
@@ -542,6 +568,20 @@ int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream) {
   if (grid > 4096) grid = 4096;
   const size_t lds = (size_t)kMaxStack * kBlock * sizeof(uint32_t);
   hipLaunchKernelGGL(filter_bitmap_kernel, dim3((unsigned)grid), dim3(kBlock), lds, S(stream), q, out_words);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_epilogue(const uint64_t* slab, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
+                    int32_t num_blocks, uint64_t* out, const uint8_t* segs, int32_t seg_stride, int32_t num_segs,
+                    const uint8_t* maps, unsigned long long* stats, void* stream) {
+  SlotKinds k{};
+  for (int i = 0; i < num_slots && i < kMaxSlots; ++i) k.k[i] = slot_kind[i];
+  const int64_t reduce_blocks = ((int64_t)num_slots * num_keys + 7) / 8;
+  const int64_t leap_blocks = num_segs > 0 ? (num_segs + 3) / 4 : 0;
+  if (reduce_blocks + leap_blocks < 1) return 0;
+  hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)(reduce_blocks + leap_blocks)), dim3(256), 0, S(stream), slab, k,
+                     num_keys, num_slots, num_blocks, out, (int32_t)reduce_blocks, segs, seg_stride, num_segs, maps,
+                     stats);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -185,20 +185,34 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
 }
 
 // K8e: workgroup (coarse run c, chunk j) moves its share of run c into the final per-partition layout.
-// LDS: [2^cshift] counters / cursors.
+// Pass 1 counts its records per partition and reserves each partition's run (one global atomic per partition).
+// Pass 2 (kSplitBatch records at a time) sorts a batch by partition in LDS -- histogram, prefix, each record placed
+// at its bucket slot with the global position it will take -- and then writes the sorted batch back out in LDS
+// order, so consecutive lanes store consecutive positions of one partition's run (coalesced u16 keys and u64
+// values) instead of 64 lanes scattering over 2^cshift open runs.  LDS: counters / cursors / batch histogram /
+// bucket starts [2^cshift each], then the staged batch (pp.split_batch records: a multiple of kBlock, at most
+// kSplitBatch, smaller with many value streams): values u64 per stream, positions u32, keys u16.
 __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
   const int tid = threadIdx.x;
   if (pp.base.deadline && pp.base.stats[5]) return;  // K8a timed out: its counts cover only part of the docs
   const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
   const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
+  const int NP = 1 << pp.cshift;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);  // per partition: count, then the next global position
+  uint32_t* hist = cnt + NP;                          // batch histogram, then the batch's running rank
+  uint32_t* bstart = hist + NP;                       // batch bucket starts (exclusive prefix of hist)
+  const int batch = pp.split_batch;
+  uint64_t* sval = reinterpret_cast<uint64_t*>(bstart + NP + (NP & 1));
+  uint32_t* spos = reinterpret_cast<uint32_t*>(sval + (size_t)pp.num_streams * batch);
+  uint16_t* skey = reinterpret_cast<uint16_t*>(spos + batch);
+  __shared__ uint32_t wtot[kBlock / 64];
   const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
   const uint32_t r0 = cs + (uint32_t)((uint64_t)(ce - cs) * j / pp.chunks_per_coarse);
   const uint32_t r1 = cs + (uint32_t)((uint64_t)(ce - cs) * (j + 1) / pp.chunks_per_coarse);
-  for (int i = tid; i < np; i += kBlock) cnt[i] = 0u;
+  for (int i = tid; i < NP; i += kBlock) cnt[i] = 0u;
   __syncthreads();
-  constexpr int NB = 8;  // records per lane per step: loads, then LDS atomics, then stores, each issued together
+  constexpr int NB = kSplitBatch / kBlock;  // records per lane per batch
   for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
     uint32_t k[NB];
 #pragma unroll
@@ -215,28 +229,56 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     const uint32_t h = cnt[i];
     cnt[i] = h ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
   }
-  __syncthreads();
   const uint32_t low = (1u << pp.pshift) - 1u;
-  for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
-    uint32_t k[NB], pos[NB];
+  const int per = (NP + kBlock - 1) / kBlock;  // prefix: each thread a contiguous slice of the buckets
+  for (uint32_t b0 = r0; b0 < r1; b0 += batch) {
+    const uint32_t n = min((uint32_t)batch, r1 - b0);
+    for (int i = tid; i < NP; i += kBlock) hist[i] = 0u;
+    __syncthreads();  // (also: the previous batch's write-out has read the staged arrays)
+    uint32_t k[NB], rank[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const uint32_t r = base + b * kBlock;
-      k[b] = r < r1 ? pp.mid_key[r] : ~0u;
+      const uint32_t i = tid + b * kBlock;
+      k[b] = i < n ? pp.mid_key[b0 + i] : ~0u;
     }
 #pragma unroll
-    for (int b = 0; b < NB; ++b) pos[b] = k[b] != ~0u ? atomicAdd(&cnt[k[b] >> pp.pshift], 1u) : 0u;
+    for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[k[b] >> pp.pshift], 1u) : 0u;
+    __syncthreads();
+    {  // exclusive prefix of the batch histogram: slices, wave scan of the slice sums, wave totals
+      const int lane = tid & 63, w = tid >> 6;
+      uint32_t acc = 0;
+      for (int i = tid * per; i < min(NP, (tid + 1) * per); ++i) acc += hist[i];
+      uint32_t incl = acc;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) wtot[w] = incl;
+      __syncthreads();
+      uint32_t run = incl - acc;
+      for (int v = 0; v < w; ++v) run += wtot[v];
+      for (int i = tid * per; i < min(NP, (tid + 1) * per); ++i) {
+        bstart[i] = run;
+        run += hist[i];
+      }
+    }
+    __syncthreads();
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
-      if (k[b] != ~0u) pp.rec_key[pos[b]] = (uint16_t)(k[b] & low);
-    for (int s = 0; s < pp.num_streams; ++s) {
-      uint64_t v[NB];
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        v[b] = k[b] != ~0u ? pp.mid_val[(int64_t)s * pp.rec_cap + base + b * kBlock] : 0ull;
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        if (k[b] != ~0u) pp.rec_val[(int64_t)s * pp.rec_cap + pos[b]] = v[b];
+    for (int b = 0; b < NB; ++b) {
+      if (k[b] == ~0u) continue;
+      const uint32_t part = k[b] >> pp.pshift;
+      const uint32_t l = bstart[part] + rank[b];
+      spos[l] = cnt[part] + rank[b];
+      skey[l] = (uint16_t)(k[b] & low);
+      for (int s = 0; s < pp.num_streams; ++s)
+        sval[(size_t)s * batch + l] = pp.mid_val[(int64_t)s * pp.rec_cap + b0 + tid + b * kBlock];
+    }
+    __syncthreads();
+    for (int i = tid; i < NP; i += kBlock) cnt[i] += hist[i];  // the partitions' next positions
+    for (uint32_t i = tid; i < n; i += kBlock) {  // in bucket order: runs of consecutive positions
+      const uint32_t pos = spos[i];
+      pp.rec_key[pos] = skey[i];
+      for (int s = 0; s < pp.num_streams; ++s) pp.rec_val[(int64_t)s * pp.rec_cap + pos] = sval[(size_t)s * batch + i];
     }
   }
 }

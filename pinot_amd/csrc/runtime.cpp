@@ -385,7 +385,7 @@ struct Segment {
 // on its stream and records `built`; later executions (any stream) wait on that event.
 struct DeviceImage {
   std::mutex mu;
-  bool uploaded = false;
+  std::atomic<bool> uploaded{false};
   hipEvent_t built = nullptr;
   DevBuf segrec, sets, tile_seg;
   ~DeviceImage() {
@@ -1369,6 +1369,9 @@ struct ExecCtx {
   uint32_t* sets = nullptr;
   int32_t* tile_seg = nullptr;
   bool from_image = false;
+  // one-launch LDS plans: the leap-frog statistics run in the slab fold's launch (launch_epilogue)
+  const uint8_t* leap_segs = nullptr;
+  int32_t leap_nsegs = 0;
   uint64_t* table = nullptr;
   int64_t words = 0;
   int nslots = 0;
@@ -2415,6 +2418,11 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.cshift = cshift;
     pp.num_coarse = (P->num_parts + (1 << cshift) - 1) >> cshift;
     pp.chunks_per_coarse = std::max(1, 1024 / pp.num_coarse);
+    {  // K8e batch: as many records as fit 96 KB of LDS beside the per-partition counters, a multiple of kBlock
+      const int64_t fixed = (int64_t)part_split_lds(cshift, pp.num_streams, 0);
+      const int64_t b = (96 * 1024 - fixed) / (8 * pp.num_streams + 6) / kBlock * kBlock;
+      pp.split_batch = (int)std::max<int64_t>(kBlock, std::min<int64_t>(kSplitBatch, b));
+    }
     TRY(sc->block_off.ensure((size_t)P->part_grid * pp.num_coarse * 4));
     TRY(sc->coarse_fill.ensure((size_t)pp.num_coarse * 4));
     TRY(sc->fine_fill.ensure((size_t)P->num_parts * 4));
@@ -2440,9 +2448,14 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
-  if (C.num_tiles > 0 && P->any_leap2 && P->leap_reserved && !P->partitioned &&
-      launch_leap2_compose(kp.segs, kp.seg_stride, kp.num_segs, kp.leap_maps, kp.stats, stream))
-    return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (C.num_tiles > 0 && P->any_leap2 && P->leap_reserved && !P->partitioned) {
+    if (P->chunks.size() == 1 && P->mode == MODE_LDS) {  // folded into the epilogue's launch
+      X.leap_segs = kp.segs;
+      X.leap_nsegs = kp.num_segs;
+    } else if (launch_leap2_compose(kp.segs, kp.seg_stride, kp.num_segs, kp.leap_maps, kp.stats, stream)) {
+      return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+  }
   if (C.num_tiles > 0 && !P->partitioned && P->mode == MODE_LDS) X.slabs_used += grid;
   P->launches_done = c + 1;
   return 0;
@@ -2533,10 +2546,15 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     if (all == 0) {
       if (launch_table_init(X.table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
-    } else if (launch_reduce_slabs(kp.slab, P->slot_kind.data(), nslots, P->num_keys, (int32_t)all, X.table, stream)) {
+    } else if (launch_epilogue(kp.slab, P->slot_kind.data(), nslots, P->num_keys, (int32_t)all, X.table, X.leap_segs,
+                               P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream)) {
       return fail(PGPU_ERR_DEVICE, "reduce launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
+    X.leap_nsegs = 0;
   }
+  if (X.leap_nsegs > 0 &&  // deferred but no fold ran (cannot happen for a plan with scan tiles; kept exact)
+      launch_leap2_compose(X.leap_segs, P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream))
+    return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIP_TRY(hipEventRecord(sc->ev[3], stream));
   P->last_stream = stream;
   P->executed = true;
@@ -2990,7 +3008,25 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
   std::lock_guard<std::mutex> g(t->cache_mu);
   for (auto it = t->plan_cache.begin(); it != t->plan_cache.end(); ++it) {
     if (it->first != key) continue;
-    *P = *it->second;
+    pgpu_plan_s& src = *it->second;
+    // Once its device image is built, a hit needs none of the host records: copy the plan without them (the
+    // records of a 1000-segment plan are ~250 KB -- most of a hit's host time).  cache_mu is held: no other
+    // thread reads the cached image meanwhile.
+    const bool lean = src.image && src.image->uploaded.load();
+    std::vector<uint8_t> segrec;
+    std::vector<uint32_t> set_words;
+    std::vector<std::pair<int64_t, int64_t>> set_fix;
+    if (lean) {
+      segrec.swap(src.segrec);
+      set_words.swap(src.set_words);
+      set_fix.swap(src.set_fix);
+    }
+    *P = src;
+    if (lean) {
+      src.segrec.swap(segrec);
+      src.set_words.swap(set_words);
+      src.set_fix.swap(set_fix);
+    }
     t->plan_cache.splice(t->plan_cache.begin(), t->plan_cache, it);
     P->scratch = nullptr;
     P->executed = false;

@@ -100,27 +100,47 @@ __device__ __forceinline__ void reduce_slabs_block(int64_t blk, const uint64_t* 
   const int j = threadIdx.x & 31;
   const int64_t i = blk * 8 + (threadIdx.x >> 5);
   const int kind = i < words ? kinds.k[i / num_keys] : SLOT_COUNT;
+  // every 32nd slab of word i, 8 loads in flight per step (independent partial folds, combined in a fixed order)
+  constexpr int U = 8;
   uint64_t acc;
   if (kind == SLOT_SUM_F64) {
-    double a = 0.0;
+    double a[U] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (i < words)
-      for (int b = j; b < num_blocks; b += 32) a += __longlong_as_double((long long)slab[(int64_t)b * words + i]);
-    acc = (uint64_t)__double_as_longlong(a);
-  } else if (kind == SLOT_MIN_KEY) {
-    long long a = INT64_MAX;
-    if (i < words)
-      for (int b = j; b < num_blocks; b += 32) a = min(a, (long long)slab[(int64_t)b * words + i]);
-    acc = (uint64_t)a;
-  } else if (kind == SLOT_MAX_KEY) {
-    long long a = INT64_MIN;
-    if (i < words)
-      for (int b = j; b < num_blocks; b += 32) a = max(a, (long long)slab[(int64_t)b * words + i]);
-    acc = (uint64_t)a;
+      for (int b = j; b < num_blocks; b += 32 * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int bb = b + 32 * u;
+          if (bb < num_blocks) a[u] += __longlong_as_double((long long)slab[(int64_t)bb * words + i]);
+        }
+      }
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) t += a[u];
+    acc = (uint64_t)__double_as_longlong(t);
   } else {
-    uint64_t a = 0;
+    const int64_t init = kind == SLOT_MIN_KEY ? INT64_MAX : kind == SLOT_MAX_KEY ? INT64_MIN : 0;
+    int64_t a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = init;
     if (i < words)
-      for (int b = j; b < num_blocks; b += 32) a += slab[(int64_t)b * words + i];
-    acc = a;
+      for (int b = j; b < num_blocks; b += 32 * U) {
+        int64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int bb = b + 32 * u;
+          v[u] = bb < num_blocks ? (int64_t)slab[(int64_t)bb * words + i] : init;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          a[u] = kind == SLOT_MIN_KEY ? min(a[u], v[u])
+                 : kind == SLOT_MAX_KEY ? max(a[u], v[u])
+                                        : (int64_t)((uint64_t)a[u] + (uint64_t)v[u]);  // COUNT / int SUM: wrap-free
+      }
+    int64_t t = init;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      t = kind == SLOT_MIN_KEY ? min(t, a[u]) : kind == SLOT_MAX_KEY ? max(t, a[u]) : (int64_t)((uint64_t)t + (uint64_t)a[u]);
+    acc = (uint64_t)t;
   }
   part[threadIdx.x] = acc;
   __syncthreads();

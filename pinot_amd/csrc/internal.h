@@ -201,6 +201,10 @@ struct KPartParams {
   uint32_t* fine_fill;              // [num_parts] K8e reservation counters
   uint32_t* mid_key;                // [rec_cap] coarse layout: key within its coarse range
   uint64_t* mid_val;                // [num_streams][rec_cap]
+  // 1: every stream is an integer whose values fit int32 (checked over the plan's dictionaries): rec_val / mid_val
+  // hold u32 words ([num_streams][rec_cap] u32, sign-extended on read) -- 4 bytes less per record and stream in
+  // each of the four record passes
+  int32_t val32;
 };
 
 // K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).

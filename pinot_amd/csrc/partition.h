@@ -101,9 +101,16 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? c.key_base + (int64_t)ids[i] : 0;
       }
+      if (pp.val32) {
+        uint32_t* __restrict__ o32 = reinterpret_cast<uint32_t*>(two ? pp.mid_val : pp.rec_val) + (int64_t)s * pp.rec_cap;
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if ((m >> i) & 1u) out[pos[i]] = (uint64_t)v[i];
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) o32[pos[i]] = (uint32_t)v[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) out[pos[i]] = (uint64_t)v[i];
+      }
     }
   }
 }
@@ -236,10 +243,18 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     for (int i = tid; i < NP; i += kBlock) hist[i] = 0u;
     __syncthreads();  // (also: the previous batch's write-out has read the staged arrays)
     uint32_t k[NB], rank[NB];
+    uint64_t v0[NB];  // stream 0's values, loaded with the keys so they are in flight through the sort
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const uint32_t i = tid + b * kBlock;
       k[b] = i < n ? pp.mid_key[b0 + i] : ~0u;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t r = b0 + min(tid + b * kBlock, n - 1u);
+      v0[b] = pp.num_streams == 0 ? 0ull
+              : pp.val32          ? (uint64_t)reinterpret_cast<const uint32_t*>(pp.mid_val)[r]
+                                  : pp.mid_val[r];
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[k[b] >> pp.pshift], 1u) : 0u;
@@ -270,15 +285,22 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
       const uint32_t l = bstart[part] + rank[b];
       spos[l] = cnt[part] + rank[b];
       skey[l] = (uint16_t)(k[b] & low);
-      for (int s = 0; s < pp.num_streams; ++s)
-        sval[(size_t)s * batch + l] = pp.mid_val[(int64_t)s * pp.rec_cap + b0 + tid + b * kBlock];
+      const int64_t r = b0 + tid + b * kBlock;
+      if (pp.num_streams > 0) sval[l] = v0[b];
+      for (int s = 1; s < pp.num_streams; ++s)
+        sval[(size_t)s * batch + l] = pp.val32 ? (uint64_t)reinterpret_cast<const uint32_t*>(pp.mid_val)[s * pp.rec_cap + r]
+                                               : pp.mid_val[s * pp.rec_cap + r];
     }
     __syncthreads();
     for (int i = tid; i < NP; i += kBlock) cnt[i] += hist[i];  // the partitions' next positions
     for (uint32_t i = tid; i < n; i += kBlock) {  // in bucket order: runs of consecutive positions
       const uint32_t pos = spos[i];
       pp.rec_key[pos] = skey[i];
-      for (int s = 0; s < pp.num_streams; ++s) pp.rec_val[(int64_t)s * pp.rec_cap + pos] = sval[(size_t)s * batch + i];
+      if (pp.val32)
+        for (int s = 0; s < pp.num_streams; ++s)
+          reinterpret_cast<uint32_t*>(pp.rec_val)[(int64_t)s * pp.rec_cap + pos] = (uint32_t)sval[(size_t)s * batch + i];
+      else
+        for (int s = 0; s < pp.num_streams; ++s) pp.rec_val[(int64_t)s * pp.rec_cap + pos] = sval[(size_t)s * batch + i];
     }
   }
 }
@@ -294,26 +316,38 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   for (int i = tid; i < ns * PR; i += kBlock) lds[i] = slot_init(p.slot_kind[i / PR]);
   __syncthreads();
   const uint32_t r0 = pp.part_start[blockIdx.x], r1 = pp.part_start[blockIdx.x + 1];
-  constexpr int NB = 4;  // records per lane per step, their loads issued together
+  // Two workgroups per CU (the LDS table), so latency is hidden by loads in flight per lane: NB records per lane
+  // per step, every load issued unconditionally (records past r1 re-read record r0 and are not accumulated).
+  constexpr int NB = 16;
   for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
+    uint32_t ri[NB];
     int k[NB];
-    bool ok[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const uint32_t r = base + b * kBlock;
-      ok[b] = r < r1;
-      k[b] = ok[b] ? pp.rec_key[r] : 0;
+      ri[b] = r < r1 ? r : r0;
     }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) k[b] = pp.rec_key[ri[b]];
     for (int s = 0; s < ns; ++s) {
       const int kind = p.slot_kind[s];
       const int st = pp.slot_stream[s];
       uint64_t w[NB];
+      if (st < 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) w[b] = 0ull;
+      } else if (pp.val32) {
+        const int32_t* __restrict__ r32 = reinterpret_cast<const int32_t*>(pp.rec_val) + (int64_t)st * pp.rec_cap;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) w[b] = (uint64_t)(int64_t)r32[ri[b]];
+      } else {
+        const uint64_t* __restrict__ r64 = pp.rec_val + (int64_t)st * pp.rec_cap;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) w[b] = r64[ri[b]];
+      }
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        w[b] = (st >= 0 && ok[b]) ? pp.rec_val[(int64_t)st * pp.rec_cap + base + b * kBlock] : 0ull;
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        if (ok[b])
+        if (base + b * kBlock < r1)
           accumulate<MODE_LDS>(lds + (int64_t)s * PR, k[b], kind, (int64_t)w[b], __longlong_as_double((long long)w[b]));
     }
   }

@@ -859,6 +859,7 @@ struct pgpu_plan_s {
   int part_shift = 0, num_parts = 0, part_grid = 0;
   size_t part_lds = 0;
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
+  bool part_val32 = false;  // KPartParams.val32
   double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
   int64_t sel_docs = 0;
   Scratch* scratch = nullptr;
@@ -1988,6 +1989,24 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->stream_col = scol;
         P->stream_f64 = sf64;
         P->slot_stream = sstream;
+        // u32 record values when every stream is an integer column whose values fit int32 in every segment
+        // (sorted dictionaries: the first and last entries bound them)
+        bool v32 = !getenv_flag("PGPU_PART_VAL64");
+        for (size_t j = 0; j < scol.size() && v32; ++j) {
+          const int c = P->query_cols[scol[j]];
+          if (sf64[j]) v32 = false;
+          else if (c != kDocIdColumn)
+            for (const Segment* s : P->segs) {
+              const Column& col = s->cols[c];
+              int64_t lo, hi;
+              if (col.raw) { lo = col.raw_min; hi = col.raw_max; }
+              else if (!col.dict.iv.empty()) { lo = col.dict.iv.front(); hi = col.dict.iv.back(); }
+              else if (col.dict.size() == 0) continue;
+              else { v32 = false; break; }
+              if (lo < INT32_MIN || hi > INT32_MAX) { v32 = false; break; }
+            }
+        }
+        P->part_val32 = v32;
         P->part_lds = pass_lds;
         int per_cu = occupancy_part_pass(pass_lds);
         per_cu = std::max(1, std::min(per_cu, 4));
@@ -2441,6 +2460,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.rec_key = sc->rec_key.as<uint16_t>();
     pp.rec_val = sc->rec_val.as<uint64_t>();
     pp.rec_cap = cap;
+    pp.val32 = P->part_val32 ? 1 : 0;
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {

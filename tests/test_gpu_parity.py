@@ -411,14 +411,16 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
     if not partitioned:
         monkeypatch.setenv("PGPU_NO_PARTITION", "1")
     rng = np.random.default_rng(docs)
-    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE")]
+    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("n", "INT"), ("l", "LONG")]
     segs = []
     for _ in range(2):
         segs.append(oracle.make_segment(schema, {"k1": rng.integers(0, 400, size=docs),
                                                  "k2": rng.integers(0, 60, size=docs),
                                                  "k3": rng.integers(0, 50, size=docs),
                                                  "m": rng.integers(0, 1000, size=docs),
-                                                 "x": rng.uniform(-1e6, 1e6, size=docs)}))
+                                                 "x": rng.uniform(-1e6, 1e6, size=docs),
+                                                 "n": rng.integers(-2 ** 31, 2 ** 31, size=docs),
+                                                 "l": rng.integers(-2 ** 40, 2 ** 40, size=docs)}))
     t, hs = gpu_table(schema, segs)
     try:
         q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
@@ -434,6 +436,14 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
         g = r.gids.astype(np.int64)  # key = d0 + d1*c0 + d2*c0*c1 (DictionaryBasedGroupKeyGenerator.java:276-323)
         comp = (g[:, 2] * 10 ** 6 + g[:, 1]) * 10 ** 6 + g[:, 0]
         assert np.all(np.diff(comp) > 0)
+        # integer streams only: int32 values (full range, negative included) ride in 4-byte records
+        # (KPartParams.val32); a LONG stream beyond int32 keeps 8-byte records
+        for sql in ("SELECT SUM(n), MIN(n), MAX(m), COUNT(*) FROM t GROUP BY k1, k2, k3",
+                    "SELECT SUM(l), MAX(l), MIN(n), COUNT(*) FROM t GROUP BY k1, k2, k3",
+                    "SELECT COUNT(*) FROM t GROUP BY k1, k2, k3"):  # no value stream at all
+            qi = parse_query(sql, num_groups_limit=10 ** 7)
+            assert_same(t.execute_groupby(hs, qi),
+                        oracle.run_groupby(schema, segs, qi, combine=False, max_initial_capacity=10000), qi, schema)
     finally:
         t.close()
 

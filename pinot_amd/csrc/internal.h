@@ -205,6 +205,10 @@ struct KPartParams {
   // hold u32 words ([num_streams][rec_cap] u32, sign-extended on read) -- 4 bytes less per record and stream in
   // each of the four record passes
   int32_t val32;
+  // > 0 (two-level, one integer stream): K8c packs (value - pack_min) into the mid_key bits above the key's
+  // cshift + pshift bits (pack_bits of them) and writes no mid_val; K8e unpacks -- 4 bytes per record instead of 8
+  int32_t pack_bits;
+  int64_t pack_min;
 };
 
 // K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).

@@ -68,6 +68,27 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   part_keys<H>(p, S, group, key);
   const int cbits = pp.pshift + pp.cshift;  // key bits within a coarse partition
   const bool two = pp.cshift > 0;
+  if (pp.pack_bits) {  // one integer stream, packed above the key bits: one u32 per record
+    const KCol& c = S.cols[pp.stream_col[0]];
+    uint32_t ids[16];
+    decode_group<H>(c.fwd, c.bits, group, ids);
+    int64_t v[16];
+    if (c.dkey) {
+      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : pp.pack_min;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = c.key_base + (int64_t)ids[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) {
+        const uint32_t pos = atomicAdd(&cursor[key[i] >> cbits], 1u);
+        pp.mid_key[pos] = (uint32_t)(key[i] & ((1 << cbits) - 1)) | ((uint32_t)(v[i] - pp.pack_min) << cbits);
+      }
+    return;
+  }
   uint32_t pos[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -219,13 +240,15 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   const uint32_t r1 = cs + (uint32_t)((uint64_t)(ce - cs) * (j + 1) / pp.chunks_per_coarse);
   for (int i = tid; i < NP; i += kBlock) cnt[i] = 0u;
   __syncthreads();
+  const int cbits = pp.pshift + pp.cshift;
+  const uint32_t kmask = pp.pack_bits ? (1u << cbits) - 1u : ~0u;  // the key bits of a packed mid_key word
   constexpr int NB = kSplitBatch / kBlock;  // records per lane per batch
   for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
     uint32_t k[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const uint32_t r = base + b * kBlock;
-      k[b] = r < r1 ? pp.mid_key[r] : ~0u;
+      k[b] = r < r1 ? pp.mid_key[r] & kmask : ~0u;
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -249,12 +272,20 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
       const uint32_t i = tid + b * kBlock;
       k[b] = i < n ? pp.mid_key[b0 + i] : ~0u;
     }
+    if (pp.pack_bits) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const uint32_t r = b0 + min(tid + b * kBlock, n - 1u);
-      v0[b] = pp.num_streams == 0 ? 0ull
-              : pp.val32          ? (uint64_t)reinterpret_cast<const uint32_t*>(pp.mid_val)[r]
-                                  : pp.mid_val[r];
+      for (int b = 0; b < NB; ++b) {
+        v0[b] = (uint64_t)(pp.pack_min + (int64_t)(k[b] >> cbits));  // as the u32 record the aggregate reads
+        k[b] = tid + b * kBlock < n ? k[b] & kmask : ~0u;  // (a packed word may be all ones)
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t r = b0 + min(tid + b * kBlock, n - 1u);
+        v0[b] = pp.num_streams == 0 ? 0ull
+                : pp.val32          ? (uint64_t)reinterpret_cast<const uint32_t*>(pp.mid_val)[r]
+                                    : pp.mid_val[r];
+      }
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[k[b] >> pp.pshift], 1u) : 0u;

@@ -860,6 +860,7 @@ struct pgpu_plan_s {
   size_t part_lds = 0;
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
   bool part_val32 = false;  // KPartParams.val32
+  int64_t part_pack_min = 0, part_pack_range = -1;  // the single stream's value range (-1: none)
   double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
   int64_t sel_docs = 0;
   Scratch* scratch = nullptr;
@@ -2007,6 +2008,20 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
             }
         }
         P->part_val32 = v32;
+        // one integer stream: its value range, for packing values into the coarse records (KPartParams.pack_bits)
+        P->part_pack_range = -1;
+        if (v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn && !getenv_flag("PGPU_NO_PACK")) {
+          int64_t lo = INT64_MAX, hi = INT64_MIN;
+          for (const Segment* s : P->segs) {
+            const Column& col = s->cols[P->query_cols[scol[0]]];
+            if (col.raw) { lo = std::min(lo, col.raw_min); hi = std::max(hi, col.raw_max); }
+            else if (!col.dict.iv.empty()) { lo = std::min(lo, col.dict.iv.front()); hi = std::max(hi, col.dict.iv.back()); }
+          }
+          if (lo <= hi) {
+            P->part_pack_min = lo;
+            P->part_pack_range = hi - lo;
+          }
+        }
         P->part_lds = pass_lds;
         int per_cu = occupancy_part_pass(pass_lds);
         per_cu = std::max(1, std::min(per_cu, 4));
@@ -2461,6 +2476,15 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.rec_val = sc->rec_val.as<uint64_t>();
     pp.rec_cap = cap;
     pp.val32 = P->part_val32 ? 1 : 0;
+    if (cshift > 0 && P->part_pack_range >= 0) {
+      const int free_bits = 32 - (pp.pshift + cshift);
+      int vb = 0;
+      while (vb < free_bits && (P->part_pack_range >> vb) != 0) ++vb;
+      if ((P->part_pack_range >> vb) == 0) {
+        pp.pack_bits = std::max(vb, 1);
+        pp.pack_min = P->part_pack_min;
+      }
+    }
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {

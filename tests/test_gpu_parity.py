@@ -411,7 +411,8 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
     if not partitioned:
         monkeypatch.setenv("PGPU_NO_PARTITION", "1")
     rng = np.random.default_rng(docs)
-    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("n", "INT"), ("l", "LONG")]
+    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("n", "INT"), ("l", "LONG"),
+              ("q", "INT")]
     segs = []
     for _ in range(2):
         segs.append(oracle.make_segment(schema, {"k1": rng.integers(0, 400, size=docs),
@@ -420,7 +421,8 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
                                                  "m": rng.integers(0, 1000, size=docs),
                                                  "x": rng.uniform(-1e6, 1e6, size=docs),
                                                  "n": rng.integers(-2 ** 31, 2 ** 31, size=docs),
-                                                 "l": rng.integers(-2 ** 40, 2 ** 40, size=docs)}))
+                                                 "l": rng.integers(-2 ** 40, 2 ** 40, size=docs),
+                                                 "q": rng.integers(-500, 500, size=docs)}))
     t, hs = gpu_table(schema, segs)
     try:
         q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
@@ -437,8 +439,12 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
         comp = (g[:, 2] * 10 ** 6 + g[:, 1]) * 10 ** 6 + g[:, 0]
         assert np.all(np.diff(comp) > 0)
         # integer streams only: int32 values (full range, negative included) ride in 4-byte records
-        # (KPartParams.val32); a LONG stream beyond int32 keeps 8-byte records
-        for sql in ("SELECT SUM(n), MIN(n), MAX(m), COUNT(*) FROM t GROUP BY k1, k2, k3",
+        # (KPartParams.val32); a LONG stream beyond int32 keeps 8-byte records; a single stream of narrow range is
+        # packed above the key bits of the coarse records (KPartParams.pack_bits), negative values included
+        for sql in ("SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3",
+                    "SELECT SUM(q), MIN(q), MAX(q), COUNT(*) FROM t GROUP BY k1, k2, k3",
+                    "SELECT MIN(n), MAX(n), SUM(n) FROM t GROUP BY k1, k2, k3",
+                    "SELECT SUM(n), MIN(n), MAX(m), COUNT(*) FROM t GROUP BY k1, k2, k3",
                     "SELECT SUM(l), MAX(l), MIN(n), COUNT(*) FROM t GROUP BY k1, k2, k3",
                     "SELECT COUNT(*) FROM t GROUP BY k1, k2, k3"):  # no value stream at all
             qi = parse_query(sql, num_groups_limit=10 ** 7)

@@ -212,10 +212,10 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
   }
 }
 
-// K8e: workgroup (coarse run c, chunk j) moves its share of run c into the final per-partition layout.
-// Pass 1 counts its records per partition and reserves each partition's run (one global atomic per partition).
-// Pass 2 (kSplitBatch records at a time) sorts a batch by partition in LDS -- histogram, prefix, each record placed
-// at its bucket slot with the global position it will take -- and then writes the sorted batch back out in LDS
+// K8e: workgroup (coarse run c, chunk j) moves its share of run c into the final per-partition layout,
+// pp.split_batch records at a time: a batch is sorted by partition in LDS -- histogram, prefix, one global atomic
+// per non-empty partition reserving the batch's run in it, each record placed at its bucket slot with the global
+// position it will take -- and then the sorted batch is written back out in LDS
 // order, so consecutive lanes store consecutive positions of one partition's run (coalesced u16 keys and u64
 // values) instead of 64 lanes scattering over 2^cshift open runs.  LDS: counters / cursors / batch histogram /
 // bucket starts [2^cshift each], then the staged batch (pp.split_batch records: a multiple of kBlock, at most
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
   const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
   const int NP = 1 << pp.cshift;
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);  // per partition: count, then the next global position
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);  // per partition: the batch's first global position
   uint32_t* hist = cnt + NP;                          // batch histogram, then the batch's running rank
   uint32_t* bstart = hist + NP;                       // batch bucket starts (exclusive prefix of hist)
   const int batch = pp.split_batch;
@@ -238,27 +238,9 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
   const uint32_t r0 = cs + (uint32_t)((uint64_t)(ce - cs) * j / pp.chunks_per_coarse);
   const uint32_t r1 = cs + (uint32_t)((uint64_t)(ce - cs) * (j + 1) / pp.chunks_per_coarse);
-  for (int i = tid; i < NP; i += kBlock) cnt[i] = 0u;
-  __syncthreads();
   const int cbits = pp.pshift + pp.cshift;
   const uint32_t kmask = pp.pack_bits ? (1u << cbits) - 1u : ~0u;  // the key bits of a packed mid_key word
   constexpr int NB = kSplitBatch / kBlock;  // records per lane per batch
-  for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
-    uint32_t k[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const uint32_t r = base + b * kBlock;
-      k[b] = r < r1 ? pp.mid_key[r] & kmask : ~0u;
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-      if (k[b] != ~0u) atomicAdd(&cnt[k[b] >> pp.pshift], 1u);
-  }
-  __syncthreads();
-  for (int i = tid; i < np; i += kBlock) {
-    const uint32_t h = cnt[i];
-    cnt[i] = h ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
-  }
   const uint32_t low = (1u << pp.pshift) - 1u;
   const int per = (NP + kBlock - 1) / kBlock;  // prefix: each thread a contiguous slice of the buckets
   for (uint32_t b0 = r0; b0 < r1; b0 += batch) {
@@ -305,7 +287,10 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
       for (int v = 0; v < w; ++v) run += wtot[v];
       for (int i = tid * per; i < min(NP, (tid + 1) * per); ++i) {
         bstart[i] = run;
-        run += hist[i];
+        const uint32_t h = hist[i];
+        run += h;
+        // the batch's run inside partition p0 + i: reserved now (no counting pass over the coarse run first)
+        cnt[i] = h ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
       }
     }
     __syncthreads();
@@ -323,7 +308,6 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
                                                : pp.mid_val[s * pp.rec_cap + r];
     }
     __syncthreads();
-    for (int i = tid; i < NP; i += kBlock) cnt[i] += hist[i];  // the partitions' next positions
     for (uint32_t i = tid; i < n; i += kBlock) {  // in bucket order: runs of consecutive positions
       const uint32_t pos = spos[i];
       pp.rec_key[pos] = skey[i];

@@ -247,7 +247,10 @@ inline double key_double(int64_t k) {
 
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
 constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
-constexpr int64_t kPartLds = 64 * 1024;              // K8d accumulators per partition (LDS)
+#ifndef PGPU_PART_LDS_KB
+#define PGPU_PART_LDS_KB 64
+#endif
+constexpr int64_t kPartLds = PGPU_PART_LDS_KB * 1024;  // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
 constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
 constexpr int kDocIdColumn = -2;                     // query column of the virtual $docId (hidden first-doc slot)

@@ -3765,17 +3765,21 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
-  bool composite = false;
-  TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
-  if (!composite) {
-    const bool cache = plan_cache_enabled(q);
-    if (!cache || !plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get())) {
-      TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
-      if (cache) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
+  // A cached plan is never a numGroupsLimit split (composite plans are not cached) and the split decision is a
+  // function of the cache key (query, segments, pinned-state version): a hit skips it.
+  const bool cache = plan_cache_enabled(q);
+  if (!cache || !plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get())) {
+    bool composite = false;
+    TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
+    if (composite) {
+      *out = P.release();
+      return 0;
     }
-    P->end_time_ms = q->end_time_ms;
-    P->scratch = acquire_scratch(t);
+    TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
+    if (cache) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
   }
+  P->end_time_ms = q->end_time_ms;
+  P->scratch = acquire_scratch(t);
   *out = P.release();
   return 0;
 }
@@ -3800,23 +3804,30 @@ int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t
 int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
                              void* d_table, pgpu_plan* out) {
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  const double tt0 = trace_on() ? now_us() : 0;
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
-  bool composite = false;
-  TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
-  if (composite) {  // executed part by part at finalize
-    if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
-    P->executed = true;
-    *out = P.release();
-    return 0;
+  // a cache hit skips the numGroupsLimit split decision (pgpu_plan_create)
+  const bool cache = plan_cache_enabled(q);
+  const bool hit = cache && plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get());
+  const double tt1 = trace_on() ? now_us() : 0;
+  if (!hit) {
+    bool composite = false;
+    TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
+    if (composite) {  // executed part by part at finalize
+      if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
+      P->executed = true;
+      *out = P.release();
+      return 0;
+    }
   }
   StreamExec se;
   se.stream = stream ? reinterpret_cast<hipStream_t>(stream) : t->stream;
   se.d_table = d_table;
-  const bool cache = plan_cache_enabled(q);
-  const bool hit = cache && plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get());
+  const double tt2 = trace_on() ? now_us() : 0;
   P->end_time_ms = q->end_time_ms;
   P->scratch = acquire_scratch(t);  // before plan_create_impl takes the table lock (acquire_scratch locks it too)
+  const double tt3 = trace_on() ? now_us() : 0;
   int rc = 0;
   if (!hit) {
     rc = plan_create_impl(t, handles, nsegs, q, P.get(), &se);
@@ -3826,6 +3837,9 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
     if (P->hash && d_table) rc = fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
     else rc = plan_execute_impl(P.get(), se.stream, d_table);
   }
+  if (trace_on())
+    fprintf(stderr, "[pgpu] create_execute%s: cache %.1f, groups-limit split %.1f, scratch %.1f, plan+execute %.1f us\n",
+            hit ? " (hit)" : "", tt1 - tt0, tt2 - tt1, tt3 - tt2, now_us() - tt3);
   if (rc) {
     if (P->scratch) {
       // no launch of this plan may still use its scratch: wait, or (timeout) leave it to the queued work

@@ -389,6 +389,7 @@ struct Segment {
 struct DeviceImage {
   std::mutex mu;
   std::atomic<bool> uploaded{false};
+  bool ready = false;  // `built` has completed: later executions need no stream wait (under mu)
   hipEvent_t built = nullptr;
   DevBuf segrec, sets, tile_seg;
   ~DeviceImage() {
@@ -2303,8 +2304,9 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
         return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
       HIP_TRY(hipEventRecord(im.built, stream));
       im.uploaded = true;
-    } else {
-      HIP_TRY(hipStreamWaitEvent(stream, im.built, 0));
+    } else if (!im.ready) {
+      if (hipEventQuery(im.built) == hipSuccess) im.ready = true;
+      else HIP_TRY(hipStreamWaitEvent(stream, im.built, 0));
     }
     X.segrec = im.segrec.as<uint8_t>();
     X.sets = im.sets.as<uint32_t>();

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
 #include <numeric>
 #include <string>
@@ -139,7 +140,7 @@ struct In {
   const uint8_t* p;
   int64_t n, pos = 0;
   bool ok = true;
-  bool need(int64_t k) { if (pos + k > n || k < 0) ok = false; return ok; }
+  bool need(int64_t k) { if (pos < 0 || k < 0 || pos > n || k > n - pos) ok = false; return ok; }
   int32_t i32() { if (!need(4)) return 0; uint32_t v = 0; for (int k = 0; k < 4; ++k) v = v << 8 | p[pos++]; return (int32_t)v; }
   int64_t i64() { if (!need(8)) return 0; uint64_t v = 0; for (int k = 0; k < 8; ++k) v = v << 8 | p[pos++]; return (int64_t)v; }
   double f64() { int64_t v = i64(); double d; memcpy(&d, &v, 8); return d; }
@@ -189,13 +190,16 @@ const char* fn_name(int fn) {
 }
 constexpr int kObjectTypeAvgPair = 4;  // ObjectSerDeUtils.ObjectType.AvgPair
 
-// DataTable.MetadataKey ordinals (pinot-common/.../DataTable.java:90-110).
+// DataTable.MetadataKey ordinals and value types (pinot-common/.../common/utils/DataTable.java:90-110; every key a
+// reference server may attach, e.g. requestId from InstanceRequestHandler / QueryScheduler, is decoded).
 struct MetaKey { const char* name; int ordinal; int kind; };  // kind 0 string, 1 int, 2 long
 const MetaKey kMetaKeys[] = {
-    {"numDocsScanned", 2, 2}, {"numEntriesScannedInFilter", 3, 2}, {"numEntriesScannedPostFilter", 4, 2},
-    {"numSegmentsQueried", 5, 1}, {"numSegmentsProcessed", 6, 1}, {"numSegmentsMatched", 7, 1},
-    {"totalDocs", 10, 2}, {"numGroupsLimitReached", 11, 0}, {"timeUsedMs", 12, 2}, {"numResizes", 15, 1},
-    {"resizeTimeMs", 16, 2}};
+    {"unknown", 0, 0}, {"table", 1, 0}, {"numDocsScanned", 2, 2}, {"numEntriesScannedInFilter", 3, 2},
+    {"numEntriesScannedPostFilter", 4, 2}, {"numSegmentsQueried", 5, 1}, {"numSegmentsProcessed", 6, 1},
+    {"numSegmentsMatched", 7, 1}, {"numConsumingSegmentsProcessed", 8, 1}, {"minConsumingFreshnessTimeMs", 9, 2},
+    {"totalDocs", 10, 2}, {"numGroupsLimitReached", 11, 0}, {"timeUsedMs", 12, 2}, {"traceInfo", 13, 0},
+    {"requestId", 14, 2}, {"numResizes", 15, 1}, {"resizeTimeMs", 16, 2}, {"threadCpuTimeNs", 17, 2},
+    {"systemActivitiesCpuTimeNs", 18, 2}, {"responseSerializationCpuTimeNs", 19, 2}};
 const MetaKey* meta_by_name(const std::string& n) {
   for (const MetaKey& k : kMetaKeys) if (n == k.name) return &k;
   return nullptr;
@@ -231,7 +235,14 @@ bool parse_table(const uint8_t* p, int64_t n, Table* T, std::string* err) {
   int32_t sec[10];
   for (int k = 0; k < 10; ++k) sec[k] = in.i32();
   if (!in.ok) { *err = "truncated header"; return false; }
-  auto section = [&](int k) { In s{p + sec[2 * k], sec[2 * k + 1]}; if (sec[2 * k] + (int64_t)sec[2 * k + 1] > n) s.ok = false; return s; };
+  if (T->rows < 0 || ncols < 0) { *err = "negative row / column count"; return false; }
+  // every section lies inside the bytes (offsets and lengths come from the wire: negative ones are rejected)
+  for (int k = 0; k < 5; ++k)
+    if (sec[2 * k] < 0 || sec[2 * k + 1] < 0 || (int64_t)sec[2 * k] + sec[2 * k + 1] > n) {
+      *err = "section " + std::to_string(k) + " outside the DataTable bytes";
+      return false;
+    }
+  auto section = [&](int k) { return In{p + sec[2 * k], sec[2 * k + 1]}; };
   In ex = section(0);
   if (sec[1]) {
     const int32_t ne = ex.i32();
@@ -261,22 +272,20 @@ bool parse_table(const uint8_t* p, int64_t n, Table* T, std::string* err) {
     for (int64_t r = 0; r < T->rows; ++r)
       T->cells.emplace_back(p + sec[6] + r * T->row_size, p + sec[6] + (r + 1) * T->row_size);
   }
-  if (sec[9]) {
-    if (sec[8] + (int64_t)sec[9] > n) { *err = "bad variable-size section"; return false; }
-    T->var.assign(p + sec[8], p + sec[8] + sec[9]);
-  }
+  if ((int64_t)T->cells.size() != T->rows) { *err = "rows without a fixed-size section"; return false; }
+  if (sec[9]) T->var.assign(p + sec[8], p + sec[8] + sec[9]);
   // metadata follows the sections
   In m{p, n};
   m.pos = std::max<int64_t>({(int64_t)13 * 4, (int64_t)sec[0] + sec[1], (int64_t)sec[2] + sec[3], (int64_t)sec[4] + sec[5],
                              (int64_t)sec[6] + sec[7], (int64_t)sec[8] + sec[9]});
   const int32_t ml = m.i32();
+  if (!m.ok || ml < 0 || m.pos + (int64_t)ml > n) { *err = "bad metadata"; return false; }
   In md{p + m.pos, ml};
-  if (m.pos + ml > n) { *err = "bad metadata"; return false; }
   const int32_t ne = md.i32();
   for (int i = 0; i < ne && md.ok; ++i) {
     const int32_t ord = md.i32();
     const MetaKey* k = meta_by_ordinal(ord);
-    if (!k) { *err = "unknown metadata key " + std::to_string(ord); return false; }
+    if (!k) continue;  // DataTableImplV3.deserializeMetadata ignores keys it does not know (:361-365)
     if (k->kind == 1) T->meta[k->name] = std::to_string(md.i32());
     else if (k->kind == 2) T->meta[k->name] = std::to_string(md.i64());
     else T->meta[k->name] = md.str();
@@ -295,6 +304,8 @@ struct Cell {
 
 void json_double(std::string& o, double d) {
   char buf[64];
+  // Jackson writes non-finite doubles as strings ("NaN", "Infinity", "-Infinity"); bare nan / inf is not JSON
+  if (std::isnan(d)) { o += "\"NaN\""; return; }
   if (std::isinf(d)) { o += d < 0 ? "\"-Infinity\"" : "\"Infinity\""; return; }
   snprintf(buf, sizeof buf, "%.17g", d);
   o += buf;
@@ -546,7 +557,9 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
           const int32_t off = in.i32(), ln = in.i32();
           In v{t.var.data(), (int64_t)t.var.size()};
           v.pos = off;
-          if (v.i32() != kObjectTypeAvgPair || ln != 16)
+          const int32_t obj_type = v.i32();
+          if (!v.ok) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "object offset %d outside the variable-size data", off);
+          if (obj_type != kObjectTypeAvgPair || ln != 16)
             return host_fail(PGPU_ERR_UNSUPPORTED, "object column %s is not an AvgPair", names[c].c_str());
           x.kind = 3;
           x.d = v.f64();
@@ -554,8 +567,21 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
           if (!v.ok) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad object bytes");
         }
         if (c < nk) {
-          key += x.kind == 2 ? "s" + x.s : (x.kind == 0 ? "i" + std::to_string(x.i) : "d" + std::to_string(x.d));
-          key += '\0';
+          // exact encoding: the string bytes (length-prefixed), or the 8 bytes of the integer / IEEE double (a
+          // decimal rendering such as %f would merge keys that differ past its precision)
+          const char tag = x.kind == 2 ? 's' : x.kind == 0 ? 'i' : 'd';
+          key += tag;
+          if (x.kind == 2) {
+            const uint32_t ln = (uint32_t)x.s.size();
+            key.append(reinterpret_cast<const char*>(&ln), 4);
+            key += x.s;
+          } else if (x.kind == 0) {
+            key.append(reinterpret_cast<const char*>(&x.i), 8);
+          } else {
+            // Double.equals: doubleToLongBits -- -0.0 and 0.0 are distinct keys, every NaN is one key
+            const double d = std::isnan(x.d) ? std::numeric_limits<double>::quiet_NaN() : x.d;
+            key.append(reinterpret_cast<const char*>(&d), 8);
+          }
         }
       }
       if (!in.ok) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad row bytes");

@@ -439,7 +439,11 @@ int pgpu_startree_load(const void* index, int64_t index_len, const char* index_m
   Span tree;
   std::vector<std::pair<std::string, Span>> fwd;
   if (int rc = parse_index_map(index_map, index_map_len, star_tree_id, &tree, &fwd)) return rc;
-  auto in_file = [&](const Span& sp) { return sp.off >= 0 && sp.size >= 0 && sp.off + sp.size <= index_len; };
+  // offsets and sizes come from the text of the index map (up to LLONG_MAX each): compared without an add that
+  // could overflow
+  auto in_file = [&](const Span& sp) {
+    return sp.off >= 0 && sp.size >= 0 && index_len >= 0 && sp.off <= index_len && sp.size <= index_len - sp.off;
+  };
   if (!in_file(tree))
     return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "star-tree %d: no STAR_TREE entry inside the index file", star_tree_id);
   // OffHeapStarTree header, little-endian (OffHeapStarTree.java:45-80; StarTreeBuilderUtils.java:118-171)

@@ -93,3 +93,77 @@ def test_reduce_no_rows_and_bad_bytes():
         broker_reduce_sql([e[:20]], q)
     with pytest.raises(Exception):
         broker_reduce_sql([b"\0\0\0\2" + e[4:]], q)  # version 2
+
+
+def _sections(dt):
+    """(header ints, body) of a DataTable made by datatable()."""
+    return list(struct.unpack(">13i", dt[:52])), dt[52:]
+
+
+def _with_header(h, body):
+    return struct.pack(">13i", *h) + body
+
+
+def test_reduce_rejects_corrupted_tables():
+    """Hand-corrupted server responses are rejected, never read outside their bytes."""
+    names, types = ["column17", "count(*)", "avg(column6)"], ["INT", "LONG", "OBJECT"]
+    good = datatable(names, types, [[5, 2, (10.0, 2)], [9, 1, (7.0, 1)]], _meta(3))
+    q = parse_query("SELECT column17, COUNT(*), AVG(column6) FROM t GROUP BY column17")
+    assert len(broker_reduce_sql([good], q)["resultTable"]["rows"]) == 2
+    h, body = _sections(good)
+    for k in range(5):  # a negative offset, then a negative length, for every section
+        for field in (3 + 2 * k, 4 + 2 * k):
+            bad = list(h)
+            bad[field] = -8
+            with pytest.raises(Exception):
+                broker_reduce_sql([_with_header(bad, body)], q)
+    bad = list(h)
+    bad[9] = bad[10] = 0  # rows > 0 but no fixed-size section
+    with pytest.raises(Exception):
+        broker_reduce_sql([_with_header(bad, body)], q)
+    bad = list(h)
+    bad[1] = -1  # negative row count
+    with pytest.raises(Exception):
+        broker_reduce_sql([_with_header(bad, body)], q)
+    # an AvgPair cell pointing before / past the variable-size data
+    for off in (-16, 1 << 20):
+        rows = bytearray(good)
+        fixed_off = h[9]
+        row_size = 4 + 8 + 8
+        struct.pack_into(">i", rows, fixed_off + 12, off)  # first row's OBJECT offset
+        with pytest.raises(Exception):
+            broker_reduce_sql([bytes(rows)], q)
+        _ = row_size
+
+
+def test_reduce_double_keys_exact():
+    """DOUBLE group keys that differ only past the 6th decimal stay distinct groups (keys compare by value)."""
+    names, types = ["d", "count(*)"], ["DOUBLE", "LONG"]
+    a = datatable(names, types, [[1e-7, 1], [2e-7, 2], [0.1 + 0.2, 3]], _meta(6))
+    b = datatable(names, types, [[1e-7, 10], [0.3, 4], [-0.0, 5]], _meta(19))
+    q = parse_query("SELECT d, COUNT(*) FROM t GROUP BY d ORDER BY d LIMIT 10")
+    rows = broker_reduce_sql([a, b], q)["resultTable"]["rows"]
+    assert rows == [[-0.0, 5], [1e-7, 11], [2e-7, 2], [0.3, 4], [0.1 + 0.2, 3]]
+
+
+def test_reduce_reference_metadata_keys_and_nan():
+    """Responses of a reference server carry metadata keys beyond the statistics (requestId, threadCpuTimeNs,
+    traceInfo, ...; DataTable.java:90-110) -- decoded and skipped -- and a NaN aggregate is valid JSON."""
+    names, types = ["column17", "sum(column6)"], ["INT", "DOUBLE"]
+    meta = dict(_meta(4))
+    dt = datatable(names, types, [[1, float("nan")], [2, 3.0]], meta)
+    h, body = _sections(dt)
+    # rebuild the metadata with extra reference keys appended
+    extra = [(14, ">q", 123456789), (17, ">q", 42), (13, "s", "trace"), (8, ">i", 0), (9, ">q", -1)]
+    md = struct.pack(">i", len(meta) + len(extra)) + b"".join(
+        struct.pack(">i", META[k][0]) + struct.pack(">" + META[k][1], v) for k, v in meta.items())
+    for ordinal, fmt, v in extra:
+        md += struct.pack(">i", ordinal) + (_s(v) if fmt == "s" else struct.pack(fmt, v))
+    end = max(h[3 + 2 * k] + h[4 + 2 * k] for k in range(5))
+    dt2 = dt[:end] + struct.pack(">i", len(md)) + md
+    q = parse_query("SELECT column17, SUM(column6) FROM t GROUP BY column17 ORDER BY column17")
+    r = broker_reduce_sql([dt2], q)
+    rows = r["resultTable"]["rows"]
+    assert rows[1] == [2, 3.0]
+    assert rows[0] == [1, "NaN"]  # Jackson's QUOTE_NON_NUMERIC_NUMBERS form: valid JSON
+    assert r["numDocsScanned"] == 4

@@ -117,3 +117,29 @@ def test_malformed(built):
     bad[off + 20:off + 24] = struct.pack(">i", 2)
     with pytest.raises(L.UnsupportedQueryError):
         StarTree.load(SC.C4_SCHEMA, bits, bytes(bad), imap, n)
+
+
+def test_index_map_offsets_near_int64_max(built):
+    """Offsets / sizes read from the index map text up to LLONG_MAX: the bounds check must not overflow (an
+    OFFSET of 2^63-1 with SIZE 1 once passed as in-file and read far outside the buffer)."""
+    seg, st, bits, _ = built
+    index, imap, _ = star_tree_files([st], bits)
+    n = st.arrays()["num_docs"]
+    big = 2 ** 63 - 1
+    lines = []
+    for ln in imap.splitlines():
+        if ln.startswith("0.null.STAR_TREE.OFFSET"):
+            ln = "0.null.STAR_TREE.OFFSET = %d" % big
+        elif ln.startswith("0.null.STAR_TREE.SIZE"):
+            ln = "0.null.STAR_TREE.SIZE = 1"
+        lines.append(ln)
+    with pytest.raises(L.PinotGpuError):
+        StarTree.load(SC.C4_SCHEMA, bits, index, "\n".join(lines) + "\n", n)
+    # a metric chunk whose SIZE pushes offset + size past 2^63
+    lines = []
+    for ln in imap.splitlines():
+        if ln.startswith("0.sum__m.FORWARD_INDEX.SIZE"):
+            ln = "0.sum__m.FORWARD_INDEX.SIZE = %d" % big
+        lines.append(ln)
+    with pytest.raises(L.PinotGpuError):
+        StarTree.load(SC.C4_SCHEMA, bits, index, "\n".join(lines) + "\n", n)

@@ -1,13 +1,18 @@
 """Benchmark: the README AdAnalytics filtered GROUP BY (BASELINE.json configs[2], C3) on synthetic segments
 pinned in HBM, one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|c1|c2|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|c1|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-A step is one whole query on every rank: plan (per-segment predicate translation), the fused scan kernel over
-all local segments, the dense group-table merge across ranks (RCCL all-reduce over xGMI) and the compacted
-result copied back to the host.  Each rank holds --segments-per-gpu segments of 1M docs (weak scaling: the
-default 1000 segments = 1B rows per GPU).  Rank 0 prints one JSON line.
+A step is one whole query on every rank: plan (per-segment predicate translation; a plan-cache hit for a repeated
+query), the fused scan kernel over all local segments, the dense group-table merge across ranks (RCCL all-reduce
+over xGMI) and the compacted result copied back to the host.  By default the workload's BASELINE row count is split
+across the ranks (strong scaling: C3 = 1 000 segments of 1M docs = 1B rows over 1/2/4/8 GPUs, "1B rows sharded
+1/2/4/8 GPUs"); --segments-per-gpu S instead pins S segments on every rank (weak scaling).  Queries are pipelined
+--inflight deep (default 2, each in flight on its own stream and group table): query k+1 is planned and launched
+before query k's result is finalized, as a server overlaps concurrent queries -- the GPU does not idle while the
+host finalizes.  Kernel durations for the roofline come from a separate serialized pass (--inflight 1 semantics).
+Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -21,6 +26,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 SHARD_BYTES = 16 << 20  # group tables at least this large are reduce-scattered across ranks, not all-reduced
+# Rows of each workload's BASELINE.json configuration: the default strong-scaling total.
+DEFAULT_ROWS = {"adanalytics": 1_000_000_000, "adanalytics_inv": 1_000_000_000, "c1": 1_000_000, "c2": 100_000_000,
+                "c4": 64_000_000, "c5": 100_000_000}
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
 
 
@@ -36,7 +44,12 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="adanalytics")
     p.add_argument("--sql", default=None, help="override the workload's query (same table)")
-    p.add_argument("--segments-per-gpu", type=int, default=1000)
+    p.add_argument("--rows-total", type=int, default=None,
+                   help="strong scaling: this many rows split across the ranks (default: the workload's BASELINE rows)")
+    p.add_argument("--segments-per-gpu", type=int, default=None,
+                   help="weak scaling: this many segments on every rank (overrides --rows-total)")
+    p.add_argument("--inflight", type=int, default=2, help="queries in flight (1 = strictly one after another)")
+    p.add_argument("--roofline-steps", type=int, default=10, help="serialized steps timing the scan kernel")
     p.add_argument("--docs-per-segment", type=int, default=1_000_000)
     p.add_argument("--cpu-sample-segments", type=int, default=None, help="default: the workload's sample size")
     p.add_argument("--cpu-target-seconds", type=float, default=12.0)
@@ -143,8 +156,8 @@ def pmc_traffic(args):
     if not os.path.exists(rocprof) or args.workload not in CALIB_SQL:
         return None
     base = [sys.executable, "-u", os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
-            "--no-pmc", "--workload", args.workload, "--segments-per-gpu", str(args.segments_per_gpu),
-            "--docs-per-segment", str(args.docs_per_segment)]
+            "--no-pmc", "--workload", args.workload, "--segments-per-gpu", str(args.local_segments),
+            "--docs-per-segment", str(args.docs_per_segment), "--inflight", "1", "--roofline-steps", "2"]
     res = {}
     with tempfile.TemporaryDirectory() as d:
         for name, sql in (("main", args.sql), ("calib", CALIB_SQL[args.workload])):
@@ -279,13 +292,23 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    docs = args.docs_per_segment
+    if args.segments_per_gpu:  # weak scaling
+        seg_first, nseg = rank * args.segments_per_gpu, args.segments_per_gpu
+        total_segments = args.segments_per_gpu * world
+    else:  # strong scaling: the workload's rows split across the ranks
+        rows = args.rows_total or DEFAULT_ROWS.get(args.workload, 1_000_000_000)
+        total_segments = max(1, rows // docs)
+        seg_first = rank * total_segments // world
+        nseg = (rank + 1) * total_segments // world - seg_first
+    args.local_segments = nseg
     pmc = None
     if world == 1 and not args.no_pmc and not args.no_bytes:
         # before this process initialises the GPU: the profiled runs are children, not exec'd
         from pinot_amd.build import build as _build
         _build()
         pmc = pmc_traffic(args)
-    rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # PGPU_BENCH_BACKEND=gloo: rehearsal of the multi-rank control flow on a box with fewer GPUs than ranks (ranks
     # share devices, collectives staged through host memory); the measured configuration is RCCL, one GPU per rank.
@@ -320,13 +343,11 @@ def main():
     q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
     if args.no_star_tree:
         q.use_star_tree = False
-    docs = args.docs_per_segment
-    nseg = args.segments_per_gpu
     table = GpuTable(w.schema, device=device)
     t_gen = time.perf_counter()
     handles = []
     for i in range(nseg):
-        global_seg = rank * nseg + i
+        global_seg = seg_first + i
         handles.append(table.generate_segment(w.gen, row0=global_seg * docs, num_docs=docs))
     t_gen = time.perf_counter() - t_gen
     log("rank %d: %d segments generated in %.1f s" % (rank, nseg, t_gen))
@@ -342,41 +363,51 @@ def main():
         union_dictionaries(table, q.group_by)
     handles = np.array(handles, dtype=np.int64)
 
-    # A real stream for the whole step: the default stream's handle is 0, which the C ABI reads as "the table's own
-    # (non-blocking) stream" -- the collectives (RCCL, or gloo's staged copies) on torch's current stream would then
-    # not be ordered after the scan kernels writing d_table.
-    torch.cuda.set_stream(torch.cuda.Stream())
-    stream = torch.cuda.current_stream().cuda_stream
-    assert stream != 0
+    # Real streams (the default stream's handle 0 would mean "the table's own stream" to the C ABI, and the
+    # collectives on torch's stream would not be ordered after the scan writing d_table): one per query in flight,
+    # each with its own group table.
+    inflight = max(1, args.inflight)
+    streams = [torch.cuda.Stream() for _ in range(inflight)]
+    torch.cuda.set_stream(streams[0])
     probe = table.plan(handles, q)
     nslots, nkeys, kinds = probe.layout()
     probe_nslots = nslots
     probe.close()
-    d_table = torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda")
+    d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
     # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
     sharded = world > 1 and nslots * nkeys * 8 >= SHARD_BYTES
 
-    phases = {"plan": 0.0, "execute": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0,
-              "decode": 0.0}
-
+    phases = {"plan": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0, "decode": 0.0}
     star_work = [0, 0, 0]
 
-    def step():
+    def launch(k):
+        """Plan + execute query k on its stream (streamed: segment chunks launch while the rest is planned), then
+        enqueue the cross-rank merge of its table on the same stream."""
         c0 = time.perf_counter()
-        # plan + execute streamed: segment chunks are launched while the rest of the list is still planned
-        plan = table.plan_execute(handles, q, stream, d_table.data_ptr() if nkeys > 0 else None)
+        s, dt = streams[k % inflight], d_tables[k % inflight]
+        plan = table.plan_execute(handles, q, s.cuda_stream, dt.data_ptr() if nkeys > 0 else None)
         c1 = time.perf_counter()
-        c2 = c1
-        if sharded:
-            shard, k0, kn = reduce_scatter_group_table(d_table, kinds)
-        elif world > 1:
-            allreduce_group_table(d_table, kinds)
-        c3 = time.perf_counter()
-        if sharded:
-            res = plan.finalize_range(stream, shard.data_ptr(), k0, kn)
+        shard = None
+        if world > 1:
+            with torch.cuda.stream(s):
+                if sharded:
+                    shard = reduce_scatter_group_table(dt, kinds)
+                else:
+                    allreduce_group_table(dt, kinds)
+        phases["plan"] += c1 - c0
+        phases["merge"] += time.perf_counter() - c1
+        return plan, s, dt, shard
+
+    def complete(item):
+        """Finalize query k (waits for its stream only) and release its plan."""
+        plan, s, dt, shard = item
+        c0 = time.perf_counter()
+        if shard is not None:
+            sh, k0, kn = shard
+            res = plan.finalize_range(s.cuda_stream, sh.data_ptr(), k0, kn)
         else:
-            res = plan.finalize(stream, d_table.data_ptr() if nkeys > 0 else None)
-        c4 = time.perf_counter()
+            res = plan.finalize(s.cuda_stream, dt.data_ptr() if nkeys > 0 else None)
+        c1 = time.perf_counter()
         tm = plan.timing_us()
         if w.star_tree and not args.no_star_tree:  # star-tree plans: traversal + pre-aggregated document scan
             k_us = (tm[3], 1)
@@ -385,32 +416,45 @@ def main():
             k_us = (tm[1], max(int(tm[2]), 1))  # scan launches of this query: summed duration, count
         fc_us, dec_us = plan.finalize_us
         plan.close()
-        c5 = time.perf_counter()
-        for k, v in zip(phases, (c1 - c0, c2 - c1, c3 - c2, c4 - c3, c5 - c4, fc_us * 1e-6, dec_us * 1e-6)):
-            phases[k] += v
+        phases["finalize"] += c1 - c0
+        phases["close"] += time.perf_counter() - c1
+        phases["finalize_c"] += fc_us * 1e-6
+        phases["decode"] += dec_us * 1e-6
         return res, k_us
 
+    def run(n, depth):
+        """n queries, at most `depth` in flight; returns the results and kernel timings in query order."""
+        from collections import deque
+        pending, out = deque(), []
+        for k in range(n):
+            pending.append(launch(k))
+            if len(pending) >= depth:
+                out.append(complete(pending.popleft()))
+        while pending:
+            out.append(complete(pending.popleft()))
+        return out
+
     first = None
-    for _ in range(args.warmup):
-        first, _ = step()
+    if args.warmup:
+        first = run(args.warmup, inflight)[0][0]
     for k in phases:
         phases[k] = 0.0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_us = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res, k_us = step()
-        kernel_us.append(k_us)
-        if args.verify and first is not None:
-            assert res.as_dict() == first.as_dict()
+    timed = run(args.steps, inflight)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.verify and first is not None:
+        for res, _ in timed:
+            assert res.as_dict() == first.as_dict()
+    if first is None and timed:
+        first = timed[0][0]
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -420,8 +464,11 @@ def main():
         g = torch.tensor([ngroups], dtype=torch.int64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(g)
         ngroups = int(g.item())
-    total_rows = float(nseg) * docs * world
+    total_rows = float(total_segments) * docs
     value = total_rows * args.steps / elapsed
+    # The scan kernel's duration for the roofline: a serialized pass (one query in flight, so no other query's
+    # kernels share the GPU with the one being timed), after the timed region.
+    kernel_us = [k for _, k in run(max(1, args.roofline_steps), 1)]
     launches = kernel_us[0][1] if kernel_us else 1
     kernel_avg_us = float(np.mean([k for k, _ in kernel_us])) / launches if kernel_us else 0.0  # per launch
 
@@ -473,13 +520,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.segments_per_gpu else "strong",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (BASELINE.md §3 generators, built on the device)",
             "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
-                       "groups": ngroups, "setup_s": round(t_gen, 1),
+                       "groups": ngroups, "setup_s": round(t_gen, 1), "queries_in_flight": inflight,
                        "combine": "reduce_scatter" if sharded else ("all_reduce" if world > 1 else "none")},
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,

@@ -13,8 +13,16 @@
  * The Java-side bindings a maintainer adds (JNI, and the ctypes binding used by this repo's tests) are in
  * INTEGRATION.md.
  *
- * Threading: every entry point is thread-safe.  Segments are immutable once pinned; queries on one table are
- * serialised on that table's device work area (one in flight per table).
+ * Threading: every entry point is thread-safe, and any number of queries may run concurrently on one table
+ * (Pinot runs many queries at once over the same segments, BaseCombineOperator.java:85-115).  Each plan owns a
+ * per-query device arena (scratch buffers, statistics, group table) taken from the table's pool; plan creation holds
+ * the table's mutex only to take its segment references and build lazily made per-segment arrays, so concurrent
+ * cache-miss plans translate their predicates in parallel.  Give concurrent queries their own streams for their
+ * device work to overlap (stream NULL = the table's stream: correct, but those queries' kernels run one after
+ * another).  Pinned segments are immutable and reference-counted like Pinot's SegmentDataManager: unpinning a
+ * segment that a live plan references frees its device memory when that plan is destroyed.  Global dictionaries
+ * are snapshots: a pin that grows one never changes the ids of plans and results made before it.  Attach inverted
+ * indexes and star-trees at segment load, before queries reference the segment.
  */
 #ifndef PINOTGPU_H
 #define PINOTGPU_H
@@ -46,14 +54,18 @@ extern "C" {
 /* FieldSpec.DataType subset of dictionary-encoded single-value columns. */
 enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE = 3, PGPU_STRING = 4 };
 
-/* Forward-index formats: FixedBitSVForwardIndexReaderV2 (seglocal/segment/index/readers/forward/
- * FixedBitSVForwardIndexReaderV2.java:33-96: MSB-first big-endian bit packing, PinotDataBitSet layout) and
- * SortedIndexReaderImpl (seglocal/segment/index/readers/sorted/SortedIndexReaderImpl.java:37-116: BIG_ENDIAN
- * (startDocId, endDocId) int pairs per dictId). */
-/* Forward-index formats: FixedBitSVForwardIndexReaderV2 bytes; SortedIndexReaderImpl (start, end) pairs; a raw
- * (no-dictionary) fixed-width column as FixedByteChunkSVForwardIndexWriter writes it with PASS_THROUGH compression,
- * versions 2 / 3 (BaseChunkSVForwardIndexWriter.java:130-170; FixedByteChunkSVForwardIndexReader.java:30-110) --
- * cardinality 0, no dictionary; usable as an aggregation operand (SUM / MIN / MAX / AVG). */
+/* Forward-index formats:
+ *   PGPU_FWD_FIXED_BIT    FixedBitSVForwardIndexReaderV2 bytes (seglocal/segment/index/readers/forward/
+ *                         FixedBitSVForwardIndexReaderV2.java:33-96: MSB-first big-endian bit packing, PinotDataBitSet);
+ *   PGPU_FWD_SORTED_PAIRS SortedIndexReaderImpl (seglocal/segment/index/readers/sorted/SortedIndexReaderImpl.java:
+ *                         37-116: BIG_ENDIAN (startDocId, endDocId) int pairs per dictId);
+ *   PGPU_FWD_RAW_FIXED    a raw (no-dictionary) INT / LONG / FLOAT / DOUBLE column as FixedByteChunkSVForwardIndexWriter
+ *                         writes it, versions 2 / 3, chunks PASS_THROUGH, LZ4 or LZ4_LENGTH_PREFIXED
+ *                         (BaseChunkSVForwardIndexWriter.java:130-193; BaseChunkSVForwardIndexReader.java:56-154) --
+ *                         cardinality 0, no dictionary; decoded once at pin into per-doc values: an aggregation
+ *                         operand (SUM / MIN / MAX / AVG) and a raw-value predicate column (EQ / NOT_EQ / IN / NOT_IN /
+ *                         RANGE, RangePredicateEvaluatorFactory.java:60-102,268-448).  SNAPPY / ZSTANDARD chunks:
+ *                         PGPU_ERR_UNSUPPORTED. */
 enum pgpu_fwd_format { PGPU_FWD_FIXED_BIT = 0, PGPU_FWD_SORTED_PAIRS = 1, PGPU_FWD_RAW_FIXED = 2 };
 
 int pgpu_abi_version(void);
@@ -312,6 +324,14 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
 
 /* ---- results: AggregationGroupByResult (core/query/aggregation/groupby/AggregationGroupByResult.java:31-81) */
 int pgpu_result_num_groups(pgpu_result r, int64_t* n);
+/* The table-global dictionary that group-by column `key`'s ids index, as the result's plan saw it: a pin that grows
+ * the table's dictionary while the query runs does not re-label this result (GroupKeyGenerator.getKeys reads the
+ * segment dictionaries the operator was built on).  *snapshot_id identifies the snapshot (callers cache the values
+ * by it); *size its entries.  Values as for pgpu_table_dictionary_{i64,f64,str}. */
+int pgpu_result_key_dictionary(pgpu_result r, int key, uint64_t* snapshot_id, int64_t* size);
+int pgpu_result_key_dictionary_i64(pgpu_result r, int key, int64_t* out);
+int pgpu_result_key_dictionary_f64(pgpu_result r, int key, double* out);
+int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_t blob_cap, int64_t* offsets);
 /* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */
 int pgpu_result_group_ids(pgpu_result r, int32_t* out);
 /* Column `key` of the above ([n] dictIds of group-by column `key`): a plain copy, the layout the result holds. */
@@ -389,6 +409,13 @@ int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_st
  * plans created before a re-attach (or an unpin) keep the index they were planned on alive until destroyed. */
 int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
                                int64_t num_bytes);
+
+/* Host-side reader of a raw forward index (PGPU_FWD_RAW_FIXED bytes; FixedByteChunkSVForwardIndexReader.readValuesSV
+ * over every chunk, LZ4 chunks decompressed as LZ4Decompressor / LZ4WithLengthDecompressor do): num_docs values of a
+ * column of `data_type` -- INT / LONG into out_i64, every type as double into out_f64 (either may be NULL).  The
+ * decoder pgpu_pin_segment uses; pure host code. */
+int pgpu_raw_forward_index_values(const void* fwd, int64_t fwd_len, int32_t data_type, int32_t num_docs,
+                                  int64_t* out_i64, double* out_f64);
 
 /* Host-side bitmap inverted-index creator (OffHeapBitmapInvertedIndexCreator + BitmapInvertedIndexWriter,
  * seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:60-78) over a fixed-bit forward index: writes

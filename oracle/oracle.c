@@ -172,6 +172,109 @@ static inline int dict_str(const or_column* c, int id, const uint8_t** p) {
   return n;
 }
 
+/* LZ4 block decompression (the published LZ4 block format, as lz4-java's LZ4SafeDecompressor implements it for
+ * LZ4Decompressor / LZ4WithLengthDecompressor, seglocal/io/compression/LZ4Decompressor.java:40-50; lz4-java is a
+ * Maven dependency absent from /root/reference): a block is a sequence of (token, literal length extension bytes,
+ * literals, 2-byte little-endian match offset, match length extension bytes); token = literal length (high nibble)
+ * | match length - 4 (low nibble), 15 = extended by 255-continued bytes; the last sequence has literals only.
+ * Returns the decoded length, or -1 on malformed input or output overflow. */
+int64_t or_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  for (;;) {
+    if (ip >= n) return -1;
+    const int token = src[ip++];
+    int64_t lit = token >> 4;
+    if (lit == 15) {
+      int b;
+      do { if (ip >= n) return -1; b = src[ip++]; lit += b; } while (b == 255);
+    }
+    if (lit > n - ip || lit > cap - op) return -1;
+    memcpy(dst + op, src + ip, (size_t)lit);
+    ip += lit;
+    op += lit;
+    if (ip == n) return op;  /* the last sequence: literals only */
+    if (n - ip < 2) return -1;
+    const int64_t off = (int64_t)src[ip] | ((int64_t)src[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    int64_t ml = (token & 15);
+    if (ml == 15) {
+      int b;
+      do { if (ip >= n) return -1; b = src[ip++]; ml += b; } while (b == 255);
+    }
+    ml += 4;
+    if (ml > cap - op) return -1;
+    for (int64_t k = 0; k < ml; k++, op++) dst[op] = dst[op - off]; /* overlapping copies repeat the pattern */
+  }
+}
+
+/* FixedByteChunkSVForwardIndexReader over every chunk (BaseChunkSVForwardIndexReader.java:56-154): header (version,
+ * numChunks, numDocsPerChunk, sizeOfEntry; version >= 2: totalDocs, compression type, dataHeaderStart), chunk
+ * offsets (int for versions 1-2, long for 3), each chunk decompressed on its own (getChunkPosition; the last chunk
+ * runs to the end of the buffer).  Compression: PASS_THROUGH (0), LZ4 (3), LZ4_LENGTH_PREFIXED (4).  Values are the
+ * big-endian entries: ival gets INT / LONG values, dval every value as a double.  Returns 0, -1 on malformed bytes,
+ * -2 on an unsupported codec. */
+int or_raw_decode(const or_column* c, const uint8_t* b, int64_t len, int num_docs, int64_t* ival, double* dval) {
+  if (len < 16) return -1;
+  const int version = (int)be32(b), num_chunks = (int)be32(b + 4), per_chunk = (int)be32(b + 8);
+  const int size = (int)be32(b + 12);
+  int compression = 1, header_start = 16;
+  if (version > 1) {
+    if (len < 28) return -1;
+    compression = (int)be32(b + 20);
+    header_start = (int)be32(b + 24);
+  }
+  if (compression != 0 && compression != 3 && compression != 4) return -2;
+  const int entry = version <= 2 ? 4 : 8;
+  if (per_chunk <= 0 || num_chunks < 0 || (int64_t)num_chunks * per_chunk < num_docs || header_start < 0 ||
+      (size != 4 && size != 8))
+    return -1;
+  const int64_t raw_start = (int64_t)header_start + (int64_t)num_chunks * entry;
+  if (raw_start > len) return -1;
+  uint8_t* chunk = compression ? malloc((size_t)per_chunk * size) : NULL;
+  for (int k = 0; k < num_chunks && (int64_t)k * per_chunk < num_docs; k++) {
+    const uint8_t* vals;
+    const int d0 = k * per_chunk;
+    const int nd = num_docs - d0 < per_chunk ? num_docs - d0 : per_chunk;
+    if (compression == 0) {
+      /* PASS_THROUGH: FixedByteChunkSVForwardIndexReader reads docId * size from rawDataStart */
+      if (raw_start + (int64_t)(d0 + nd) * size > len) { free(chunk); return -1; }
+      vals = b + raw_start + (int64_t)d0 * size;
+    } else {
+      const uint8_t* hp = b + header_start + (int64_t)k * entry;
+      const int64_t pos = entry == 4 ? (int64_t)be32(hp) : (int64_t)be64(hp);
+      const int64_t end = k == num_chunks - 1 ? len : (entry == 4 ? (int64_t)be32(hp + 4) : (int64_t)be64(hp + 8));
+      if (pos < raw_start || end < pos || end > len) { free(chunk); return -1; }
+      const uint8_t* src = b + pos;
+      int64_t sn = end - pos;
+      if (compression == 4) { /* LZ4DecompressorWithLength: little-endian decompressed length first */
+        if (sn < 4) { free(chunk); return -1; }
+        src += 4;
+        sn -= 4;
+      }
+      const int64_t got = or_lz4_decompress(src, sn, chunk, (int64_t)per_chunk * size);
+      if (got < (int64_t)nd * size) { free(chunk); return -1; }
+      vals = chunk;
+    }
+    for (int i = 0; i < nd; i++) {
+      const uint8_t* v = vals + (int64_t)i * size;
+      const uint64_t hi = be32(v), lo = size == 8 ? be32(v + 4) : 0;
+      double d;
+      int64_t x = 0;
+      switch (c->data_type) {
+        case OR_INT: x = (int32_t)hi; d = (double)x; break;
+        case OR_LONG: x = (int64_t)((hi << 32) | lo); d = (double)x; break;
+        case OR_FLOAT: { uint32_t u = (uint32_t)hi; float f; memcpy(&f, &u, 4); d = (double)f; break; }
+        default: { uint64_t u = (hi << 32) | lo; memcpy(&d, &u, 8); break; }
+      }
+      if (ival) ival[d0 + i] = x;
+      if (dval) dval[d0 + i] = d;
+    }
+  }
+  free(chunk);
+  return 0;
+}
+
 /* Dictionary.readDoubleValues -> getDoubleValue per type (IntDictionary.java:62-64 etc.). */
 double or_raw_get_double(const or_column* c, int doc) {
   const uint8_t* b = c->fwd;
@@ -417,12 +520,116 @@ int or_build_column_str(const uint8_t* blob, const int64_t* offsets, int64_t n, 
 /* One dictionary-based PredicateEvaluator for one segment (core/operator/filter/predicate/). */
 typedef struct {
   int always_true, always_false;
-  int kind;         /* 0 = range [start,end), 1 = dictId set, 2 = single id, 3 = not single id, 4 = not in set */
+  int kind;         /* 0 = range [start,end), 1 = dictId set, 2 = single id, 3 = not single id, 4 = not in set,
+                       5 = raw-value evaluator (no-dictionary column) */
   int start, end;
   int id;
   uint8_t* set;     /* card flags for kinds 1 / 4 */
   int num_matching;
+  /* kind 5 (BaseRawValueBasedPredicateEvaluator subclasses): the column's values per doc, decoded from its chunks */
+  int ptype, dtype;                 /* predicate type, column data type */
+  int64_t* rival;                   /* INT / LONG values */
+  double* rdval;                    /* FLOAT / DOUBLE values (widened) */
+  int64_t ilo, ihi;                 /* RANGE / EQ / NOT_EQ bounds (integers) */
+  double dlo, dhi;                  /* RANGE / EQ / NOT_EQ bounds (FLOAT: float values) */
+  int lo_inc, hi_inc;
+  int64_t* vset;                    /* IN / NOT_IN: Integer/Long values, or doubleToLongBits / floatToIntBits */
+  int nvset;
 } pred_eval;
+
+static void pred_eval_free(pred_eval* e) {
+  free(e->set); free(e->rival); free(e->rdval); free(e->vset);
+  e->set = NULL; e->rival = NULL; e->rdval = NULL; e->vset = NULL;
+}
+
+/* Double.doubleToLongBits / Float.floatToIntBits (canonical NaN): the equality of fastutil's Double / Float
+ * OpenHashSets (fastutil 8.2.3, absent here) behind InPredicateEvaluatorFactory's raw IN evaluators. */
+static int64_t java_double_bits(double d) {
+  if (d != d) return 0x7ff8000000000000LL;
+  int64_t b; memcpy(&b, &d, 8); return b;
+}
+static int64_t java_float_bits(float f) {
+  if (f != f) return 0x7fc00000;
+  int32_t b; memcpy(&b, &f, 4); return b;
+}
+
+/* Literal conversion of the raw evaluators: Integer.parseInt / Long.parseLong / Float.parseFloat /
+ * Double.parseDouble (RangePredicateEvaluatorFactory.java:65-102, EqualsPredicateEvaluatorFactory.java:60-70,
+ * InPredicateEvaluatorFactory.java:69-126). */
+static int parse_java_long(const char* s, int64_t lo, int64_t hi, int64_t* out);
+static int raw_literal(int dtype, const char* s, int64_t* iv, double* dv) {
+  if (dtype == OR_INT) return parse_java_long(s, INT32_MIN, INT32_MAX, iv);
+  if (dtype == OR_LONG) return parse_java_long(s, INT64_MIN, INT64_MAX, iv);
+  char* end = NULL;
+  double d = strtod(s, &end);
+  if (end == s) return -1;
+  while (*end == 'd' || *end == 'D' || *end == 'f' || *end == 'F') end++;
+  if (*end) return -1;
+  *dv = dtype == OR_FLOAT ? (double)(float)d : d;
+  return 0;
+}
+
+static int build_raw_eval(const or_segment* seg, const or_column* c, const or_predicate* p, pred_eval* e) {
+  e->kind = 5;
+  e->ptype = p->type;
+  e->dtype = c->data_type;
+  const int fp = c->data_type == OR_FLOAT || c->data_type == OR_DOUBLE;
+  const int nd = seg->num_docs > 0 ? seg->num_docs : 1;
+  if (fp) e->rdval = malloc(sizeof(double) * (size_t)nd);
+  else e->rival = malloc(sizeof(int64_t) * (size_t)nd);
+  if (c->data_type == OR_STRING || or_raw_decode(c, c->fwd, c->fwd_len, seg->num_docs, e->rival, e->rdval))
+    return -3;
+  switch (p->type) {
+    case OR_PRED_EQ: case OR_PRED_NOT_EQ:
+      if (raw_literal(c->data_type, p->values[0], &e->ilo, &e->dlo)) return -2;
+      return 0;
+    case OR_PRED_IN: case OR_PRED_NOT_IN:
+      e->vset = malloc(sizeof(int64_t) * (size_t)(p->num_values ? p->num_values : 1));
+      for (int i = 0; i < p->num_values; i++) {
+        int64_t iv = 0; double dv = 0;
+        if (raw_literal(c->data_type, p->values[i], &iv, &dv)) return -2;
+        e->vset[e->nvset++] = !fp ? iv : c->data_type == OR_FLOAT ? java_float_bits((float)dv) : java_double_bits(dv);
+      }
+      return 0;
+    default: { /* RANGE: unbounded = inclusive MIN / MAX (-inf / +inf) of the type */
+      const char* lo = p->values[0];
+      const char* hi = p->values[1];
+      const int lu = strcmp(lo, "*") == 0, hu = strcmp(hi, "*") == 0;
+      e->lo_inc = lu || p->lower_inclusive;
+      e->hi_inc = hu || p->upper_inclusive;
+      if (lu) { e->ilo = c->data_type == OR_INT ? INT32_MIN : INT64_MIN; e->dlo = -INFINITY; }
+      else if (raw_literal(c->data_type, lo, &e->ilo, &e->dlo)) return -2;
+      if (hu) { e->ihi = c->data_type == OR_INT ? INT32_MAX : INT64_MAX; e->dhi = INFINITY; }
+      else if (raw_literal(c->data_type, hi, &e->ihi, &e->dhi)) return -2;
+      return 0;
+    }
+  }
+}
+
+/* applySV of the raw evaluators (RangePredicateEvaluatorFactory.java:268-448 Int/Long/Float/Double...Range, Equals
+ * :113-187 `==`, NotEquals `!=`, In / NotIn: set contains). */
+static int raw_apply(const pred_eval* e, int doc) {
+  const int fp = e->rdval != NULL;
+  switch (e->ptype) {
+    case OR_PRED_EQ: return fp ? e->rdval[doc] == e->dlo : e->rival[doc] == e->ilo;
+    case OR_PRED_NOT_EQ: return fp ? e->rdval[doc] != e->dlo : e->rival[doc] != e->ilo;
+    case OR_PRED_IN: case OR_PRED_NOT_IN: {
+      const int64_t k = !fp ? e->rival[doc] : e->dtype == OR_FLOAT ? java_float_bits((float)e->rdval[doc])
+                                                                   : java_double_bits(e->rdval[doc]);
+      int hit = 0;
+      for (int i = 0; i < e->nvset && !hit; i++) hit = e->vset[i] == k;
+      return e->ptype == OR_PRED_IN ? hit : !hit;
+    }
+    default:
+      if (fp) {
+        const double v = e->rdval[doc];
+        return (e->lo_inc ? e->dlo <= v : e->dlo < v) && (e->hi_inc ? e->dhi >= v : e->dhi > v);
+      } else {
+        const int64_t v = e->rival[doc];
+        return (e->lo_inc ? e->ilo <= v : e->ilo < v) && (e->hi_inc ? e->ihi >= v : e->ihi > v);
+      }
+  }
+}
 
 static int dict_index_of(const or_column* c, const char* lit, int* err) {
   int idx = or_dict_insertion_index_of(c, lit, err);
@@ -434,6 +641,12 @@ static int build_pred_eval(const or_segment* seg, const or_predicate* p, pred_ev
   if (p->column < 0 || p->column >= seg->num_columns) { snprintf(msg, ml, "bad predicate column"); return -1; }
   const or_column* c = &seg->columns[p->column];
   int err = 0;
+  if (c->raw) { /* no dictionary: a raw-value evaluator, never always-true / always-false (FilterPlanNode) */
+    const int st = build_raw_eval(seg, c, p, e);
+    if (st == -2) goto bad;
+    if (st) { snprintf(msg, ml, "raw forward index of column %d is unreadable", p->column); pred_eval_free(e); return -1; }
+    return 0;
+  }
   switch (p->type) {
     case OR_PRED_EQ: { /* EqualsPredicateEvaluatorFactory.java:86-99 */
       int id = dict_index_of(c, p->values[0], &err);
@@ -495,7 +708,7 @@ static int build_pred_eval(const or_segment* seg, const or_predicate* p, pred_ev
   }
 bad:
   snprintf(msg, ml, "BadQueryRequestException: cannot convert literal for column %d", p->column);
-  free(e->set); e->set = NULL;
+  pred_eval_free(e);
   return -2;
 }
 
@@ -630,6 +843,7 @@ static int node_match(const fnode* n, const or_segment* seg, const pred_eval* ev
     case FN_ALL: return 1;
     case FN_SCAN: case FN_SORTED: case FN_BITMAP: {
       const or_column* c = &seg->columns[q->predicates[n->pred].column];
+      if (evals[n->pred].kind == 5) return raw_apply(&evals[n->pred], doc);
       return pred_apply(&evals[n->pred], fixedbit_read(c->fwd, doc, c->bits));
     }
     case FN_AND: for (int i = 0; i < n->nchild; i++) if (!node_match(n->child[i], seg, evals, q, doc)) return 0; return 1;
@@ -1086,10 +1300,10 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   pred_eval* evals = calloc((size_t)(np ? np : 1), sizeof(pred_eval));
   for (int i = 0; i < np; i++) {
     int st = build_pred_eval(seg, &q->predicates[i], &evals[i], r->msg, sizeof r->msg);
-    if (st) { r->status = st; for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return; }
+    if (st) { r->status = st; for (int j = 0; j < i; j++) pred_eval_free(&evals[j]); free(evals); return; }
   }
   fnode* root = build_filter_tree(seg, q, evals, r->msg, sizeof r->msg);
-  if (!root) { r->status = -1; for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return; }
+  if (!root) { r->status = -1; for (int j = 0; j < np; j++) pred_eval_free(&evals[j]); free(evals); return; }
   iter_pool pool = {0};
   iter* it = it_build(root, seg, evals, q, &pool);
 
@@ -1131,6 +1345,18 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   int32_t* mids = malloc(sizeof(int32_t) * MAX_DOC_PER_CALL);
   double* dvals = malloc(sizeof(double) * MAX_DOC_PER_CALL);
   int nproj = num_projected(q);
+  /* raw aggregation operands: the column's chunks decoded once per segment (ChunkReaderContext caches the chunk in
+   * use; the values read are the same) */
+  double** raw_vals = calloc((size_t)q->num_aggs + 1, sizeof(double*));
+  for (int a = 0; a < q->num_aggs; a++) {
+    const or_column* c = q->aggs[a].column >= 0 ? &seg->columns[q->aggs[a].column] : NULL;
+    if (!c || !c->raw) continue;
+    raw_vals[a] = malloc(sizeof(double) * (size_t)(seg->num_docs > 0 ? seg->num_docs : 1));
+    if (or_raw_decode(c, c->fwd, c->fwd_len, seg->num_docs, NULL, raw_vals[a])) {
+      snprintf(r->msg, sizeof r->msg, "raw forward index of column %d is unreadable", q->aggs[a].column);
+      r->status = -1;
+    }
+  }
 
   int eof = 0;
   while (!eof) {
@@ -1200,7 +1426,7 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
       }
       const or_column* c = &seg->columns[ag->column];
       if (c->raw) { /* DataFetcher.readDoubleValues on a raw column: ForwardIndexReader.readValuesSV */
-        for (int d = 0; d < pos; d++) dvals[d] = or_raw_get_double(c, docs[d]);
+        for (int d = 0; d < pos; d++) dvals[d] = raw_vals[a][docs[d]];
       } else {
         or_read_dict_ids(c->fwd, c->bits, seg->num_docs, docs, pos, mids);   /* DataFetcher.readDoubleValues */
         for (int d = 0; d < pos; d++) dvals[d] = or_dict_get_double(c, mids[d]);
@@ -1273,10 +1499,12 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   if (g.holder == OR_HOLDER_INT_MAP) free(g.imap.kv);
   if (g.holder == OR_HOLDER_LONG_MAP || g.holder == OR_HOLDER_ARRAY_MAP) gm_free(&g.gmap);
   free(docs); free(gids); free(mids); free(dvals);
+  for (int a = 0; a < q->num_aggs; a++) free(raw_vals[a]);
+  free(raw_vals);
   for (int i = 0; i < g.nk; i++) free(dids[i]);
   pool_free(&pool);
   fn_free(root);
-  for (int j = 0; j < np; j++) free(evals[j].set);
+  for (int j = 0; j < np; j++) pred_eval_free(&evals[j]);
   free(evals);
 }
 
@@ -1424,15 +1652,15 @@ int or_filter_bitmap(const or_segment* seg, const or_query* q, uint64_t* bits, c
   pred_eval* evals = calloc((size_t)(np ? np : 1), sizeof(pred_eval));
   for (int i = 0; i < np; i++) {
     int st = build_pred_eval(seg, &q->predicates[i], &evals[i], msg, ml);
-    if (st) { for (int j = 0; j < i; j++) free(evals[j].set); free(evals); return st; }
+    if (st) { for (int j = 0; j < i; j++) pred_eval_free(&evals[j]); free(evals); return st; }
   }
   fnode* root = build_filter_tree(seg, q, evals, msg, ml);
-  if (!root) { for (int j = 0; j < np; j++) free(evals[j].set); free(evals); return -1; }
+  if (!root) { for (int j = 0; j < np; j++) pred_eval_free(&evals[j]); free(evals); return -1; }
   memset(bits, 0, sizeof(uint64_t) * (size_t)((seg->num_docs + 63) / 64));
   for (int d = 0; d < seg->num_docs; d++)
     if (node_match(root, seg, evals, q, d)) bits[d >> 6] |= 1ull << (d & 63);
   fn_free(root);
-  for (int j = 0; j < np; j++) free(evals[j].set);
+  for (int j = 0; j < np; j++) pred_eval_free(&evals[j]);
   free(evals);
   return 0;
 }

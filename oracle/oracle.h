@@ -54,11 +54,19 @@ typedef struct {
   const uint8_t* fwd;   /* MSB-first packed dictIds (FixedBitSVForwardIndexWriter.java:39-50), or for a raw column the
                            FixedByteChunkSVForwardIndexWriter bytes (PASS_THROUGH chunks) */
   int32_t raw;          /* 1: no-dictionary column (cardinality 0), values read by FixedByteChunkSVForwardIndexReader */
+  int64_t fwd_len;      /* bytes of fwd (raw columns: the chunk file, whose last chunk runs to its end) */
 } or_column;
 
 /* FixedByteChunkSVForwardIndexReader.getInt / getLong / getFloat / getDouble on an uncompressed (PASS_THROUGH)
  * file (BaseChunkSVForwardIndexReader.java:57-98: header, chunk offsets, raw data from rawDataStart). */
 double or_raw_get_double(const or_column* c, int doc);
+/* LZ4 block decompression (LZ4Decompressor / LZ4WithLengthDecompressor, seglocal/io/compression/): decoded length, or
+ * -1 on malformed input / output overflow. */
+int64_t or_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+/* Every value of a raw column's forward index (BaseChunkSVForwardIndexReader.java:56-154, PASS_THROUGH / LZ4 /
+ * LZ4_LENGTH_PREFIXED chunks): INT / LONG into ival, all types as double into dval (either may be NULL).
+ * 0, -1 malformed, -2 unsupported codec. */
+int or_raw_decode(const or_column* c, const uint8_t* fwd, int64_t len, int num_docs, int64_t* ival, double* dval);
 
 typedef struct {
   int32_t num_docs;

@@ -57,6 +57,7 @@ class PredicateC(ctypes.Structure):
 # pgpu_leaf_type: Pinot's leaf operator of a predicate in one segment (pgpu_filter_entries_scanned)
 OPT_NO_STAR_TREE = 1
 OPT_SQL_GROUP_BY = 2
+OPT_NO_PLAN_CACHE = 4
 LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP = 0, 1, 2, 3, 4
 
 
@@ -154,6 +155,7 @@ _PROTOS = {
     "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_attach_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),
     "pgpu_build_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32, c_voidp, c_i64, c_i64p]),
+    "pgpu_raw_forward_index_values": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i64p, c_f64p]),
     "pgpu_startree_build": (c_int, [ctypes.POINTER(SegmentDesc), c_i32p, c_i32p, c_i32, c_i32p, c_i32,
                                     ctypes.POINTER(AggC), c_i32, c_i32, ctypes.POINTER(c_voidp)]),
     "pgpu_startree_load": (c_int, [c_voidp, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32, c_char_pp, c_i32p,
@@ -162,6 +164,10 @@ _PROTOS = {
     "pgpu_startree_num_raw_records": (c_int, [c_voidp, c_i32p]),
     "pgpu_startree_destroy": (c_int, [c_voidp]),
     "pgpu_result_num_groups": (c_int, [c_voidp, c_i64p]),
+    "pgpu_result_key_dictionary": (c_int, [c_voidp, c_int, c_u64p, c_i64p]),
+    "pgpu_result_key_dictionary_i64": (c_int, [c_voidp, c_int, c_i64p]),
+    "pgpu_result_key_dictionary_f64": (c_int, [c_voidp, c_int, c_f64p]),
+    "pgpu_result_key_dictionary_str": (c_int, [c_voidp, c_int, c_u8p, c_i64, c_i64p]),
     "pgpu_result_group_ids": (c_int, [c_voidp, c_i32p]),
     "pgpu_result_group_ids_column": (c_int, [c_voidp, c_int, c_i32p]),
     "pgpu_result_group_ids_view": (c_int, [c_voidp, c_int, ctypes.POINTER(c_voidp)]),

@@ -191,6 +191,36 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
 }
 
+// Raw-value leaf test of one 32-doc group (raw_leaf_bitmap_kernel): the docs' int64 keys (contiguous: the compiler
+// pairs the loads into 16-byte ones) against inclusive bounds [lo, hi] (LEAF_RAW_RANGE) or the `hi` sorted keys at
+// set_keys (LEAF_RAW_IN).
+__device__ __forceinline__ uint32_t raw_group_mask(int kind, int64_t lo, int64_t hi, const int64_t* set_keys,
+                                                   const int64_t* keys, int64_t group) {
+  gmem<int64_t>* __restrict__ s = gp(set_keys);
+  gmem<int64_t>* __restrict__ v = gp(keys) + group * 32;
+  uint32_t m = 0;
+  if (kind == LEAF_RAW_RANGE) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int64_t x = v[i];
+      m |= (uint32_t)(lo <= x && x <= hi) << i;
+    }
+  } else {
+    const int n = (int)hi;
+    for (int i = 0; i < 32; ++i) {
+      const int64_t key = v[i];
+      int a = 0, b = n;  // first set key >= key
+      while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (s[mid] < key) a = mid + 1;
+        else b = mid;
+      }
+      m |= (uint32_t)(a < n && s[a] == key) << i;
+    }
+  }
+  return m;
+}
+
 __device__ __forceinline__ uint32_t leaf_mask(const KLeaf& L, const KCol& C, int64_t group) {
   return leaf_eval(L.kind, L.negate, L.lo, L.span, L.set, C.fwd, C.bits, group);
 }
@@ -375,7 +405,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
                                                 const bool (&ok)[NB], uint64_t* __restrict__ tbl, int64_t G) {
   int64_t key[NB];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) key[b] = 0;
+  for (int b = 0; b < NB; ++b) key[b] = -p.key_bias;  // filter-restricted key space (0 for hash / staged keys)
   int st = 0;  // MODE_HASH key stages (key spaces beyond 64 bits)
   for (int j = 0; j < p.num_keys; ++j) {
     const int kc = p.key_col[j];
@@ -501,7 +531,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
   uint32_t ids[16];
   int32_t key[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) key[i] = 0;
+  for (int i = 0; i < 16; ++i) key[i] = -(int32_t)p.key_bias;  // dense key spaces: < 2^31 after the bias
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);

@@ -81,6 +81,8 @@ struct pgpu_result_s {
   // what the rows are (DataTable / trimming): table columns and types of the group-by keys, per aggregation its
   // function and table column (-1: COUNT(*)), and numGroupsLimitReached
   std::vector<int32_t> key_cols, key_types, agg_fn, agg_col;
+  // per group-by key: the table-global dictionary snapshot its group ids index (runtime.cpp's Dict)
+  std::vector<std::shared_ptr<const void>> key_dicts;
   bool groups_limit_reached = false;
   ~pgpu_result_s() {
     if (pool) pool->give(buf);
@@ -103,6 +105,7 @@ namespace pgpu {
 
 // Read-only view of a table-global dictionary (group ids of results index it), for the response code.
 struct DictView {
+  std::shared_ptr<const void> keep;  // the snapshot the pointers below point into
   int type = PGPU_INT;
   const std::vector<int64_t>* iv = nullptr;
   const std::vector<double>* dv = nullptr;
@@ -110,5 +113,7 @@ struct DictView {
   std::string name;
 };
 int table_dict_view(pgpu_table t, int col, DictView* out);
+// The dictionary snapshot group-by key `key` of result r indexes (the table's current one for results without).
+int result_key_dict_view(const pgpu_result_s* r, pgpu_table t, int key, DictView* out);
 
 }  // namespace pgpu

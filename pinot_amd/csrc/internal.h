@@ -36,7 +36,11 @@ constexpr int kFastLeaves = 4;              // pure-AND programs up to this many
 // LEAF_BITMAP: a predicate on a column with a bitmap inverted index (BitmapBasedFilterOperator, core/operator/filter/
 // BitmapBasedFilterOperator.java:63-100): `set` is the segment's materialised docId bitmap (bit i of word g = doc
 // 32g + i), the OR of the matching dictIds' Roaring bitmaps, built per query by inv_materialize_kernel.
-enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4, LEAF_BITMAP = 5 };
+// LEAF_RAW_RANGE / LEAF_RAW_IN: host-side kinds of a raw-value predicate on a no-dictionary column
+// (RangePredicateEvaluatorFactory / InPredicateEvaluatorFactory raw evaluators).  raw_leaf_bitmap_kernel evaluates
+// them per query into a docId bitmap (KRawTask), which the scans read as a LEAF_BITMAP leaf.
+enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4, LEAF_BITMAP = 5,
+                          LEAF_RAW_RANGE = 6, LEAF_RAW_IN = 7 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
 enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
 enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };
@@ -93,6 +97,7 @@ struct KParams {
   int32_t key_col[kMaxKeys];
   int64_t key_stride[kMaxKeys];
   int64_t num_keys_total;  // dense table width G, or hash capacity
+  int64_t key_bias;        // subtracted from every composite key (filter-restricted key spaces; 0 otherwise)
   int32_t num_slots;
   int32_t slot_kind[kMaxSlots];
   int32_t slot_col[kMaxSlots];
@@ -164,6 +169,7 @@ struct KStarParams {
   int32_t num_slots;
   int64_t key_stride[kMaxKeys];
   int64_t num_keys_total;
+  int64_t key_bias;                       // as KParams.key_bias
   int32_t slot_kind[kMaxSlots];
   int32_t slot_int[kMaxSlots];            // 1: the slot's column is INT/LONG (MIN/MAX keys are the value)
   int32_t lds_table_words;
@@ -239,6 +245,26 @@ struct KBitBlock {
   int32_t num_tasks;
 };
 
+// One raw-value leaf of one segment (ScanBasedFilterOperator over a raw forward index with a raw-value
+// PredicateEvaluator): the column's per-doc int64 keys (integer value, or order-preserving key of the double; padded
+// to whole 32-doc groups) tested against [lo, hi] (LEAF_RAW_RANGE) or the hi sorted keys raw_vals[lo, lo + hi)
+// (LEAF_RAW_IN), negated for NOT_EQ / NOT_IN, into ceil(num_docs / 32) docbits words from `dst` (bits past numDocs
+// clear).
+struct KRawTask {
+  const int64_t* keys;
+  int64_t dst;
+  int64_t lo, hi;
+  int32_t num_docs;
+  int32_t kind;
+  int32_t negate;
+  int32_t pad;
+};
+// raw_leaf_bitmap_kernel work item: groups [group0, group0 + 256) of task `task`.
+struct KRawJob {
+  int32_t task;
+  int32_t group0;
+};
+
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
@@ -260,7 +286,8 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
 // compact_ordered_chunks(num_keys) u32.
 int64_t compact_ordered_chunks(int64_t num_keys);
 int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
-                           const int64_t* key_stride, const int64_t* key_card, int32_t num_key_cols,
+                           const int64_t* key_stride, const int64_t* key_card, const int64_t* key_off,
+                           int32_t num_key_cols,
                            uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream);
 // Partitioned group-by (k_partition.hip): K8a count, scan, K8c scatter, K8d aggregate into p.base.table.
@@ -280,6 +307,8 @@ int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_se
 int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream);
+int launch_raw_leaf_bitmaps(const KRawJob* jobs, int64_t num_jobs, const KRawTask* tasks, const int64_t* raw_vals,
+                            uint32_t* docbits, void* stream);
 constexpr int kStarMaxSegs = 4096;  // star-tree segments per K6 launch (their group prefix lives in LDS)
 int launch_deadline_gate(uint64_t deadline, unsigned long long* stats, void* stream);
 int launch_startree_traverse(const KStarSeg* segs, int32_t num_segs, int64_t* seg_total, uint64_t deadline,

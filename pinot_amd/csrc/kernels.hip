@@ -249,6 +249,7 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(uint32_t* __restrict
 struct KeyDecode {
   int64_t stride[kMaxKeys];
   int64_t card[kMaxKeys];
+  int64_t off[kMaxKeys];  // first global id of each key digit
   int64_t base;  // composite key of table column 0 (a key-range shard of the table)
   int32_t n;
 };
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint64_t* __
       const int64_t j = (int64_t)pos + before + rank;
       if (j < cap) {
         for (int c = 0; c < kd.n; ++c)
-          gid[(int64_t)c * cap + j] = (int32_t)(((kd.base + k) / kd.stride[c]) % kd.card[c]);
+          gid[(int64_t)c * cap + j] = (int32_t)(((kd.base + k) / kd.stride[c]) % kd.card[c] + kd.off[c]);
         for (int s = 0; s < num_slots; ++s) words[(int64_t)s * cap + j] = table[(int64_t)s * num_keys + k];
       }
     }
@@ -455,6 +456,33 @@ int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, i
   return PGPU_HIP_OK(hipGetLastError());
 }
 
+// Raw-value filter leaves: one thread per 32-doc group writes its docbits word (raw_group_mask, negated for
+// NOT_EQ / NOT_IN, bits past numDocs cleared).  The scans then read the leaf as a LEAF_BITMAP.
+__global__ __launch_bounds__(256) void raw_leaf_bitmap_kernel(const KRawJob* __restrict__ jobs,
+                                                              const KRawTask* __restrict__ tasks,
+                                                              const int64_t* __restrict__ raw_vals,
+                                                              uint32_t* __restrict__ docbits) {
+  const KRawJob J = jobs[blockIdx.x];
+  const KRawTask T = tasks[J.task];
+  const int64_t g = (int64_t)J.group0 + threadIdx.x;
+  const int64_t ngroups = ((int64_t)T.num_docs + 31) >> 5;
+  if (g >= ngroups) return;
+  uint32_t m = raw_group_mask(T.kind, T.lo, T.hi, T.kind == LEAF_RAW_IN ? raw_vals + T.lo : nullptr, T.keys, g);
+  if (T.negate) m = ~m;
+  const int64_t rem = (int64_t)T.num_docs - (g << 5);
+  if (rem < 32) m &= (1u << rem) - 1u;
+  docbits[T.dst + g] = m;
+}
+
+int launch_raw_leaf_bitmaps(const KRawJob* jobs, int64_t num_jobs, const KRawTask* tasks, const int64_t* raw_vals,
+                            uint32_t* docbits, void* stream) {
+  if (num_jobs <= 0) return 0;
+  if (num_jobs > INT32_MAX) return -1;
+  hipLaunchKernelGGL(raw_leaf_bitmap_kernel, dim3((unsigned)num_jobs), dim3(256), 0, S(stream), jobs, tasks, raw_vals,
+                     docbits);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
 int launch_inv_materialize(const KBitBlock* blocks, int64_t num_blocks, const KBitTask* tasks, uint32_t* docbits,
                            void* stream) {
   if (num_blocks <= 0) return 0;
@@ -564,15 +592,19 @@ int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream) {
 int64_t compact_ordered_chunks(int64_t num_keys) { return (num_keys + kCompactChunk - 1) / kCompactChunk; }
 
 int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
-                           const int64_t* key_stride, const int64_t* key_card, int32_t num_key_cols,
-                           uint32_t* chunk_scratch,
+                           const int64_t* key_stride, const int64_t* key_card, const int64_t* key_off,
+                           int32_t num_key_cols, uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream) {
   const int64_t nch = compact_ordered_chunks(num_keys);
   if (nch < 1 || nch > INT32_MAX || num_key_cols > kMaxKeys || (cap & 1)) return -1;
   KeyDecode kd{};
   kd.n = num_key_cols;
   kd.base = key_base;
-  for (int j = 0; j < num_key_cols; ++j) { kd.stride[j] = key_stride[j]; kd.card[j] = key_card[j]; }
+  for (int j = 0; j < num_key_cols; ++j) {
+    kd.stride[j] = key_stride[j];
+    kd.card[j] = key_card[j];
+    kd.off[j] = key_off[j];
+  }
   hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch);
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);
   hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_slots, num_keys,

@@ -41,7 +41,7 @@ template <int H>
 __device__ __forceinline__ void part_keys(const KParams& p, const SegView& S, int64_t group, int32_t (&key)[16]) {
   uint32_t ids[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) key[i] = 0;
+  for (int i = 0; i < 16; ++i) key[i] = -(int32_t)p.key_bias;
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);

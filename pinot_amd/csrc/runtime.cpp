@@ -8,6 +8,11 @@
 //           over the table-global dictionaries), result decoding;
 //   device: everything per document (kernels.hip).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
@@ -22,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <list>
 #include <map>
 #include <unordered_map>
@@ -42,6 +48,60 @@ using namespace pgpu;
 
 // ================================================================================================ errors
 namespace {
+
+// PGPU_CRASH_TRACE=1 (diagnostics): on SIGSEGV / SIGBUS / SIGABRT print the faulting address and the native frames
+// (backtrace_symbols_fd: object, symbol or offset -- resolve offsets with addr2line -f -C -e <object>), then hand the
+// signal to the previously installed handler (Python's faulthandler prints the Python stacks).
+struct sigaction g_prev_segv, g_prev_bus, g_prev_abrt;
+void crash_trace_handler(int sig, siginfo_t* si, void* uc) {
+  char line[160];
+  int len = snprintf(line, sizeof line, "[pgpu] fatal signal %d at address %p (thread %lu)\n", sig,
+                     si ? si->si_addr : nullptr, (unsigned long)pthread_self());
+  if (len > 0) { ssize_t w = write(2, line, (size_t)len); (void)w; }
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  for (int i = 0; i < n; ++i) {  // offsets into their objects, for addr2line
+    Dl_info info;
+    if (dladdr(frames[i], &info) && info.dli_fname) {
+      len = snprintf(line, sizeof line, "[pgpu]   #%d %s +0x%lx\n", i, info.dli_fname,
+                     (unsigned long)((uintptr_t)frames[i] - (uintptr_t)info.dli_fbase));
+      if (len > 0) { ssize_t w = write(2, line, (size_t)len); (void)w; }
+    }
+  }
+  const struct sigaction* prev = sig == SIGSEGV ? &g_prev_segv : sig == SIGBUS ? &g_prev_bus : &g_prev_abrt;
+  if (prev->sa_flags & SA_SIGINFO) {
+    if (prev->sa_sigaction) { prev->sa_sigaction(sig, si, uc); return; }
+  } else if (prev->sa_handler != SIG_DFL && prev->sa_handler != SIG_IGN && prev->sa_handler) {
+    prev->sa_handler(sig);
+    return;
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+struct CrashTraceInstaller {
+  void install() {
+    const char* v = getenv("PGPU_CRASH_TRACE");
+    if (!v || v[0] != '1') return;
+    void* warm[2];
+    backtrace(warm, 2);  // loads the unwinder now, not inside the handler
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = crash_trace_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
+    static const char msg[] = "[pgpu] crash trace installed\n";
+    ssize_t w = write(2, msg, sizeof msg - 1);
+    (void)w;
+  }
+};
+void install_crash_trace() {
+  static std::once_flag once;
+  std::call_once(once, [] { CrashTraceInstaller().install(); });
+}
 
 thread_local std::string g_err;
 
@@ -131,6 +191,16 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Device memory owned through shared_ptr: freed with its last owner.  A column's LUT is rebuilt out of place when
+// the table-global dictionary grows, so a plan still running keeps reading the LUT it was planned with.
+struct DevMem {
+  void* p = nullptr;
+  DevMem() = default;
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+  ~DevMem() { if (p) hipFree(p); }
+};
+
 // Host worker pool for per-query planning of long segment lists (the per-segment predicate translation that
 // Pinot runs on its query worker threads, one task per segment: BaseCombineOperator.java:85-115).  Workers are
 // started once and parked on a condition variable; run() executes fn(0..n-1) on the workers and the caller.
@@ -163,7 +233,9 @@ class HostPool {
     for (int i; (i = next_.fetch_add(1)) < n;) { fn(i); ++mine; }
     std::unique_lock<std::mutex> g(mu_);
     done_ += mine;
-    done_cv_.wait(g, [&] { return done_ >= n_; });
+    // every worker that joined this batch must have left its claim loop before the next batch resets next_ (a
+    // straggler's fetch_add would otherwise claim an index of the next batch and call this batch's fn)
+    done_cv_.wait(g, [&] { return done_ >= n_ && active_ == 0; });
     fn_ = nullptr;
   }
 
@@ -180,19 +252,22 @@ class HostPool {
         seen = gen_;
         fn = fn_;
         n = n_;
+        if (!fn) continue;  // the batch already completed
+        ++active_;
       }
       int mine = 0;
       for (int i; (i = next_.fetch_add(1)) < n;) { (*fn)(i); ++mine; }
       std::lock_guard<std::mutex> g(mu_);
       done_ += mine;
-      if (done_ >= n_) done_cv_.notify_all();
+      --active_;
+      if (done_ >= n_ && active_ == 0) done_cv_.notify_all();
     }
   }
   std::vector<std::thread> threads_;
   std::mutex mu_, run_mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)>* fn_ = nullptr;
-  int n_ = 0, done_ = 0;
+  int n_ = 0, done_ = 0, active_ = 0;
   std::atomic<int> next_{0};
   uint64_t gen_ = 0;
   bool stop_ = false;
@@ -231,6 +306,17 @@ inline void wr_be32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
 inline void wr_be64(uint8_t* p, uint64_t v) { wr_be32(p, (uint32_t)(v >> 32)); wr_be32(p + 4, (uint32_t)v); }
+
+// Double.doubleToLongBits's NaN (0x7ff8000000000000): raw values and IN-set literals use it for every NaN.
+const double kCanonicalNaN = [] {
+  const uint64_t b = 0x7ff8000000000000ull;
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}();
+// Raw (no-dictionary) columns: per-doc value arrays padded to whole 32-doc groups (the raw filter leaves read a
+// lane's whole group).
+inline int64_t raw_padded_docs(int64_t n) { return std::max<int64_t>((n + 31) & ~int64_t(31), 32); }
 
 // Order-preserving int64 key of a double (MIN/MAX operand on the device).
 inline int64_t double_key(double d) {
@@ -302,9 +388,13 @@ int cmp_bytes(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
 }
 
 // ================================================================================================ model
-// Host copy of one dictionary (segment-local or table-global), sorted ascending.
+// Host copy of one dictionary (segment-local or table-global), sorted ascending.  A table-global dictionary is an
+// immutable snapshot (copy on growth, `id` unique per snapshot): plans and their results keep the snapshot their
+// group ids index, so a pin that grows the dictionary while a query runs never re-labels that query's groups.
+std::atomic<uint64_t> g_dict_ids{1};
 struct Dict {
   int type = PGPU_INT;
+  uint64_t id = 0;
   std::vector<int64_t> iv;       // INT / LONG
   std::vector<double> dv;        // FLOAT / DOUBLE
   std::vector<std::string> sv;   // STRING (unpadded)
@@ -336,8 +426,8 @@ struct Column {
   bool sorted = false;              // SortedIndexReaderImpl column: docIds of dictId i are [sorted_start[i], sorted_start[i+1])
   std::vector<int32_t> sorted_start;
   std::vector<uint8_t> raw_dict;    // BIG_ENDIAN bytes as pinned (string padding semantics, column_bytes)
-  // lazily built device arrays
-  int32_t* d_lut = nullptr;
+  // lazily built device arrays (under the table mutex)
+  std::shared_ptr<DevMem> lut;      // int32 local -> global dictId; replaced, never rewritten, on dictionary growth
   uint64_t lut_version = ~0ull;
   int32_t lut_off = -1;             // >= 0: the LUT is lut[i] = lut_off + i (KCol.lut_off)
   int64_t* d_key = nullptr;
@@ -374,12 +464,38 @@ struct StarTreeDev {
   }
 };
 
+// A pinned segment.  Reference-counted like Pinot's SegmentDataManager (acquire / release per query,
+// BaseTableDataManager.java:245-258): the table and every plan that references the segment hold it, so an unpin
+// while a query still runs defers the device free until that query's plan is destroyed.
 struct Segment {
   int64_t handle = 0;
   int32_t num_docs = 0;
   void* d_block = nullptr;
   std::vector<Column> cols;
   std::unique_ptr<StarTreeDev> star;
+  Segment() = default;
+  Segment(const Segment&) = delete;
+  Segment& operator=(const Segment&) = delete;
+  ~Segment() {
+    for (auto& c : cols) {
+      if (c.d_key) hipFree(c.d_key);
+      if (c.d_val) hipFree(c.d_val);
+    }
+    if (d_block) hipFree(d_block);
+    if (star && star->d_block) hipFree(star->d_block);
+  }
+};
+
+// What a plan keeps alive while it exists (shared by the copies a plan-cache hit makes): its segments and the LUT
+// versions its records point at.
+struct PlanRefs {
+  std::vector<std::shared_ptr<Segment>> segs;
+  std::vector<std::shared_ptr<DevMem>> luts;
+};
+// A group-by key column's LUT in one plan segment, as planned: lut null = consecutive run (global = id + off).
+struct KeyLut {
+  const int32_t* lut = nullptr;
+  int32_t off = 0;
 };
 
 // Device copy of a cached plan's launch inputs: the per-segment records (SET pointers patched to its own bitset
@@ -402,12 +518,17 @@ struct DeviceImage {
 
 struct Scratch {
   DevBuf docbits, bittasks, bitblocks;  // inverted-index leaves: materialised docId bitmaps and their container tasks
+  DevBuf rawtasks;                      // raw-value leaves: tasks, jobs, IN keys (one buffer)
+  HostPinned rawstage;
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
   DevBuf stage_keys;  // ARRAY_MAP key spaces: the prefix hash table
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
-  HostPinned stage, starstage, bitstage, maskstage;
+  // Pinned staging: `stage` is the source of the execution's asynchronous uploads (records, bitsets); `readback`
+  // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
+  // free it while its uploads may still be queued behind other queries' work on a shared stream.
+  HostPinned stage, readback, starstage, bitstage, maskstage;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
   // A query that timed out returns while its device work may still run (wait_plan): the scratch goes back to the
@@ -420,9 +541,10 @@ struct Scratch {
     abandoned = false;
     for (auto& e : cev) if (e) hipEventDestroy(e);
     cev.clear();
-    docbits.release(); bittasks.release(); bitblocks.release();
+    docbits.release(); bittasks.release(); bitblocks.release(); rawtasks.release(); rawstage.release();
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
-    ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); starrec.release();
+    ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); readback.release();
+    starrec.release();
     starstage.release();
     bitstage.release();
     starwork.release();
@@ -444,10 +566,10 @@ struct pgpu_table_s {
   std::vector<std::string> names;
   std::vector<int32_t> types;
   std::mutex mu;
-  std::unordered_map<int64_t, std::unique_ptr<Segment>> segments;
-  std::vector<Segment*> by_handle;  // handle -> segment (handles are dense), nullptr once unpinned
+  std::unordered_map<int64_t, std::shared_ptr<Segment>> segments;
+  std::vector<std::shared_ptr<Segment>> by_handle;  // handle -> segment (handles are dense), null once unpinned
   int64_t next_handle = 1;
-  std::vector<Dict> global;
+  std::vector<std::shared_ptr<const Dict>> global;  // current snapshot per column (replaced under mu)
   std::vector<uint64_t> global_version;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Scratch>> scratch_pool;
@@ -484,12 +606,30 @@ struct pgpu_table_s {
 
 int pgpu::table_dict_view(pgpu_table t, int col, DictView* out) {
   if (!t || col < 0 || col >= (int)t->names.size()) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad column %d", col);
-  const Dict& d = t->global[col];
-  out->type = d.type;
-  out->iv = &d.iv;
-  out->dv = &d.dv;
-  out->sv = &d.sv;
+  std::shared_ptr<const Dict> d;
+  {
+    std::lock_guard<std::mutex> g(t->mu);
+    d = t->global[col];
+  }
+  out->keep = d;
+  out->type = d->type;
+  out->iv = &d->iv;
+  out->dv = &d->dv;
+  out->sv = &d->sv;
   out->name = t->names[col];
+  return 0;
+}
+
+int pgpu::result_key_dict_view(const pgpu_result_s* r, pgpu_table t, int key, DictView* out) {
+  if (!r || key < 0 || key >= r->num_keys) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad group-by key %d", key);
+  if ((int)r->key_dicts.size() <= key || !r->key_dicts[key]) return table_dict_view(t, r->key_cols[key], out);
+  auto d = std::static_pointer_cast<const Dict>(r->key_dicts[key]);
+  out->keep = d;
+  out->type = d->type;
+  out->iv = &d->iv;
+  out->dv = &d->dv;
+  out->sv = &d->sv;
+  out->name = t && r->key_cols[key] >= 0 && r->key_cols[key] < (int)t->names.size() ? t->names[r->key_cols[key]] : "";
   return 0;
 }
 
@@ -557,30 +697,30 @@ bool dbl_less(double a, double b) {  // Double.compare order for the sorted glob
   return x < y;
 }
 
-// Merges sorted `src` into the global dictionary `dst`; returns true if it grew.
-bool merge_dict(Dict& dst, const Dict& src) {
-  const size_t before = dst.size();
+// Merges sorted `src` into the global dictionary snapshot `g`: a new snapshot replaces it when the union grew.
+// Returns true if it grew.
+bool merge_dict(std::shared_ptr<const Dict>& g, const Dict& src) {
+  const Dict& dst = *g;
+  auto out = std::make_shared<Dict>();
+  out->type = dst.type;
   if (is_int_type(dst.type)) {
-    std::vector<int64_t> out;
-    out.reserve(dst.iv.size() + src.iv.size());
-    std::set_union(dst.iv.begin(), dst.iv.end(), src.iv.begin(), src.iv.end(), std::back_inserter(out));
-    dst.iv.swap(out);
+    out->iv.reserve(dst.iv.size() + src.iv.size());
+    std::set_union(dst.iv.begin(), dst.iv.end(), src.iv.begin(), src.iv.end(), std::back_inserter(out->iv));
   } else if (is_fp_type(dst.type)) {
     std::vector<double> s = src.dv;
     std::sort(s.begin(), s.end(), dbl_less);
-    std::vector<double> out;
-    out.reserve(dst.dv.size() + s.size());
-    std::set_union(dst.dv.begin(), dst.dv.end(), s.begin(), s.end(), std::back_inserter(out), dbl_less);
-    dst.dv.swap(out);
+    out->dv.reserve(dst.dv.size() + s.size());
+    std::set_union(dst.dv.begin(), dst.dv.end(), s.begin(), s.end(), std::back_inserter(out->dv), dbl_less);
   } else {
     std::vector<std::string> s = src.sv;
     std::sort(s.begin(), s.end());
-    std::vector<std::string> out;
-    out.reserve(dst.sv.size() + s.size());
-    std::set_union(dst.sv.begin(), dst.sv.end(), s.begin(), s.end(), std::back_inserter(out));
-    dst.sv.swap(out);
+    out->sv.reserve(dst.sv.size() + s.size());
+    std::set_union(dst.sv.begin(), dst.sv.end(), s.begin(), s.end(), std::back_inserter(out->sv));
   }
-  return dst.size() != before;
+  if (out->size() == dst.size()) return false;
+  out->id = g_dict_ids.fetch_add(1);
+  g = std::move(out);
+  return true;
 }
 
 // BaseImmutableDictionary.insertionIndexOf behind PredicateUtils.getStoredValue (Dictionary.java:49-100,
@@ -601,19 +741,19 @@ int64_t global_index_of(const Dict& g, const Dict& local, size_t i) {
 // Makes the local->global LUT of (seg, col) current.
 int ensure_lut(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
   Column& c = s.cols[col];
-  if (c.lut_version == t->global_version[col] && c.d_lut) return 0;
+  if (c.lut_version == t->global_version[col] && c.lut) return 0;
   std::vector<int32_t> lut(std::max<int32_t>(c.card, 1));
   for (int32_t i = 0; i < c.card; ++i) {
-    int64_t g = global_index_of(t->global[col], c.dict, i);
+    int64_t g = global_index_of(*t->global[col], c.dict, i);
     if (g < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "value missing from the global dictionary (column %d)", col);
     lut[i] = (int32_t)g;
   }
-  if (!c.d_lut) {
-    HIP_TRY(hipMalloc(&c.d_lut, sizeof(int32_t) * lut.size()));
-    t->device_bytes += sizeof(int32_t) * lut.size();
-  }
-  HIP_TRY(hipMemcpyAsync(c.d_lut, lut.data(), sizeof(int32_t) * lut.size(), hipMemcpyHostToDevice, stream));
+  auto m = std::make_shared<DevMem>();
+  HIP_TRY(hipMalloc(&m->p, sizeof(int32_t) * lut.size()));
+  if (!c.lut) t->device_bytes += sizeof(int32_t) * lut.size();
+  HIP_TRY(hipMemcpyAsync(m->p, lut.data(), sizeof(int32_t) * lut.size(), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  c.lut = std::move(m);  // the previous version lives on in the plans that reference it
   c.lut_version = t->global_version[col];
   // strictly increasing (both dictionaries sorted), so the ends decide whether it is a contiguous run
   c.lut_off = c.card > 0 && lut[c.card - 1] - lut[0] == c.card - 1 ? lut[0] : -1;
@@ -683,40 +823,82 @@ int ensure_docid(pgpu_table_s* t, int64_t n, hipStream_t stream) {
   return 0;
 }
 
-void free_segment(pgpu_table_s* t, Segment* s) {
-  for (auto& c : s->cols) {
-    if (c.d_lut) hipFree(c.d_lut);
-    if (c.d_key) hipFree(c.d_key);
-    if (c.d_val) hipFree(c.d_val);
-    if (c.inv) {
-      t->device_bytes -= c.inv->bytes;
-      c.inv.reset();
-    }
-    t->device_bytes -= (c.d_lut ? 4 * std::max(c.card, 1) : 0) +
-                       (c.d_key ? 16 * (c.raw ? std::max(s->num_docs, 1) : std::max(c.card, 1)) : 0);
+// Unpin accounting: the segment's device bytes leave the table's total now; the memory itself goes with the last
+// reference (~Segment).
+void account_unpin(pgpu_table_s* t, const Segment* s) {
+  int64_t fwd_words = 0;
+  for (const auto& c : s->cols) {
+    if (c.inv) t->device_bytes -= c.inv->bytes;
+    t->device_bytes -= (c.lut ? 4 * std::max(c.card, 1) : 0) +
+                       (c.d_key ? 16 * (c.raw ? raw_padded_docs(s->num_docs) : std::max(c.card, 1)) : 0);
+    if (!c.raw) fwd_words += (c.fwd_words + 63) & ~int64_t(63);
   }
-  if (s->d_block) hipFree(s->d_block);
-  if (s->star && s->star->d_block) {
-    hipFree(s->star->d_block);
-    t->device_bytes -= s->star->bytes;
-  }
+  if (s->d_block) t->device_bytes -= std::max<int64_t>(fwd_words, 64) * 4;
+  if (s->star) t->device_bytes -= s->star->bytes;
 }
 
 int64_t padded_fwd_words(int64_t num_docs, int bits) {
   return ((num_docs + kTileDocs - 1) / kTileDocs) * (int64_t)kBlock * bits + kFwdPadWords;
 }
 
-// A raw fixed-width column (FixedByteChunkSVForwardIndexWriter, PASS_THROUGH chunks; BaseChunkSVForwardIndexReader
-// .java:57-98 header): the per-doc values as the aggregation kernels read them -- int64 key (integer value, or the
-// order-preserving key of the double) and double -- for docs [0, num_docs).
+// LZ4 block decoder (the LZ4 block format of lz4-java's LZ4SafeDecompressor, behind Pinot's LZ4Decompressor /
+// LZ4WithLengthDecompressor, seglocal/io/compression/LZ4Decompressor.java:40-50).  Every length and offset is
+// checked against both buffers; returns the decoded length or -1.
+int64_t lz4_decode_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+  const uint8_t* ip = src;
+  const uint8_t* const iend = src + n;
+  uint8_t* op = dst;
+  uint8_t* const oend = dst + cap;
+  auto ext_len = [&](int64_t& len) -> bool {  // 255-continued length bytes
+    uint32_t b;
+    do {
+      if (ip >= iend) return false;
+      b = *ip++;
+      len += b;
+    } while (b == 255);
+    return true;
+  };
+  while (ip < iend) {
+    const uint32_t token = *ip++;
+    int64_t lit = token >> 4;
+    if (lit == 15 && !ext_len(lit)) return -1;
+    if (lit > iend - ip || lit > oend - op) return -1;
+    memcpy(op, ip, (size_t)lit);
+    ip += lit;
+    op += lit;
+    if (ip == iend) return op - dst;  // last sequence: literals only
+    if (iend - ip < 2) return -1;
+    const int64_t off = (int64_t)ip[0] | ((int64_t)ip[1] << 8);
+    ip += 2;
+    int64_t ml = token & 15;
+    if (ml == 15 && !ext_len(ml)) return -1;
+    ml += 4;
+    if (off == 0 || off > op - dst || ml > oend - op) return -1;
+    const uint8_t* m = op - off;
+    if (off >= ml) {
+      memcpy(op, m, (size_t)ml);
+      op += ml;
+    } else {  // overlapping: the last `off` bytes repeat
+      for (int64_t k = 0; k < ml; ++k) op[k] = m[k];
+      op += ml;
+    }
+  }
+  return -1;  // an empty block has no token
+}
+
+// A raw fixed-width forward index (FixedByteChunkSVForwardIndexWriter; BaseChunkSVForwardIndexReader.java:56-154):
+// the header (version, numChunks, numDocsPerChunk, sizeOfEntry; versions 2-3: totalDocs, compression type,
+// dataHeaderStart), the chunk offsets (int / long), the chunks -- PASS_THROUGH (read in place), LZ4 or
+// LZ4_LENGTH_PREFIXED (ChunkCompressionType 3 / 4, each chunk decoded on its own: getChunkPosition, the last
+// chunk to the end of the buffer).  Out: per doc the int64 key the kernels read (integer value, or the
+// order-preserving key of the double; NaN canonical, as Double.doubleToLongBits) and the double value.
 struct RawValues {
   std::vector<int64_t> key;
   std::vector<double> val;
+  int64_t lo = 0, hi = 0;  // integer range (sum bounds)
 };
-int parse_raw_column(int type, const pgpu_column_buffers& cb, int32_t num_docs, int c, Column* col, RawValues* out) {
+int decode_raw_forward_index(int type, const uint8_t* b, int64_t n, int32_t num_docs, int c, RawValues* out) {
   if (type == PGPU_STRING) return fail(PGPU_ERR_UNSUPPORTED, "column %d: raw STRING columns are not on the GPU path", c);
-  const int64_t n = cb.fwd_len;
-  const uint8_t* b = cb.fwd;
   if (!b || n < 16) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index too short", c);
   const int32_t version = (int32_t)rd_be32(b), num_chunks = (int32_t)rd_be32(b + 4);
   const int32_t per_chunk = (int32_t)rd_be32(b + 8), size = (int32_t)rd_be32(b + 12);
@@ -725,60 +907,94 @@ int parse_raw_column(int type, const pgpu_column_buffers& cb, int32_t num_docs, 
   if (n < 28) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index header truncated", c);
   const int32_t total = (int32_t)rd_be32(b + 16), compression = (int32_t)rd_be32(b + 20);
   const int32_t header_start = (int32_t)rd_be32(b + 24);
-  if (compression != 0)
-    return fail(PGPU_ERR_UNSUPPORTED, "column %d: compressed raw chunks (type %d): PASS_THROUGH only", c, compression);
+  // ChunkCompressionType: PASS_THROUGH 0, SNAPPY 1, ZSTANDARD 2, LZ4 3, LZ4_LENGTH_PREFIXED 4
+  if (compression != 0 && compression != 3 && compression != 4)
+    return fail(PGPU_ERR_UNSUPPORTED, "column %d: raw chunk compression type %d (PASS_THROUGH, LZ4 and "
+                "LZ4_LENGTH_PREFIXED are read)", c, compression);
   const int want = (type == PGPU_INT || type == PGPU_FLOAT) ? 4 : 8;
   if (size != want) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw entry size %d, type needs %d", c, size, want);
   if (num_chunks < 0 || per_chunk <= 0 || total < num_docs || (int64_t)num_chunks * per_chunk < num_docs)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index covers %d docs, segment has %d", c, total,
                 num_docs);
-  const int64_t data = (int64_t)header_start + (int64_t)num_chunks * (version == 2 ? 4 : 8);
-  if (header_start < 28 || data + (int64_t)num_docs * size > n)
+  const int entry = version == 2 ? 4 : 8;
+  const int64_t data = (int64_t)header_start + (int64_t)num_chunks * entry;
+  if (header_start < 28 || data > n || (compression == 0 && data + (int64_t)num_docs * size > n))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index too short for %d docs", c, num_docs);
-  col->raw = true;
-  col->card = 0;
-  col->bits = 0;
-  col->fwd_bytes = n;
-  out->key.resize(std::max<int32_t>(num_docs, 1));
-  out->val.resize(std::max<int32_t>(num_docs, 1));
+  out->key.assign(std::max<int32_t>(num_docs, 1), 0);
+  out->val.assign(std::max<int32_t>(num_docs, 1), 0.0);
   int64_t lo = INT64_MAX, hi = INT64_MIN;
-  for (int32_t i = 0; i < num_docs; ++i) {
-    const uint8_t* v = b + data + (int64_t)i * size;
-    switch (type) {
-      case PGPU_INT: { const int64_t x = (int32_t)rd_be32(v); out->key[i] = x; out->val[i] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
-      case PGPU_LONG: { const int64_t x = (int64_t)rd_be64(v); out->key[i] = x; out->val[i] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
-      case PGPU_FLOAT: {
-        const uint32_t u = rd_be32(v);
-        float f;
-        memcpy(&f, &u, 4);
-        out->val[i] = (double)f;
-        out->key[i] = double_key(out->val[i]);
-        break;
-      }
-      default: {
-        const uint64_t u = rd_be64(v);
-        double x;
-        memcpy(&x, &u, 8);
-        out->val[i] = x;
-        out->key[i] = double_key(x);
+  std::vector<uint8_t> chunk(compression ? (size_t)per_chunk * size : 0);
+  for (int64_t k = 0, d0 = 0; d0 < num_docs; ++k, d0 += per_chunk) {
+    const int64_t nd = std::min<int64_t>(per_chunk, num_docs - d0);
+    const uint8_t* v = b + data + d0 * size;
+    if (compression) {
+      auto chunk_pos = [&](int64_t i) {
+        const uint8_t* e = b + header_start + i * entry;
+        return entry == 4 ? (int64_t)rd_be32(e) : (int64_t)rd_be64(e);
+      };
+      const int64_t pos = chunk_pos(k), end = k + 1 < num_chunks ? chunk_pos(k + 1) : n;
+      if (pos < data || end < pos || end > n)
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: chunk %lld outside the forward index", c, (long long)k);
+      int64_t skip = compression == 4 ? 4 : 0;  // LZ4WithLength: little-endian decompressed length first
+      if (end - pos < skip) return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: chunk %lld truncated", c, (long long)k);
+      const int64_t got = lz4_decode_block(b + pos + skip, end - pos - skip, chunk.data(), (int64_t)chunk.size());
+      if (got < nd * size)
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: LZ4 chunk %lld is malformed or short", c, (long long)k);
+      v = chunk.data();
+    }
+    for (int64_t i = 0; i < nd; ++i, v += size) {
+      const int64_t d = d0 + i;
+      switch (type) {
+        case PGPU_INT: { const int64_t x = (int32_t)rd_be32(v); out->key[d] = x; out->val[d] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
+        case PGPU_LONG: { const int64_t x = (int64_t)rd_be64(v); out->key[d] = x; out->val[d] = (double)x; lo = std::min(lo, x); hi = std::max(hi, x); break; }
+        case PGPU_FLOAT: {
+          const uint32_t u = rd_be32(v);
+          float f;
+          memcpy(&f, &u, 4);
+          out->val[d] = (double)f;
+          out->key[d] = double_key(std::isnan(out->val[d]) ? kCanonicalNaN : out->val[d]);
+          break;
+        }
+        default: {
+          const uint64_t u = rd_be64(v);
+          double x;
+          memcpy(&x, &u, 8);
+          out->val[d] = x;
+          out->key[d] = double_key(std::isnan(x) ? kCanonicalNaN : x);
+        }
       }
     }
   }
-  col->raw_min = num_docs > 0 && lo <= hi ? lo : 0;
-  col->raw_max = num_docs > 0 && lo <= hi ? hi : 0;
+  out->lo = num_docs > 0 && lo <= hi ? lo : 0;
+  out->hi = num_docs > 0 && lo <= hi ? hi : 0;
+  return 0;
+}
+
+int parse_raw_column(int type, const pgpu_column_buffers& cb, int32_t num_docs, int c, Column* col, RawValues* out) {
+  TRY(decode_raw_forward_index(type, cb.fwd, cb.fwd_len, num_docs, c, out));
+  col->raw = true;
+  col->card = 0;
+  col->bits = 0;
+  col->fwd_bytes = cb.fwd_len;
+  col->raw_min = out->lo;
+  col->raw_max = out->hi;
   return 0;
 }
 
 // Registers a segment whose columns have parsed dictionaries and device forward indexes.
-int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg) {
+void plan_cache_clear(pgpu_table_s* t);
+
+int64_t register_segment(pgpu_table_s* t, std::unique_ptr<Segment> seg_in) {
+  std::shared_ptr<Segment> seg(std::move(seg_in));
   t->version++;
   for (size_t c = 0; c < seg->cols.size(); ++c)
     if (merge_dict(t->global[c], seg->cols[c].dict)) t->global_version[c]++;
   int64_t h = t->next_handle++;
   seg->handle = h;
-  if ((int64_t)t->by_handle.size() <= h) t->by_handle.resize(h + 1, nullptr);
-  t->by_handle[h] = seg.get();
+  if ((int64_t)t->by_handle.size() <= h) t->by_handle.resize(h + 1);
+  t->by_handle[h] = seg;
   t->segments[h] = std::move(seg);
+  plan_cache_clear(t);
   return h;
 }
 
@@ -789,6 +1005,7 @@ struct LeafHost {
   uint32_t dict_lo = 0, dict_span = 0;  // LEAF_DOCRANGE: the dictId range it came from (star-tree matching)
   std::vector<uint32_t> set;  // bitset words for LEAF_SET
   std::vector<int32_t> inv_ids;  // LEAF_BITMAP: matching dictIds whose inverted-index bitmaps are ORed
+  std::vector<int64_t> raw;      // LEAF_RAW_RANGE: inclusive key bounds {lo, hi}; LEAF_RAW_IN: sorted distinct keys
   double inv_frac = 0;           // LEAF_BITMAP: fraction of the segment's docs in those bitmaps
 };
 
@@ -812,6 +1029,11 @@ struct StreamExec {
 struct pgpu_plan_s {
   pgpu_table_s* table = nullptr;
   std::vector<Segment*> segs;
+  std::shared_ptr<PlanRefs> refs;         // keeps segs and the LUTs the records point at alive
+  std::vector<KeyLut> key_lut;            // [segment][group-by column] LUT as planned (taken under the table mutex)
+  const uint32_t* docid_fwd = nullptr;    // the $docId column as planned (identity forward index + values)
+  const int64_t* docid_key = nullptr;
+  int docid_bits = 0;
   std::vector<int32_t> query_cols;        // table column of each query column slot
   int num_leaves = 0;
   std::vector<int32_t> leaf_slot;         // query column slot of each leaf
@@ -819,7 +1041,10 @@ struct pgpu_plan_s {
   bool pure_and = false;
   int max_depth = 0;
   std::vector<int32_t> key_cols;          // table columns of group-by expressions
-  std::vector<int64_t> key_card;          // global cardinalities
+  std::vector<std::shared_ptr<const Dict>> key_dicts;  // global dictionary snapshots the key space is built on
+  std::vector<int64_t> key_card;          // key digit ranges (global cardinalities, or the filter's bound)
+  std::vector<int64_t> key_off;           // first global id of each key digit (filter-restricted key spaces)
+  int64_t key_bias = 0;                   // sum key_off[j] * key_stride[j]: subtracted from composite keys
   std::vector<int64_t> key_stride;
   int64_t num_keys = 0;                   // dense G or hash capacity
   int mode = MODE_LDS;
@@ -836,6 +1061,8 @@ struct pgpu_plan_s {
   std::vector<std::pair<int64_t, int64_t>> bit_fix;  // (offset of KLeaf.set field in segrec, docbits word offset)
   std::vector<KBitTask> bit_tasks;        // containers ORed into the docbits by inv_materialize_kernel
   std::vector<KBitBlock> bit_blocks;      // every 65536-doc block of the docbits, with its tasks
+  std::vector<KRawTask> raw_tasks;        // raw-value leaves evaluated into docbits regions (raw_leaf_bitmap_kernel)
+  std::vector<int64_t> raw_vals;          // their IN / NOT_IN keys
   std::vector<std::shared_ptr<InvIndex>> inv_refs;  // inverted indexes the bit tasks point into (kept alive)
   std::shared_ptr<DeviceImage> image;     // cached plans: device-resident records / tile map (one-launch plans)
   int64_t num_tiles = 0;
@@ -1152,6 +1379,69 @@ int translate_predicate_dict(const Column& c, const pgpu_predicate& p, const Par
   }
 }
 
+// Raw-value predicate evaluators (no dictionary; BaseRawValueBasedPredicateEvaluator subclasses, never always-true /
+// -false for FilterPlanNode): the leaf tests the column's per-doc int64 keys -- the value for INT / LONG, the
+// order-preserving key of the double for FLOAT / DOUBLE (NaN canonical) -- against
+//   RANGE (RangePredicateEvaluatorFactory.java:60-102, 268-448): unbounded = inclusive MIN / MAX (+-inf); Java's
+//          comparisons turned into inclusive key bounds (exclusive: the next representable value; 0.0 and -0.0
+//          compare equal, NaN never matches);
+//   EQ / NOT_EQ (EqualsPredicateEvaluatorFactory.java:60-70 `==`, NotEquals `!=`): the range [v, v] (negated);
+//   IN / NOT_IN (InPredicateEvaluatorFactory.java:69-126): fastutil Int/Long/Float/DoubleOpenHashSet.contains --
+//          bit equality (Float.floatToIntBits / Double.doubleToLongBits: 0.0 != -0.0, NaN == NaN).
+void translate_raw_predicate(int type, const pgpu_predicate& p, const ParsedPred& pp, LeafHost* L) {
+  L->raw.clear();
+  L->negate = 0;
+  const bool fp = is_fp_type(type);
+  auto empty = [&] { L->kind = LEAF_RAW_RANGE; L->raw = {1, 0}; };
+  auto fkey = [](double v) { return double_key(std::isnan(v) ? kCanonicalNaN : v); };
+  switch (p.type) {
+    case PGPU_PRED_EQ: case PGPU_PRED_NOT_EQ: {
+      L->negate = p.type == PGPU_PRED_NOT_EQ;
+      L->kind = LEAF_RAW_RANGE;
+      if (!fp) { L->raw = {pp.lits[0].i, pp.lits[0].i}; return; }
+      const double v = pp.lits[0].d;
+      if (std::isnan(v)) { empty(); L->negate = p.type == PGPU_PRED_NOT_EQ; return; }
+      if (v == 0.0) L->raw = {fkey(-0.0), fkey(0.0)};
+      else L->raw = {fkey(v), fkey(v)};
+      return;
+    }
+    case PGPU_PRED_IN: case PGPU_PRED_NOT_IN: {
+      L->negate = p.type == PGPU_PRED_NOT_IN;
+      L->kind = LEAF_RAW_IN;
+      for (const Literal& v : pp.lits) L->raw.push_back(fp ? fkey(v.d) : v.i);
+      std::sort(L->raw.begin(), L->raw.end());
+      L->raw.erase(std::unique(L->raw.begin(), L->raw.end()), L->raw.end());
+      L->span = (uint32_t)L->raw.size();
+      return;
+    }
+    default: {  // RANGE
+      L->kind = LEAF_RAW_RANGE;
+      const Literal& a = pp.lits[0];
+      const Literal& b = pp.lits[1];
+      if (!fp) {
+        const int64_t tmin = type == PGPU_INT ? INT32_MIN : INT64_MIN, tmax = type == PGPU_INT ? INT32_MAX : INT64_MAX;
+        int64_t lo = a.star ? tmin : a.i, hi = b.star ? tmax : b.i;
+        if (!a.star && !p.lower_inclusive) { if (lo == INT64_MAX) { empty(); return; } ++lo; }
+        if (!b.star && !p.upper_inclusive) { if (hi == INT64_MIN) { empty(); return; } --hi; }
+        L->raw = {lo, hi};
+        return;
+      }
+      const double inf = std::numeric_limits<double>::infinity();
+      double lo = a.star ? -inf : a.d, hi = b.star ? inf : b.d;
+      if (std::isnan(lo) || std::isnan(hi)) { empty(); return; }
+      int64_t klo, khi;
+      if (a.star || p.lower_inclusive) klo = lo == 0.0 ? fkey(-0.0) : fkey(lo);
+      else if (lo == inf) { empty(); return; }
+      else klo = fkey(lo == 0.0 ? std::nextafter(0.0, inf) : std::nextafter(lo, inf));
+      if (b.star || p.upper_inclusive) khi = hi == 0.0 ? fkey(0.0) : fkey(hi);
+      else if (hi == -inf) { empty(); return; }
+      else khi = fkey(hi == 0.0 ? std::nextafter(-0.0, -inf) : std::nextafter(hi, -inf));
+      L->raw = {klo, khi};
+      return;
+    }
+  }
+}
+
 // Constant folding of the program against the leaves' constants (FilterPlanNode.java:146-176).
 // Fraction of docs the filter program passes if every dictId were equally frequent (leaf fractions combined as
 // independent events).  Only picks the scan kernel instance (dense / sparse): never affects results.
@@ -1263,9 +1553,8 @@ void leaf_bitset(const LeafHost& L, int32_t card, std::vector<uint32_t>& w) {
 
 // Plans segment `s` on its star-tree when the query fits it (StarTreeUtils.isFitForStarTree, :151-176, and the
 // function-column pairs of the aggregations, :67-86).  *used = false leaves the segment to the scan path.
-int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_query* q,
-                      const std::vector<std::vector<int>>& comps, const std::vector<LeafHost>& leaves,
-                      hipStream_t stream, bool* used) {
+int plan_star_segment(pgpu_plan_s* P, size_t seg_index, Segment* s, const pgpu_query* q,
+                      const std::vector<std::vector<int>>& comps, const std::vector<LeafHost>& leaves, bool* used) {
   *used = false;
   const StarTreeDev* st = s->star.get();
   if (!st || st->num_dims > kMaxStarDims || st->num_nodes < 1 || P->first_doc_slot) return 0;
@@ -1336,8 +1625,8 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
   }
   for (size_t j = 0; j < P->key_cols.size(); ++j) {
     const int c = P->key_cols[j];
-    TRY(ensure_lut(t, *s, c, stream));
-    k.key_lut[j] = s->cols[c].d_lut;
+    // K6 always gathers through the LUT (the planned version, taken under the table mutex)
+    k.key_lut[j] = reinterpret_cast<const int32_t*>(P->refs->luts[seg_index * P->key_cols.size() + j]->p);
     k.key_dim[j] = st->dim_of(c);
     k.dim_card[k.key_dim[j]] = s->cols[c].card;
     if (!(k.pred_mask & (1 << k.key_dim[j]))) k.group_mask |= 1 << k.key_dim[j];
@@ -1358,6 +1647,7 @@ int plan_star_segment(pgpu_table_s* t, pgpu_plan_s* P, Segment* s, const pgpu_qu
   const int idx = (int)P->star.size();
   for (int d = 0; d < st->num_dims; ++d) {
     if (!(k.pred_mask & (1 << d))) continue;
+    if (P->set_words.size() & 1) P->set_words.push_back(0);
     P->star_match_fix.emplace_back(idx, d, (int64_t)P->set_words.size());
     P->set_words.insert(P->set_words.end(), match[d].begin(), match[d].end());
   }
@@ -1465,14 +1755,20 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   double tr[8] = {0};
   int ntr = 0;
   auto mark = [&] { if (trace_on() && ntr < 8) tr[ntr++] = now_us(); };
+  // Segment references (SegmentDataManager acquire): the table mutex is held only to take them here and, below, to
+  // build the lazily made LUT / value arrays and snapshot the global dictionary sizes -- the per-segment translation
+  // runs unlocked, so concurrent queries on one table plan in parallel.
+  P->refs = std::make_shared<PlanRefs>();
   {
     std::lock_guard<std::mutex> g(t->mu);
     P->segs.reserve(nsegs);
+    P->refs->segs.reserve(nsegs);
     for (int i = 0; i < nsegs; ++i) {
       const int64_t h = handles[i];
-      Segment* sp = h > 0 && h < (int64_t)t->by_handle.size() ? t->by_handle[h] : nullptr;
-      if (!sp) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
-      P->segs.push_back(sp);
+      const std::shared_ptr<Segment>* sp = h > 0 && h < (int64_t)t->by_handle.size() ? &t->by_handle[h] : nullptr;
+      if (!sp || !*sp) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+      P->segs.push_back(sp->get());
+      P->refs->segs.push_back(*sp);
     }
   }
   // query columns
@@ -1494,12 +1790,16 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->key_cols.push_back(c);
     slot_of(c);
   }
-  // raw (no-dictionary) columns are aggregation operands only: a predicate or a group-by on one runs on Pinot's own
-  // raw-value scan (RawValueBasedFilter / NoDictionaryGroupKeyGenerator), not here
+  // raw (no-dictionary) columns: aggregation operands and raw-value predicate leaves (below); a group-by on one runs
+  // on Pinot's NoDictionary*GroupKeyGenerator, not here
+  bool any_raw_leaf = false;
   for (Segment* s : P->segs) {
-    for (int i = 0; i < q->num_predicates; ++i)
-      if (s->cols[q->predicates[i].column].raw)
-        return fail(PGPU_ERR_UNSUPPORTED, "predicate on raw (no-dictionary) column %d", q->predicates[i].column);
+    for (int i = 0; i < q->num_predicates; ++i) {
+      const Column& c = s->cols[q->predicates[i].column];
+      any_raw_leaf |= c.raw;
+      if (c.raw && t->types[q->predicates[i].column] == PGPU_STRING)
+        return fail(PGPU_ERR_UNSUPPORTED, "predicate on raw STRING column %d", q->predicates[i].column);
+    }
     for (int i = 0; i < q->num_group_by; ++i)
       if (s->cols[q->group_by[i]].raw)
         return fail(PGPU_ERR_UNSUPPORTED, "group-by on raw (no-dictionary) column %d", q->group_by[i]);
@@ -1597,16 +1897,105 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       if (prod > q->num_groups_limit) P->limit_sensitive = true;
     }
   }
+  // Under the table mutex: the global dictionary sizes the key layout is built on, and every segment's device LUT /
+  // value arrays of the referenced columns (built once per segment, rebuilt out of place when the global dictionary
+  // grows) -- taken together, so the LUTs the plan points at map into exactly the key space it sizes.
+  std::vector<int64_t> gcard(P->key_cols.size());
+  {
+    const hipStream_t stream = t->stream;
+    const size_t nk = P->key_cols.size();
+    std::lock_guard<std::mutex> table_lock(t->mu);
+    P->key_dicts.resize(nk);
+    for (size_t j = 0; j < nk; ++j) {
+      P->key_dicts[j] = t->global[P->key_cols[j]];
+      gcard[j] = (int64_t)P->key_dicts[j]->size();
+    }
+    P->key_lut.resize(P->segs.size() * nk);
+    P->refs->luts.reserve(P->segs.size() * nk);
+    for (size_t i = 0; i < P->segs.size(); ++i) {
+      Segment* s = P->segs[i];
+      for (size_t j = 0; j < nk; ++j) {
+        const int c = P->key_cols[j];
+        TRY(ensure_lut(t, *s, c, stream));
+        const Column& col = s->cols[c];
+        P->refs->luts.push_back(col.lut);
+        KeyLut& kl = P->key_lut[i * nk + j];
+        kl.lut = col.lut_off >= 0 && !dict_gathers_forced() ? nullptr : reinterpret_cast<const int32_t*>(col.lut->p);
+        kl.off = col.lut_off;
+      }
+      for (size_t k = 1; k < P->slot_kind.size(); ++k)
+        if (P->slot_tcol[k] != kDocIdColumn) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
+      if (P->first_doc_slot) TRY(ensure_docid(t, s->num_docs, stream));
+    }
+    P->docid_fwd = t->d_docid_fwd;
+    P->docid_key = t->d_docid_key;
+    P->docid_bits = t->docid_bits;
+  }
+  // Key space restricted by the filter: a group-by column that a top-level conjunct of the filter bounds (EQ / IN /
+  // RANGE on the same numeric column) can only produce the global ids inside that bound -- C3's GROUP BY
+  // daysSinceEpoch under "daysSinceEpoch BETWEEN 17849 AND 17856" has 8 possible keys, not 365.  Column j's key
+  // digit becomes (global id - key_off[j]); the kernels subtract key_bias = sum key_off[j] * stride[j] once.  Same
+  // groups, a table (and slab fold, and compaction) sized by what the filter admits.
+  std::vector<int64_t> klo(P->key_cols.size(), 0), kspan(gcard);
+  if (P->pure_and && !getenv_flag("PGPU_NO_KEY_RESTRICT")) {
+    for (size_t j = 0; j < P->key_cols.size(); ++j) {
+      const int c = P->key_cols[j];
+      const Dict& gd = *P->key_dicts[j];
+      if (!is_int_type(gd.type) && !is_fp_type(gd.type)) continue;
+      int64_t lo = 0, hi = (int64_t)gd.size();
+      for (int l = 0; l < q->num_predicates; ++l) {
+        const pgpu_predicate& pr = q->predicates[l];
+        if (pr.column != c || (pr.type != PGPU_PRED_EQ && pr.type != PGPU_PRED_IN && pr.type != PGPU_PRED_RANGE)) continue;
+        ParsedPred pp;
+        TRY(parse_predicate(t->types[c], pr, &pp));
+        auto search = [&](const Literal& v) {
+          return is_int_type(gd.type) ? sorted_search<int64_t>(gd.iv, v.i) : sorted_search<double>(gd.dv, v.d);
+        };
+        int64_t a = 0, b = 0;
+        if (pr.type == PGPU_PRED_RANGE) {  // as translate_predicate_dict's RANGE, on the global dictionary
+          if (pp.lits[0].star) a = 0;
+          else { const int ins = search(pp.lits[0]); a = ins < 0 ? -(ins + 1) : (pr.lower_inclusive ? ins : ins + 1); }
+          if (pp.lits[1].star) b = (int64_t)gd.size();
+          else { const int ins = search(pp.lits[1]); b = ins < 0 ? -(ins + 1) : (pr.upper_inclusive ? ins + 1 : ins); }
+        } else {
+          a = INT64_MAX;
+          b = INT64_MIN;
+          for (const Literal& v : pp.lits) {
+            const int ins = search(v);
+            if (ins >= 0) { a = std::min<int64_t>(a, ins); b = std::max<int64_t>(b, ins + 1); }
+          }
+          if (a > b) a = b = 0;
+        }
+        lo = std::max(lo, a);
+        hi = std::min(hi, b);
+      }
+      if (hi <= lo) { lo = 0; hi = 1; }  // nothing admitted: no doc can match, keep a one-key digit
+      klo[j] = lo;
+      kspan[j] = hi - lo;
+    }
+    int64_t prod = 1;  // ARRAY_MAP stage plans keep the full key space (their stages restart the strides)
+    bool ovf = false;
+    for (size_t j = 0; j < P->key_cols.size(); ++j) {
+      const int64_t card = std::max<int64_t>(kspan[j], 1);
+      if (prod > INT64_MAX / card) ovf = true;
+      else prod *= card;
+    }
+    if (ovf) { std::fill(klo.begin(), klo.end(), 0); kspan = gcard; }
+  }
+  P->key_off = klo;
   // group-key layout over the table-global dictionaries (mixed radix, first column fastest: ArrayBasedHolder)
   bool overflow = false;
   int64_t G = 1;
-  for (int c : P->key_cols) {
-    const int64_t card = std::max<int64_t>((int64_t)t->global[c].size(), 1);
+  for (size_t j = 0; j < P->key_cols.size(); ++j) {
+    const int64_t card = std::max<int64_t>(kspan[j], 1);
     P->key_card.push_back(card);
     P->key_stride.push_back(G);
     if (!overflow && G > INT64_MAX / card) overflow = true;
     else if (!overflow) G *= card;
   }
+  P->key_bias = 0;
+  if (!overflow)
+    for (size_t j = 0; j < P->key_cols.size(); ++j) P->key_bias += P->key_off[j] * P->key_stride[j];
   if (overflow) {
     // ArrayMapBasedHolder (DictionaryBasedGroupKeyGenerator.java:127-137: the cardinality product overflows a long).
     // The key columns split into consecutive groups whose keys fit 62 bits: group s's key (the previous group's slot x
@@ -1676,7 +2065,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   P->seg_scanned.reserve(P->segs.size());
   P->seg_stride = (int)(sizeof(KSegHdr) + sizeof(KCol) * nqc + sizeof(KLeaf) * std::max(P->num_leaves, 0));
   P->seg_stride = (P->seg_stride + 15) & ~15;
-  hipStream_t stream = t->stream;
   P->segrec.reserve(P->segs.size() * (size_t)P->seg_stride);
   std::vector<ParsedPred> parsed(P->num_leaves);
   for (int l = 0; l < P->num_leaves; ++l)
@@ -1704,20 +2092,20 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       if (q->aggs[i].column >= 0 && s->cols[q->aggs[i].column].raw) return true;
     return false;
   };
-  std::lock_guard<std::mutex> table_lock(t->mu);  // lazily built LUT / value arrays are shared segment state
   bool any_star = false, any_inv = false;
   mark();
   for (Segment* s : P->segs) {
     any_star |= star_allowed && s->star != nullptr;
     for (int l = 0; l < q->num_predicates; ++l)
       any_inv |= s->cols[q->predicates[l].column].inv != nullptr;
-    // device LUT / value arrays of the referenced columns (built once per segment, rebuilt when the global
-    // dictionary grows); done up front so the per-segment translation below only reads segment state
-    for (int c : P->key_cols) TRY(ensure_lut(t, *s, c, stream));
-    for (size_t k = 1; k < P->slot_kind.size(); ++k)
-      if (P->slot_tcol[k] != kDocIdColumn) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
-    if (P->first_doc_slot) TRY(ensure_docid(t, s->num_docs, stream));
   }
+  // per query column: its group-by key index (-1: none) and whether an accumulator reads its values
+  std::vector<int> qcol_key(P->query_cols.size(), -1);
+  std::vector<char> qcol_val(P->query_cols.size(), 0);
+  for (size_t j = 0; j < P->key_cols.size(); ++j)
+    for (size_t i = 0; i < P->query_cols.size(); ++i)
+      if (P->query_cols[i] == P->key_cols[j]) qcol_key[i] = (int)j;
+  for (size_t k = 1; k < P->slot_col.size(); ++k) qcol_val[P->slot_col[k]] = 1;
   // Per-segment translation (PredicateEvaluatorProvider + FilterPlanNode per segment) in contiguous chunks,
   // on the host worker pool for large segment lists; records carry chunk-relative tile / set offsets, fixed up
   // when the chunks are concatenated in segment order.
@@ -1728,6 +2116,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     std::vector<std::pair<int64_t, int64_t>> bit_fix;
     std::vector<KBitTask> bit_tasks;
     std::vector<KBitBlock> bit_blocks;
+    std::vector<KRawTask> raw_tasks;
+    std::vector<int64_t> raw_vals;
     std::vector<std::shared_ptr<InvIndex>> inv_refs;
     std::vector<pgpu_plan_s::GenericStat> generic;  // rec: chunk-relative record index
     bool any_leap2 = false;
@@ -1777,7 +2167,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       for (int l = 0; l < P->num_leaves; ++l) {
         LeafHost& lh = leaves[l];
         lh.kind = LEAF_NONE; lh.negate = 0; lh.lo = 0; lh.span = 0;
-        TRY(translate_predicate(s->cols[q->predicates[l].column], q->predicates[l], parsed[l], &lh, ids_scratch));
+        const Column& pc = s->cols[q->predicates[l].column];
+        if (pc.raw) translate_raw_predicate(t->types[q->predicates[l].column], q->predicates[l], parsed[l], &lh);
+        else TRY(translate_predicate(pc, q->predicates[l], parsed[l], &lh, ids_scratch));
         if (!P->no_inverted && !s->star) to_inverted_leaf(s->cols[q->predicates[l].column], q->predicates[l], *s, &lh);
         tri[l] = leaves[l].kind == LEAF_NONE ? T_NONE : leaves[l].kind == LEAF_ALL ? T_ALL : T_VAR;
       }
@@ -1789,7 +2181,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       if (exempt_kind && whole == T_ALL && !raw_minmax(s)) C.exempt += s->num_docs;
       if (star_allowed && s->star) {  // only on the sequential path (any_star)
         bool used = false;
-        TRY(plan_star_segment(t, P, s, q, star_comps, leaves, stream, &used));
+        TRY(plan_star_segment(P, i, s, q, star_comps, leaves, &used));
         if (used) continue;
       }
       // numEntriesScannedInFilter (filter_stats.h): Pinot's leaf operators in this segment, its folded operator
@@ -1823,6 +2215,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           double f = lh.kind == LEAF_ALL ? 1.0 : lh.kind == LEAF_NONE ? 0.0 : lh.kind == LEAF_RANGE ? lh.span / card : 0.0;
           if (lh.kind == LEAF_DOCRANGE) f = (double)lh.span / std::max(1, s->num_docs);
           if (lh.kind == LEAF_BITMAP) f = lh.inv_frac;
+          if (lh.kind == LEAF_RAW_RANGE || lh.kind == LEAF_RAW_IN) f = 0.5;  // no dictionary to estimate from
           if (lh.kind == LEAF_SET) {
             int64_t ones = 0;
             for (uint32_t w : lh.set) ones += __builtin_popcount(w);
@@ -1842,29 +2235,34 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       KCol* kc = reinterpret_cast<KCol*>(rec.data() + sizeof(KSegHdr));
       for (int j = 0; j < nqc; ++j) {
         if (P->query_cols[j] == kDocIdColumn) {
-          kc[j].fwd = t->d_docid_fwd;
+          kc[j].fwd = P->docid_fwd;
           kc[j].lut = nullptr;
-          kc[j].dkey = t->d_docid_key;
+          kc[j].dkey = P->docid_key;
           kc[j].dval = nullptr;
-          kc[j].bits = t->docid_bits;
+          kc[j].bits = P->docid_bits;
           continue;
         }
         const Column& c = s->cols[P->query_cols[j]];
         if (c.raw) {  // values per doc, addressed through the identity docId index
-          kc[j].fwd = t->d_docid_fwd;
+          kc[j].fwd = P->docid_fwd;
           kc[j].lut = nullptr;
           kc[j].dkey = c.d_key;
           kc[j].dval = c.d_val;
-          kc[j].bits = t->docid_bits;
+          kc[j].bits = P->docid_bits;
           continue;
         }
         kc[j].fwd = c.d_fwd;
-        kc[j].lut = c.lut_off >= 0 && !dict_gathers_forced() ? nullptr : c.d_lut;
-        kc[j].lut_off = c.lut_off;
-        kc[j].dkey = c.key_affine && !dict_gathers_forced() ? nullptr : c.d_key;
-        kc[j].key_base = c.key_base;
-        kc[j].dval = c.d_val;
         kc[j].bits = c.bits;
+        if (qcol_key[j] >= 0) {  // group-by key: the LUT version planned (the segment's current one may be newer)
+          const KeyLut& kl = P->key_lut[i * P->key_cols.size() + qcol_key[j]];
+          kc[j].lut = kl.lut;
+          kc[j].lut_off = kl.off;
+        }
+        if (qcol_val[j]) {  // accumulator operand: value arrays, built once (ensure_values) and never replaced
+          kc[j].dkey = c.key_affine && !dict_gathers_forced() ? nullptr : c.d_key;
+          kc[j].key_base = c.key_base;
+          kc[j].dval = c.d_val;
+        }
       }
       KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
       const int64_t rec_off = (int64_t)C.rec.size();
@@ -1879,6 +2277,32 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           C.set_fix.emplace_back(field, (int64_t)C.set_words.size());
           C.set_words.insert(C.set_words.end(), lh.set.begin(), lh.set.end());
+          if (C.set_words.size() & 1) C.set_words.push_back(0);  // every leaf's words 8-byte aligned
+        }
+        if (lh.kind == LEAF_RAW_RANGE || lh.kind == LEAF_RAW_IN) {
+          // raw-value leaf: evaluated per query into a docId bitmap region (raw_leaf_bitmap_kernel, negation
+          // included) that the scan reads as a LEAF_BITMAP
+          const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
+          C.bit_fix.emplace_back(field, C.docbit_words);
+          KRawTask rt;
+          memset(&rt, 0, sizeof rt);
+          rt.keys = s->cols[q->predicates[perm[k]].column].d_key;
+          rt.dst = C.docbit_words;
+          rt.num_docs = s->num_docs;
+          rt.kind = lh.kind;
+          rt.negate = lh.negate;
+          if (lh.kind == LEAF_RAW_RANGE) {
+            rt.lo = lh.raw[0];
+            rt.hi = lh.raw[1];
+          } else {
+            rt.lo = (int64_t)C.raw_vals.size();
+            rt.hi = (int64_t)lh.raw.size();
+            C.raw_vals.insert(C.raw_vals.end(), lh.raw.begin(), lh.raw.end());
+          }
+          C.raw_tasks.push_back(rt);
+          C.docbit_words += ((((int64_t)s->num_docs + 31) / 32) + 1) & ~int64_t(1);
+          kl[k].kind = LEAF_BITMAP;
+          kl[k].negate = 0;
         }
         if (lh.kind == LEAF_BITMAP) {  // docId bitmap region: whole 65536-doc containers
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
@@ -2037,6 +2461,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // Appends a planned chunk to the plan; tile_shift is added to its records' chunk-relative tile_base (0 keeps
   // them relative, as a streamed launch of the chunk reads them).
   auto merge_chunk = [&](Chunk& C, int64_t tile_shift) {
+    if (P->set_words.size() & 1) P->set_words.push_back(0);  // chunk words keep their 8-byte alignment
     const int64_t rec0 = (int64_t)P->segrec.size(), set0 = (int64_t)P->set_words.size();
     if (tile_shift)
       for (size_t r = 0; r < C.rec.size(); r += P->seg_stride)
@@ -2049,6 +2474,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->bit_blocks.push_back(blk);
     }
     P->bit_tasks.insert(P->bit_tasks.end(), C.bit_tasks.begin(), C.bit_tasks.end());
+    for (KRawTask rt : C.raw_tasks) {
+      rt.dst += P->docbit_words;
+      if (rt.kind == LEAF_RAW_IN) rt.lo += (int64_t)P->raw_vals.size();
+      P->raw_tasks.push_back(rt);
+    }
+    P->raw_vals.insert(P->raw_vals.end(), C.raw_vals.begin(), C.raw_vals.end());
     P->inv_refs.insert(P->inv_refs.end(), C.inv_refs.begin(), C.inv_refs.end());
     for (auto& g : C.generic) {
       g.rec += rec0 / std::max(P->seg_stride, 1);
@@ -2076,7 +2507,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !part_eligible;
   P->leaf_perm = perm;
   const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
-  if (se && !any_star && !any_inv && !part_eligible && stream_chunks > 1) {
+  if (se && !any_star && !any_inv && !any_raw_leaf && !part_eligible && stream_chunks > 1) {
     for (Segment* s : P->segs) {
       P->tile_bound += (s->num_docs + kTileDocs - 1) / kTileDocs;
       for (int l = 0; l < P->num_leaves; ++l) {
@@ -2232,6 +2663,32 @@ int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
   }
 }
 
+// Raw-value leaves of a plan: its tasks, their 256-group jobs and IN keys staged through pinned memory in one device
+// buffer, then raw_leaf_bitmap_kernel writes the leaves' docbits regions (sc->docbits, sized by the caller).
+int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
+  if (P->raw_tasks.empty()) return 0;
+  std::vector<KRawJob> jobs;
+  for (size_t i = 0; i < P->raw_tasks.size(); ++i) {
+    const int64_t ngroups = ((int64_t)P->raw_tasks[i].num_docs + 31) / 32;
+    for (int64_t g0 = 0; g0 < ngroups; g0 += kBlock) jobs.push_back(KRawJob{(int32_t)i, (int32_t)g0});
+  }
+  const size_t tb = P->raw_tasks.size() * sizeof(KRawTask), jb = (jobs.size() * sizeof(KRawJob) + 15) & ~size_t(15);
+  const size_t vb = std::max<size_t>(P->raw_vals.size(), 1) * 8;
+  TRY(sc->rawtasks.ensure(tb + jb + vb));
+  TRY(sc->rawstage.ensure(tb + jb + vb));
+  uint8_t* hs = reinterpret_cast<uint8_t*>(sc->rawstage.p);
+  memcpy(hs, P->raw_tasks.data(), tb);
+  if (!jobs.empty()) memcpy(hs + tb, jobs.data(), jobs.size() * sizeof(KRawJob));
+  if (!P->raw_vals.empty()) memcpy(hs + tb + jb, P->raw_vals.data(), P->raw_vals.size() * 8);
+  HIP_TRY(hipMemcpyAsync(sc->rawtasks.p, hs, tb + jb + vb, hipMemcpyHostToDevice, stream));
+  uint8_t* d = sc->rawtasks.as<uint8_t>();
+  if (launch_raw_leaf_bitmaps(reinterpret_cast<const KRawJob*>(d + tb), (int64_t)jobs.size(),
+                              reinterpret_cast<const KRawTask*>(d), reinterpret_cast<const int64_t*>(d + tb + jb),
+                              sc->docbits.as<uint32_t>(), stream))
+    return fail(PGPU_ERR_DEVICE, "raw-value filter launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
 // ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
 // (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
@@ -2312,8 +2769,8 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     X.sets = im.sets.as<uint32_t>();
     X.tile_seg = im.tile_seg.as<int32_t>();
   }
-  if (P->docbit_words > 0) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
-    TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
+  if (P->docbit_words > 0) TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
+  if (!P->bit_blocks.empty()) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
     TRY(sc->bittasks.ensure(std::max<size_t>(P->bit_tasks.size(), 1) * sizeof(KBitTask)));
     TRY(sc->bitblocks.ensure(P->bit_blocks.size() * sizeof(KBitBlock)));
     // staged through pinned memory: asynchronous copies (pageable sources would block the host)
@@ -2329,6 +2786,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
       return fail(PGPU_ERR_DEVICE, "inverted-index materialise launch failed: %s",
                   hipGetErrorString(hipGetLastError()));
   }
+  TRY(launch_raw_leaves(P, sc, stream));  // raw-value leaves' docbits regions
   uint64_t* table = d_table ? reinterpret_cast<uint64_t*>(d_table) : sc->table.as<uint64_t>();
   X.table = table;
   P->d_table_used = table;
@@ -2350,6 +2808,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     kp.key_stride[j] = P->key_stride[j];
   }
   kp.num_keys_total = P->num_keys;
+  kp.key_bias = P->key_bias;
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = stats;
@@ -2421,6 +2880,42 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, cons
 
 // Launches the scan of chunk c (records already uploaded): tile map of its records, then the scan kernel (or the
 // partitioned group-by) over its tiles into slab region c.
+// PGPU_CHECK_LAUNCH=1 (diagnostics): before a scan launch, the records and tile map the kernel will read are copied
+// back and compared with the plan's host records (pointer fields patched at upload skipped); a mismatch fails the
+// query (PGPU_ERR_DEVICE) instead of launching on them.
+bool check_launch_on() {
+  static const bool on = getenv("PGPU_CHECK_LAUNCH") && getenv("PGPU_CHECK_LAUNCH")[0] == '1';
+  return on;
+}
+int check_launch_inputs(const pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, const LaunchChunk& C) {
+  HIP_TRY(hipStreamSynchronize(stream));
+  const size_t r0 = (size_t)C.rec_begin * P->seg_stride, rn = (size_t)C.num_recs * P->seg_stride;
+  std::vector<uint8_t> dev(rn);
+  std::vector<int32_t> tiles((size_t)std::max<int64_t>(C.num_tiles, 0));
+  if (rn) HIP_TRY(hipMemcpy(dev.data(), X.segrec + r0, rn, hipMemcpyDeviceToHost));
+  if (!tiles.empty()) HIP_TRY(hipMemcpy(tiles.data(), X.tile_seg + C.tile_begin, tiles.size() * 4, hipMemcpyDeviceToHost));
+  if (P->segrec.size() >= r0 + rn) {
+    std::vector<char> skip(rn, 0);
+    auto mark = [&](int64_t off) {
+      if (off >= (int64_t)r0 && off + 8 <= (int64_t)(r0 + rn)) memset(skip.data() + (off - r0), 1, 8);
+    };
+    for (const auto& f : P->set_fix) mark(f.first);
+    for (const auto& f : P->bit_fix) mark(f.first);
+    for (size_t i = 0; i < rn; ++i)
+      if (!skip[i] && dev[i] != P->segrec[r0 + i])
+        return fail(PGPU_ERR_DEVICE, "launch check: device record byte %zu differs from the plan (%u vs %u)", r0 + i,
+                    dev[i], P->segrec[r0 + i]);
+  }
+  int32_t prev = 0;
+  for (size_t i = 0; i < tiles.size(); ++i) {
+    if (tiles[i] < prev || tiles[i] >= C.num_recs)
+      return fail(PGPU_ERR_DEVICE, "launch check: tile %zu maps to record %d of %lld", i, tiles[i],
+                  (long long)C.num_recs);
+    prev = tiles[i];
+  }
+  return 0;
+}
+
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c) {
   Scratch* sc = P->scratch;
   KParams kp = X.kp;
@@ -2438,6 +2933,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
                                                    kp.deadline, kp.stats, stream)) {
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
+  if (check_launch_on()) TRY(check_launch_inputs(P, stream, X, C));
   if (c == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   HIP_TRY(hipEventRecord(sc->cev[2 * c], stream));
   if (C.num_tiles > 0 && P->partitioned) {
@@ -2546,6 +3042,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     sp.range_cache = P->star_range_cache;
     sp.num_keys = (int)P->key_cols.size();
     for (size_t j = 0; j < P->key_cols.size(); ++j) sp.key_stride[j] = P->key_stride[j];
+    sp.key_bias = P->key_bias;
     sp.num_keys_total = P->num_keys;
     sp.num_slots = nslots;
     for (int sl = 0; sl < nslots; ++sl) {
@@ -2625,7 +3122,7 @@ int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table) {
 // Group-by dictIds of composite key k: (k / stride[j]) % card[j] (DictionaryBasedGroupKeyGenerator.java:276-323).
 void decode_keys(const pgpu_plan_s* P, pgpu_result_s* R, int64_t row, uint64_t key) {
   for (int j = 0; j < R->num_keys; ++j)
-    R->gid(j)[row] = (int32_t)((key / (uint64_t)P->key_stride[j]) % (uint64_t)P->key_card[j]);
+    R->gid(j)[row] = (int32_t)((key / (uint64_t)P->key_stride[j]) % (uint64_t)P->key_card[j] + P->key_off[j]);
 }
 
 // key_begin / key_count: a shard [slots][key_count] of the dense table holding keys [key_begin, key_begin +
@@ -2646,8 +3143,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   R->pool = P->table->result_pool;
   if (!P->hash && words * 8 <= kHostCompactBytes) {
     // small dense table: one copy (table + stats) and one sync, compacted on the host in key order
-    TRY(sc->stage.ensure((size_t)words * 8 + 64));
-    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    TRY(sc->readback.ensure((size_t)words * 8 + 64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     if (reinterpret_cast<const uint8_t*>(P->d_stats) == reinterpret_cast<const uint8_t*>(table) + words * 8) {
       HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 48, hipMemcpyDeviceToHost, stream));  // table + stats
     } else {
@@ -2678,12 +3175,13 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->counter.ensure(64));
     TRY(sc->cslots.ensure((size_t)std::max<int64_t>(nch, 1) * 4));
     TRY(sc->ckeys.ensure((size_t)cap * (4 * nk + 8 * nslots) + 8));
-    if (launch_compact_ordered(table, nslots, G, key_begin, P->key_stride.data(), P->key_card.data(), nk,
+    if (launch_compact_ordered(table, nslots, G, key_begin, P->key_stride.data(), P->key_card.data(),
+                               P->key_off.data(), nk,
                                sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(), sc->ckeys.p, cap,
                                stream))
       return fail(PGPU_ERR_DEVICE, "compact launch failed: %s", hipGetErrorString(hipGetLastError()));
-    TRY(sc->stage.ensure(64));
-    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    TRY(sc->readback.ensure(64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
@@ -2713,8 +3211,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     if (launch_compact(table, sc->hash_keys.as<unsigned long long>(), nslots, G, sc->counter.as<unsigned long long>(),
                        sc->ckeys.as<uint64_t>(), cap, stream))
       return fail(PGPU_ERR_DEVICE, "compact launch failed");
-    TRY(sc->stage.ensure(64));
-    uint64_t* st = reinterpret_cast<uint64_t*>(sc->stage.p);
+    TRY(sc->readback.ensure(64));
+    uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
@@ -2725,8 +3223,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     star_scanned = st[2] + st[3];
     P->star_docs_read = (int64_t)st[4];
     if (n > 0) {
-      TRY(sc->stage.ensure((size_t)n * rec * 8));
-      st = reinterpret_cast<uint64_t*>(sc->stage.p);
+      TRY(sc->readback.ensure((size_t)n * rec * 8));
+      st = reinterpret_cast<uint64_t*>(sc->readback.p);
       HIP_TRY(hipMemcpyAsync(st, sc->ckeys.p, (size_t)n * rec * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
     }
@@ -2768,6 +3266,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   R->num_aggs = na;
   R->agg_slot = P->agg_slot;
   R->key_cols = P->key_cols;
+  R->key_dicts.assign(P->key_dicts.begin(), P->key_dicts.end());
   R->key_types.clear();
   for (int c : P->key_cols) R->key_types.push_back(P->table->types[c]);
   R->agg_fn = P->agg_fn;
@@ -2834,12 +3333,12 @@ int split_for_groups_limit(pgpu_table_s* t, const int64_t* handles, int32_t nseg
     for (int k = 0; k < q->num_group_by; ++k) {
       const int c = q->group_by[k];
       if (c < 0 || c >= (int)t->names.size()) return 0;
-      const int64_t card = std::max<int64_t>((int64_t)t->global[c].size(), 1);
+      const int64_t card = std::max<int64_t>((int64_t)t->global[c]->size(), 1);
       global_keys = global_keys > INT64_MAX / card ? INT64_MAX : global_keys * card;
     }
     for (int i = 0; i < nsegs; ++i) {
       const int64_t h = handles[i];
-      Segment* sp = h > 0 && h < (int64_t)t->by_handle.size() ? t->by_handle[h] : nullptr;
+      const Segment* sp = h > 0 && h < (int64_t)t->by_handle.size() ? t->by_handle[h].get() : nullptr;
       if (!sp) return 0;  // plan_create_impl reports it
       for (int k = 0; k < q->num_group_by; ++k) {
         const int c = q->group_by[k];
@@ -2930,10 +3429,24 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
   std::vector<Key> keys;
   std::vector<uint64_t> vals;
   int64_t counter = 0;
+  // The parts were planned one after another: a pin in between may have grown a global dictionary, so their group
+  // ids can index different snapshots.  Merge in the newest (largest: dictionaries only grow) and re-label the
+  // other parts' ids through their values.
+  std::vector<std::shared_ptr<const Dict>> kd(nk);
+  for (const auto& part : P->parts)
+    for (int j = 0; j < nk; ++j)
+      if (!kd[j] || part.plan->key_dicts[j]->size() > kd[j]->size()) kd[j] = part.plan->key_dicts[j];
   for (size_t i = 0; i < P->parts.size(); ++i) {
     const auto& part = P->parts[i];
     pgpu_result_s* Ri = rs[i].get();
     const pgpu_plan_s* Q = part.plan.get();
+    for (int j = 0; j < nk; ++j) {
+      if (Q->key_dicts[j] == kd[j]) continue;
+      const Dict& old = *Q->key_dicts[j];
+      std::vector<int32_t> relabel(old.size());
+      for (size_t x = 0; x < old.size(); ++x) relabel[x] = (int32_t)global_index_of(*kd[j], old, x);
+      for (int64_t r = 0; r < Ri->n; ++r) Ri->gid(j)[r] = relabel[Ri->gid(j)[r]];
+    }
     std::vector<int64_t> order(Ri->n);
     std::iota(order.begin(), order.end(), 0);
     if (part.first_seen) {
@@ -2999,6 +3512,7 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
   R->num_aggs = R0->num_aggs;
   R->agg_slot = R0->agg_slot;
   R->key_cols = R0->key_cols;
+  R->key_dicts.assign(kd.begin(), kd.end());
   R->key_types = R0->key_types;
   R->agg_fn = R0->agg_fn;
   R->agg_col = R0->agg_col;
@@ -3061,20 +3575,23 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     // Once its device image is built, a hit needs none of the host records: copy the plan without them (the
     // records of a 1000-segment plan are ~250 KB -- most of a hit's host time).  cache_mu is held: no other
     // thread reads the cached image meanwhile.
-    const bool lean = src.image && src.image->uploaded.load();
+    const bool lean = src.image && src.image->uploaded.load() && !check_launch_on();
     std::vector<uint8_t> segrec;
     std::vector<uint32_t> set_words;
     std::vector<std::pair<int64_t, int64_t>> set_fix;
+    std::vector<KeyLut> key_lut;
     if (lean) {
       segrec.swap(src.segrec);
       set_words.swap(src.set_words);
       set_fix.swap(src.set_fix);
+      key_lut.swap(src.key_lut);
     }
     *P = src;
     if (lean) {
       src.segrec.swap(segrec);
       src.set_words.swap(set_words);
       src.set_fix.swap(set_fix);
+      src.key_lut.swap(key_lut);
     }
     t->plan_cache.splice(t->plan_cache.begin(), t->plan_cache, it);
     P->scratch = nullptr;
@@ -3088,6 +3605,17 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
   return false;
 }
 
+// Every change of pinned state (pin, unpin, index attach, dictionary growth) bumps the table version, which is part
+// of every cache key: the cached plans of earlier versions can never hit again, and they hold segment and LUT
+// references, so they are dropped right away.
+void plan_cache_clear(pgpu_table_s* t) {
+  std::list<std::pair<std::string, std::shared_ptr<pgpu_plan_s>>> old;
+  {
+    std::lock_guard<std::mutex> g(t->cache_mu);
+    old.swap(t->plan_cache);
+  }
+}
+
 void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
   if (P.chunks.size() == 1 && P.docbit_words == 0 && !P.set_words_bound && !P.tile_bound)
     P.image = std::make_shared<DeviceImage>();  // built by the first execution, shared by every later hit
@@ -3099,6 +3627,22 @@ void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
 }
 
 }  // namespace
+
+// PGPU_SERIALIZE_ABI=1 (diagnostics): every entry point of this file runs under one process-wide lock, so
+// concurrent callers are serialised (isolates host-side races from device-side ones).
+namespace {
+std::recursive_mutex g_abi_mu;
+bool abi_serialize() {
+  static const bool on = getenv("PGPU_SERIALIZE_ABI") && getenv("PGPU_SERIALIZE_ABI")[0] == '1';
+  return on;
+}
+struct AbiGuard {
+  bool on;
+  AbiGuard() : on(abi_serialize()) { if (on) g_abi_mu.lock(); }
+  ~AbiGuard() { if (on) g_abi_mu.unlock(); }
+};
+}  // namespace
+#define PGPU_ABI_GUARD AbiGuard _abi_guard
 
 // ================================================================================================ C ABI
 extern "C" {
@@ -3115,6 +3659,7 @@ int pgpu_last_error(char* buf, size_t len) {
 }
 
 int pgpu_device_count(int* count) {
+  PGPU_ABI_GUARD;
   if (!count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null count");
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -3124,6 +3669,8 @@ int pgpu_device_count(int* count) {
 }
 
 int pgpu_table_create(int device, int num_columns, const char* const* names, const int32_t* types, pgpu_table* out) {
+  PGPU_ABI_GUARD;
+  install_crash_trace();
   if (!out || num_columns <= 0 || !types) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad table arguments");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PGPU_ERR_DEVICE, "no HIP device available");
@@ -3135,9 +3682,10 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
   for (int i = 0; i < num_columns; ++i) {
     t->names.push_back(names && names[i] ? names[i] : ("col" + std::to_string(i)));
     t->types.push_back(types[i]);
-    Dict d;
-    d.type = types[i];
-    t->global.push_back(d);
+    auto d = std::make_shared<Dict>();
+    d->type = types[i];
+    d->id = g_dict_ids.fetch_add(1);
+    t->global.push_back(std::move(d));
     t->global_version.push_back(0);
   }
   DeviceGuard g(device);
@@ -3150,11 +3698,12 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
 }
 
 int pgpu_table_destroy(pgpu_table t) {
+  PGPU_ABI_GUARD;
   if (!t) return 0;
   DeviceGuard g(t->device);
   hipStreamSynchronize(t->stream);
-  for (auto& kv : t->segments) free_segment(t, kv.second.get());
-  t->segments.clear();
+  plan_cache_clear(t);
+  t->segments.clear();  // freed here unless a live plan still holds a segment (destroy plans first)
   t->by_handle.clear();
   for (auto& s : t->scratch_pool) if (s) s->release();
   t->gen.pos.release(); t->gen.presence.release(); t->gen.code_to_pos.release(); t->gen.cdf.release();
@@ -3170,6 +3719,7 @@ int pgpu_table_destroy(pgpu_table t) {
 }
 
 int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) {
+  PGPU_ABI_GUARD;
   if (!t || !d || !handle) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (d->num_columns != (int)t->names.size())
     return fail(PGPU_ERR_INVALID_ARGUMENT, "segment has %d columns, table has %zu", d->num_columns, t->names.size());
@@ -3242,7 +3792,9 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
   for (int c = 0; c < d->num_columns; ++c) {
     Column& col = seg->cols[c];
     if (col.raw) {
-      const size_t n = std::max<int32_t>(d->num_docs, 1);
+      const size_t n = (size_t)raw_padded_docs(d->num_docs);
+      raw_values[c].key.resize(n, 0);
+      raw_values[c].val.resize(n, 0.0);
       HIP_TRY(hipMalloc(&col.d_key, n * 8));
       HIP_TRY(hipMalloc(&col.d_val, n * 8));
       t->device_bytes += 16 * (int64_t)n;
@@ -3269,16 +3821,22 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
 }
 
 int pgpu_unpin_segment(pgpu_table t, int64_t h) {
+  PGPU_ABI_GUARD;
   if (t) t->version++;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   DeviceGuard g(t->device);
-  std::lock_guard<std::mutex> lk(t->mu);
-  auto it = t->segments.find(h);
-  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
-  hipStreamSynchronize(t->stream);
-  free_segment(t, it->second.get());
-  t->by_handle[h] = nullptr;
-  t->segments.erase(it);
+  std::shared_ptr<Segment> seg;  // released after the table mutex (the free may wait for the device)
+  {
+    std::lock_guard<std::mutex> lk(t->mu);
+    auto it = t->segments.find(h);
+    if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+    seg = std::move(it->second);
+    account_unpin(t, seg.get());
+    t->by_handle[h].reset();
+    t->segments.erase(it);
+  }
+  plan_cache_clear(t);  // cached plans reference the segment set of their time
+  hipStreamSynchronize(t->stream);  // work queued on the table's own stream (pins, reads) is done with it
   return 0;
 }
 
@@ -3422,6 +3980,7 @@ void serialize_roaring_plain(const int32_t* docs, int64_t n, std::vector<uint8_t
 // forward index -> per dictId the sorted docIds -> (card + 1) BE offsets + serialised bitmaps.
 int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, int32_t num_docs, int32_t cardinality,
                               void* out, int64_t out_cap, int64_t* out_len) {
+  PGPU_ABI_GUARD;
   if (!fwd || !out_len || bits < 1 || bits > 31 || num_docs < 0 || cardinality < 1 ||
       fwd_len < ((int64_t)num_docs * bits + 7) / 8)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad inverted-index build arguments");
@@ -3465,8 +4024,24 @@ int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, in
   return 0;
 }
 
+int pgpu_raw_forward_index_values(const void* fwd, int64_t fwd_len, int32_t data_type, int32_t num_docs,
+                                  int64_t* out_i64, double* out_f64) {
+  PGPU_ABI_GUARD;
+  if (!fwd || num_docs < 0 || data_type < PGPU_INT || data_type > PGPU_STRING)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  RawValues v;
+  TRY(decode_raw_forward_index(data_type, reinterpret_cast<const uint8_t*>(fwd), fwd_len, num_docs, 0, &v));
+  for (int32_t i = 0; i < num_docs; ++i) {
+    if (out_i64) out_i64[i] = is_int_type(data_type) ? v.key[i] : 0;
+    if (out_f64) out_f64[i] = v.val[i];
+  }
+  return 0;
+}
+
 int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
+  PGPU_ABI_GUARD;
   if (t) t->version++;
+  if (t) plan_cache_clear(t);
   if (!t || (!bytes && num_bytes)) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   DeviceGuard g(t->device);
   std::lock_guard<std::mutex> lk(t->mu);
@@ -3562,7 +4137,9 @@ int validate_startree(const pgpu_startree_desc* d, const std::vector<int32_t>& d
 extern "C" {
 
 int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
+  PGPU_ABI_GUARD;
   if (t) t->version++;
+  if (t) plan_cache_clear(t);
   if (!t || !d) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (d->num_dims < 1 || d->num_dims > kMaxStarDims || d->num_nodes < 1 || d->num_docs < 0 || d->num_metrics < 1)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree shape (dims %d, nodes %d, docs %d, metrics %d)",
@@ -3649,6 +4226,7 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
 }
 
 int pgpu_table_num_segments(pgpu_table t, int32_t* count) {
+  PGPU_ABI_GUARD;
   if (!t || !count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(t->mu);
   *count = (int32_t)t->segments.size();
@@ -3659,7 +4237,9 @@ int64_t pgpu_table_device_bytes(pgpu_table t) { return t ? t->device_bytes : 0; 
 
 int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int64_t* vi, const double* vd,
                                      const uint8_t* blob, const int64_t* offsets) {
+  PGPU_ABI_GUARD;
   if (t) t->version++;
+  if (t) plan_cache_clear(t);
   if (!t || col < 0 || col >= (int)t->names.size() || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   Dict d;
   d.type = t->types[col];
@@ -3683,35 +4263,39 @@ int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int
 }
 
 int pgpu_table_dictionary_size(pgpu_table t, int col, int64_t* size) {
+  PGPU_ABI_GUARD;
   if (!t || !size || col < 0 || col >= (int)t->names.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
-  *size = (int64_t)t->global[col].size();
+  *size = (int64_t)t->global[col]->size();
   return 0;
 }
 
 int pgpu_table_dictionary_i64(pgpu_table t, int col, int64_t* out) {
+  PGPU_ABI_GUARD;
   if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_int_type(t->types[col]))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
-  std::copy(t->global[col].iv.begin(), t->global[col].iv.end(), out);
+  std::copy(t->global[col]->iv.begin(), t->global[col]->iv.end(), out);
   return 0;
 }
 
 int pgpu_table_dictionary_f64(pgpu_table t, int col, double* out) {
+  PGPU_ABI_GUARD;
   if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_fp_type(t->types[col]))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
-  std::copy(t->global[col].dv.begin(), t->global[col].dv.end(), out);
+  std::copy(t->global[col]->dv.begin(), t->global[col]->dv.end(), out);
   return 0;
 }
 
 int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap, int64_t* offsets) {
+  PGPU_ABI_GUARD;
   if (!t || !offsets || col < 0 || col >= (int)t->names.size() || t->types[col] != PGPU_STRING)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
   int64_t off = 0;
   offsets[0] = 0;
-  const auto& sv = t->global[col].sv;
+  const auto& sv = t->global[col]->sv;
   for (size_t i = 0; i < sv.size(); ++i) {
     if (blob) {
       if (off + (int64_t)sv[i].size() > cap) return fail(PGPU_ERR_INVALID_ARGUMENT, "blob too small");
@@ -3724,14 +4308,15 @@ int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap,
 }
 
 int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, int32_t n, int32_t* out) {
+  PGPU_ABI_GUARD;
   if (!t || (n > 0 && (!docs || !out))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
-  Segment* s;
+  std::shared_ptr<Segment> s;
   {
     std::lock_guard<std::mutex> lk(t->mu);
     auto it = t->segments.find(h);
     if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle");
-    s = it->second.get();
+    s = it->second;
   }
   if (col < 0 || col >= (int)s->cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column");
   if (n <= 0) return 0;
@@ -3752,6 +4337,7 @@ int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, in
 
 int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bits, int64_t start, int64_t n,
                                  int32_t* d_out, void* stream) {
+  PGPU_ABI_GUARD;
   if (bits < 1 || bits > 31 || start < 0 || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   // the two-word gather reads up to word ((start+n-1)*bits >> 5) + 1
   const int64_t last_word = n > 0 ? (((start + n - 1) * bits) >> 5) + 1 : 0;
@@ -3764,6 +4350,7 @@ int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bit
 }
 
 int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan* out) {
+  PGPU_ABI_GUARD;
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
@@ -3787,6 +4374,7 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
 }
 
 int pgpu_plan_destroy(pgpu_plan P) {
+  PGPU_ABI_GUARD;
   if (!P) return 0;
   for (auto& part : P->parts) release_scratch(P->table, part.plan->scratch);
   release_scratch(P->table, P->scratch);
@@ -3795,6 +4383,7 @@ int pgpu_plan_destroy(pgpu_plan P) {
 }
 
 int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
+  PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: its parts have their own group tables");
   if (num_slots) *num_slots = (int32_t)P->slot_kind.size();
@@ -3805,6 +4394,7 @@ int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t
 
 int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
                              void* d_table, pgpu_plan* out) {
+  PGPU_ABI_GUARD;
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const double tt0 = trace_on() ? now_us() : 0;
   DeviceGuard g(t->device);
@@ -3857,8 +4447,10 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
 }
 
 int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
+  PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   if (P->composite) {
+  PGPU_ABI_GUARD;
     if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
     P->executed = true;
     return 0;
@@ -3870,6 +4462,7 @@ int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
 }
 
 int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_result* out) {
+  PGPU_ABI_GUARD;
   if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
@@ -3887,6 +4480,7 @@ int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_resu
 
 int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shard, int64_t key_begin,
                              int64_t key_count, pgpu_result* out) {
+  PGPU_ABI_GUARD;
   if (!P || !out || !d_table_shard || key_begin < 0 || key_count < 0 || key_begin + key_count > P->num_keys)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (P->hash) return fail(PGPU_ERR_UNSUPPORTED, "hash-mode group tables are not key-range shardable");
@@ -3902,6 +4496,7 @@ int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shar
 
 int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
                          pgpu_result* out) {
+  PGPU_ABI_GUARD;
   pgpu_plan P = nullptr;
   TRY(pgpu_plan_create_execute(t, handles, nsegs, q, stream, nullptr, &P));
   int rc = pgpu_plan_finalize(P, stream, nullptr, out);
@@ -3912,12 +4507,14 @@ int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, co
 }
 
 int pgpu_plan_scanned_segments(pgpu_plan P, uint8_t* out) {
+  PGPU_ABI_GUARD;
   if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (!P->seg_scanned.empty()) memcpy(out, P->seg_scanned.data(), P->seg_scanned.size());
   return 0;
 }
 
 int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
+  PGPU_ABI_GUARD;
   if (!P || !out3) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   int64_t nodes = 0;
   for (const KStarSeg& k : P->star) nodes += k.num_nodes;
@@ -3928,6 +4525,7 @@ int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
 }
 
 int pgpu_plan_timing(pgpu_plan P, double* out3) {
+  PGPU_ABI_GUARD;
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: timing is per part");
   Scratch* sc = P->scratch;
@@ -3950,11 +4548,55 @@ int pgpu_plan_timing(pgpu_plan P, double* out3) {
 }
 
 int pgpu_result_num_groups(pgpu_result r, int64_t* n) {
+  PGPU_ABI_GUARD;
   if (!r || !n) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   *n = r->n;
   return 0;
 }
+static const Dict* result_dict(pgpu_result r, int key) {
+  if (!r || key < 0 || key >= r->num_keys || key >= (int)r->key_dicts.size() || !r->key_dicts[key]) return nullptr;
+  return static_cast<const Dict*>(r->key_dicts[key].get());
+}
+int pgpu_result_key_dictionary(pgpu_result r, int key, uint64_t* snapshot_id, int64_t* size) {
+  PGPU_ABI_GUARD;
+  const Dict* d = result_dict(r, key);
+  if (!d) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad group-by key %d", key);
+  if (snapshot_id) *snapshot_id = d->id;
+  if (size) *size = (int64_t)d->size();
+  return 0;
+}
+int pgpu_result_key_dictionary_i64(pgpu_result r, int key, int64_t* out) {
+  PGPU_ABI_GUARD;
+  const Dict* d = result_dict(r, key);
+  if (!d || !out || !is_int_type(d->type)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::copy(d->iv.begin(), d->iv.end(), out);
+  return 0;
+}
+int pgpu_result_key_dictionary_f64(pgpu_result r, int key, double* out) {
+  PGPU_ABI_GUARD;
+  const Dict* d = result_dict(r, key);
+  if (!d || !out || !is_fp_type(d->type)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::copy(d->dv.begin(), d->dv.end(), out);
+  return 0;
+}
+int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_t cap, int64_t* offsets) {
+  PGPU_ABI_GUARD;
+  const Dict* d = result_dict(r, key);
+  if (!d || !offsets || d->type != PGPU_STRING) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  int64_t off = 0;
+  offsets[0] = 0;
+  for (size_t i = 0; i < d->sv.size(); ++i) {
+    if (blob) {
+      if (off + (int64_t)d->sv[i].size() > cap) return fail(PGPU_ERR_INVALID_ARGUMENT, "blob too small");
+      memcpy(blob + off, d->sv[i].data(), d->sv[i].size());
+    }
+    off += (int64_t)d->sv[i].size();
+    offsets[i + 1] = off;
+  }
+  return 0;
+}
 int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
+  PGPU_ABI_GUARD;
   if (!r || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const int nk = r->num_keys;
   for (int j = 0; j < nk; ++j) {
@@ -3964,16 +4606,19 @@ int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
   return 0;
 }
 int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out) {
+  PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->n) memcpy(out, r->gid(key), (size_t)r->n * 4);
   return 0;
 }
 int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out) {
+  PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   *out = r->gid(key);
   return 0;
 }
 int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form) {
+  PGPU_ABI_GUARD;
   if (!r || agg < -1 || agg >= r->num_aggs || !out || !form) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (agg == -1) {  // the COUNT slot (AvgPair.count of every AVG)
     *out = r->slot(0);
@@ -3985,6 +4630,7 @@ int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t
   return 0;
 }
 int pgpu_result_values(pgpu_result r, int agg, double* out) {
+  PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const uint64_t* w = r->slot(r->agg_slot[agg]);
   switch (r->agg_conv[agg]) {
@@ -3995,32 +4641,38 @@ int pgpu_result_values(pgpu_result r, int agg, double* out) {
   return 0;
 }
 int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) {
+  PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->n) memcpy(out, r->slot(0), (size_t)r->n * 8);  // slot 0 = COUNT = AvgPair.count
   return 0;
 }
 int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
+  PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->agg_conv[agg] != RCONV_I64) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
   if (r->n) memcpy(out, r->slot(r->agg_slot[agg]), (size_t)r->n * 8);
   return 0;
 }
 int pgpu_result_stats(pgpu_result r, int64_t* out6) {
+  PGPU_ABI_GUARD;
   if (!r || !out6) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   memcpy(out6, r->stats, sizeof r->stats);
   return 0;
 }
 int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out) {
+  PGPU_ABI_GUARD;
   if (!r || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   *out = r->groups_limit_reached ? 1 : 0;
   return 0;
 }
 int pgpu_result_destroy(pgpu_result r) {
+  PGPU_ABI_GUARD;
   delete r;
   return 0;
 }
 
 int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* out_words) {
+  PGPU_ABI_GUARD;
   if (!t || !q || !out_words) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
   // A plan over the one segment with a COUNT-by-first-column shape; only its filter part is used.
@@ -4031,7 +4683,7 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
   fq.num_aggs = 0;
   fq.aggs = nullptr;
   auto P = std::make_unique<pgpu_plan_s>();
-  P->no_inverted = true;  // the standalone filter kernel reads scan / sorted leaves only
+  P->no_inverted = true;  // the standalone filter kernel reads scan / sorted / raw-value leaves only
   TRY(plan_create_impl(t, &h, 1, &fq, P.get()));
   Segment* s = P->segs[0];
   const int64_t ngroups = ((int64_t)s->num_docs + 31) / 32;
@@ -4048,6 +4700,14 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
     for (auto& f : P->set_fix) {
       const uint32_t* p = sc->sets.as<uint32_t>() + f.second;
       memcpy(P->segrec.data() + f.first, &p, sizeof p);
+    }
+    if (!P->raw_tasks.empty()) {  // raw-value leaves: their docbits regions first (inverted leaves are off here)
+      if ((rc = sc->docbits.ensure((size_t)P->docbit_words * 4))) break;
+      for (auto& f : P->bit_fix) {
+        const uint32_t* p = sc->docbits.as<uint32_t>() + f.second;
+        memcpy(P->segrec.data() + f.first, &p, sizeof p);
+      }
+      if ((rc = launch_raw_leaves(P.get(), sc, t->stream))) break;
     }
     if ((rc = sc->bitmap.ensure((size_t)nwords * 8))) break;
     hipMemsetAsync(sc->bitmap.p, 0, (size_t)nwords * 8, t->stream);
@@ -4080,6 +4740,7 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
 
 int pgpu_generate_segment(pgpu_table t, const pgpu_gen_column* gc, int32_t ncols, int64_t row0, int32_t num_docs,
                           int64_t* handle) {
+  PGPU_ABI_GUARD;
   if (!t || !gc || !handle || ncols != (int)t->names.size() || num_docs < 0)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
@@ -4212,6 +4873,7 @@ int pgpu_generate_segment(pgpu_table t, const pgpu_gen_column* gc, int32_t ncols
 
 int pgpu_segment_column_info(pgpu_table t, int64_t h, int col, int32_t* card, int32_t* bits, int64_t* dict_len,
                              int64_t* fwd_len) {
+  PGPU_ABI_GUARD;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   std::lock_guard<std::mutex> lk(t->mu);
   auto it = t->segments.find(h);
@@ -4226,14 +4888,15 @@ int pgpu_segment_column_info(pgpu_table t, int64_t h, int col, int32_t* card, in
 }
 
 int pgpu_segment_column_bytes(pgpu_table t, int64_t h, int col, uint8_t* dict_out, uint8_t* fwd_out) {
+  PGPU_ABI_GUARD;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   DeviceGuard g(t->device);
-  Segment* s;
+  std::shared_ptr<Segment> s;
   {
     std::lock_guard<std::mutex> lk(t->mu);
     auto it = t->segments.find(h);
     if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle");
-    s = it->second.get();
+    s = it->second;
   }
   if (col < 0 || col >= (int)s->cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column");
   const Column& c = s->cols[col];

@@ -123,6 +123,7 @@ int copy_rows(const pgpu_result_s* R, const std::vector<int64_t>& rows, pgpu_res
   O->agg_fn = R->agg_fn;
   O->agg_col = R->agg_col;
   O->groups_limit_reached = R->groups_limit_reached;
+  O->key_dicts = R->key_dicts;
   *out = O;
   return 0;
 }
@@ -387,7 +388,7 @@ int pgpu_result_datatable(pgpu_result r, pgpu_table t, void* out, int64_t cap, i
   std::vector<std::string> names, types;
   std::vector<int> tsz;
   for (int j = 0; j < nk; ++j) {
-    if (table_dict_view(t, r->key_cols[j], &dv[j])) return PGPU_ERR_INVALID_ARGUMENT;
+    if (result_key_dict_view(r, t, j, &dv[j])) return PGPU_ERR_INVALID_ARGUMENT;
     names.push_back(dv[j].name);  // ExpressionContext.toString of an identifier
     types.push_back(column_type_name(r->key_types[j]));
   }

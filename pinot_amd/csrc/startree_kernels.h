@@ -164,7 +164,7 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
   using KeyT = typename std::conditional<MODE == MODE_HASH, int64_t, int32_t>::type;
   KeyT key[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) key[i] = 0;
+  for (int i = 0; i < 16; ++i) key[i] = -(KeyT)p.key_bias;  // filter-restricted key space (KParams.key_bias)
   int koff = 0;
   for (int j = 0; j < p.num_keys; ++j) {
     const int d = S.key_dim[j];

@@ -207,6 +207,7 @@ class GpuTable:
         L.check(self.lib.pgpu_table_create(device, len(self.names), names, types, ctypes.byref(h)))
         self.handle = h
         self._dict_cache = {}
+        self._snapshots = {}  # dictionary snapshot id -> values (results index the snapshot their plan saw)
 
     def close(self):
         if self.handle:
@@ -369,6 +370,37 @@ class GpuTable:
             b = blob.tobytes()
             vals = [b[off[i]:off[i + 1]].decode("utf-8", errors="surrogateescape") for i in range(n.value)]
         self._dict_cache[column] = vals
+        return vals
+
+    def result_dictionary(self, r, key, column):
+        """Values of the table-global dictionary snapshot that group-by key `key` of C result `r` indexes (cached
+        by snapshot id: unchanged until a pin grows the column's dictionary)."""
+        sid, n = ctypes.c_uint64(), ctypes.c_int64()
+        L.check(self.lib.pgpu_result_key_dictionary(r, key, ctypes.byref(sid), ctypes.byref(n)))
+        vals = self._snapshots.get(sid.value)
+        if vals is not None:
+            return vals
+        n = n.value
+        t = self.types[self.index[column]]
+        if t in (L.INT, L.LONG):
+            a = np.zeros(max(n, 1), dtype=np.int64)
+            L.check(self.lib.pgpu_result_key_dictionary_i64(r, key, L.ptr(a, ctypes.c_int64)))
+            vals = [int(x) for x in a[:n]]
+        elif t in (L.FLOAT, L.DOUBLE):
+            a = np.zeros(max(n, 1), dtype=np.float64)
+            L.check(self.lib.pgpu_result_key_dictionary_f64(r, key, L.ptr(a, ctypes.c_double)))
+            vals = [float(x) for x in a[:n]]
+        else:
+            off = np.zeros(n + 1, dtype=np.int64)
+            L.check(self.lib.pgpu_result_key_dictionary_str(r, key, None, 0, L.ptr(off, ctypes.c_int64)))
+            blob = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
+            L.check(self.lib.pgpu_result_key_dictionary_str(r, key, L.ptr(blob, ctypes.c_uint8), len(blob),
+                                                            L.ptr(off, ctypes.c_int64)))
+            b = blob.tobytes()
+            vals = [b[off[i]:off[i + 1]].decode("utf-8", errors="surrogateescape") for i in range(n)]
+        if len(self._snapshots) > 64:
+            self._snapshots.clear()
+        self._snapshots[sid.value] = vals
         return vals
 
     # ------------------------------------------------------------------ readers
@@ -544,7 +576,7 @@ def _decode_result(table, query, holder):
     for j in range(nk):
         L.check(lib.pgpu_result_group_ids_view(r, j, ctypes.byref(ptr)))
         cols.append(_view(holder, ptr.value, n, np.int32))
-    dicts = [table.dictionary(c) for c in query.group_by]
+    dicts = [table.result_dictionary(r, j, c) for j, c in enumerate(query.group_by)]
     aggs = []
     exact = {}
     form = ctypes.c_int32()

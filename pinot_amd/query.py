@@ -194,7 +194,8 @@ class QueryContext:
 
     def _options(self):
         return (0 if getattr(self, "use_star_tree", True) else L.OPT_NO_STAR_TREE) | \
-            (L.OPT_SQL_GROUP_BY if getattr(self, "sql_group_by", False) else 0)
+            (L.OPT_SQL_GROUP_BY if getattr(self, "sql_group_by", False) else 0) | \
+            (L.OPT_NO_PLAN_CACHE if getattr(self, "no_plan_cache", False) else 0)
 
     def _build_c(self, column_index):
         keep = []

@@ -96,33 +96,46 @@ RAW_DOCS_PER_CHUNK = 1000  # SingleValueFixedByteRawIndexCreator.NUM_DOCS_PER_CH
 _RAW_FMT = {L.INT: ">i", L.LONG: ">q", L.FLOAT: ">f", L.DOUBLE: ">d"}
 
 
-def raw_forward_index_bytes(data_type, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK):
-    """A no-dictionary fixed-width column as FixedByteChunkSVForwardIndexWriter writes it with PASS_THROUGH chunks
-    (BaseChunkSVForwardIndexWriter.java:130-193): header (version, numChunks, numDocsPerChunk, sizeOfEntry, then for
-    version > 1 totalDocs, compression type 0, dataHeaderStart), the chunk offsets (int for version 2, long for 3),
-    then the chunks, big-endian values back to back."""
+# ChunkCompressionType (segspi/compression/ChunkCompressionType.java:22)
+COMPRESSION = {"PASS_THROUGH": 0, "SNAPPY": 1, "ZSTANDARD": 2, "LZ4": 3, "LZ4_LENGTH_PREFIXED": 4}
+
+
+def raw_forward_index_bytes(data_type, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK,
+                            compression="PASS_THROUGH"):
+    """A no-dictionary fixed-width column as FixedByteChunkSVForwardIndexWriter writes it
+    (BaseChunkSVForwardIndexWriter.java:71-193): header (version, numChunks, numDocsPerChunk, sizeOfEntry, then for
+    version > 1 totalDocs, compression type, dataHeaderStart), the chunk offsets (int for version 2, long for 3; each
+    the absolute position of its chunk), then the chunks: big-endian values back to back, each chunk compressed on
+    its own (writeChunk; the last chunk holds the remaining docs) -- PASS_THROUGH as is, LZ4 as an LZ4 block,
+    LZ4_LENGTH_PREFIXED as the little-endian decompressed length + the block (pinot_amd.lz4)."""
     import struct
+    from . import lz4
     if version not in (2, 3):
         raise ValueError("raw forward index version %d (2 or 3)" % version)
+    codec = COMPRESSION[compression]
+    if codec not in (0, 3, 4):
+        raise ValueError("writer supports PASS_THROUGH, LZ4 and LZ4_LENGTH_PREFIXED chunks")
     fmt = _RAW_FMT[data_type]
     size = struct.calcsize(fmt)
     n = len(values)
     num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
     entry = 4 if version == 2 else 8
     header_size = 7 * 4 + num_chunks * entry
-    hdr = struct.pack(">iiiiiii", version, num_chunks, docs_per_chunk, size, n, 0, 7 * 4)
-    offsets, off = [], header_size
-    for c in range(num_chunks):
-        offsets.append(off)
-        off += min(docs_per_chunk, n - c * docs_per_chunk) * size
-    hdr += b"".join(struct.pack(">i" if version == 2 else ">q", o) for o in offsets)
+    hdr = struct.pack(">iiiiiii", version, num_chunks, docs_per_chunk, size, n, codec, 7 * 4)
     cast = float if data_type in (L.FLOAT, L.DOUBLE) else int
-    body = b"".join(struct.pack(fmt, cast(v)) for v in values)
-    return hdr + body
+    chunks, offsets, off = [], [], header_size
+    for c in range(num_chunks):
+        raw = b"".join(struct.pack(fmt, cast(v)) for v in values[c * docs_per_chunk:(c + 1) * docs_per_chunk])
+        body = raw if codec == 0 else lz4.compress_block(raw) if codec == 3 else lz4.compress_with_length(raw)
+        offsets.append(off)
+        chunks.append(body)
+        off += len(body)
+    hdr += b"".join(struct.pack(">i" if version == 2 else ">q", o) for o in offsets)
+    return hdr + b"".join(chunks)
 
 
-def build_raw_column(type_name, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK):
+def build_raw_column(type_name, values, version=2, docs_per_chunk=RAW_DOCS_PER_CHUNK, compression="PASS_THROUGH"):
     """ColumnData of a raw (no-dictionary) INT / LONG / FLOAT / DOUBLE column."""
     t = L.TYPE_NAMES[type_name] if isinstance(type_name, str) else int(type_name)
-    fwd = raw_forward_index_bytes(t, values, version, docs_per_chunk)
+    fwd = raw_forward_index_bytes(t, values, version, docs_per_chunk, compression)
     return ColumnData(t, 0, 0, 4 if t in (L.INT, L.FLOAT) else 8, b"", fwd, fwd_format=L.FWD_RAW_FIXED)

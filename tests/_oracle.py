@@ -29,7 +29,7 @@ class OrColumn(ctypes.Structure):
     _fields_ = [("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("entry_width", ctypes.c_int32), ("padding_byte", ctypes.c_int32), ("is_sorted", ctypes.c_int32),
                 ("has_inverted", ctypes.c_int32), ("dict", ctypes.c_void_p), ("fwd", ctypes.c_void_p),
-                ("raw", ctypes.c_int32)]
+                ("raw", ctypes.c_int32), ("fwd_len", ctypes.c_int64)]
 
 
 class OrSegment(ctypes.Structure):
@@ -178,7 +178,7 @@ class _OrSeg:
             cols[i] = OrColumn(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.padding_byte,
                                int(c.is_sorted), int(getattr(c, "inv_bytes", None) is not None),
                                ctypes.cast(d, ctypes.c_void_p), ctypes.cast(f, ctypes.c_void_p),
-                               int(c.fwd_format == L.FWD_RAW_FIXED))
+                               int(c.fwd_format == L.FWD_RAW_FIXED), len(c.fwd_bytes))
         self.keep.append(cols)
         self.seg = OrSegment(seg.num_docs, len(schema), cols)
 

@@ -38,7 +38,7 @@ def test_round_trip_through_the_oracle_reader(oracle, version, type_name):
     lib.or_raw_get_double.restype = ctypes.c_double
     lib.or_raw_get_double.argtypes = [ctypes.POINTER(oracle.OrColumn), ctypes.c_int]
     buf = ctypes.create_string_buffer(raw, len(raw))
-    col = oracle.OrColumn(t, 0, 0, size, 0, 0, 0, None, ctypes.cast(buf, ctypes.c_void_p), 1)
+    col = oracle.OrColumn(t, 0, 0, size, 0, 0, 0, None, ctypes.cast(buf, ctypes.c_void_p), 1, len(raw))
     for i in list(range(0, NUM_VALUES, 97)) + [PER_CHUNK - 1, PER_CHUNK, NUM_VALUES - 1]:
         assert lib.or_raw_get_double(ctypes.byref(col), i) == float(vals[i]), i
 

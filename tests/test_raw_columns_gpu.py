@@ -1,7 +1,10 @@
-"""Raw (no-dictionary) metric columns on the GPU: segments whose metric columns are FixedByteChunk PASS_THROUGH
-forward indexes (FixedByteChunkSVForwardIndexReader.java:30-110) aggregate exactly as the oracle's operator reads
-them (DataFetcher over ForwardIndexReader.readValuesSV); predicates and group-by on a raw column, and compressed
-chunks, are declined (PGPU_ERR_UNSUPPORTED: Pinot's own operator runs them)."""
+"""Raw (no-dictionary) columns on the GPU: segments whose metric columns are FixedByteChunk forward indexes
+(FixedByteChunkSVForwardIndexReader.java:30-110; PASS_THROUGH, LZ4 and LZ4_LENGTH_PREFIXED chunks, decoded at pin)
+aggregate exactly as the oracle's operator reads them (DataFetcher over ForwardIndexReader.readValuesSV), and
+raw-value predicates on them (RangePredicateEvaluatorFactory / Equals / In raw evaluators: a scan of the values,
+every entry counted) select exactly the oracle's docs -- special doubles included (NaN never compares, 0.0 == -0.0
+for EQ / RANGE, IN uses bit equality).  Group-by on a raw column and SNAPPY / ZSTANDARD chunks are declined
+(PGPU_ERR_UNSUPPORTED: Pinot's own operator runs them)."""
 import numpy as np
 import pytest
 
@@ -70,14 +73,101 @@ def test_raw_columns_declined_where_pinot_scans_raw_values(oracle, gpu_lib):
     t = GpuTable(SCHEMA)
     try:
         h = t.pin_segment(segs[0])
-        for sql in ["SELECT COUNT(*) FROM t WHERE m > 5 GROUP BY d", "SELECT SUM(f) FROM t GROUP BY m"]:
-            with pytest.raises(L.UnsupportedQueryError):
-                t.execute_groupby([h], parse_query(sql))
+        with pytest.raises(L.UnsupportedQueryError):
+            t.execute_groupby([h], parse_query("SELECT SUM(f) FROM t GROUP BY m"))
         from dataclasses import replace
         bad = bytearray(segs[0].columns["m"].fwd_bytes)
         bad[20:24] = (1).to_bytes(4, "big")  # SNAPPY chunks
         seg = SegmentBuffers(100, {**segs[0].columns, "m": replace(segs[0].columns["m"], fwd_bytes=bytes(bad))})
         with pytest.raises(L.UnsupportedQueryError):
             t.pin_segment(seg)
+    finally:
+        t.close()
+
+
+def _lz4_segments(oracle, sizes, compression, seed=5):
+    """Segments whose raw columns use `compression` chunks, with special values in the DOUBLE / FLOAT columns."""
+    rng = np.random.default_rng(seed)
+    specials = [float("nan"), 0.0, -0.0, float("inf"), float("-inf"), 1.5, -2.25]
+    segs = []
+    for n in sizes:
+        cols = {"d": rng.integers(0, 40, n).tolist(), "f": rng.integers(0, 1000, n).tolist()}
+        base = oracle.make_segment([("d", "INT"), ("f", "INT")], cols)
+        x = rng.integers(-4, 5, n).astype(np.float64) * 0.75
+        y = np.float32(rng.integers(-8, 9, n) * 0.5).astype(np.float64)
+        pick = rng.integers(0, len(specials), n)
+        sp = rng.random(n) < 0.2
+        x[sp] = np.array(specials)[pick[sp]]
+        y[sp] = np.array(specials)[pick[sp]]
+        raw = {"m": build_raw_column("INT", rng.integers(-50, 50, n).tolist(), compression=compression,
+                                     docs_per_chunk=777),
+               "l": build_raw_column("LONG", (rng.integers(-3, 4, n) * 2 ** 40).tolist(), version=3,
+                                     compression=compression),
+               "x": build_raw_column("DOUBLE", x.tolist(), compression=compression),
+               "y": build_raw_column("FLOAT", y.tolist(), compression=compression)}
+        segs.append(SegmentBuffers(n, {**base.columns, **raw}))
+    return segs
+
+
+RAW_FILTERS = [
+    "m > 10", "m >= -3 AND m < 7", "m = 0", "m <> 0", "m IN (1, 2, 3, -49)", "m NOT IN (1, 2, 3)",
+    "m BETWEEN -5 AND 5 AND f < 500", "m < -40 OR f > 900", "NOT m > 0",
+    "l = 1099511627776", "l <> 0", "l IN (0, -3298534883328)", "l < 0",
+    "x > 0", "x >= 0", "x < 0", "x = 0", "x <> 0", "x = 1.5", "x BETWEEN -1.5 AND 1.5", "x > -1e308",
+    "x IN (0, 1.5, -2.25)", "x NOT IN (0)", "x IN (-0.0)", "x = -1.5", "x <= 0.75",
+    "y > 0", "y = 0", "y <> 1.5", "y IN (1.5, -0.0)", "y BETWEEN -2 AND 2", "y < 1e39",
+]
+
+
+@pytest.mark.parametrize("compression", ["LZ4", "LZ4_LENGTH_PREFIXED"])
+def test_raw_predicates_and_lz4_chunks(oracle, gpu_lib, compression):
+    segs = _lz4_segments(oracle, [5003, 1, 64, 12000], compression)
+    t = GpuTable(SCHEMA)
+    try:
+        hs = [t.pin_segment(s) for s in segs]
+        for where in RAW_FILTERS:
+            sql = "SELECT COUNT(*), SUM(m), MAX(l), SUM(x), MIN(y) FROM t WHERE %s GROUP BY d" % where
+            q = parse_query(sql)
+            o = oracle.run_groupby(SCHEMA, segs, q)
+            r = t.execute_groupby(hs, q)
+            assert r.stats.as_tuple() == o.stats, where  # numEntriesScannedInFilter of the raw scans included
+            g, e = r.as_dict(), o.groups
+            assert set(g) == set(e), where
+            for k in e:
+                gv, ev = g[k], e[k]
+                assert gv[0] == ev[0] and gv[1] == ev[1] and gv[2] == ev[2], (where, k)
+                for a, b in ((gv[3], ev[3]), (gv[4], ev[4])):  # SUM / MIN over doubles with inf / nan
+                    assert (a != a and b != b) or a == b or a == pytest.approx(b, rel=1e-9), (where, k, a, b)
+        # aggregation-only with a raw filter; filter bitmaps of raw leaves
+        q = parse_query("SELECT COUNT(*), SUM(l) FROM t WHERE x > 0 AND m < 20")
+        o = oracle.run_groupby(SCHEMA, segs, q)
+        r = t.execute_aggregation(hs, q)
+        assert list(r.values) == list(list(o.groups.values())[0]) and r.stats.as_tuple() == o.stats
+        for h, s in zip(hs, segs):
+            q = parse_query("SELECT COUNT(*) FROM t WHERE y <> 1.5 AND m IN (1, 2, 3) GROUP BY d")
+            got = t.filter_bitmap(h, q, s.num_docs)
+            want = oracle.filter_bitmap(SCHEMA, s, q)
+            assert np.array_equal(got[:len(want)], want)
+    finally:
+        t.close()
+
+
+def test_nodictionary_compression_reference_case(oracle, gpu_lib):
+    """NoDictionaryCompressionQueriesTest.testLZ4IntegerFilterQueriesWithCompressionCodec: 1000 rows, every 10th row
+    1001, `LZ4_INTEGER > 1000` selects exactly those 100 rows."""
+    rng = np.random.default_rng(11)
+    ints = [1001 if i % 10 == 0 else int(rng.integers(0, 1000)) for i in range(1000)]
+    longs = [1001 if i % 10 == 0 else int(rng.integers(0, 1000)) for i in range(1000)]
+    schema = [("LZ4_INTEGER", "INT"), ("LZ4_LONG", "LONG")]
+    seg = SegmentBuffers(1000, {"LZ4_INTEGER": build_raw_column("INT", ints, compression="LZ4"),
+                                "LZ4_LONG": build_raw_column("LONG", longs, compression="LZ4")})
+    t = GpuTable(schema)
+    try:
+        h = t.pin_segment(seg)
+        for sql, want in [("SELECT COUNT(*), SUM(LZ4_LONG) FROM t WHERE LZ4_INTEGER > 1000", [100, 100 * 1001.0]),
+                          ("SELECT COUNT(*), SUM(LZ4_LONG) FROM t WHERE LZ4_LONG > 1000", [100, 100 * 1001.0])]:
+            r = t.execute_aggregation([h], parse_query(sql))
+            assert list(r.values) == want
+            assert r.stats.num_entries_scanned_in_filter == 1000
     finally:
         t.close()

@@ -57,7 +57,9 @@ def build(force=False, verbose=False, defines=(), out=None):
     for src, extra, name in SOURCES:
         obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
-        cmd = [hipcc] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        # host sources carry line tables (-g does not change -O3 host code): crash traces resolve with addr2line
+        dbg = ["-g"] if src.endswith(".cpp") else []
+        cmd = [hipcc] + flags + dbg + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,

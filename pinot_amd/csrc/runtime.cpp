@@ -3378,6 +3378,7 @@ int split_for_groups_limit(pgpu_table_s* t, const int64_t* handles, int32_t nseg
   }
   if (!rest.empty()) TRY(add_part(rest, false, false));
   P->composite = true;
+  *composite = true;
   P->table = t;
   P->num_groups_limit = L;
   P->pql_cap = pql;

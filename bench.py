@@ -327,7 +327,8 @@ def main():
 
     from pinot_amd import _lib as L
     from pinot_amd.build import build
-    from pinot_amd.combine import allreduce_group_table, reduce_scatter_group_table, union_dictionaries
+    from pinot_amd.combine import (allreduce_group_table, exchange_hash_table, exchange_result, plan_combine_mode,
+                                   reduce_scatter_group_table, union_dictionaries)
     from pinot_amd.executor import GpuTable
     from pinot_amd.query import parse_query
     from pinot_amd.workloads import WORKLOADS
@@ -369,13 +370,19 @@ def main():
     inflight = max(1, args.inflight)
     streams = [torch.cuda.Stream() for _ in range(inflight)]
     torch.cuda.set_stream(streams[0])
+    # how the ranks' results merge (agreed by every rank): dense tables element-wise, hash-mode tables by a device
+    # all-to-all, numGroupsLimit / ARRAY_MAP plans by their finalized rows
+    mode = plan_combine_mode(table, handles, q) if world > 1 else "local"
     probe = table.plan(handles, q)
-    nslots, nkeys, kinds = probe.layout()
+    try:
+        nslots, nkeys, kinds = probe.layout()
+    except L.PinotGpuError:  # numGroupsLimit plan: its parts have their own tables
+        nslots, nkeys, kinds = 1, 0, []
     probe_nslots = nslots
     probe.close()
     d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
     # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
-    sharded = world > 1 and nslots * nkeys * 8 >= SHARD_BYTES
+    sharded = (world > 1 and mode == "dense" and nslots * nkeys * 8 >= SHARD_BYTES) or mode in ("hash", "rows")
 
     phases = {"plan": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0, "decode": 0.0}
     star_work = [0, 0, 0]
@@ -388,12 +395,17 @@ def main():
         plan = table.plan_execute(handles, q, s.cuda_stream, dt.data_ptr() if nkeys > 0 else None)
         c1 = time.perf_counter()
         shard = None
-        if world > 1:
+        if mode == "dense":
             with torch.cuda.stream(s):
                 if sharded:
                     shard = reduce_scatter_group_table(dt, kinds)
                 else:
                     allreduce_group_table(dt, kinds)
+        elif mode == "hash":
+            with torch.cuda.stream(s):
+                exchange_hash_table(plan)
+        elif mode == "rows":
+            shard = "rows"
         phases["plan"] += c1 - c0
         phases["merge"] += time.perf_counter() - c1
         return plan, s, dt, shard
@@ -402,7 +414,9 @@ def main():
         """Finalize query k (waits for its stream only) and release its plan."""
         plan, s, dt, shard = item
         c0 = time.perf_counter()
-        if shard is not None:
+        if shard == "rows":
+            res = exchange_result(table, plan.finalize(s.cuda_stream))
+        elif shard is not None:
             sh, k0, kn = shard
             res = plan.finalize_range(s.cuda_stream, sh.data_ptr(), k0, kn)
         else:
@@ -527,7 +541,8 @@ def main():
             "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
                        "groups": ngroups, "setup_s": round(t_gen, 1), "queries_in_flight": inflight,
-                       "combine": "reduce_scatter" if sharded else ("all_reduce" if world > 1 else "none")},
+                       "combine": {"hash": "all_to_all", "rows": "all_to_all_rows"}.get(mode, "reduce_scatter" if sharded else
+                                                                                        ("all_reduce" if world > 1 else "none"))},
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,

@@ -235,6 +235,23 @@ int pgpu_plan_finalize(pgpu_plan plan, void* stream, const void* d_table, pgpu_r
 int pgpu_plan_finalize_range(pgpu_plan plan, void* stream, const void* d_table_shard, int64_t key_begin,
                              int64_t key_count, pgpu_result* out);
 
+/* ---- cross-GPU combine of hash-mode tables (key spaces past 2^26): a hash-partitioned all-to-all instead of the
+ * element-wise merge of dense tables.  Replaces GroupByOrderByCombineOperator's IndexedTable.upsert loop
+ * (core/operator/combine/GroupByOrderByCombineOperator.java:170-181) across GPUs: every rank splits its executed
+ * table's groups by owner rank (a hash of the global composite key, the same on every rank), the records travel over
+ * RCCL (all_to_all), and each owner merges what it receives into a fresh table and finalizes its own disjoint groups.
+ * A record is 1 + num_slots int64 words: the composite key, then the slot words.  `kinds` (num_slots entries, or
+ * NULL = the plan's own) are the kinds every rank agreed on: an int64 SUM may travel as float64 when another rank's
+ * sum of that slot is float64.  Plans with ARRAY_MAP key stages (rank-local keys) and numGroupsLimit plans exchange
+ * their finalized result rows instead (pgpu_result_exchange_rows). */
+/* Per-owner group counts of the executed table (counts[nparts], nparts <= 64); waits for the plan's work. */
+int pgpu_plan_exchange_counts(pgpu_plan plan, void* stream, int32_t nparts, int64_t* counts);
+/* The records, grouped by owner in rank order, into d_out (device, cap records). */
+int pgpu_plan_exchange_export(pgpu_plan plan, void* stream, int32_t nparts, const int32_t* kinds, void* d_out,
+                              int64_t cap);
+/* Replaces the plan's table by the merge of n received records (device); pgpu_plan_finalize then returns them. */
+int pgpu_plan_exchange_merge(pgpu_plan plan, void* stream, const int32_t* kinds, const void* d_records, int64_t n);
+
 /* One-call form: plan + execute + finalize (the whole per-server query path). */
 int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,
                          void* stream, pgpu_result* out);
@@ -355,6 +372,15 @@ int pgpu_result_stats(pgpu_result r, int64_t* out6);
 /* numGroupsLimitReached (GroupByCombineOperator.java:215-219, PQL mode): 1 when the combined groups reach
  * numGroupsLimit. */
 int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out);
+/* Accumulator slots of a result (num_slots, and kinds[num_slots], enum pgpu_slot_kind; slot 0 = COUNT). */
+int pgpu_result_slot_kinds(pgpu_result r, int32_t* num_slots, int32_t* kinds);
+/* Cross-rank merge of finalized results (any plan kind; each GPU as one Pinot server): the result's rows as int64
+ * records [num_keys dictIds, num_slots words] grouped by owner rank (a hash of the dictIds), into rows (n records),
+ * counts[nparts] per owner; `kinds` as for pgpu_plan_exchange_export.  The ranks' dictionaries must agree (union). */
+int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kinds, int64_t* rows, int64_t* counts);
+/* The owner's merge of n received records (GroupByDataTableReducer's merge across servers, AggregationFunction.merge)
+ * into a new result in ascending key order, with tmpl's aggregations, dictionaries and statistics. */
+int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, const int32_t* kinds, pgpu_result* out);
 int pgpu_result_destroy(pgpu_result r);
 
 /* Docid match bitmap of one segment's filter (the FilterOperator's doc set, K2): bit d of 64-bit word d/64.

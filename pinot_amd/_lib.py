@@ -147,6 +147,9 @@ _PROTOS = {
     "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
     "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
     "pgpu_plan_finalize_range": (c_int, [c_voidp, c_voidp, c_voidp, c_i64, c_i64, ctypes.POINTER(c_voidp)]),
+    "pgpu_plan_exchange_counts": (c_int, [c_voidp, c_voidp, c_i32, c_i64p]),
+    "pgpu_plan_exchange_export": (c_int, [c_voidp, c_voidp, c_i32, c_i32p, c_voidp, c_i64]),
+    "pgpu_plan_exchange_merge": (c_int, [c_voidp, c_voidp, c_i32p, c_voidp, c_i64]),
     "pgpu_execute_groupby": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp,
                                      ctypes.POINTER(c_voidp)]),
     "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),
@@ -177,6 +180,9 @@ _PROTOS = {
     "pgpu_result_values_i64": (c_int, [c_voidp, c_int, c_i64p]),
     "pgpu_result_stats": (c_int, [c_voidp, c_i64p]),
     "pgpu_result_groups_limit_reached": (c_int, [c_voidp, ctypes.POINTER(ctypes.c_int32)]),
+    "pgpu_result_slot_kinds": (c_int, [c_voidp, c_i32p, c_i32p]),
+    "pgpu_result_exchange_rows": (c_int, [c_voidp, c_i32, c_i32p, c_i64p, c_i64p]),
+    "pgpu_result_merge_rows": (c_int, [c_voidp, c_i64p, c_i64, c_i32p, ctypes.POINTER(c_voidp)]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
     "pgpu_result_trim_sql": (c_int, [c_voidp, ctypes.POINTER(SqlTrimC), ctypes.POINTER(c_voidp)]),

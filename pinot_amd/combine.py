@@ -98,3 +98,144 @@ def union_dictionaries(table, columns, group=None):
         dist.all_gather_object(gathered, mine, group=group)
         union = sorted(set(v for vals in gathered for v in vals))
         table.add_dictionary_values(col, union)
+
+
+# ---------------------------------------------------------------------------------------------- hash / row exchange
+# Key spaces past 2^26 (hash-mode tables) and numGroupsLimit plans do not share a dense layout across ranks, so their
+# merge is a hash-partitioned all-to-all (GroupByOrderByCombineOperator's IndexedTable.upsert across servers,
+# core/operator/combine/GroupByOrderByCombineOperator.java:170-181): every group goes to one owner rank, which merges
+# what it receives; the ranks end with disjoint groups, as Pinot servers return partial tables to the broker.
+# numGroupsLimit applies per rank, as per server (each GPU is one server of the table).
+
+def agreed_slot_kinds(kinds, group=None):
+    """The slot kinds every rank exchanges in: a rank's int64 SUM travels as float64 when another rank's sum of the
+    same slot is float64 (an int64 sum could overflow on that rank's segments: SumAggregationFunction's double)."""
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, [int(k) for k in kinds], group=group)
+    out = []
+    for s, k in enumerate(kinds):
+        ks = {g[s] for g in gathered}
+        if ks <= {L.SLOT_SUM_I64, L.SLOT_SUM_F64}:
+            out.append(L.SLOT_SUM_F64 if L.SLOT_SUM_F64 in ks else L.SLOT_SUM_I64)
+        elif len(ks) == 1:
+            out.append(int(k))
+        else:
+            raise ValueError("ranks disagree on slot %d: kinds %s" % (s, sorted(ks)))
+    return out
+
+
+def all_to_all_rows(send, counts, group=None):
+    """send: [n, width] int64 records grouped by destination rank, counts[r] records for rank r.  Returns the
+    [m, width] records every rank sent to this one (rank order)."""
+    import numpy as np
+    world = dist.get_world_size(group)
+    width = send.shape[1]
+    staged = _staged(group)
+    dev = torch.device("cpu") if staged or not send.is_cuda else send.device
+    cnt = torch.as_tensor(np.asarray(counts, dtype=np.int64), device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.tolist()]
+    src = send.to(dev).contiguous().view(-1)
+    out = torch.empty((sum(rc), width), dtype=torch.int64, device=dev)
+    if world == 1:
+        out.copy_(send.to(dev))
+    else:
+        dist.all_to_all_single(out.view(-1), src, output_split_sizes=[c * width for c in rc],
+                               input_split_sizes=[int(c) * width for c in counts], group=group)
+    return out.to(send.device) if out.device != send.device else out
+
+
+def exchange_hash_table(plan, group=None):
+    """Cross-rank merge of an executed hash-mode plan (run without a caller table, on torch's current stream): its
+    groups are split by owner on the device, exchanged with all_to_all (RCCL over xGMI on a node), and merged into
+    this rank's table; plan.finalize(stream) then returns this rank's disjoint share of the merged groups."""
+    world = dist.get_world_size(group)
+    stream = torch.cuda.current_stream().cuda_stream
+    nslots, _, kinds = plan.layout()
+    kinds = agreed_slot_kinds(kinds, group)
+    counts = plan.exchange_counts(stream, world)
+    total = int(counts.sum())
+    send = torch.empty((max(total, 1), 1 + nslots), dtype=torch.int64, device="cuda")
+    plan.exchange_export(stream, world, kinds, send.data_ptr(), total)
+    recv = all_to_all_rows(send[:total], counts, group)
+    plan.exchange_merge(stream, kinds, recv.data_ptr() if recv.shape[0] else None, recv.shape[0])
+    plan._exchange_keep = recv  # read by the merge kernel queued on the stream: alive until the plan is finalized
+    return plan
+
+
+def exchange_result(table, res, group=None):
+    """Cross-rank merge of finalized results of any plan kind (numGroupsLimit plans, ARRAY_MAP key stages): the rows
+    [dictIds, slot words] are split by owner on the host, exchanged with all_to_all, and merged by the owner
+    (pgpu_result_merge_rows).  Returns this rank's disjoint share of the merged groups as a GroupByResult."""
+    import ctypes
+
+    import numpy as np
+
+    from .executor import _decode_result, _ResultHolder
+    lib = table.lib
+    world = dist.get_world_size(group)
+    r = res._holder.r
+    ns = ctypes.c_int32()
+    kinds = (ctypes.c_int32 * 32)()
+    L.check(lib.pgpu_result_slot_kinds(r, ctypes.byref(ns), kinds))
+    mine = [kinds[i] for i in range(ns.value)]
+    agreed = np.asarray(agreed_slot_kinds(mine, group), dtype=np.int32)
+    # group ids index the ranks' dictionary snapshots: they must be the same (union_dictionaries before the query)
+    sizes = []
+    for j in range(len(res._query.group_by)):
+        n = ctypes.c_int64()
+        L.check(lib.pgpu_result_key_dictionary(r, j, None, ctypes.byref(n)))
+        sizes.append(n.value)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, sizes, group=group)
+    if any(g != sizes for g in gathered):
+        raise ValueError("ranks' group-by dictionaries differ (%s): union them before the query" % gathered)
+    nk = len(res._query.group_by)
+    n = len(res)
+    rows = np.empty((max(n, 1), nk + ns.value), dtype=np.int64)
+    counts = np.zeros(world, dtype=np.int64)
+    L.check(lib.pgpu_result_exchange_rows(r, world, L.ptr(agreed, ctypes.c_int32), L.ptr(rows, ctypes.c_int64),
+                                          L.ptr(counts, ctypes.c_int64)))
+    send = torch.from_numpy(rows[:n])
+    if not _staged(group):
+        send = send.cuda()
+    recv = all_to_all_rows(send, counts, group).cpu().numpy()
+    recv = np.ascontiguousarray(recv, dtype=np.int64)
+    out = ctypes.c_void_p()
+    L.check(lib.pgpu_result_merge_rows(r, L.ptr(recv, ctypes.c_int64) if len(recv) else None, len(recv),
+                                       L.ptr(agreed, ctypes.c_int32), ctypes.byref(out)))
+    return _decode_result(table, res._query, _ResultHolder(lib, out))
+
+
+def plan_combine_mode(table, handles, query, group=None):
+    """How this query's per-rank results merge, agreed by every rank: "dense" (element-wise all-reduce /
+    reduce-scatter of the dense tables), "hash" (device all-to-all of hash-mode tables) or "rows" (host rows of the
+    finalized results: numGroupsLimit plans and ARRAY_MAP key stages).  A rank whose segments make the query a
+    numGroupsLimit plan puts every rank on the row path (the modes must match for the collectives to pair up)."""
+    from . import _lib
+    world = dist.get_world_size(group)
+    probe = table.plan(handles, query)
+    try:
+        try:
+            nslots, nkeys, kinds = probe.layout()
+            mode = "dense" if nkeys > 0 else "hash"
+        except _lib.PinotGpuError:
+            mode = "rows"  # numGroupsLimit plan (its parts have their own tables)
+        if mode == "hash":
+            # ARRAY_MAP key stages (rank-local slot numbers in the keys) cannot exchange device records; the check
+            # comes before the execution state, so the unexecuted probe answers it
+            try:
+                probe.exchange_counts(None, world)
+            except _lib.PinotGpuError as e:
+                if e.code == _lib.PGPU_ERR_UNSUPPORTED:
+                    mode = "rows"
+    finally:
+        probe.close()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mode, group=group)
+    for m in ("rows", "hash"):
+        if m in gathered:
+            return m
+    return "dense"

@@ -76,6 +76,7 @@ struct pgpu_result_s {
   pgpu::HostPinned buf;
   std::shared_ptr<pgpu::ResultPool> pool;
   std::vector<int32_t> agg_slot;          // per aggregation: its slot
+  std::vector<int32_t> slot_kind;         // per slot: how its words accumulate (internal.h SLOT_*)
   std::vector<uint8_t> agg_conv;          // per aggregation: how the slot word reads (RCONV_*)
   int64_t stats[6] = {0, 0, 0, 0, 0, 0};
   // what the rows are (DataTable / trimming): table columns and types of the group-by keys, per aggregation its

@@ -290,6 +290,16 @@ int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num
                            int32_t num_key_cols,
                            uint32_t* chunk_scratch,
                            unsigned long long* total, void* out, int64_t cap, void* stream);
+// Cross-GPU exchange of hash-mode tables: per-owner group counts (counts[nparts], zeroed by the caller), records
+// [key, num_slots words] grouped by owner (cursor[p] = owner p's first record; conv bit s: int64 word -> double), and
+// the owner's merge of n records into an initialised hash table.
+int launch_exchange_count(const uint64_t* table, const unsigned long long* hash_keys, int64_t num_keys, int32_t nparts,
+                          unsigned long long* counts, void* stream);
+int launch_exchange_scatter(const uint64_t* table, const unsigned long long* hash_keys, int64_t num_keys,
+                            int32_t num_slots, int32_t nparts, uint32_t conv, unsigned long long* cursor, uint64_t* out,
+                            void* stream);
+int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
+                         unsigned long long* hash_keys, int64_t num_keys, void* stream);
 // Partitioned group-by (k_partition.hip): K8a count, scan, K8c scatter, K8d aggregate into p.base.table.
 int occupancy_part_pass(size_t lds_bytes);
 int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* stream);

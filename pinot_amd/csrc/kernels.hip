@@ -286,6 +286,94 @@ __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint64_t* __
   }
 }
 
+// ---------------------------------------------------------------------------------------------- cross-GPU exchange
+// Hash-mode group tables across GPUs (GroupByOrderByCombineOperator's IndexedTable.upsert merge,
+// core/operator/combine/GroupByOrderByCombineOperator.java:170-181, as a hash-partitioned all-to-all): every rank
+// splits its table's groups by owner rank (a mix of the global composite key, so every rank sends each key to the same
+// owner), the records travel over RCCL, and the owner merges what it receives into a fresh table of its own.
+constexpr int kMaxExchangeParts = 64;
+__device__ __forceinline__ int32_t exchange_part(uint64_t key, int32_t nparts) {
+  uint64_t h = key * 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  return (int32_t)(h % (uint64_t)nparts);
+}
+
+// Per-owner group counts: block-local LDS histogram, one global atomic per (block, owner).
+__global__ __launch_bounds__(256) void exchange_count_kernel(const uint64_t* __restrict__ table,
+                                                             const unsigned long long* __restrict__ hash_keys,
+                                                             int64_t num_keys, int32_t nparts,
+                                                             unsigned long long* __restrict__ counts) {
+  __shared__ uint32_t h[kMaxExchangeParts];
+  if (threadIdx.x < kMaxExchangeParts) h[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < num_keys; i += (int64_t)gridDim.x * blockDim.x)
+    if (table[i] != 0) atomicAdd(&h[exchange_part((uint64_t)hash_keys[i], nparts)], 1u);  // row 0 = COUNT
+  __syncthreads();
+  if (threadIdx.x < nparts && h[threadIdx.x]) atomicAdd(counts + threadIdx.x, (unsigned long long)h[threadIdx.x]);
+}
+
+// Records [key, slot words] grouped by owner: cursor[p] starts at owner p's first record.  A wave reserves its
+// records of one owner with one atomic (ballot per owner), so the few hot cursors see one update per wave and owner.
+// conv bit s: slot s is an int64 SUM whose agreed cross-rank kind is float64 (one rank's sum could overflow int64):
+// its word leaves as the double of the value.
+__global__ __launch_bounds__(256) void exchange_scatter_kernel(const uint64_t* __restrict__ table,
+                                                               const unsigned long long* __restrict__ hash_keys,
+                                                               int64_t num_keys, int32_t num_slots, int32_t nparts,
+                                                               uint32_t conv, unsigned long long* __restrict__ cursor,
+                                                               uint64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < num_keys; base += stride) {  // wave-uniform trip count
+    const int64_t i = base + threadIdx.x;
+    const bool f = i < num_keys && table[i] != 0;
+    const uint64_t key = f ? (uint64_t)hash_keys[i] : 0ull;
+    const int32_t part = f ? exchange_part(key, nparts) : -1;
+    int64_t j = -1;
+    for (int p = 0; p < nparts; ++p) {
+      const unsigned long long m = __ballot(part == p);
+      if (!m) continue;
+      unsigned long long b = 0;
+      const int leader = __builtin_ctzll(m);
+      if (lane == leader) b = atomicAdd(cursor + p, (unsigned long long)__popcll(m));
+      b = __shfl(b, leader);
+      if (part == p)
+        j = (int64_t)b + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    if (j >= 0) {
+      uint64_t* o = out + j * (1 + num_slots);
+      o[0] = key;
+      for (int s = 0; s < num_slots; ++s) {
+        uint64_t w = table[(int64_t)s * num_keys + i];
+        if ((conv >> s) & 1u) w = (uint64_t)__double_as_longlong((double)(long long)w);
+        o[1 + s] = w;
+      }
+    }
+  }
+}
+
+// The owner's merge: every received record is upserted into the (freshly initialised) hash table, its words folded
+// per slot kind -- AggregationFunction.merge of SUM / COUNT / MIN / MAX (MIN / MAX on order-preserving keys).
+__global__ __launch_bounds__(256) void merge_records_kernel(const uint64_t* __restrict__ rec, int64_t n,
+                                                            int32_t num_slots, SlotKinds kinds,
+                                                            uint64_t* __restrict__ table,
+                                                            unsigned long long* __restrict__ hash_keys,
+                                                            int64_t num_keys) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* e = rec + r * (1 + num_slots);
+    const int64_t slot = hash_slot(hash_keys, num_keys, e[0]);
+    for (int s = 0; s < num_slots; ++s) {
+      uint64_t* w = table + (int64_t)s * num_keys + slot;
+      const uint64_t v = e[1 + s];
+      switch (kinds.k[s]) {
+        case SLOT_COUNT: case SLOT_SUM_I64: atomicAdd(reinterpret_cast<unsigned long long*>(w), (unsigned long long)v); break;
+        case SLOT_SUM_F64: atomicAdd(reinterpret_cast<double*>(w), __longlong_as_double((long long)v)); break;
+        case SLOT_MIN_KEY: atomicMin(reinterpret_cast<long long*>(w), (long long)v); break;
+        default: atomicMax(reinterpret_cast<long long*>(w), (long long)v); break;
+      }
+    }
+  }
+}
+
 // K2 alone: the FilterOperator's docId bitmap of the plan's first segment, one 32-bit word per lane group.
 __global__ __launch_bounds__(kBlock) void filter_bitmap_kernel(const KParams p, uint32_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -579,6 +667,40 @@ int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, i
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(compact_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_slots,
                      num_keys, counter, out, out_cap);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_exchange_count(const uint64_t* table, const unsigned long long* hash_keys, int64_t num_keys, int32_t nparts,
+                          unsigned long long* counts, void* stream) {
+  if (nparts < 1 || nparts > kMaxExchangeParts) return -1;
+  int64_t grid = (num_keys + 255) / 256;
+  grid = grid < 1 ? 1 : grid > 2048 ? 2048 : grid;
+  hipLaunchKernelGGL(exchange_count_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_keys,
+                     nparts, counts);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_exchange_scatter(const uint64_t* table, const unsigned long long* hash_keys, int64_t num_keys,
+                            int32_t num_slots, int32_t nparts, uint32_t conv, unsigned long long* cursor, uint64_t* out,
+                            void* stream) {
+  if (nparts < 1 || nparts > kMaxExchangeParts || num_slots > kMaxSlots) return -1;
+  int64_t grid = (num_keys + 255) / 256;
+  grid = grid < 1 ? 1 : grid > 2048 ? 2048 : grid;
+  hipLaunchKernelGGL(exchange_scatter_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_keys,
+                     num_slots, nparts, conv, cursor, out);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
+                         unsigned long long* hash_keys, int64_t num_keys, void* stream) {
+  if (n <= 0) return 0;
+  if (num_slots > kMaxSlots) return -1;
+  SlotKinds k{};
+  for (int i = 0; i < num_slots; ++i) k.k[i] = slot_kind[i];
+  int64_t grid = (n + 255) / 256;
+  grid = grid > 4096 ? 4096 : grid;
+  hipLaunchKernelGGL(merge_records_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), rec, n, num_slots, k, table,
+                     hash_keys, num_keys);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

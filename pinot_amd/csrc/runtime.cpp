@@ -525,6 +525,8 @@ struct Scratch {
   DevBuf stage_keys;  // ARRAY_MAP key spaces: the prefix hash table
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
+  DevBuf xcursor;                       // cross-GPU exchange: per-owner record cursors
+  HostPinned xstage;                    // their initial values (pinned: the upload is asynchronous)
   // Pinned staging: `stage` is the source of the execution's asynchronous uploads (records, bitsets); `readback`
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
   // free it while its uploads may still be queued behind other queries' work on a shared stream.
@@ -551,6 +553,7 @@ struct Scratch {
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release(); stage_keys.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
+    xcursor.release(); xstage.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -1113,6 +1116,10 @@ struct pgpu_plan_s {
   std::vector<int32_t> stage_end;
   std::vector<int64_t> stage_cap, stage_mult, stage_space;
   unsigned long long* d_stats = nullptr;  // statistics words of the last execution (scratch)
+  // cross-GPU exchange of a hash-mode table (pgpu_plan_exchange_*): per-owner group counts of the local table, and
+  // the records merged into the owner's table (-1: the table holds the local groups)
+  std::vector<int64_t> xchg_counts;
+  int64_t merged_records = -1;
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -3203,7 +3210,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     }
   } else {
     // hash table: unordered compaction, then key order on the host
-    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)));
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0 ? P->merged_records
+                                                                                         : std::max<int64_t>(P->total_docs, 1)));
     const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
     TRY(sc->counter.ensure(64));
     TRY(sc->ckeys.ensure((size_t)cap * 8 * rec));
@@ -3265,6 +3273,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   const int na = (int)P->agg_fn.size();
   R->num_aggs = na;
   R->agg_slot = P->agg_slot;
+  R->slot_kind = P->slot_kind;
   R->key_cols = P->key_cols;
   R->key_dicts.assign(P->key_dicts.begin(), P->key_dicts.end());
   R->key_types.clear();
@@ -3512,6 +3521,7 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
   const pgpu_result_s* R0 = rs[0].get();
   R->num_aggs = R0->num_aggs;
   R->agg_slot = R0->agg_slot;
+  R->slot_kind = kind;
   R->key_cols = R0->key_cols;
   R->key_dicts.assign(kd.begin(), kd.end());
   R->key_types = R0->key_types;
@@ -4491,6 +4501,255 @@ int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shar
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   auto R = std::make_unique<pgpu_result_s>();
   TRY(plan_finalize_impl(P, s, d_table_shard, key_begin, key_count, R.get()));
+  *out = R.release();
+  return 0;
+}
+
+// ---- cross-GPU combine of hash-mode tables (device records) and of any finalized result (host rows)
+namespace {
+int exchangeable(pgpu_plan P) {
+  if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: exchange its finalized result rows");
+  if (!P->hash) return fail(PGPU_ERR_UNSUPPORTED, "dense group tables merge element-wise (all-reduce / reduce-scatter)");
+  if (!P->stage_end.empty())
+    return fail(PGPU_ERR_UNSUPPORTED, "ARRAY_MAP key stages are rank-local: exchange the finalized result rows");
+  if (!P->executed || !P->scratch) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  return 0;
+}
+// The agreed kinds of the exchange: the plan's own, except that an int64 SUM may travel (and merge) as float64 when
+// another rank's sum of the same slot is float64 (int_sum_fits differs by the ranks' segments).
+int check_kinds(const std::vector<int32_t>& mine, const int32_t* kinds, uint32_t* conv) {
+  *conv = 0;
+  if (!kinds) return 0;
+  for (size_t s = 0; s < mine.size(); ++s) {
+    if (kinds[s] == mine[s]) continue;
+    if (mine[s] == SLOT_SUM_I64 && kinds[s] == SLOT_SUM_F64) { *conv |= 1u << s; continue; }
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "slot %zu: kind %d cannot become %d", s, mine[s], kinds[s]);
+  }
+  return 0;
+}
+// Owner rank of a finalized group (its dictId tuple): the same on every rank.
+int32_t row_owner(const int64_t* ids, int nk, int32_t nparts) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int j = 0; j < nk; ++j) h = (h ^ (uint64_t)ids[j]) * 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  return (int32_t)(h % (uint64_t)nparts);
+}
+}  // namespace
+
+int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t* counts) {
+  PGPU_ABI_GUARD;
+  TRY(exchangeable(P));
+  if (nparts < 1 || nparts > 64 || !counts) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (P->merged_records >= 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "the table already holds merged records");
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  Scratch* sc = P->scratch;
+  TRY(sc->counter.ensure((size_t)nparts * 8 + 64));
+  HIP_TRY(hipMemsetAsync(sc->counter.p, 0, (size_t)nparts * 8, s));
+  if (launch_exchange_count(reinterpret_cast<const uint64_t*>(P->d_table_used), sc->hash_keys.as<unsigned long long>(),
+                            P->num_keys, nparts, sc->counter.as<unsigned long long>(), s))
+    return fail(PGPU_ERR_DEVICE, "exchange count launch failed: %s", hipGetErrorString(hipGetLastError()));
+  TRY(sc->xstage.ensure((size_t)nparts * 8 + 64));
+  uint64_t* st = reinterpret_cast<uint64_t*>(sc->xstage.p);
+  HIP_TRY(hipMemcpyAsync(st, sc->counter.p, (size_t)nparts * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(st + nparts, P->d_stats, 48, hipMemcpyDeviceToHost, s));
+  TRY(wait_plan(P, s));
+  if (st[nparts + 5]) return timeout_fail(P);
+  P->xchg_counts.assign(nparts, 0);
+  for (int p = 0; p < nparts; ++p) counts[p] = P->xchg_counts[p] = (int64_t)st[p];
+  return 0;
+}
+
+int pgpu_plan_exchange_export(pgpu_plan P, void* stream, int32_t nparts, const int32_t* kinds, void* d_out,
+                              int64_t cap) {
+  PGPU_ABI_GUARD;
+  TRY(exchangeable(P));
+  if ((int32_t)P->xchg_counts.size() != nparts || nparts < 1)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "pgpu_plan_exchange_counts with %d parts first", nparts);
+  int64_t total = 0;
+  for (int64_t c : P->xchg_counts) total += c;
+  if (total > 0 && (!d_out || cap < total))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "the records need %lld rows", (long long)total);
+  uint32_t conv = 0;
+  TRY(check_kinds(P->slot_kind, kinds, &conv));
+  if (total == 0) return 0;
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  Scratch* sc = P->scratch;
+  TRY(sc->xcursor.ensure((size_t)nparts * 8));
+  TRY(sc->xstage.ensure((size_t)nparts * 8 + 64));
+  uint64_t* st = reinterpret_cast<uint64_t*>(sc->xstage.p);
+  uint64_t off = 0;
+  for (int p = 0; p < nparts; ++p) { st[p] = off; off += (uint64_t)P->xchg_counts[p]; }
+  HIP_TRY(hipMemcpyAsync(sc->xcursor.p, st, (size_t)nparts * 8, hipMemcpyHostToDevice, s));
+  if (launch_exchange_scatter(reinterpret_cast<const uint64_t*>(P->d_table_used), sc->hash_keys.as<unsigned long long>(),
+                              P->num_keys, (int32_t)P->slot_kind.size(), nparts, conv,
+                              sc->xcursor.as<unsigned long long>(), reinterpret_cast<uint64_t*>(d_out), s))
+    return fail(PGPU_ERR_DEVICE, "exchange scatter launch failed: %s", hipGetErrorString(hipGetLastError()));
+  // the staged cursors must stay put until the upload ran: the next use of xstage waits for this stream
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, const void* d_records, int64_t n) {
+  PGPU_ABI_GUARD;
+  TRY(exchangeable(P));
+  if (n < 0 || (n > 0 && !d_records)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  uint32_t conv = 0;
+  TRY(check_kinds(P->slot_kind, kinds, &conv));
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  Scratch* sc = P->scratch;
+  const int nslots = (int)P->slot_kind.size();
+  if (kinds) P->slot_kind.assign(kinds, kinds + nslots);
+  // the statistics words leave the table buffer (it is resized below)
+  TRY(sc->stats.ensure(64));
+  if (P->d_stats != sc->stats.as<unsigned long long>()) {
+    HIP_TRY(hipMemcpyAsync(sc->stats.p, P->d_stats, 64, hipMemcpyDeviceToDevice, s));
+    P->d_stats = sc->stats.as<unsigned long long>();
+  }
+  int64_t G = 1024;
+  while (G < 2 * n) G <<= 1;
+  // DevBuf growth frees the old buffer with hipFree, which waits for the device: nothing queued still reads it
+  TRY(sc->table.ensure((size_t)nslots * G * 8 + 64));
+  TRY(sc->hash_keys.ensure((size_t)G * 8));
+  P->num_keys = G;
+  P->d_table_used = sc->table.p;
+  P->merged_records = n;
+  if (launch_table_init(sc->table.as<uint64_t>(), P->slot_kind.data(), nslots, G, sc->hash_keys.as<unsigned long long>(), s))
+    return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (launch_merge_records(reinterpret_cast<const uint64_t*>(d_records), n, nslots, P->slot_kind.data(),
+                           sc->table.as<uint64_t>(), sc->hash_keys.as<unsigned long long>(), G, s))
+    return fail(PGPU_ERR_DEVICE, "merge launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int pgpu_result_slot_kinds(pgpu_result r, int32_t* num_slots, int32_t* kinds) {
+  PGPU_ABI_GUARD;
+  if (!r) return fail(PGPU_ERR_INVALID_ARGUMENT, "null result");
+  if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
+  if (num_slots) *num_slots = r->num_slots;
+  if (kinds) for (int i = 0; i < r->num_slots; ++i) kinds[i] = r->slot_kind[i];
+  return 0;
+}
+
+int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kinds, int64_t* rows, int64_t* counts) {
+  PGPU_ABI_GUARD;
+  if (!r || nparts < 1 || !counts || (r->n > 0 && !rows)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
+  uint32_t conv = 0;
+  TRY(check_kinds(r->slot_kind, kinds, &conv));
+  const int nk = r->num_keys, ns = r->num_slots, w = nk + ns;
+  std::vector<int32_t> owner((size_t)r->n);
+  std::vector<int64_t> off(nparts + 1, 0), ids(std::max(nk, 1));
+  for (int64_t i = 0; i < r->n; ++i) {
+    for (int j = 0; j < nk; ++j) ids[j] = r->gid(j)[i];
+    owner[i] = row_owner(ids.data(), nk, nparts);
+    ++off[owner[i] + 1];
+  }
+  for (int p = 0; p < nparts; ++p) { counts[p] = off[p + 1]; off[p + 1] += off[p]; }
+  for (int64_t i = 0; i < r->n; ++i) {
+    int64_t* o = rows + off[owner[i]]++ * w;
+    for (int j = 0; j < nk; ++j) o[j] = r->gid(j)[i];
+    for (int k = 0; k < ns; ++k) {
+      uint64_t v = r->slot(k)[i];
+      if ((conv >> k) & 1u) {
+        const double d = (double)(int64_t)v;
+        memcpy(&v, &d, 8);
+      }
+      o[nk + k] = (int64_t)v;
+    }
+  }
+  return 0;
+}
+
+int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, const int32_t* kinds, pgpu_result* out) {
+  PGPU_ABI_GUARD;
+  if (!tmpl || !out || n < 0 || (n > 0 && !rows)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if ((int)tmpl->slot_kind.size() != tmpl->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
+  uint32_t conv = 0;
+  TRY(check_kinds(tmpl->slot_kind, kinds, &conv));
+  const int nk = tmpl->num_keys, ns = tmpl->num_slots, w = nk + ns;
+  std::vector<int32_t> kind(tmpl->slot_kind);
+  if (kinds) kind.assign(kinds, kinds + ns);
+  // GroupByDataTableReducer / IndexedTable.upsert across servers: rows of one group merge by AggregationFunction.merge
+  using Key = std::array<int64_t, kMaxKeys>;
+  struct KeyHash {
+    size_t operator()(const Key& k) const {
+      uint64_t h = 0;
+      for (int64_t v : k) h = (h ^ (uint64_t)v) * 0x9E3779B97F4A7C15ull;
+      return (size_t)(h ^ (h >> 29));
+    }
+  };
+  std::unordered_map<Key, int64_t, KeyHash> index;
+  index.reserve((size_t)n);
+  std::vector<int64_t> first;  // per merged group: its first row, then the folded words
+  std::vector<uint64_t> vals;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t* e = rows + r * w;
+    Key key{};
+    for (int j = 0; j < nk; ++j) {
+      if (e[j] < 0 || e[j] > INT32_MAX) return fail(PGPU_ERR_INVALID_ARGUMENT, "row %lld: bad dictId", (long long)r);
+      key[j] = e[j];
+    }
+    auto it = index.find(key);
+    if (it == index.end()) {
+      index.emplace(key, (int64_t)first.size());
+      first.push_back(r);
+      for (int s = 0; s < ns; ++s) vals.push_back((uint64_t)e[nk + s]);
+      continue;
+    }
+    uint64_t* dst = vals.data() + it->second * ns;
+    for (int s = 0; s < ns; ++s) {
+      const uint64_t v = (uint64_t)e[nk + s];
+      switch (kind[s]) {
+        case SLOT_COUNT: case SLOT_SUM_I64: dst[s] += v; break;
+        case SLOT_SUM_F64: {
+          double a, b;
+          memcpy(&a, &dst[s], 8);
+          memcpy(&b, &v, 8);
+          a += b;
+          memcpy(&dst[s], &a, 8);
+          break;
+        }
+        case SLOT_MIN_KEY: if ((int64_t)v < (int64_t)dst[s]) dst[s] = v; break;
+        default: if ((int64_t)v > (int64_t)dst[s]) dst[s] = v; break;
+      }
+    }
+  }
+  const int64_t m = (int64_t)first.size();
+  std::vector<int64_t> order(m);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {  // ascending, last group-by column most significant
+    const int64_t* x = rows + first[a] * w;
+    const int64_t* y = rows + first[b] * w;
+    for (int j = nk - 1; j >= 0; --j)
+      if (x[j] != y[j]) return x[j] < y[j];
+    return false;
+  });
+  auto R = std::make_unique<pgpu_result_s>();
+  R->pool = tmpl->pool;
+  TRY(R->alloc(nk, ns, m));
+  for (int64_t i = 0; i < m; ++i) {
+    const int64_t* e = rows + first[order[i]] * w;
+    for (int j = 0; j < nk; ++j) R->gid(j)[i] = (int32_t)e[j];
+    for (int s = 0; s < ns; ++s) R->slot(s)[i] = vals[order[i] * ns + s];
+  }
+  R->num_aggs = tmpl->num_aggs;
+  R->agg_slot = tmpl->agg_slot;
+  R->slot_kind = kind;
+  R->agg_conv = tmpl->agg_conv;
+  for (int a = 0; a < R->num_aggs; ++a)
+    if ((tmpl->agg_fn[a] == PGPU_AGG_SUM || tmpl->agg_fn[a] == PGPU_AGG_AVG) && kind[R->agg_slot[a]] == SLOT_SUM_F64)
+      R->agg_conv[a] = RCONV_F64;
+  R->key_cols = tmpl->key_cols;
+  R->key_types = tmpl->key_types;
+  R->key_dicts = tmpl->key_dicts;
+  R->agg_fn = tmpl->agg_fn;
+  R->agg_col = tmpl->agg_col;
+  memcpy(R->stats, tmpl->stats, sizeof R->stats);
+  R->groups_limit_reached = tmpl->groups_limit_reached;
   *out = R.release();
   return 0;
 }

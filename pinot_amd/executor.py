@@ -522,6 +522,25 @@ class Plan:
         self.finalize_us = ((t1 - t0) * 1e6, (time.perf_counter() - t1) * 1e6)
         return res
 
+    def exchange_counts(self, stream, nparts):
+        """Per-owner group counts of this executed hash-mode table (pgpu_plan_exchange_counts; waits for the plan)."""
+        counts = np.zeros(nparts, dtype=np.int64)
+        L.check(self.lib.pgpu_plan_exchange_counts(self.handle, ctypes.c_void_p(stream or 0), nparts,
+                                                   L.ptr(counts, ctypes.c_int64)))
+        return counts
+
+    def exchange_export(self, stream, nparts, kinds, d_out, cap):
+        """The table's records [key, slot words] grouped by owner rank into device memory d_out (cap records)."""
+        k = np.ascontiguousarray(kinds, dtype=np.int32)
+        L.check(self.lib.pgpu_plan_exchange_export(self.handle, ctypes.c_void_p(stream or 0), nparts,
+                                                   L.ptr(k, ctypes.c_int32), ctypes.c_void_p(d_out or 0), cap))
+
+    def exchange_merge(self, stream, kinds, d_records, n):
+        """Replaces the table by the merge of n received records (device); finalize returns them."""
+        k = np.ascontiguousarray(kinds, dtype=np.int32)
+        L.check(self.lib.pgpu_plan_exchange_merge(self.handle, ctypes.c_void_p(stream or 0), L.ptr(k, ctypes.c_int32),
+                                                  ctypes.c_void_p(d_records or 0), n))
+
     def finalize_range(self, stream, d_shard, key_begin, key_count):
         """Finalize of this rank's key-range shard of the merged dense table (combine.reduce_scatter_group_table):
         the groups with keys in [key_begin, key_begin + key_count)."""

@@ -148,3 +148,51 @@ def test_union_dictionaries_single_process_group(tmp_path):
         assert t.dictionary("d") == [1, 3, 5]
     finally:
         dist.destroy_process_group()
+
+
+def _exchange_worker(rank, port, out_dir):
+    """The hash / row exchange's collectives (pinot_amd.combine): slot-kind agreement and the owner all-to-all."""
+    from pinot_amd.combine import agreed_slot_kinds, all_to_all_rows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        # rank 1's SUM could overflow int64 on its segments (float64 slot): every rank exchanges that slot as float64
+        mine = [L.SLOT_COUNT, L.SLOT_SUM_I64 if rank == 0 else L.SLOT_SUM_F64, L.SLOT_MIN_KEY]
+        agreed = agreed_slot_kinds(mine)
+        # rows [key, rank, i] grouped by owner = key % WORLD; rank r sends 3 + r rows
+        keys = np.arange(10 * rank, 10 * rank + 3 + rank, dtype=np.int64)
+        owner = keys % WORLD
+        order = np.argsort(owner, kind="stable")
+        rows = np.stack([keys, np.full_like(keys, rank), np.arange(len(keys))], axis=1)[order]
+        counts = np.bincount(owner, minlength=WORLD)
+        recv = all_to_all_rows(torch.from_numpy(np.ascontiguousarray(rows)), counts).numpy()
+        np.save(os.path.join(out_dir, "recv_%d.npy" % rank), recv)
+        np.save(os.path.join(out_dir, "kinds_%d.npy" % rank), np.array(agreed, dtype=np.int64))
+        bad = [L.SLOT_COUNT, L.SLOT_MIN_KEY if rank == 0 else L.SLOT_MAX_KEY, L.SLOT_MIN_KEY]
+        try:
+            agreed_slot_kinds(bad)
+            np.save(os.path.join(out_dir, "bad_%d.npy" % rank), np.array([0]))
+        except ValueError:
+            np.save(os.path.join(out_dir, "bad_%d.npy" % rank), np.array([1]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_row_exchange(tmp_path):
+    """Every row reaches its owner rank exactly once (rank order), and the ranks agree on the exchanged slot kinds:
+    an int64 SUM travels as float64 when another rank's is float64; kinds that cannot be reconciled fail on every
+    rank."""
+    mp.spawn(_exchange_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    sent = []
+    for r in range(WORLD):
+        keys = np.arange(10 * r, 10 * r + 3 + r)
+        sent += [(int(k), r) for k in keys]
+    for r in range(WORLD):
+        recv = np.load(tmp_path / ("recv_%d.npy" % r))
+        assert all(int(k) % WORLD == r for k in recv[:, 0])
+        assert list(recv[:, 1]) == sorted(recv[:, 1])  # rank order
+        assert sorted((int(a), int(b)) for a, b, _ in recv) == sorted(x for x in sent if x[0] % WORLD == r)
+        assert list(np.load(tmp_path / ("kinds_%d.npy" % r))) == [L.SLOT_COUNT, L.SLOT_SUM_F64, L.SLOT_MIN_KEY]
+        assert int(np.load(tmp_path / ("bad_%d.npy" % r))[0]) == 1

@@ -1,12 +1,18 @@
 """The multi-GPU query flow end to end on the device, world_size 2 (both ranks on the box's one GPU, gloo with
 host-staged collectives; on a node the same code runs over RCCL): each rank pins its own segments, the ranks union
-their group-by dictionaries (one key space), plan + execute streams into a caller-owned device table
-(pgpu_plan_create_execute), the tables are merged with an all-reduce (small key spaces) or a reduce-scatter by key
-range (large ones, then pgpu_plan_finalize_range per rank), and the merged answer must equal the oracle over the
-union of all segments (GroupByCombineOperator semantics, core/operator/combine/GroupByCombineOperator.java:113-160).
+their group-by dictionaries (one key space), and every combine mode bench.py / a server uses is checked against the
+oracle (GroupByCombineOperator semantics, core/operator/combine/GroupByCombineOperator.java:113-160):
+
+- dense, small: plan + execute into a caller-owned device table (pgpu_plan_create_execute), all-reduce;
+- dense, large: reduce-scatter by key range, pgpu_plan_finalize_range per rank (disjoint groups);
+- C5 shape: 1M-doc segments, a 160 MB table built by the partitioned group-by, reduce-scattered;
+- star-tree: segments answered from their star-trees, writing into the caller table, all-reduced;
+- hash mode (key space past 2^26): device records hash-partitioned by owner rank, all_to_all, merged by the owner
+  (GroupByOrderByCombineOperator's IndexedTable.upsert, :170-181);
+- numGroupsLimit: each rank is one Pinot server (per-segment first-seen truncation and the PQL 2x cap per rank), the
+  finalized rows are exchanged by owner and merged as the broker merges server responses.
 This is bench.py's step for --gpus N."""
 import datetime
-import json
 import os
 import socket
 import time
@@ -17,17 +23,26 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pinot_amd.combine import allreduce_group_table, reduce_scatter_group_table, union_dictionaries
+from pinot_amd.combine import (allreduce_group_table, exchange_hash_table, exchange_result, plan_combine_mode,
+                               reduce_scatter_group_table, union_dictionaries)
 from pinot_amd.query import parse_query
 
 pytestmark = pytest.mark.gpu
 
 SCHEMA = [("d", "INT"), ("e", "INT"), ("f", "INT"), ("mi", "INT"), ("md", "DOUBLE")]
-SMALL = "SELECT COUNT(*), SUM(mi), MIN(mi), MAX(mi), SUM(md) FROM t WHERE f < 40 GROUP BY d"
-LARGE = "SELECT SUM(mi), COUNT(*) FROM t GROUP BY d, e"
 WORLD = 2
 SEGS_PER_RANK = 3
 DOCS = 20000
+LIMIT = 5000
+# name -> (sql, numGroupsLimit, expected combine mode)
+CASES = {
+    "small": ("SELECT COUNT(*), SUM(mi), MIN(mi), MAX(mi), SUM(md) FROM t WHERE f < 40 GROUP BY d", 10 ** 9, "dense"),
+    "large": ("SELECT SUM(mi), COUNT(*) FROM t GROUP BY d, e", 10 ** 9, "dense"),
+    "hash": ("SELECT COUNT(*), SUM(mi), MIN(md), MAX(mi) FROM t WHERE f >= 10 GROUP BY e, mi", 10 ** 9, "hash"),
+    "limit": ("SELECT COUNT(*), SUM(mi), MAX(md) FROM t GROUP BY e, f", LIMIT, "rows"),
+}
+C5_DOCS = 1_000_000
+C4_DOCS = 200_000
 
 
 def _segment_columns(seg_index):
@@ -38,42 +53,93 @@ def _segment_columns(seg_index):
             "mi": rng.integers(-5000, 70000, DOCS).astype(np.int64), "md": rng.uniform(-1e6, 1e6, DOCS)}
 
 
+def _dump(path, table, res, q):
+    """A result as value-space key columns + aggregation values (the order of groups does not matter)."""
+    cols = res.gid_columns
+    keys = np.stack([np.asarray(table.dictionary(c))[g] for c, g in zip(q.group_by, cols)], axis=1) if len(res) else \
+        np.zeros((0, len(q.group_by)))
+    vals = [(v if v is not None else e.astype(np.float64)) for fn, v, e, c in res._col[2]]
+    vals = np.array(vals).reshape(len(q.aggregations), len(res))
+    np.savez(path, keys=keys.astype(np.float64), vals=vals)
+
+
+def _run_dense(table, handles, q, stream, shard):
+    probe = table.plan(handles, q)
+    nslots, nkeys, kinds = probe.layout()
+    probe.close()
+    d_table = torch.empty((nslots, nkeys), dtype=torch.int64, device="cuda")
+    plan = table.plan_execute(handles, q, stream, d_table.data_ptr())
+    if shard:
+        part, k0, kn = reduce_scatter_group_table(d_table, kinds)
+        res = plan.finalize_range(stream, part.data_ptr(), k0, kn)
+    else:
+        allreduce_group_table(d_table, kinds)
+        res = plan.finalize(stream, d_table.data_ptr())
+    plan.close()
+    return res
+
+
 def _worker(rank, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     # a rank that fails must not leave the other waiting in a collective forever
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=60))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=90))
     try:
         import _oracle
+        from bench import attach_star_trees
         from pinot_amd.executor import GpuTable
+        from pinot_amd.workloads import WORKLOADS
         torch.cuda.set_device(0)
-        table = GpuTable(SCHEMA, device=0)
-        mine = [rank * SEGS_PER_RANK + i for i in range(SEGS_PER_RANK)]
-        handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(s))) for s in mine]
-        union_dictionaries(table, ["d", "e"])
         # a real stream: handle 0 (the default stream) means "the table's own stream" to the C ABI, and the
         # collectives' copies on torch's stream would not wait for the scan
         torch.cuda.set_stream(torch.cuda.Stream())
         stream = torch.cuda.current_stream().cuda_stream
         assert stream != 0
-        for name, sql, shard in (("small", SMALL, False), ("large", LARGE, True)):
-            q = parse_query(sql, num_groups_limit=10 ** 9)
-            probe = table.plan(handles, q)
-            nslots, nkeys, kinds = probe.layout()
-            probe.close()
-            d_table = torch.empty((nslots, nkeys), dtype=torch.int64, device="cuda")
-            plan = table.plan_execute(handles, q, stream, d_table.data_ptr())
-            if shard:
-                part, k0, kn = reduce_scatter_group_table(d_table, kinds)
-                res = plan.finalize_range(stream, part.data_ptr(), k0, kn)
+        table = GpuTable(SCHEMA, device=0)
+        mine = [rank * SEGS_PER_RANK + i for i in range(SEGS_PER_RANK)]
+        handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(s))) for s in mine]
+        union_dictionaries(table, ["d", "e", "f", "mi"])
+        modes = {}
+        for name, (sql, limit, _) in CASES.items():
+            q = parse_query(sql, num_groups_limit=limit)
+            mode = modes[name] = plan_combine_mode(table, handles, q)
+            if mode == "dense":
+                res = _run_dense(table, handles, q, stream, shard=name == "large")
+            elif mode == "hash":
+                plan = table.plan_execute(handles, q, stream)
+                exchange_hash_table(plan)
+                res = plan.finalize(stream)
+                plan.close()
             else:
-                allreduce_group_table(d_table, kinds)
-                res = plan.finalize(stream, d_table.data_ptr())
-            plan.close()
-            rows = [[[int(x) for x in k], [float(x) for x in v]] for k, v in res.as_dict().items()]
-            with open(os.path.join(out_dir, "%s_%d.json" % (name, rank)), "w") as f:
-                json.dump(rows, f)
+                res = exchange_result(table, table.execute_groupby(handles, q, stream))
+            _dump(os.path.join(out_dir, "%s_%d.npz" % (name, rank)), table, res, q)
         table.close()
+        with open(os.path.join(out_dir, "modes_%d.txt" % rank), "w") as f:
+            f.write(" ".join("%s=%s" % kv for kv in sorted(modes.items())))
+
+        # C5 shape: one 1M-doc segment per rank, 10M-key dense table (partitioned group-by), reduce-scattered
+        w = WORKLOADS["c5"]()
+        t5 = GpuTable(w.schema, device=0)
+        h5 = [t5.generate_segment(w.gen, row0=rank * C5_DOCS, num_docs=C5_DOCS)]
+        union_dictionaries(t5, ["k1", "k2", "k3"])
+        q5 = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+        _dump(os.path.join(out_dir, "c5_%d.npz" % rank), t5, _run_dense(t5, h5, q5, stream, shard=True), q5)
+        t5.close()
+
+        # star-tree: one C4 segment per rank with its star-tree, into the caller table, all-reduced
+        w = WORKLOADS["c4"]()
+        t4 = GpuTable(w.schema, device=0)
+        h4 = [t4.generate_segment(w.gen, row0=rank * C4_DOCS, num_docs=C4_DOCS)]
+        attach_star_trees(t4, h4, w, C4_DOCS)
+        union_dictionaries(t4, ["d1", "d2"])
+        q4 = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+        probe = t4.plan(h4, q4)
+        star_segments = probe.star_work()  # segments the plan answers from their star-trees
+        probe.close()
+        _dump(os.path.join(out_dir, "c4_%d.npz" % rank), t4, _run_dense(t4, h4, q4, stream, shard=False), q4)
+        with open(os.path.join(out_dir, "c4_star_%d.txt" % rank), "w") as f:
+            f.write(str(star_segments[0]))
+        t4.close()
     finally:
         dist.destroy_process_group()
 
@@ -86,12 +152,7 @@ def _free_port():
     return p
 
 
-def _load(path):
-    with open(path) as f:
-        return {tuple(k): v for k, v in json.load(f)}
-
-
-def _run_ranks(tmp_path, limit_s=100):
+def _run_ranks(tmp_path, limit_s=200):
     ctx = mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=False)
     t0 = time.time()
     while not ctx.join(timeout=5):
@@ -102,26 +163,96 @@ def _run_ranks(tmp_path, limit_s=100):
             pytest.fail("ranks did not finish within %d s" % limit_s)
 
 
-@pytest.mark.timeout(150)
+def _load(path):
+    z = np.load(path)
+    return z["keys"], z["vals"]
+
+
+def _as_map(keys, vals):
+    return {tuple(k): vals[:, i] for i, k in enumerate(keys.tolist())}
+
+
+def _broker_merge(parts, fns):
+    """Server responses merged by key (AggregationFunction.merge): COUNT / SUM add, MIN / MAX fold."""
+    out = {}
+    for keys, vals in parts:
+        for i, k in enumerate(keys.tolist()):
+            k = tuple(k)
+            v = vals[:, i]
+            if k not in out:
+                out[k] = v.copy()
+                continue
+            for a, fn in enumerate(fns):
+                out[k][a] = min(out[k][a], v[a]) if fn == "MIN" else max(out[k][a], v[a]) if fn == "MAX" else \
+                    out[k][a] + v[a]
+    return out
+
+
+def _oracle_arrays(oracle, schema, segs, q, **kw):
+    keys, vals, _, _ = oracle.run_groupby_arrays(schema, segs, q, **kw)
+    return keys.astype(np.float64), vals
+
+
+def _compare(name, got, exp, q, fp_cols):
+    missing, extra = set(exp) - set(got), set(got) - set(exp)
+    assert not missing and not extra, (name, len(missing), len(extra), sorted(missing)[:3], sorted(extra)[:3])
+    for key, ev in exp.items():
+        gv = got[key]
+        for a, (fn, col) in enumerate(q.aggregations):
+            if col in fp_cols and fn in ("SUM", "AVG"):
+                assert gv[a] == pytest.approx(ev[a], rel=1e-9, abs=1e-6), (name, key, fn, col)
+            else:
+                assert gv[a] == ev[a], (name, key, fn, col, gv[a], ev[a])
+
+
+@pytest.mark.timeout(300)
 def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path):
     _run_ranks(tmp_path)
+    for r in range(WORLD):
+        modes = dict(kv.split("=") for kv in open(tmp_path / ("modes_%d.txt" % r)).read().split())
+        assert modes == {name: c[2] for name, c in CASES.items()}, modes
     segs = [oracle.make_segment(SCHEMA, _segment_columns(s)) for s in range(WORLD * SEGS_PER_RANK)]
-    for name, sql, shard in (("small", SMALL, False), ("large", LARGE, True)):
-        q = parse_query(sql, num_groups_limit=10 ** 9)
-        exp = oracle.run_groupby(SCHEMA, segs, q, nthreads=4).groups
-        parts = [_load(tmp_path / ("%s_%d.json" % (name, r))) for r in range(WORLD)]
-        if shard:  # disjoint key ranges: the ranks' results together are the answer
-            assert not set(parts[0]) & set(parts[1])
-            got = dict(parts[0])
-            got.update(parts[1])
-        else:  # all-reduce: both ranks hold the whole answer
-            assert parts[0] == parts[1], "all-reduce left the ranks with different answers"
-            got = parts[0]
-        missing, extra = set(exp) - set(got), set(got) - set(exp)
-        assert not missing and not extra, (name, len(missing), len(extra), sorted(missing)[:5], sorted(extra)[:5])
-        for key, vals in exp.items():
-            for (fn, col), x, y in zip(q.aggregations, got[key], vals):
-                if col == "md":
-                    assert x == pytest.approx(float(y), rel=1e-9, abs=1e-6), (name, key)
-                else:
-                    assert x == float(y), (name, key, fn)
+    for name, (sql, limit, mode) in CASES.items():
+        q = parse_query(sql, num_groups_limit=limit)
+        parts = [_load(tmp_path / ("%s_%d.npz" % (name, r))) for r in range(WORLD)]
+        maps = [_as_map(*p) for p in parts]
+        if name == "small":  # all-reduce: both ranks hold the whole answer
+            assert maps[0].keys() == maps[1].keys() and all((maps[0][k] == maps[1][k]).all() for k in maps[0])
+            got = maps[0]
+        else:  # disjoint shares: together they are the answer
+            assert not set(maps[0]) & set(maps[1]), name
+            got = {**maps[0], **maps[1]}
+        fns = [fn for fn, _ in q.aggregations]
+        if name == "limit":  # each rank a server under numGroupsLimit, then the broker's merge
+            per_rank = [_oracle_arrays(oracle, SCHEMA, segs[r * SEGS_PER_RANK:(r + 1) * SEGS_PER_RANK], q,
+                                       max_initial_capacity=min(10000, LIMIT)) for r in range(WORLD)]
+            assert all(len(k) <= 2 * LIMIT for k, _ in per_rank)  # the PQL cap bound on every rank
+            exp = _broker_merge(per_rank, fns)
+        else:
+            exp = _as_map(*_oracle_arrays(oracle, SCHEMA, segs, q))
+        _compare(name, got, exp, q, {"md"})
+
+    from pinot_amd import _lib as L
+    from pinot_amd.workloads import WORKLOADS
+    for wname, docs in (("c5", C5_DOCS), ("c4", C4_DOCS)):
+        w = WORKLOADS[wname]()
+        q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+        wsegs = []
+        for r in range(WORLD):
+            from pinot_amd.segment import SegmentBuffers
+            cols = {n: oracle.build_column(L.TYPE_NAMES[t], oracle.gen_values(g, r * docs, docs))
+                    for (n, t), g in zip(w.schema, w.gen)}
+            wsegs.append(SegmentBuffers(docs, cols))
+        parts = [_load(tmp_path / ("%s_%d.npz" % (wname, r))) for r in range(WORLD)]
+        if wname == "c5":
+            assert not set(map(tuple, parts[0][0].tolist())) & set(map(tuple, parts[1][0].tolist()))
+            keys = np.concatenate([p[0] for p in parts])
+            vals = np.concatenate([p[1] for p in parts], axis=1)
+        else:
+            keys, vals = parts[0]
+            assert np.array_equal(keys, parts[1][0]) and np.array_equal(vals, parts[1][1])
+            assert all(int(open(tmp_path / ("c4_star_%d.txt" % r)).read()) == 1 for r in range(WORLD))
+        ek, ev = _oracle_arrays(oracle, w.schema, wsegs, q)
+        og, oe = np.lexsort(keys.T[::-1]), np.lexsort(ek.T[::-1])
+        np.testing.assert_array_equal(keys[og], ek[oe], err_msg=wname)
+        np.testing.assert_array_equal(vals[:, og], ev[:, oe], err_msg=wname)

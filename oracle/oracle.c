@@ -1529,6 +1529,84 @@ static uint64_t hash_bytes(const uint8_t* p, int64_t n) {
   return h;
 }
 
+/* One hash shard of the combine's merged map (keys with (hash >> 40) % nshards == shard), in segment order. */
+typedef struct { bbuf kb; int64_t* koff; double* vals; int64_t* cnts; int64_t ng; } merge_shard;
+typedef struct {
+  seg_result* res; int nsegs; const or_query* q; int64_t limit; int nshards; merge_shard* shard; atomic_int next;
+} merge_ctx;
+static void merge_one(merge_ctx* mc, int sh) {
+  const int na = mc->q->num_aggs;
+  merge_shard* m = &mc->shard[sh];
+  int64_t counter = 0;
+  blob_map bm; bm.cap = 1024; bm.slot = malloc(sizeof(int64_t) * (size_t)bm.cap);
+  for (int64_t i = 0; i < bm.cap; i++) bm.slot[i] = -1;
+  bbuf kb = {0};
+  int64_t* koff = malloc(sizeof(int64_t) * 2); int64_t kcap = 2;
+  double* vals = NULL; int64_t* cnts = NULL; int64_t ng = 0, vcap = 0;
+  koff[0] = 0;
+  for (int s = 0; s < mc->nsegs; s++) {
+    seg_result* r = &mc->res[s];
+    for (int64_t gi = 0; gi < r->ngroups; gi++) {
+      const uint8_t* k = r->keys.b + r->koff[gi];
+      int64_t kn = r->koff[gi + 1] - r->koff[gi];
+      uint64_t h = hash_bytes(k, kn);
+      if (mc->nshards > 1 && (int)((h >> 40) % (uint64_t)mc->nshards) != sh) continue;
+      int64_t sidx = (int64_t)(h & (uint64_t)(bm.cap - 1));
+      int64_t found = -1;
+      while (bm.slot[sidx] >= 0) {
+        int64_t cand = bm.slot[sidx];
+        if (koff[cand + 1] - koff[cand] == kn && memcmp(kb.b + koff[cand], k, (size_t)kn) == 0) { found = cand; break; }
+        sidx = (sidx + 1) & (bm.cap - 1);
+      }
+      const double* v = r->vals + gi * na;
+      const int64_t* c = r->cnts + gi * na;
+      if (found < 0) {
+        if (counter++ >= mc->limit) continue; /* _numGroups.getAndIncrement() < _interSegmentNumGroupsLimit */
+        if (ng + 2 > kcap) { kcap *= 2; koff = realloc(koff, sizeof(int64_t) * (size_t)kcap); }
+        if (ng + 1 > vcap) { vcap = vcap ? vcap * 2 : 64; vals = realloc(vals, sizeof(double) * vcap * (na ? na : 1)); cnts = realloc(cnts, sizeof(int64_t) * vcap * (na ? na : 1)); }
+        bb_put(&kb, k, kn);
+        koff[ng + 1] = kb.n;
+        for (int a = 0; a < na; a++) { vals[ng * na + a] = v[a]; cnts[ng * na + a] = c[a]; }
+        bm.slot[sidx] = ng;
+        ng++;
+        if (ng * 2 > bm.cap) {
+          int64_t nc = bm.cap * 2;
+          int64_t* ns = malloc(sizeof(int64_t) * (size_t)nc);
+          for (int64_t i = 0; i < nc; i++) ns[i] = -1;
+          for (int64_t e = 0; e < ng; e++) {
+            uint64_t hh = hash_bytes(kb.b + koff[e], koff[e + 1] - koff[e]);
+            int64_t p = (int64_t)(hh & (uint64_t)(nc - 1));
+            while (ns[p] >= 0) p = (p + 1) & (nc - 1);
+            ns[p] = e;
+          }
+          free(bm.slot); bm.slot = ns; bm.cap = nc;
+        }
+      } else {
+        for (int a = 0; a < na; a++) { /* AggregationFunction.merge */
+          double* dst = &vals[found * na + a];
+          switch (mc->q->aggs[a].fn) {
+            case OR_AGG_MIN: if (!(*dst < v[a])) *dst = v[a]; break; /* MinAggregationFunction.merge */
+            case OR_AGG_MAX: if (!(*dst > v[a])) *dst = v[a]; break;
+            case OR_AGG_COUNT: *dst = (double)((int64_t)*dst + (int64_t)v[a]); break; /* Long merge */
+            default: *dst += v[a]; cnts[found * na + a] += c[a]; break;        /* SUM / AvgPair.apply */
+          }
+        }
+      }
+    }
+  }
+  free(bm.slot);
+  m->kb = kb; m->koff = koff; m->vals = vals; m->cnts = cnts; m->ng = ng;
+}
+static void* merge_worker(void* arg) {
+  merge_ctx* mc = arg;
+  for (;;) {
+    int sh = atomic_fetch_add(&mc->next, 1);
+    if (sh >= mc->nshards) break;
+    merge_one(mc, sh);
+  }
+  return NULL;
+}
+
 int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int nthreads, or_result* out,
                        char* msg, int msg_len) {
   memset(out, 0, sizeof *out);
@@ -1557,17 +1635,15 @@ int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int
       return st;
     }
 
-  /* GroupByCombineOperator.processSegments merge (:113-160), segments in order. */
+  /* GroupByCombineOperator.processSegments merge (:113-160).  Pinot's worker threads merge their segments into one
+   * ConcurrentHashMap (compute per key, :136); when the 2 x numGroupsLimit admission cap cannot bind (the segments
+   * hold no more groups than it admits) the merge here runs on `nthreads` threads too, each owning the keys of one
+   * hash shard -- the same merged map.  Otherwise segments are merged in order (one of the admission orders Pinot's
+   * threads can produce). */
   int na = q->num_aggs;
   int64_t limit = q->combine ? (int64_t)q->num_groups_limit * 2 : INT64_MAX; /* INTER_SEGMENT_NUM_GROUPS_LIMIT_FACTOR */
   if (limit > INT32_MAX) limit = INT32_MAX;
-  int64_t counter = 0;
-  blob_map bm; bm.cap = 1024; bm.slot = malloc(sizeof(int64_t) * (size_t)bm.cap);
-  for (int64_t i = 0; i < bm.cap; i++) bm.slot[i] = -1;
-  bbuf kb = {0};
-  int64_t* koff = malloc(sizeof(int64_t) * 2); int64_t kcap = 2;
-  double* vals = NULL; int64_t* cnts = NULL; int64_t ng = 0, vcap = 0;
-  koff[0] = 0;
+  int64_t total_groups = 0;
   for (int s = 0; s < nsegs; s++) {
     seg_result* r = &res[s];
     out->num_docs_scanned += r->docs_scanned;
@@ -1576,53 +1652,43 @@ int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int
     out->num_total_docs += r->total_docs;
     out->holder_kind = r->holder;
     out->num_groups_limit_reached |= r->limit_reached;
-    for (int64_t gi = 0; gi < r->ngroups; gi++) {
-      const uint8_t* k = r->keys.b + r->koff[gi];
-      int64_t kn = r->koff[gi + 1] - r->koff[gi];
-      uint64_t h = hash_bytes(k, kn);
-      int64_t sidx = (int64_t)(h & (uint64_t)(bm.cap - 1));
-      int64_t found = -1;
-      while (bm.slot[sidx] >= 0) {
-        int64_t cand = bm.slot[sidx];
-        if (koff[cand + 1] - koff[cand] == kn && memcmp(kb.b + koff[cand], k, (size_t)kn) == 0) { found = cand; break; }
-        sidx = (sidx + 1) & (bm.cap - 1);
-      }
-      const double* v = r->vals + gi * na;
-      const int64_t* c = r->cnts + gi * na;
-      if (found < 0) {
-        if (counter++ >= limit) continue; /* _numGroups.getAndIncrement() < _interSegmentNumGroupsLimit */
-        if (ng + 2 > kcap) { kcap *= 2; koff = realloc(koff, sizeof(int64_t) * (size_t)kcap); }
-        if (ng + 1 > vcap) { vcap = vcap ? vcap * 2 : 64; vals = realloc(vals, sizeof(double) * vcap * (na ? na : 1)); cnts = realloc(cnts, sizeof(int64_t) * vcap * (na ? na : 1)); }
-        bb_put(&kb, k, kn);
-        koff[ng + 1] = kb.n;
-        for (int a = 0; a < na; a++) { vals[ng * na + a] = v[a]; cnts[ng * na + a] = c[a]; }
-        bm.slot[sidx] = ng;
-        ng++;
-        if (ng * 2 > bm.cap) {
-          int64_t nc = bm.cap * 2;
-          int64_t* ns = malloc(sizeof(int64_t) * (size_t)nc);
-          for (int64_t i = 0; i < nc; i++) ns[i] = -1;
-          for (int64_t e = 0; e < ng; e++) {
-            uint64_t hh = hash_bytes(kb.b + koff[e], koff[e + 1] - koff[e]);
-            int64_t p = (int64_t)(hh & (uint64_t)(nc - 1));
-            while (ns[p] >= 0) p = (p + 1) & (nc - 1);
-            ns[p] = e;
-          }
-          free(bm.slot); bm.slot = ns; bm.cap = nc;
-        }
-      } else {
-        for (int a = 0; a < na; a++) { /* AggregationFunction.merge */
-          double* dst = &vals[found * na + a];
-          switch (q->aggs[a].fn) {
-            case OR_AGG_MIN: if (!(*dst < v[a])) *dst = v[a]; break; /* MinAggregationFunction.merge */
-            case OR_AGG_MAX: if (!(*dst > v[a])) *dst = v[a]; break;
-            case OR_AGG_COUNT: *dst = (double)((int64_t)*dst + (int64_t)v[a]); break; /* Long merge */
-            default: *dst += v[a]; cnts[found * na + a] += c[a]; break;        /* SUM / AvgPair.apply */
-          }
-        }
-      }
-    }
+    total_groups += r->ngroups;
   }
+  int nshards = total_groups <= limit && total_groups >= 65536 ? nthreads : 1;
+  merge_ctx mc = {res, nsegs, q, limit, nshards, NULL, 0};
+  mc.shard = calloc((size_t)nshards, sizeof(merge_shard));
+  if (nshards > 1) {
+    pthread_t* mt = malloc(sizeof(pthread_t) * (size_t)nshards);
+    for (int i = 0; i < nshards; i++) pthread_create(&mt[i], NULL, merge_worker, &mc);
+    for (int i = 0; i < nshards; i++) pthread_join(mt[i], NULL);
+    free(mt);
+  } else {
+    merge_worker(&mc);
+  }
+  /* the shards' maps back to back (keys are disjoint across shards) */
+  int64_t ng = 0, kbytes = 0;
+  for (int i = 0; i < nshards; i++) { ng += mc.shard[i].ng; kbytes += mc.shard[i].kb.n; }
+  bbuf kb = {0};
+  kb.b = malloc((size_t)(kbytes ? kbytes : 1));
+  kb.cap = kbytes ? kbytes : 1;
+  int64_t* koff = malloc(sizeof(int64_t) * (size_t)(ng + 2));
+  double* vals = malloc(sizeof(double) * (size_t)(ng * na + 1));
+  int64_t* cnts = malloc(sizeof(int64_t) * (size_t)(ng * na + 1));
+  koff[0] = 0;
+  int64_t g0 = 0;
+  for (int i = 0; i < nshards; i++) {
+    merge_shard* m = &mc.shard[i];
+    if (m->kb.n) memcpy(kb.b + kb.n, m->kb.b, (size_t)m->kb.n);
+    for (int64_t e = 0; e < m->ng; e++) koff[g0 + e + 1] = kb.n + m->koff[e + 1];
+    kb.n += m->kb.n;
+    if (m->ng && na) {
+      memcpy(vals + g0 * na, m->vals, sizeof(double) * (size_t)(m->ng * na));
+      memcpy(cnts + g0 * na, m->cnts, sizeof(int64_t) * (size_t)(m->ng * na));
+    }
+    g0 += m->ng;
+    free(m->kb.b); free(m->koff); free(m->vals); free(m->cnts);
+  }
+  free(mc.shard);
   out->num_groups = ng;
   /* GroupByCombineOperator.mergeResults (:215-219): the merged map holds >= numGroupsLimit groups (PQL combine);
    * without the combine, a segment's holder reached its bound. */
@@ -1636,7 +1702,7 @@ int or_execute_groupby(const or_segment* segs, int nsegs, const or_query* q, int
       out->values[a * ng + gi] = vals[gi * na + a];
       out->avg_counts[a * ng + gi] = cnts[gi * na + a];
     }
-  free(vals); free(cnts); free(bm.slot);
+  free(vals); free(cnts);
   for (int j = 0; j < nsegs; j++) { free(res[j].keys.b); free(res[j].koff); free(res[j].vals); free(res[j].cnts); }
   free(res);
   return 0;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -66,6 +67,12 @@ struct ResultPool {
 
 }  // namespace pgpu
 
+struct pgpu_result_s;
+namespace pgpu {
+// Builds the columnar form of a result held in compact form (runtime.cpp); 0 or a PGPU_ERR_* status.
+int result_expand(pgpu_result_s* r);
+}  // namespace pgpu
+
 struct pgpu_result_s {
   int64_t n = 0;
   int num_keys = 0;
@@ -85,9 +92,25 @@ struct pgpu_result_s {
   // per group-by key: the table-global dictionary snapshot its group ids index (runtime.cpp's Dict)
   std::vector<std::shared_ptr<const void>> key_dicts;
   bool groups_limit_reached = false;
+  // Compact form (large dense tables, e.g. C5's 10M groups): the groups are the set bits of the bitmap at the start
+  // of `cbuf` over the composite keys [ckey_base, ckey_base + cbits), and slot s holds their words in key order,
+  // cwidth[s] bytes each (two's complement, sign-extended) at cbuf + cslot_off[s].  The columnar form above is built
+  // from it on first access to gid() / slot() (pgpu::result_expand), as Pinot's group-key iterator decodes raw keys.
+  pgpu::HostPinned cbuf;
+  std::atomic<bool> compact{false};
+  std::mutex expand_mu;
+  int64_t ckey_base = 0, cbits = 0;
+  std::vector<int64_t> cstride, ccard, coff;
+  std::vector<int32_t> cwidth;
+  std::vector<size_t> cslot_off;
   ~pgpu_result_s() {
-    if (pool) pool->give(buf);
-    else buf.release();
+    if (pool) {
+      pool->give(buf);
+      pool->give(cbuf);
+    } else {
+      buf.release();
+      cbuf.release();
+    }
   }
   static size_t slot_offset(int nk, int64_t n) { return ((size_t)nk * n * 4 + 7) & ~size_t(7); }
   int alloc(int nk, int ns, int64_t rows) {
@@ -97,8 +120,16 @@ struct pgpu_result_s {
     if (pool && !buf.p) buf = pool->take();
     return buf.ensure(std::max<size_t>(slot_offset(nk, rows) + (size_t)ns * rows * 8, 64));
   }
-  int32_t* gid(int j) { return reinterpret_cast<int32_t*>(buf.p) + (size_t)j * n; }
-  uint64_t* slot(int s) { return reinterpret_cast<uint64_t*>((uint8_t*)buf.p + slot_offset(num_keys, n)) + (size_t)s * n; }
+  int32_t* gid_raw(int j) { return reinterpret_cast<int32_t*>(buf.p) + (size_t)j * n; }
+  uint64_t* slot_raw(int s) { return reinterpret_cast<uint64_t*>((uint8_t*)buf.p + slot_offset(num_keys, n)) + (size_t)s * n; }
+  int32_t* gid(int j) {
+    if (compact.load(std::memory_order_acquire)) pgpu::result_expand(this);
+    return gid_raw(j);
+  }
+  uint64_t* slot(int s) {
+    if (compact.load(std::memory_order_acquire)) pgpu::result_expand(this);
+    return slot_raw(s);
+  }
 };
 enum { RCONV_I64 = 0, RCONV_F64 = 1, RCONV_KEY_F64 = 2 };
 

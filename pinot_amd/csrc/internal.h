@@ -300,6 +300,20 @@ int launch_exchange_scatter(const uint64_t* table, const unsigned long long* has
                             void* stream);
 int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
                          unsigned long long* hash_keys, int64_t num_keys, void* stream);
+// Compact form of a large dense table: counts per chunk + exclusive scan (total into *total) + each slot's range over
+// the present groups (minmax [2][num_slots]); then the presence bitmap (ceil(num_keys / 64) words) and the slots'
+// words of the present groups in key order at compact_slot_width bytes, slot s from out_slots + s * cap * 8.
+int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t num_keys, uint32_t* chunk_scratch,
+                               unsigned long long* total, long long* minmax, void* stream);
+int launch_compact_dense_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int32_t* slot_kind,
+                                 const uint32_t* chunk_scratch, const long long* minmax, uint64_t* bitmap,
+                                 void* out_slots, int64_t cap, void* stream);
+int compact_slot_width(long long lo, long long hi, int kind);
+// The ordered scatter alone (chunk offsets from launch_compact_dense_count): the columnar explicit form.
+int launch_compact_ordered_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
+                                   const int64_t* key_stride, const int64_t* key_card, const int64_t* key_off,
+                                   int32_t num_key_cols, const uint32_t* chunk_scratch, void* out, int64_t cap,
+                                   void* stream);
 // Partitioned group-by (k_partition.hip): K8a count, scan, K8c scatter, K8d aggregate into p.base.table.
 int occupancy_part_pass(size_t lds_bytes);
 int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* stream);

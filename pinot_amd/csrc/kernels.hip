@@ -200,19 +200,107 @@ __global__ void compact_kernel(const uint64_t* __restrict__ table, const unsigne
 // slot s at out + (1 + s) * cap.
 constexpr int kCompactChunk = 4096;  // keys per workgroup (16 rounds of 256)
 
+// minmax (optional, [2][num_slots] int64, pre-set to 0x7F.. / 0x80.. bytes): the range of every slot's words over
+// the present groups, from which the dense-bitmap scatter picks each slot's byte width.
 __global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t* __restrict__ table, int64_t num_keys,
-                                                            uint32_t* __restrict__ chunk_cnt) {
+                                                            uint32_t* __restrict__ chunk_cnt, int32_t num_slots,
+                                                            long long* __restrict__ minmax) {
   __shared__ uint32_t wsum[4];
+  __shared__ long long smm[2 * kMaxSlots];
   const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
   uint32_t c = 0;
+  if (minmax) {
+    if (threadIdx.x < 2 * num_slots) smm[threadIdx.x] = threadIdx.x < num_slots ? INT64_MAX : INT64_MIN;
+    __syncthreads();
+  }
   for (int r = 0; r < kCompactChunk / 256; ++r) {
     const int64_t k = base + r * 256 + threadIdx.x;
-    c += (k < num_keys && table[k] != 0) ? 1u : 0u;  // row 0 = COUNT
+    const bool f = k < num_keys && table[k] != 0;  // row 0 = COUNT
+    c += f ? 1u : 0u;
+    if (minmax) {
+      for (int s = 0; s < num_slots; ++s) {
+        long long lo = f ? (long long)table[(int64_t)s * num_keys + k] : INT64_MAX, hi = f ? lo : INT64_MIN;
+        for (int off = 32; off > 0; off >>= 1) {
+          lo = min(lo, (long long)__shfl_xor(lo, off));
+          hi = max(hi, (long long)__shfl_xor(hi, off));
+        }
+        if ((threadIdx.x & 63) == 0 && lo <= hi) {
+          atomicMin(&smm[s], lo);
+          atomicMax(&smm[num_slots + s], hi);
+        }
+      }
+    }
   }
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (minmax && threadIdx.x < num_slots && smm[threadIdx.x] <= smm[num_slots + threadIdx.x]) {
+    atomicMin(minmax + threadIdx.x, smm[threadIdx.x]);
+    atomicMax(minmax + num_slots + threadIdx.x, smm[num_slots + threadIdx.x]);
+  }
+}
+
+// Byte width of a slot's words in the compact form: the narrowest two's-complement width holding [lo, hi]
+// (float64 sums always 8).
+__device__ __host__ inline int slot_width(long long lo, long long hi, int kind) {
+  if (kind == SLOT_SUM_F64) return 8;
+  if (lo >= -128 && hi <= 127) return 1;
+  if (lo >= -32768 && hi <= 32767) return 2;
+  if (lo >= (long long)INT32_MIN && hi <= (long long)INT32_MAX) return 4;
+  return 8;
+}
+
+// Compact form of a dense table (large key spaces where most keys are present, C5): a presence bitmap over the
+// keys (bit k of word k / 64; one ballot per 64 keys) and each slot's words of the present keys in key order at the
+// width slot_width picks from the count kernel's ranges -- keys need no bytes at all, and narrow words cut the
+// copy to the host (the AggregationGroupByResult iterator decodes keys from the holder's raw keys in the same way).
+// out: [ceil(num_keys / 64) u64 bitmap] then slot s at out_slots + s * cap * 8 (narrow values from its start).
+__global__ __launch_bounds__(256) void compact_dense_scatter_kernel(const uint64_t* __restrict__ table,
+                                                                    int32_t num_slots, int64_t num_keys,
+                                                                    const uint32_t* __restrict__ chunk_off,
+                                                                    SlotKinds kinds,
+                                                                    const long long* __restrict__ minmax,
+                                                                    uint64_t* __restrict__ bitmap,
+                                                                    uint8_t* __restrict__ out_slots, int64_t cap) {
+  __shared__ uint32_t wcnt[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
+  int width[kMaxSlots];
+  for (int s = 0; s < num_slots; ++s) width[s] = slot_width(minmax[s], minmax[num_slots + s], kinds.k[s]);
+  uint32_t pos = chunk_off[blockIdx.x];
+  for (int r = 0; r < kCompactChunk / 256; ++r) {
+    const int64_t k = base + r * 256 + threadIdx.x;
+    const bool f = k < num_keys && table[k] != 0;
+    const unsigned long long bal = __ballot(f);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (lane == 0) {
+      wcnt[wave] = (uint32_t)__popcll(bal);
+      const int64_t wk = base + r * 256 + wave * 64;  // first key of this wave: a multiple of 64
+      if (wk < num_keys) bitmap[wk >> 6] = bal;
+    }
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += wcnt[w];
+    const uint32_t round_total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (f) {
+      const int64_t j = (int64_t)pos + before + rank;
+      if (j < cap) {
+        for (int s = 0; s < num_slots; ++s) {
+          const uint64_t v = table[(int64_t)s * num_keys + k];
+          uint8_t* o = out_slots + (int64_t)s * cap * 8;
+          switch (width[s]) {
+            case 1: o[j] = (uint8_t)v; break;
+            case 2: reinterpret_cast<uint16_t*>(o)[j] = (uint16_t)v; break;
+            case 4: reinterpret_cast<uint32_t*>(o)[j] = (uint32_t)v; break;
+            default: reinterpret_cast<uint64_t*>(o)[j] = v; break;
+          }
+        }
+      }
+    }
+    pos += round_total;
+    __syncthreads();
+  }
 }
 
 // One workgroup: exclusive prefix of chunk_cnt (in place) and the total into *total.
@@ -727,8 +815,53 @@ int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num
     kd.card[j] = key_card[j];
     kd.off[j] = key_off[j];
   }
-  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch);
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch,
+                     num_slots, static_cast<long long*>(nullptr));
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);
+  hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_slots, num_keys,
+                     chunk_scratch, kd, reinterpret_cast<uint8_t*>(out), cap);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t num_keys, uint32_t* chunk_scratch,
+                               unsigned long long* total, long long* minmax, void* stream) {
+  const int64_t nch = compact_ordered_chunks(num_keys);
+  if (nch < 1 || nch > INT32_MAX || num_slots > kMaxSlots) return -1;
+  if (hipMemsetAsync(minmax, 0x7F, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
+  if (hipMemsetAsync(minmax + num_slots, 0x80, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch,
+                     num_slots, minmax);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int launch_compact_dense_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int32_t* slot_kind,
+                                 const uint32_t* chunk_scratch, const long long* minmax, uint64_t* bitmap,
+                                 void* out_slots, int64_t cap, void* stream) {
+  const int64_t nch = compact_ordered_chunks(num_keys);
+  if (nch < 1 || nch > INT32_MAX || num_slots > kMaxSlots) return -1;
+  SlotKinds k{};
+  for (int i = 0; i < num_slots; ++i) k.k[i] = slot_kind[i];
+  hipLaunchKernelGGL(compact_dense_scatter_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_slots,
+                     num_keys, chunk_scratch, k, minmax, bitmap, reinterpret_cast<uint8_t*>(out_slots), cap);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
+int compact_slot_width(long long lo, long long hi, int kind) { return slot_width(lo, hi, kind); }
+int launch_compact_ordered_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
+                                   const int64_t* key_stride, const int64_t* key_card, const int64_t* key_off,
+                                   int32_t num_key_cols, const uint32_t* chunk_scratch, void* out, int64_t cap,
+                                   void* stream) {
+  const int64_t nch = compact_ordered_chunks(num_keys);
+  if (nch < 1 || nch > INT32_MAX || num_key_cols > kMaxKeys || (cap & 1)) return -1;
+  KeyDecode kd{};
+  kd.n = num_key_cols;
+  kd.base = key_base;
+  for (int j = 0; j < num_key_cols; ++j) {
+    kd.stride[j] = key_stride[j];
+    kd.card[j] = key_card[j];
+    kd.off[j] = key_off[j];
+  }
   hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_slots, num_keys,
                      chunk_scratch, kd, reinterpret_cast<uint8_t*>(out), cap);
   return PGPU_HIP_OK(hipGetLastError());

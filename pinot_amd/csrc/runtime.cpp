@@ -3174,38 +3174,85 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       ++j;
     }
   } else if (!P->hash) {
-    // large dense table: ordered compaction on the device (count / scan / scatter, dictIds decoded there),
-    // copied back row by row into the pinned result buffer
-    int64_t cap = std::max<int64_t>(2, std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)));
-    cap = (cap + 1) & ~int64_t(1);
+    // large dense table: ordered compaction on the device (count / scan, then a scatter in key order), copied back
+    // into the pinned result buffer.  Two forms: the columnar dictIds + 8-byte words, or -- when it moves fewer
+    // bytes, as for C5's 10M groups of 10M keys -- a presence bitmap over the keys plus each slot's words at the
+    // narrowest width their range allows (decoded on the host on first access).
     const int64_t nch = compact_ordered_chunks(G);
-    TRY(sc->counter.ensure(64));
+    TRY(sc->counter.ensure(64 + (size_t)nslots * 16));
     TRY(sc->cslots.ensure((size_t)std::max<int64_t>(nch, 1) * 4));
-    TRY(sc->ckeys.ensure((size_t)cap * (4 * nk + 8 * nslots) + 8));
-    if (launch_compact_ordered(table, nslots, G, key_begin, P->key_stride.data(), P->key_card.data(),
-                               P->key_off.data(), nk,
-                               sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(), sc->ckeys.p, cap,
-                               stream))
-      return fail(PGPU_ERR_DEVICE, "compact launch failed: %s", hipGetErrorString(hipGetLastError()));
-    TRY(sc->readback.ensure(64));
+    long long* d_minmax = reinterpret_cast<long long*>(sc->counter.as<uint8_t>() + 64);
+    if (launch_compact_dense_count(table, nslots, G, sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(),
+                                   d_minmax, stream))
+      return fail(PGPU_ERR_DEVICE, "compact count launch failed: %s", hipGetErrorString(hipGetLastError()));
+    TRY(sc->readback.ensure(64 + (size_t)nslots * 16));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st + 8, d_minmax, (size_t)nslots * 16, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
-    n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
+    n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)G);
     matched = st[1];
     star_scanned = st[2] + st[3];
     P->star_docs_read = (int64_t)st[4];
-    TRY(R->alloc(nk, nslots, n));
-    if (n > 0) {
-      const uint8_t* dev = sc->ckeys.as<uint8_t>();
-      for (int j = 0; j < nk; ++j)
-        HIP_TRY(hipMemcpyAsync(R->gid(j), dev + (size_t)j * cap * 4, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    std::vector<int32_t> width(nslots, 8);
+    int64_t narrow_bytes = 0;
+    for (int s = 0; s < nslots; ++s) {
+      const long long lo = (long long)st[8 + s], hi = (long long)st[8 + nslots + s];
+      width[s] = n > 0 ? compact_slot_width(lo, hi, P->slot_kind[s]) : 8;
+      narrow_bytes += n * width[s];
+    }
+    const int64_t bitmap_words = (G + 63) / 64;
+    static const bool no_compact = getenv_flag("PGPU_NO_COMPACT_RESULT");
+    const bool compact = !no_compact && n > 0 && bitmap_words * 8 + narrow_bytes < n * (4 * nk + 8 * nslots);
+    if (compact) {
+      const int64_t cap = n;
+      TRY(sc->ckeys.ensure((size_t)bitmap_words * 8 + (size_t)nslots * cap * 8));
+      uint8_t* dev = sc->ckeys.as<uint8_t>();
+      if (launch_compact_dense_scatter(table, nslots, G, P->slot_kind.data(), sc->cslots.as<uint32_t>(), d_minmax,
+                                       reinterpret_cast<uint64_t*>(dev), dev + bitmap_words * 8, cap, stream))
+        return fail(PGPU_ERR_DEVICE, "compact scatter launch failed: %s", hipGetErrorString(hipGetLastError()));
+      R->num_keys = nk;
+      R->num_slots = nslots;
+      R->n = n;
+      R->ckey_base = key_begin;
+      R->cbits = G;
+      R->cstride = P->key_stride;
+      R->ccard = P->key_card;
+      R->coff = P->key_off;
+      R->cwidth = width;
+      R->cslot_off.assign(nslots, 0);
+      size_t off = (size_t)bitmap_words * 8;
+      for (int s = 0; s < nslots; ++s) {
+        R->cslot_off[s] = off;
+        off += ((size_t)n * width[s] + 7) & ~size_t(7);
+      }
+      if (R->pool) R->cbuf = R->pool->take();
+      TRY(R->cbuf.ensure(off));
+      uint8_t* h = reinterpret_cast<uint8_t*>(R->cbuf.p);
+      HIP_TRY(hipMemcpyAsync(h, dev, (size_t)bitmap_words * 8, hipMemcpyDeviceToHost, stream));
       for (int s = 0; s < nslots; ++s)
-        HIP_TRY(hipMemcpyAsync(R->slot(s), dev + (size_t)nk * cap * 4 + (size_t)s * cap * 8, (size_t)n * 8,
+        HIP_TRY(hipMemcpyAsync(h + R->cslot_off[s], dev + bitmap_words * 8 + (size_t)s * cap * 8, (size_t)n * width[s],
                                hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      R->compact.store(true, std::memory_order_release);
+    } else {
+      const int64_t cap = std::max<int64_t>(2, (n + 1) & ~int64_t(1));
+      TRY(sc->ckeys.ensure((size_t)cap * (4 * nk + 8 * nslots) + 8));
+      if (launch_compact_ordered_scatter(table, nslots, G, key_begin, P->key_stride.data(), P->key_card.data(),
+                                         P->key_off.data(), nk, sc->cslots.as<uint32_t>(), sc->ckeys.p, cap, stream))
+        return fail(PGPU_ERR_DEVICE, "compact launch failed: %s", hipGetErrorString(hipGetLastError()));
+      TRY(R->alloc(nk, nslots, n));
+      if (n > 0) {
+        const uint8_t* dev = sc->ckeys.as<uint8_t>();
+        for (int j = 0; j < nk; ++j)
+          HIP_TRY(hipMemcpyAsync(R->gid_raw(j), dev + (size_t)j * cap * 4, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+        for (int s = 0; s < nslots; ++s)
+          HIP_TRY(hipMemcpyAsync(R->slot_raw(s), dev + (size_t)nk * cap * 4 + (size_t)s * cap * 8, (size_t)n * 8,
+                                 hipMemcpyDeviceToHost, stream));
+      }
       HIP_TRY(hipStreamSynchronize(stream));
     }
   } else {
@@ -3317,6 +3364,69 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
             t_sync1 - t_start, t_sync2 - t_sync1, now_us() - t_sync2, (long long)n);
   return 0;
 }
+
+}  // namespace
+
+// Columnar form of a compact result: rows are the bitmap's set bits in key order; each block of 4096 bitmap words is
+// decoded by one task of the host pool (a prefix of its popcounts gives its first row).
+int pgpu::result_expand(pgpu_result_s* R) {
+  std::lock_guard<std::mutex> g(R->expand_mu);
+  if (!R->compact.load(std::memory_order_acquire)) return 0;
+  const int nk = R->num_keys, ns = R->num_slots;
+  const int64_t n = R->n;
+  TRY(R->alloc(nk, ns, n));
+  const uint64_t* bm = reinterpret_cast<const uint64_t*>(R->cbuf.p);
+  const int64_t words = (R->cbits + 63) / 64;
+  constexpr int64_t kBlockWords = 4096;
+  const int64_t nb = (words + kBlockWords - 1) / kBlockWords;
+  std::vector<int64_t> first(nb + 1, 0);
+  auto count = [&](int b) {
+    int64_t c = 0;
+    for (int64_t w = b * kBlockWords; w < std::min(words, (b + 1) * kBlockWords); ++w) c += __builtin_popcountll(bm[w]);
+    first[b + 1] = c;
+  };
+  auto decode = [&](int b) {
+    int64_t row = first[b];
+    std::vector<int32_t*> gid(nk);
+    for (int j = 0; j < nk; ++j) gid[j] = R->gid_raw(j);
+    for (int64_t w = b * kBlockWords; w < std::min(words, (b + 1) * kBlockWords); ++w) {
+      for (uint64_t bits = bm[w]; bits; bits &= bits - 1, ++row) {
+        if (row >= n) return;
+        const uint64_t key = (uint64_t)(R->ckey_base + w * 64 + __builtin_ctzll(bits));
+        for (int j = 0; j < nk; ++j)
+          gid[j][row] = (int32_t)((key / (uint64_t)R->cstride[j]) % (uint64_t)R->ccard[j] + R->coff[j]);
+      }
+    }
+  };
+  if (nb > 1) host_pool().run((int)nb, count);
+  else if (nb == 1) count(0);
+  for (int64_t b = 0; b < nb; ++b) first[b + 1] += first[b];
+  if (nb > 1) host_pool().run((int)nb, decode);
+  else if (nb == 1) decode(0);
+  // the words, sign-extended from their compact widths
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(R->cbuf.p);
+  constexpr int64_t kRows = 1 << 20;
+  const int64_t tasks = (n + kRows - 1) / kRows;
+  auto widen = [&](int t) {
+    const int64_t r0 = t * kRows, r1 = std::min(n, r0 + kRows);
+    for (int s = 0; s < ns; ++s) {
+      const uint8_t* src = base + R->cslot_off[s];
+      uint64_t* dst = R->slot_raw(s);
+      switch (R->cwidth[s]) {
+        case 1: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int8_t*>(src)[r]; break;
+        case 2: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int16_t*>(src)[r]; break;
+        case 4: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(src)[r]; break;
+        default: memcpy(dst + r0, reinterpret_cast<const uint64_t*>(src) + r0, (size_t)(r1 - r0) * 8); break;
+      }
+    }
+  };
+  if (tasks > 1) host_pool().run((int)tasks, widen);
+  else if (tasks == 1) widen(0);
+  R->compact.store(false, std::memory_order_release);
+  return 0;
+}
+
+namespace {
 
 // ------------------------------------------------------------------------------------------ numGroupsLimit
 // Pinot's group-key generators admit a segment's groups in first-seen docId order until numGroupsLimit and drop the

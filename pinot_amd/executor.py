@@ -52,16 +52,32 @@ class GroupByResult:
     ({key tuple: [aggregation results]}) is built on first use of `keys` / `values` / `as_dict()`."""
 
     def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None, holder=None, table=None,
-                 query=None):
+                 query=None, n=None):
         self.stats = stats
         self.num_groups_limit_reached = False
         self._holder, self._table, self._query = holder, table, query  # the C result behind the columnar views
-        self.exact = exact or {}    # agg index -> np.int64 array of exact integer accumulators
+        self._exact = exact         # agg index -> np.int64 array of exact integer accumulators
         self._keys, self._values = keys, values
         # columnar: (dicts, [per group-by column: [n] int32 dictIds], per-agg (fn, values f64 | None,
-        # exact i64 | None, counts | None), n) -- numpy views of the C result's pinned buffer
-        self._col = columnar
-        self._n = len(keys) if keys is not None else (columnar[3] if columnar is not None else 0)
+        # exact i64 | None, counts | None), n) -- numpy views of the C result's pinned buffer; or a loader
+        # returning (columnar, exact), called on first use (a compact C result is decoded then, not before)
+        self._col_data = None if callable(columnar) else columnar
+        self._col_loader = columnar if callable(columnar) else None
+        self._n = len(keys) if keys is not None else (n if n is not None else
+                                                       (columnar[3] if self._col_data is not None else 0))
+
+    @property
+    def _col(self):
+        if self._col_loader is not None:
+            self._col_data, self._exact = self._col_loader()
+            self._col_loader = None
+        return self._col_data
+
+    @property
+    def exact(self):
+        if self._col_loader is not None:
+            self._col  # noqa: B018 -- loads the columns (and the exact accumulators)
+        return self._exact or {}
 
     @property
     def gid_columns(self):
@@ -584,41 +600,45 @@ def _view(holder, addr, n, dtype):
 
 
 def _decode_result(table, query, holder):
-    """Columnar result over zero-copy views of the C result (pgpu_result_*_view)."""
+    """Columnar result over zero-copy views of the C result (pgpu_result_*_view), built on first use: a result the
+    C side holds in compact form (large dense tables) is only decoded when its rows are read."""
     lib, r = table.lib, holder.r
     n = ctypes.c_int64()
     L.check(lib.pgpu_result_num_groups(r, ctypes.byref(n)))
     n = n.value
     nk = len(query.group_by)
-    ptr = ctypes.c_void_p()
-    cols = []
-    for j in range(nk):
-        L.check(lib.pgpu_result_group_ids_view(r, j, ctypes.byref(ptr)))
-        cols.append(_view(holder, ptr.value, n, np.int32))
-    dicts = [table.result_dictionary(r, j, c) for j, c in enumerate(query.group_by)]
-    aggs = []
-    exact = {}
-    form = ctypes.c_int32()
-    for a, (fn, _) in enumerate(query.aggregations):
-        L.check(lib.pgpu_result_words_view(r, a, ctypes.byref(ptr), ctypes.byref(form)))
-        e = v = c = None
-        if form.value == 0:
-            exact[a] = e = _view(holder, ptr.value, n, np.int64)
-        elif form.value == 1:
-            v = _view(holder, ptr.value, n, np.float64)
-        else:
-            v = np.empty(max(n, 1), dtype=np.float64)
-            L.check(lib.pgpu_result_values(r, a, L.ptr(v, ctypes.c_double)))
-            v = v[:n]
-        if fn == "AVG":
-            L.check(lib.pgpu_result_words_view(r, -1, ctypes.byref(ptr), ctypes.byref(form)))
-            c = _view(holder, ptr.value, n, np.int64)
-        aggs.append((fn, v, e, c))
+
+    def load():
+        ptr = ctypes.c_void_p()
+        cols = []
+        for j in range(nk):
+            L.check(lib.pgpu_result_group_ids_view(r, j, ctypes.byref(ptr)))
+            cols.append(_view(holder, ptr.value, n, np.int32))
+        dicts = [table.result_dictionary(r, j, c) for j, c in enumerate(query.group_by)]
+        aggs = []
+        exact = {}
+        form = ctypes.c_int32()
+        for a, (fn, _) in enumerate(query.aggregations):
+            L.check(lib.pgpu_result_words_view(r, a, ctypes.byref(ptr), ctypes.byref(form)))
+            e = v = c = None
+            if form.value == 0:
+                exact[a] = e = _view(holder, ptr.value, n, np.int64)
+            elif form.value == 1:
+                v = _view(holder, ptr.value, n, np.float64)
+            else:
+                v = np.empty(max(n, 1), dtype=np.float64)
+                L.check(lib.pgpu_result_values(r, a, L.ptr(v, ctypes.c_double)))
+                v = v[:n]
+            if fn == "AVG":
+                L.check(lib.pgpu_result_words_view(r, -1, ctypes.byref(ptr), ctypes.byref(form)))
+                c = _view(holder, ptr.value, n, np.int64)
+            aggs.append((fn, v, e, c))
+        return (dicts, cols, aggs, n), exact
+
     st = np.zeros(6, dtype=np.int64)
     L.check(lib.pgpu_result_stats(r, L.ptr(st, ctypes.c_int64)))
     reached = ctypes.c_int32()
     L.check(lib.pgpu_result_groups_limit_reached(r, ctypes.byref(reached)))
-    res = GroupByResult(stats=ExecutionStatistics(st), exact=exact, columnar=(dicts, cols, aggs, n), holder=holder,
-                        table=table, query=query)
+    res = GroupByResult(stats=ExecutionStatistics(st), columnar=load, holder=holder, table=table, query=query, n=n)
     res.num_groups_limit_reached = bool(reached.value)
     return res

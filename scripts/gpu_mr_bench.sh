@@ -14,5 +14,6 @@ run() {  # name, args...
   return $rc
 }
 run dense --workload c2 --rows-total 4000000 &&
-run hash --workload c5 --rows-total 2000000 --sql "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3, m" &&
+run hash --workload c5 --rows-total 2000000 --num-groups-limit 1000000000 --sql "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k3, m" &&
+run limit --workload c5 --rows-total 2000000 --sql "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3, m" &&
 run rows --workload c1 --rows-total 2000000 --sql "SELECT SUM(metric), COUNT(*) FROM t GROUP BY filt, metric"

@@ -458,6 +458,9 @@ def main():
         first = run(args.warmup, inflight)[0][0]
     for k in phases:
         phases[k] = 0.0
+    import gc
+    gc.collect()
+    gc.disable()  # as timeit does: a collector pass inside a sub-millisecond step is the harness's cost, not the query's
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -469,6 +472,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if args.verify and first is not None:  # FLOAT/DOUBLE sums vary in their last bits (atomicAdd order): 1e-9
         ref = first.as_dict()
         for res, _ in timed:

@@ -188,6 +188,11 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
     const uint32_t m = gp(set)[group];
     return negate ? ~m : m;
   }
+  if (kind == LEAF_BITDIR) {
+    const uint32_t* blk = reinterpret_cast<const uint32_t*>(gp(reinterpret_cast<const uint64_t*>(set))[group >> 11]);
+    const uint32_t m = blk ? gp(blk)[group & 2047] : 0u;
+    return negate ? ~m : m;
+  }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
 }
 
@@ -354,6 +359,29 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
 __device__ __forceinline__ int64_t wave_max_i64(int64_t x) {
   for (int off = 32; off > 0; off >>= 1) { const int64_t y = __shfl_xor(x, off); x = y > x ? y : x; }
   return x;
+}
+
+// Per-workgroup statistics counters: the waves' partial sums meet in LDS and one atomic per workgroup and counter
+// reaches global memory (a thousand waves' atomics on one address serialise in a kernel's tail: 70 us on C3's
+// 125-segment scan, measured).  Call from every thread of the workgroup; v holds the lane's partial of counter k.
+template <int N, int BLOCK = kBlock>
+__device__ __forceinline__ void block_stats_add(unsigned long long* __restrict__ stats, const int (&idx)[N],
+                                                unsigned long long (&v)[N]) {
+  __shared__ unsigned long long red[BLOCK / 64][N];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (lane == 0) red[wave][k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k)  // constant k: idx[] and v[] stay in registers (a dynamic index would use scratch)
+    if (threadIdx.x == k) {
+      unsigned long long t = 0;
+      for (int w = 0; w < BLOCK / 64; ++w) t += red[w][k];
+      if (t) atomicAdd(stats + idx[k], t);
+    }
 }
 
 // Lane partials of one slot (cnt docs; isum / fsum sums; imin / imax extremes) -> one atomic on `word`.

@@ -39,8 +39,11 @@ constexpr int kFastLeaves = 4;              // pure-AND programs up to this many
 // LEAF_RAW_RANGE / LEAF_RAW_IN: host-side kinds of a raw-value predicate on a no-dictionary column
 // (RangePredicateEvaluatorFactory / InPredicateEvaluatorFactory raw evaluators).  raw_leaf_bitmap_kernel evaluates
 // them per query into a docId bitmap (KRawTask), which the scans read as a LEAF_BITMAP leaf.
+// LEAF_BITDIR: a LEAF_BITMAP of one dictId whose Roaring containers are all BITMAP containers -- read in place, as
+// BitmapBasedFilterOperator uses a single bitmap without an OR (BitmapBasedFilterOperator.java:77-79): `set` is a
+// directory of one device pointer per 65536-doc block (the container's 2048 words; null = no docs in the block).
 enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4, LEAF_BITMAP = 5,
-                          LEAF_RAW_RANGE = 6, LEAF_RAW_IN = 7 };
+                          LEAF_RAW_RANGE = 6, LEAF_RAW_IN = 7, LEAF_BITDIR = 8 };
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
 enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
 enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };
@@ -88,6 +91,7 @@ struct KParams {
   int32_t num_cols;
   int32_t num_segs;
   int32_t num_tiles;
+  int32_t tile_shift;      // small plans: each 8192-doc tile is split into 1 << tile_shift tiles (16 / 8 docs per lane)
   int32_t num_ops;         // 0 = match all
   int32_t pure_and;        // program is LEAF... AND(n): evaluate leaves with early exit, no stack
   int32_t ops[kMaxOps];    // (opcode << 16) | arg

@@ -197,8 +197,11 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
     }
   }
   if (!SCATTER) {
-    for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
-    if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
+    {
+      const int idx[1] = {0};
+      unsigned long long v[1] = {matched};
+      block_stats_add<1>(p.stats, idx, v);
+    }
     __syncthreads();
     // partition totals, and this workgroup's run inside every coarse partition it touches
     for (int i = tid; i < pp.num_parts; i += kBlock)

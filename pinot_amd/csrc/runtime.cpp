@@ -1069,6 +1069,7 @@ struct pgpu_plan_s {
   std::vector<std::shared_ptr<InvIndex>> inv_refs;  // inverted indexes the bit tasks point into (kept alive)
   std::shared_ptr<DeviceImage> image;     // cached plans: device-resident records / tile map (one-launch plans)
   int64_t num_tiles = 0;
+  int tile_shift = 0;                     // small plans: 8192-doc tiles split in 2^tile_shift (KParams.tile_shift)
   int64_t total_docs = 0;
   int64_t scanned_entries_model = 0;      // numEntriesScannedInFilter of the STATS_CONST segments (host)
   bool in_kernel_stats = false;           // the scan kernel counts STATS_CHAIN / STATS_LEAP2 segments
@@ -2311,7 +2312,32 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           kl[k].kind = LEAF_BITMAP;
           kl[k].negate = 0;
         }
-        if (lh.kind == LEAF_BITMAP) {  // docId bitmap region: whole 65536-doc containers
+        bool bitdir = false;
+        if (lh.kind == LEAF_BITMAP && lh.inv_ids.size() == 1 && !getenv_flag("PGPU_NO_BITDIR")) {
+          // one dictId whose containers are all BITMAPs: the scan reads them in place through a block directory
+          const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
+          const InvIndex::Entry& e = inv.ids[lh.inv_ids[0]];
+          bitdir = true;
+          for (int32_t ci = e.begin; ci < e.begin + e.count && bitdir; ++ci) bitdir = inv.conts[ci].type == CONT_BITMAP;
+          if (bitdir) {
+            const int64_t nblk = ((int64_t)s->num_docs + 65535) >> 16;
+            std::vector<uint64_t> dir((size_t)nblk, 0);
+            for (int32_t ci = e.begin; ci < e.begin + e.count; ++ci) {
+              const InvIndex::Cont& ct = inv.conts[ci];
+              if (ct.key >= 0 && ct.key < nblk)
+                dir[ct.key] = reinterpret_cast<uint64_t>(reinterpret_cast<const uint32_t*>(inv.d_block) + ct.word);
+            }
+            C.inv_refs.push_back(s->cols[q->predicates[perm[k]].column].inv);
+            const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
+            C.set_fix.emplace_back(field, (int64_t)C.set_words.size());
+            for (uint64_t d : dir) {
+              C.set_words.push_back((uint32_t)d);
+              C.set_words.push_back((uint32_t)(d >> 32));
+            }
+            kl[k].kind = LEAF_BITDIR;
+          }
+        }
+        if (lh.kind == LEAF_BITMAP && !bitdir) {  // docId bitmap region: whole 65536-doc containers
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
           C.inv_refs.push_back(s->cols[q->predicates[perm[k]].column].inv);
@@ -2576,6 +2602,21 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     merge_chunk(C, tile_base);
     tile_base += C.tiles;
   }
+  // Small plans (C1: one 1M-doc segment = 123 tiles on 256 CUs): split every tile into 2 or 4 so that at least two
+  // tiles per CU run.  The scan kernel's direct path only: not with leap-frog statistics (their per-(tile, wave)
+  // bytes are whole 32-doc groups) nor the partitioned group-by (its own passes).
+  if (tile_base > 0 && tile_base < 2 * (int64_t)t->num_cus && !P->any_leap2 && P->star.empty() &&
+      !(P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes) && !getenv_flag("PGPU_NO_TILE_SPLIT")) {
+    int sh = 1;
+    while (sh < 2 && (tile_base << sh) < 2 * (int64_t)t->num_cus) ++sh;
+    P->tile_shift = sh;
+    for (size_t r = 0; r + sizeof(KSegHdr) <= P->segrec.size(); r += P->seg_stride) {
+      KSegHdr* h = reinterpret_cast<KSegHdr*>(P->segrec.data() + r);
+      h->tile_base <<= sh;
+      h->num_tiles <<= sh;
+    }
+    tile_base <<= sh;
+  }
   TRY(configure(tile_base));
   P->chunks.assign(1, LaunchChunk{0, (int64_t)(P->segrec.size() / std::max(P->seg_stride, 1)), 0, P->num_tiles, 0,
                                   (int64_t)P->set_fix.size(), 0, (int64_t)P->set_words.size()});
@@ -2816,6 +2857,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   }
   kp.num_keys_total = P->num_keys;
   kp.key_bias = P->key_bias;
+  kp.tile_shift = P->tile_shift;
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = stats;

@@ -125,10 +125,15 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
         stats = S.hdr->stats;
         if (fast) PGPU_LOAD_LEAVES();
       }
-      const int64_t group = (t - tile_base) * kBlock + tid;
+      const int64_t lt = t - tile_base;
+      const int64_t group = (lt >> p.tile_shift) * kBlock + tid;
       const int64_t ngroups = ((int64_t)nd + 31) >> 5;
       const int64_t doc0 = group << 5;
       uint32_t mask = doc0 >= nd ? 0u : (nd - doc0 >= 32 ? ~0u : ((1u << (nd - doc0)) - 1u));
+      if (p.tile_shift) {  // a split tile: this lane's 32 / 2^shift docs of its group
+        const int w = 32 >> p.tile_shift;
+        mask &= (0xFFFFFFFFu >> (32 - w)) << (w * (int)(lt & ((1 << p.tile_shift) - 1)));
+      }
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
       if (fast) {
         // STATS_LEAP2 (two scans in leap-frog): both masks are needed for the entry count, no early exit
@@ -200,15 +205,23 @@ __global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_gro
       for (int k = lane; k < kk; k += 64)
         p.leap_maps[(t_begin + (int64_t)k * t_step) * (kBlock / 64) + wave] = lmaps[k * (kBlock / 64) + wave];
   }
-  // numDocsScanned: wave reduce, one atomic per wave.
+  // numDocsScanned / numEntriesScannedInFilter: one atomic per workgroup (block_stats_add)
+#if PGPU_STATS_PER_WAVE
   for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
-  if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
   unsigned long long entries = in_filter;
   for (int off = 32; off > 0; off >>= 1) entries += __shfl_xor(entries, off);
+  if ((tid & 63) == 0 && matched) atomicAdd(p.stats, matched);
   if ((tid & 63) == 0 && entries) atomicAdd(p.stats + 2, entries);
+  if (MODE == MODE_LDS) __syncthreads();
+#else
+  {
+    const int idx[2] = {0, 2};
+    unsigned long long v[2] = {matched, (unsigned long long)in_filter};
+    block_stats_add<2>(p.stats, idx, v);
+  }
+#endif
 
   if (MODE == MODE_LDS) {
-    __syncthreads();
     uint64_t* out = p.slab + (int64_t)blockIdx.x * table_words;
     for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
   }

@@ -390,15 +390,10 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
       if (__any((mask >> 16) != 0u)) star_aggregate_half<MODE, 16>(p, S, g, mask, cache, cached, tbl, G);
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    matched += __shfl_xor(matched, o);
-    scanned += __shfl_xor(scanned, o);
-    read += __shfl_xor(read, o);
-  }
-  if ((tid & 63) == 0) {
-    if (matched) atomicAdd(p.stats, matched);
-    if (scanned) atomicAdd(p.stats + 1, scanned);
-    if (read) atomicAdd(p.stats + 3, read);
+  {
+    const int idx[3] = {0, 1, 3};
+    unsigned long long v[3] = {(unsigned long long)matched, (unsigned long long)scanned, (unsigned long long)read};
+    block_stats_add<3, BLOCK>(p.stats, idx, v);
   }
   if (MODE == MODE_LDS) {
     __syncthreads();

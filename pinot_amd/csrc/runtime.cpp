@@ -2400,7 +2400,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->star_chunks = (int)(want_env > 0 ? want_env : (int64_t)t->num_cus * per_cu);
     }
     // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
-    P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16;
+    P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16 && !getenv_flag("PGPU_NO_DENSE");
     {
       static std::mutex occ_mu;
       static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU

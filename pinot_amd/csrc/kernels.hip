@@ -213,21 +213,32 @@ __global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t* __re
     if (threadIdx.x < 2 * num_slots) smm[threadIdx.x] = threadIdx.x < num_slots ? INT64_MAX : INT64_MIN;
     __syncthreads();
   }
-  for (int r = 0; r < kCompactChunk / 256; ++r) {
-    const int64_t k = base + r * 256 + threadIdx.x;
-    const bool f = k < num_keys && table[k] != 0;  // row 0 = COUNT
-    c += f ? 1u : 0u;
-    if (minmax) {
-      for (int s = 0; s < num_slots; ++s) {
-        long long lo = f ? (long long)table[(int64_t)s * num_keys + k] : INT64_MAX, hi = f ? lo : INT64_MIN;
-        for (int off = 32; off > 0; off >>= 1) {
-          lo = min(lo, (long long)__shfl_xor(lo, off));
-          hi = max(hi, (long long)__shfl_xor(hi, off));
+  if (!minmax) {
+    for (int r = 0; r < kCompactChunk / 256; ++r) {
+      const int64_t k = base + r * 256 + threadIdx.x;
+      c += (k < num_keys && table[k] != 0) ? 1u : 0u;  // row 0 = COUNT
+    }
+  } else {
+    // one slot at a time: the lane folds its 16 keys, then one wave reduction per slot
+    for (int s = 0; s < num_slots; ++s) {
+      long long lo = INT64_MAX, hi = INT64_MIN;
+      for (int r = 0; r < kCompactChunk / 256; ++r) {
+        const int64_t k = base + r * 256 + threadIdx.x;
+        const bool f = k < num_keys && table[k] != 0;
+        if (s == 0) c += f ? 1u : 0u;
+        if (f) {
+          const long long v = (long long)table[(int64_t)s * num_keys + k];
+          lo = min(lo, v);
+          hi = max(hi, v);
         }
-        if ((threadIdx.x & 63) == 0 && lo <= hi) {
-          atomicMin(&smm[s], lo);
-          atomicMax(&smm[num_slots + s], hi);
-        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, (long long)__shfl_xor(lo, off));
+        hi = max(hi, (long long)__shfl_xor(hi, off));
+      }
+      if ((threadIdx.x & 63) == 0 && lo <= hi) {
+        atomicMin(&smm[s], lo);
+        atomicMax(&smm[num_slots + s], hi);
       }
     }
   }

@@ -551,6 +551,67 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
   }
 }
 
+// The 16 docs of a half-group into one slot row of the table.  In LDS the atomics are issued for every doc, the
+// unmatched ones with the kind's neutral value at key 0: no per-doc exec-mask branch and no per-doc switch on the
+// slot kind (measured on C2: SALU instructions outnumbered VALU ones with the branches), and an LDS atomic costs the
+// same with 32 or 64 lanes active.  Global tables keep the branches (a neutral global atomic is real traffic).
+template <int MODE>
+__device__ __forceinline__ void accumulate16_i(uint64_t* __restrict__ row, const int32_t (&key)[16], uint32_t m,
+                                               int kind, const int64_t (&v)[16]) {
+  if (MODE == MODE_LDS) {
+    unsigned long long* u = reinterpret_cast<unsigned long long*>(row);
+    long long* l = reinterpret_cast<long long*>(row);
+    switch (kind) {
+      case SLOT_SUM_I64:
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) atomicAdd(u + key[i], (unsigned long long)v[i]);
+        break;
+      case SLOT_MIN_KEY:
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) atomicMin(l + key[i], (long long)v[i]);
+        break;
+      default:
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((m >> i) & 1u) atomicMax(l + key[i], (long long)v[i]);
+        break;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) accumulate<MODE>(row, key[i], kind, v[i], 0.0);
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void accumulate16_count(uint64_t* __restrict__ row, const int32_t (&key)[16], uint32_t m) {
+  if (MODE == MODE_LDS) {
+    unsigned long long* u = reinterpret_cast<unsigned long long*>(row);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) atomicAdd(u + key[i], 1ull);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_COUNT, 0, 0.0);
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void accumulate16_f(uint64_t* __restrict__ row, const int32_t (&key)[16], uint32_t m,
+                                               const double (&v)[16]) {
+  if (MODE == MODE_LDS) {
+    double* d = reinterpret_cast<double*>(row);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) atomicAdd(d + key[i], v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_SUM_F64, 0, v[i]);
+  }
+}
+
 // One half (docs H..H+15 of the lane's group) of aggregate_group.
 template <int MODE, int H>
 __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
@@ -582,11 +643,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     if (kind == SLOT_COUNT) {
       uint64_t* __restrict__ row = tbl + (int64_t)s * G;
       if (G == 1) accumulate_wave(row, SLOT_COUNT, __popc(m), 0, 0.0);
-      else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_COUNT, 0, 0.0);
-      }
+      else accumulate16_count<MODE>(row, key, m);
       ++s;
       continue;
     }
@@ -622,9 +679,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
           accumulate_wave(row, kr, __popc(m), acc, 0.0);
           continue;
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], kr, v[i], 0.0);
+        accumulate16_i<MODE>(row, key, m, kr, v);
       }
     }
     if (need_f) {
@@ -643,9 +698,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
           accumulate_wave(row, SLOT_SUM_F64, __popc(m), 0, acc);
           continue;
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) accumulate<MODE>(row, key[i], SLOT_SUM_F64, 0, v[i]);
+        accumulate16_f<MODE>(row, key, m, v);
       }
     }
     s = e;

@@ -53,7 +53,10 @@ template <int MODE, bool DENSE>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
-__global__ __launch_bounds__(kBlock, DENSE ? 3 : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
+#ifndef PGPU_DENSE_MIN_WAVES
+#define PGPU_DENSE_MIN_WAVES 3
+#endif
+__global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t G = p.num_keys_total;

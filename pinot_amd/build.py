@@ -79,5 +79,17 @@ def build(force=False, verbose=False, defines=(), out=None):
     return lib_path
 
 
+def build_tools():
+    """tools/qps_native: concurrent callers of the C ABI without Python (links the in-tree library)."""
+    hipcc = _hipcc()
+    out = os.path.join(ROOT, "tools", "qps_native")
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-O2", "-std=c++17", os.path.join(ROOT, "tools", "qps_native.cpp"), "-I" + os.path.join(ROOT, "include"),
+           "-L" + HERE, "-lpinotgpu", "-Wl,-rpath,$ORIGIN/../pinot_amd", "-o", out]
+    res = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc (tools) failed:\n" + res.stdout[-4000:])
+    return out
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))

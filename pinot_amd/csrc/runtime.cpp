@@ -2858,6 +2858,13 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_keys_total = P->num_keys;
   kp.key_bias = P->key_bias;
   kp.tile_shift = P->tile_shift;
+  // Tile order: interleaved (the tiles in flight on an XCD come from ~one segment: its dictionaries stay in that
+  // XCD's L2 for the dense path's per-doc gathers) or chunked (a workgroup's tiles follow each other in one segment:
+  // its records and leaf registers are loaded once per run).  PGPU_TILE_ORDER=0/1 forces one (A/B).
+  {
+    static const char* fo = getenv("PGPU_TILE_ORDER");
+    kp.tile_chunks = fo ? (atoi(fo) == 1 ? 1 : 0) : (P->dense ? 0 : 1);
+  }
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.stats = stats;

@@ -89,7 +89,15 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
   uint32_t in_filter = 0;  // STATS_CHAIN entries of this lane (< 2^32: at most 4 leaves x 32 docs x tiles)
   const int64_t T = p.num_tiles;
   int64_t t_begin, t_end, t_step;
-  if (gridDim.x >= 64 && (gridDim.x & 7) == 0) {
+  if (gridDim.x >= 64 && (gridDim.x & 7) == 0 && p.tile_chunks) {
+    // chunked: each workgroup a contiguous run of its XCD's eighth -- consecutive tiles of one segment, so the
+    // segment's records are read once per run instead of once per tile (plans without per-doc gathers)
+    const int64_t x = blockIdx.x & 7, i = blockIdx.x >> 3, nx = gridDim.x >> 3;
+    const int64_t lo = x * T / 8, len = (x + 1) * T / 8 - lo;
+    t_begin = lo + i * len / nx;
+    t_end = lo + (i + 1) * len / nx;
+    t_step = 1;
+  } else if (gridDim.x >= 64 && (gridDim.x & 7) == 0) {
     const int64_t x = blockIdx.x & 7;
     t_begin = x * T / 8 + (blockIdx.x >> 3);
     t_end = (x + 1) * T / 8;

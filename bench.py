@@ -383,6 +383,7 @@ def main():
     probe_nslots = nslots
     probe.close()
     d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
+    caller_table = nkeys > 0 and (world > 1 or os.environ.get("PGPU_BENCH_CALLER_TABLE") == "1")
     # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
     sharded = (world > 1 and mode == "dense" and nslots * nkeys * 8 >= SHARD_BYTES) or mode in ("hash", "rows")
 
@@ -394,7 +395,9 @@ def main():
         enqueue the cross-rank merge of its table on the same stream."""
         c0 = time.perf_counter()
         s, dt = streams[k % inflight], d_tables[k % inflight]
-        plan = table.plan_execute(handles, q, s.cuda_stream, dt.data_ptr() if nkeys > 0 else None)
+        # the merge across ranks needs the table in caller memory; one GPU keeps the plan's own table, whose
+        # statistics words follow it (one copy back instead of two)
+        plan = table.plan_execute(handles, q, s.cuda_stream, dt.data_ptr() if caller_table else None)
         c1 = time.perf_counter()
         shard = None
         if mode == "dense":
@@ -422,7 +425,7 @@ def main():
             sh, k0, kn = shard
             res = plan.finalize_range(s.cuda_stream, sh.data_ptr(), k0, kn)
         else:
-            res = plan.finalize(s.cuda_stream, dt.data_ptr() if nkeys > 0 else None)
+            res = plan.finalize(s.cuda_stream, dt.data_ptr() if caller_table else None)
         c1 = time.perf_counter()
         try:
             tm = plan.timing_us()

@@ -30,10 +30,15 @@ __global__ __launch_bounds__(256) void startree_traverse_kernel(const KStarSeg* 
   if (blockIdx.x == 0 && threadIdx.x == 0 && past_deadline(deadline)) flag_timeout(stats);  // read by K6
   const KStarSeg& S = segs[blockIdx.x];
   __shared__ int cur_n, next_n, nr, rem;
+  // the BFS frontiers in LDS when the tree is small enough (C4: ~100 nodes per segment): a level's expansion then
+  // costs no global round trip; larger trees use the global scratch
+  constexpr int kLdsFront = 2048;
+  __shared__ int lfront[2][3 * kLdsFront];
   const int tid = threadIdx.x;
   const int* __restrict__ nodes = S.nodes;
-  int* fa = S.frontier;
-  int* fb = S.frontier + 3 * S.num_nodes;
+  const bool in_lds = S.num_nodes <= kLdsFront;
+  int* fa = in_lds ? lfront[0] : S.frontier;
+  int* fb = in_lds ? lfront[1] : S.frontier + 3 * S.num_nodes;
   if (tid == 0) {
     fa[0] = 0;  // root
     fa[1] = S.pred_mask;

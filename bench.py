@@ -40,8 +40,8 @@ def log(msg):
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=200)  # sub-millisecond steps: a long enough timed region
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="adanalytics")
     p.add_argument("--sql", default=None, help="override the workload's query (same table)")
     p.add_argument("--rows-total", type=int, default=None,

@@ -69,6 +69,13 @@ enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE =
 enum pgpu_fwd_format { PGPU_FWD_FIXED_BIT = 0, PGPU_FWD_SORTED_PAIRS = 1, PGPU_FWD_RAW_FIXED = 2 };
 
 int pgpu_abi_version(void);
+/* Process start-up / shut-down of the executor (the server's lifecycle around PlanMaker, ServerInstance.java:86-90):
+ * pgpu_init brings up the HIP runtime on devices 0..n_gpus-1 (n_gpus <= 0: every visible device) so the first query
+ * pays no context creation, and returns the number of devices initialised (or a negative status); pgpu_shutdown
+ * waits for every initialised device's queued work.  Tables, plans and results own their memory and are released by
+ * their destroy calls (segments on unpin / table destroy, as ImmutableSegmentImpl.destroy frees them). */
+int pgpu_init(int n_gpus);
+int pgpu_shutdown(void);
 /* Copies the calling thread's last error message (NUL-terminated, truncated to len). Returns its full length. */
 int pgpu_last_error(char* buf, size_t len);
 int pgpu_device_count(int* count);
@@ -382,6 +389,8 @@ int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kind
  * into a new result in ascending key order, with tmpl's aggregations, dictionaries and statistics. */
 int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, const int32_t* kinds, pgpu_result* out);
 int pgpu_result_destroy(pgpu_result r);
+/* The same as pgpu_result_destroy (the name SURVEY.md §8b lists). */
+int pgpu_free_result(pgpu_result r);
 
 /* Docid match bitmap of one segment's filter (the FilterOperator's doc set, K2): bit d of 64-bit word d/64.
  * out_words must hold ceil(num_docs / 64) words. */

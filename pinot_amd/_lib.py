@@ -124,6 +124,8 @@ class QueryTimeoutError(PinotGpuError):
 
 _PROTOS = {
     "pgpu_abi_version": (c_int, []),
+    "pgpu_init": (c_int, [c_int]),
+    "pgpu_shutdown": (c_int, []),
     "pgpu_last_error": (c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pgpu_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "pgpu_table_create": (c_int, [c_int, c_int, c_char_pp, c_i32p, ctypes.POINTER(c_voidp)]),
@@ -184,6 +186,7 @@ _PROTOS = {
     "pgpu_result_exchange_rows": (c_int, [c_voidp, c_i32, c_i32p, c_i64p, c_i64p]),
     "pgpu_result_merge_rows": (c_int, [c_voidp, c_i64p, c_i64, c_i32p, ctypes.POINTER(c_voidp)]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
+    "pgpu_free_result": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
     "pgpu_result_trim_sql": (c_int, [c_voidp, ctypes.POINTER(SqlTrimC), ctypes.POINTER(c_voidp)]),
     "pgpu_result_trim_pql": (c_int, [c_voidp, c_i32, c_i32, c_i64p, c_i64, c_i64p]),

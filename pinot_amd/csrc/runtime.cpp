@@ -3819,6 +3819,44 @@ extern "C" {
 
 int pgpu_abi_version(void) { return PGPU_ABI_VERSION; }
 
+namespace {
+std::mutex g_init_mu;
+int g_init_devices = 0;
+}  // namespace
+
+int pgpu_init(int n_gpus) {
+  PGPU_ABI_GUARD;
+  install_crash_trace();
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  if (n_gpus > count) return fail(PGPU_ERR_INVALID_ARGUMENT, "%d devices requested, %d visible", n_gpus, count);
+  const int n = n_gpus > 0 ? n_gpus : count;
+  std::lock_guard<std::mutex> g(g_init_mu);
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  for (int d = g_init_devices; d < n; ++d) {
+    HIP_TRY(hipSetDevice(d));
+    HIP_TRY(hipFree(nullptr));  // creates the device's context now
+  }
+  HIP_TRY(hipSetDevice(prev));
+  g_init_devices = std::max(g_init_devices, n);
+  host_pool();  // the planning workers start here, not inside the first query
+  return n;
+}
+
+int pgpu_shutdown(void) {
+  PGPU_ABI_GUARD;
+  std::lock_guard<std::mutex> g(g_init_mu);
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  for (int d = 0; d < g_init_devices; ++d) {
+    HIP_TRY(hipSetDevice(d));
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  HIP_TRY(hipSetDevice(prev));
+  return 0;
+}
+
 int pgpu_last_error(char* buf, size_t len) {
   if (buf && len) {
     size_t n = std::min(len - 1, g_err.size());
@@ -5089,6 +5127,7 @@ int pgpu_result_destroy(pgpu_result r) {
   delete r;
   return 0;
 }
+int pgpu_free_result(pgpu_result r) { return pgpu_result_destroy(r); }
 
 int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* out_words) {
   PGPU_ABI_GUARD;

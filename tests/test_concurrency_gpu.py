@@ -218,3 +218,29 @@ def test_pins_grow_dictionaries_under_running_queries(oracle, gpu_lib):
             _same(t.execute_groupby(hs + new, q).as_dict(), oracle.run_groupby(w.schema, all_segs, q).groups)
     finally:
         t.close()
+
+
+def test_init_shutdown_and_free_result(gpu_lib):
+    """Process lifecycle entry points: pgpu_init brings up every visible device (idempotent),
+    pgpu_free_result releases a result, pgpu_shutdown drains the devices."""
+    import ctypes
+    lib = L.load()
+    n = lib.pgpu_init(0)
+    assert n >= 1, L.last_error()
+    assert lib.pgpu_init(1) == 1
+    assert lib.pgpu_init(n + 1) == L.PGPU_ERR_INVALID_ARGUMENT
+    w = WORKLOADS["c1"]()
+    t = GpuTable(w.schema)
+    try:
+        h = t.generate_segment(w.gen, row0=0, num_docs=10000)
+        q, keep = parse_query(w.sql).to_c(t.index)
+        hs = (ctypes.c_int64 * 1)(h)
+        r = ctypes.c_void_p()
+        L.check(lib.pgpu_execute_groupby(t.handle, hs, 1, ctypes.byref(q), None, ctypes.byref(r)))
+        ng = ctypes.c_int64()
+        L.check(lib.pgpu_result_num_groups(r, ctypes.byref(ng)))
+        assert ng.value == 16
+        assert lib.pgpu_free_result(r) == 0
+    finally:
+        t.close()
+    assert lib.pgpu_shutdown() == 0

@@ -444,17 +444,26 @@ def main():
         phases["decode"] += dec_us * 1e-6
         return res, k_us
 
-    def run(n, depth):
-        """n queries, at most `depth` in flight; returns the results and kernel timings in query order."""
+    def run(n, depth, keep_all=False):
+        """n queries, at most `depth` in flight; returns (results, kernel timings) in query order.  Only the first
+        result is kept unless keep_all (--verify): a server hands each result on and frees it, and holding hundreds
+        of them (C5: 51 MB of pinned host memory each) would starve the result buffer pool."""
         from collections import deque
-        pending, out = deque(), []
+        pending, res, kus = deque(), [], []
+
+        def done(item):
+            r, k = complete(item)
+            if keep_all or not res:
+                res.append(r)
+            kus.append(k)
+
         for k in range(n):
             pending.append(launch(k))
             if len(pending) >= depth:
-                out.append(complete(pending.popleft()))
+                done(pending.popleft())
         while pending:
-            out.append(complete(pending.popleft()))
-        return out
+            done(pending.popleft())
+        return res, kus
 
     first = None
     if args.warmup:
@@ -469,7 +478,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    timed = run(args.steps, inflight)
+    timed, _ = run(args.steps, inflight, keep_all=args.verify)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -478,13 +487,13 @@ def main():
     gc.enable()
     if args.verify and first is not None:  # FLOAT/DOUBLE sums vary in their last bits (atomicAdd order): 1e-9
         ref = first.as_dict()
-        for res, _ in timed:
+        for res in timed:
             got = res.as_dict()
             assert got.keys() == ref.keys(), "groups differ between steps"
             for k, v in got.items():
                 assert all(x == y or abs(x - y) <= 1e-9 * max(abs(x), abs(y)) for x, y in zip(v, ref[k])), k
     if first is None and timed:
-        first = timed[0][0]
+        first = timed[0]
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -498,7 +507,7 @@ def main():
     value = total_rows * args.steps / elapsed
     # The scan kernel's duration for the roofline: a serialized pass (one query in flight, so no other query's
     # kernels share the GPU with the one being timed), after the timed region.
-    kernel_us = [k for _, k in run(max(1, args.roofline_steps), 1)]
+    kernel_us = run(max(1, args.roofline_steps), 1)[1]
     launches = kernel_us[0][1] if kernel_us else 1
     kernel_avg_us = float(np.mean([k for k, _ in kernel_us])) / launches if kernel_us else 0.0  # per launch
 

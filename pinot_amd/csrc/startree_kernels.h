@@ -32,11 +32,17 @@ __global__ __launch_bounds__(256) void startree_traverse_kernel(const KStarSeg* 
   __shared__ int cur_n, next_n, nr, rem;
   // the BFS frontiers in LDS when the tree is small enough (C4: ~100 nodes per segment): a level's expansion then
   // costs no global round trip; larger trees use the global scratch
-  constexpr int kLdsFront = 2048;
+  // ... and the node array itself (7 ints per node, one coalesced copy): every level's node and child reads are
+  // then LDS reads instead of dependent global round trips
+  constexpr int kLdsFront = 1024;
   __shared__ int lfront[2][3 * kLdsFront];
+  __shared__ int lnodes[7 * kLdsFront];
   const int tid = threadIdx.x;
-  const int* __restrict__ nodes = S.nodes;
   const bool in_lds = S.num_nodes <= kLdsFront;
+  if (in_lds) {
+    for (int i = tid; i < 7 * S.num_nodes; i += blockDim.x) lnodes[i] = S.nodes[i];
+  }
+  const int* __restrict__ nodes = in_lds ? lnodes : S.nodes;
   int* fa = in_lds ? lfront[0] : S.frontier;
   int* fb = in_lds ? lfront[1] : S.frontier + 3 * S.num_nodes;
   if (tid == 0) {

@@ -3,6 +3,7 @@
 # VARIANTS="PGPU_DICT_GATHERS=0 PGPU_DICT_GATHERS=1" BENCH_ARGS="--workload c2 --segments-per-gpu 100"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
+touch pinot_amd/libpinotgpu*.so
 tag=$(echo "${BENCH_ARGS:-default}" | tr -c 'a-zA-Z0-9' '_')
 for rep in 1 2; do
   for v in ${VARIANTS}; do

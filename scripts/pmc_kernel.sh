@@ -4,6 +4,7 @@
 # PASSES="A B C;D E" (passes separated by ;).  Each pass is its own rocprofv3 run (counter slots per pass are limited); CSVs under gpurun_out/pmc/<tag>/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+touch pinot_amd/libpinotgpu*.so  # the prebuilt library is current
 TAG=${TAG:-k}
 OUT=gpurun_out/pmc/$TAG
 mkdir -p $OUT

@@ -2401,10 +2401,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
     P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16 && !getenv_flag("PGPU_NO_DENSE");
+    int per_cu;  // resident workgroups per CU
     {
       static std::mutex occ_mu;
       static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU
-      int per_cu;
       {
         std::lock_guard<std::mutex> g(occ_mu);
         const auto k = std::make_tuple(t->device, (int)P->mode, (int)P->dense, P->lds_bytes);
@@ -2416,7 +2416,12 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       per_cu = std::min(per_cu, 4);
       P->grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
     }
-    if (P->grid >= 64) P->grid &= ~7;  // a multiple of the 8 XCDs: the kernel's XCD-aware tile order
+    // a multiple of the 8 XCDs (the kernel's XCD-aware tile order): rounded up when every tile has a workgroup of its
+    // own and the resident capacity allows -- rounded down, an XCD's eighth of the tiles would outnumber its
+    // workgroups and one of them would scan two tiles in a row (C1: 492 tiles on 488 workgroups)
+    if (P->grid >= 64)
+      P->grid = (P->grid == tile_base && ((P->grid + 7) & ~7) <= (int64_t)t->num_cus * per_cu) ? (P->grid + 7) & ~7
+                                                                                                  : P->grid & ~7;
     if (P->any_leap2 || (se && P->in_kernel_stats)) {
       P->leap_reserved = true;
       // STATS_LEAP2 bytes of a workgroup's tiles are buffered in LDS (one per tile and wave) until the end of the

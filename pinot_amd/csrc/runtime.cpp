@@ -4797,7 +4797,8 @@ int pgpu_plan_exchange_export(pgpu_plan P, void* stream, int32_t nparts, const i
 int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, const void* d_records, int64_t n) {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
-  if (n < 0 || (n > 0 && !d_records)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (n < 0 || (n > 0 && !d_records) || n > (INT64_C(1) << 40))  // the table below holds >= 2n slots
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   uint32_t conv = 0;
   TRY(check_kinds(P->slot_kind, kinds, &conv));
   DeviceGuard g(P->table->device);
@@ -4838,7 +4839,8 @@ int pgpu_result_slot_kinds(pgpu_result r, int32_t* num_slots, int32_t* kinds) {
 
 int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kinds, int64_t* rows, int64_t* counts) {
   PGPU_ABI_GUARD;
-  if (!r || nparts < 1 || !counts || (r->n > 0 && !rows)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (!r || nparts < 1 || nparts > (1 << 20) || !counts || (r->n > 0 && !rows))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
   uint32_t conv = 0;
   TRY(check_kinds(r->slot_kind, kinds, &conv));

@@ -57,6 +57,7 @@ def parse_args():
     p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
     p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
     p.add_argument("--host-profile", action="store_true", help="report host time per phase of a step")
+    p.add_argument("--step-trace", default=None, help="write per-query host timestamps of the timed region (JSON)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE passes (roofline.traffic)")
     p.add_argument("--no-star-tree", action="store_true", help="query option useStarTree=false (scan path)")
     p.add_argument("--num-groups-limit", type=int, default=None, help="query option numGroupsLimit (default: the "
@@ -312,25 +313,24 @@ def main():
         _build()
         pmc = pmc_traffic(args)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # PGPU_BENCH_BACKEND=gloo: rehearsal of the multi-rank control flow on a box with fewer GPUs than ranks (ranks
-    # share devices, collectives staged through host memory); the measured configuration is RCCL, one GPU per rank.
-    backend = os.environ.get("PGPU_BENCH_BACKEND", "nccl")
+    # The combine across ranks is the C ABI's (pgpu_comm + pgpu_plan_combine): RCCL over xGMI, one GPU per rank.
+    # PGPU_BENCH_BACKEND=host rehearses the same combine code on a box with fewer GPUs than ranks (ranks share
+    # devices, collectives staged through host memory).  torch.distributed (gloo, CPU) only hands the communicator
+    # id to the ranks and brackets the timed region (barrier, max over ranks).
+    backend = os.environ.get("PGPU_BENCH_BACKEND", "rccl")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        local_rank = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+        local_rank = local_rank % max(1, torch.cuda.device_count()) if backend == "host" else local_rank
         torch.cuda.set_device(local_rank)
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     device = local_rank if world > 1 else 0
 
     from pinot_amd import _lib as L
     from pinot_amd.build import build
-    from pinot_amd.combine import (allreduce_group_table, exchange_hash_table, exchange_result, plan_combine_mode,
-                                   reduce_scatter_group_table, union_dictionaries)
+    from pinot_amd.combine import (Communicator, combine_mode, combine_plan, combine_result_rows,
+                                   union_dictionaries_comm)
     from pinot_amd.executor import GpuTable
     from pinot_amd.query import parse_query
     from pinot_amd.workloads import WORKLOADS
@@ -362,8 +362,10 @@ def main():
         t_inv = time.perf_counter()
         attach_inverted_indexes(table, handles, w, docs)
         log("rank %d: inverted indexes built and pinned in %.1f s" % (rank, time.perf_counter() - t_inv))
+    comm = None
     if world > 1:
-        union_dictionaries(table, q.group_by)
+        comm = Communicator.from_process_group(L.COMM_HOST if backend == "host" else L.COMM_RCCL, device)
+        union_dictionaries_comm(table, q.group_by, comm)
     handles = np.array(handles, dtype=np.int64)
 
     # Real streams (the default stream's handle 0 would mean "the table's own stream" to the C ABI, and the
@@ -372,20 +374,21 @@ def main():
     inflight = max(1, args.inflight)
     streams = [torch.cuda.Stream() for _ in range(inflight)]
     torch.cuda.set_stream(streams[0])
-    # how the ranks' results merge (agreed by every rank): dense tables element-wise, hash-mode tables by a device
-    # all-to-all, numGroupsLimit / ARRAY_MAP plans by their finalized rows
-    mode = plan_combine_mode(table, handles, q) if world > 1 else "local"
+    # how the ranks' results merge, agreed by every rank (pgpu_plan_combine_mode): dense tables element-wise
+    # (all-reduce, or reduce-scatter by key range when large), hash-mode tables by a device all-to-all,
+    # numGroupsLimit / ARRAY_MAP plans by their finalized rows
     probe = table.plan(handles, q)
+    mode, kinds = combine_mode(probe, comm, SHARD_BYTES) if world > 1 else (L.COMBINE_LOCAL, None)
     try:
-        nslots, nkeys, kinds = probe.layout()
+        nslots, nkeys, _ = probe.layout()
     except L.PinotGpuError:  # numGroupsLimit plan: its parts have their own tables
-        nslots, nkeys, kinds = 1, 0, []
+        nslots, nkeys = 1, 0
     probe_nslots = nslots
     probe.close()
+    # PGPU_BENCH_CALLER_TABLE=1: plans write into caller-owned device tables instead of their scratch tables
+    caller_table = nkeys > 0 and os.environ.get("PGPU_BENCH_CALLER_TABLE") == "1"
     d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
-    caller_table = nkeys > 0 and (world > 1 or os.environ.get("PGPU_BENCH_CALLER_TABLE") == "1")
-    # large key spaces (C5) are reduce-scattered by key range and every rank finalizes its own shard
-    sharded = (world > 1 and mode == "dense" and nslots * nkeys * 8 >= SHARD_BYTES) or mode in ("hash", "rows")
+    sharded = mode in (L.COMBINE_REDUCE_SCATTER, L.COMBINE_HASH, L.COMBINE_ROWS)  # disjoint per-rank results
 
     phases = {"plan": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0, "decode": 0.0}
     star_work = [0, 0, 0]
@@ -394,37 +397,28 @@ def main():
         """Plan + execute query k on its stream (streamed: segment chunks launch while the rest is planned), then
         enqueue the cross-rank merge of its table on the same stream."""
         c0 = time.perf_counter()
+        trace.append([k, c0, 0.0, 0.0, 0.0])
         s, dt = streams[k % inflight], d_tables[k % inflight]
-        # the merge across ranks needs the table in caller memory; one GPU keeps the plan's own table, whose
-        # statistics words follow it (one copy back instead of two)
-        plan = table.plan_execute(handles, q, s.cuda_stream, dt.data_ptr() if caller_table else None)
+        # the plan's own table by default (its statistics words follow it: one copy back instead of two); the
+        # combine merges whichever table the plan wrote
+        dptr = dt.data_ptr() if caller_table else None
+        plan = table.plan_execute(handles, q, s.cuda_stream, dptr)
         c1 = time.perf_counter()
-        shard = None
-        if mode == "dense":
-            with torch.cuda.stream(s):
-                if sharded:
-                    shard = reduce_scatter_group_table(dt, kinds)
-                else:
-                    allreduce_group_table(dt, kinds)
-        elif mode == "hash":
-            with torch.cuda.stream(s):
-                exchange_hash_table(plan)
-        elif mode == "rows":
-            shard = "rows"
+        if mode in (L.COMBINE_ALL_REDUCE, L.COMBINE_REDUCE_SCATTER, L.COMBINE_HASH):
+            combine_plan(plan, comm, s.cuda_stream, mode, kinds, d_table=dptr)
         phases["plan"] += c1 - c0
         phases["merge"] += time.perf_counter() - c1
-        return plan, s, dt, shard
+        trace[-1][2] = time.perf_counter()
+        return plan, s, dt, len(trace) - 1
 
     def complete(item):
         """Finalize query k (waits for its stream only) and release its plan."""
-        plan, s, dt, shard = item
+        plan, s, dt, ti = item
         c0 = time.perf_counter()
-        if shard == "rows":
-            res = exchange_result(table, plan.finalize(s.cuda_stream))
-        elif shard is not None:
-            sh, k0, kn = shard
-            res = plan.finalize_range(s.cuda_stream, sh.data_ptr(), k0, kn)
-        else:
+        trace[ti][3] = c0
+        if mode == L.COMBINE_ROWS:
+            res = combine_result_rows(table, plan.finalize(s.cuda_stream), comm)
+        else:  # a reduce-scattered / exchanged plan finalizes this rank's share
             res = plan.finalize(s.cuda_stream, dt.data_ptr() if caller_table else None)
         c1 = time.perf_counter()
         try:
@@ -440,6 +434,7 @@ def main():
         plan.close()
         phases["finalize"] += c1 - c0
         phases["close"] += time.perf_counter() - c1
+        trace[ti][4] = time.perf_counter()
         phases["finalize_c"] += fc_us * 1e-6
         phases["decode"] += dec_us * 1e-6
         return res, k_us
@@ -477,14 +472,20 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    del trace[:]
     t0 = time.perf_counter()
     timed, _ = run(args.steps, inflight, keep_all=args.verify)
+    timed_trace = [[r[0]] + [round((x - t0) * 1e6, 1) for x in r[1:]] for r in trace]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    if args.step_trace and rank == 0:
+        with open(args.step_trace, "w") as f:
+            json.dump({"elapsed_us": elapsed * 1e6, "queries": timed_trace,
+                       "fields": ["k", "launch_start_us", "launch_end_us", "finalize_start_us", "complete_end_us"]}, f)
     if args.verify and first is not None:  # FLOAT/DOUBLE sums vary in their last bits (atomicAdd order): 1e-9
         ref = first.as_dict()
         for res in timed:
@@ -495,12 +496,12 @@ def main():
     if first is None and timed:
         first = timed[0]
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ngroups = len(first) if first is not None else 0
     if sharded:  # disjoint per-rank shards: the query's groups are their sum
-        g = torch.tensor([ngroups], dtype=torch.int64, device="cpu" if backend == "gloo" else "cuda")
+        g = torch.tensor([ngroups], dtype=torch.int64)
         dist.all_reduce(g)
         ngroups = int(g.item())
     total_rows = float(total_segments) * docs
@@ -566,14 +567,15 @@ def main():
             "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
                        "groups": ngroups, "setup_s": round(t_gen, 1), "queries_in_flight": inflight,
-                       "combine": {"hash": "all_to_all", "rows": "all_to_all_rows"}.get(mode, "reduce_scatter" if sharded else
-                                                                                        ("all_reduce" if world > 1 else "none"))},
+                       "combine": L.COMBINE_NAMES[mode] + (" (pgpu_plan_combine, %s)" % backend if world > 1 else "")},
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     table.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

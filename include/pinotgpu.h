@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 2  /* 2: pgpu_query.end_time_ms, PGPU_ERR_TIMEOUT */
+#define PGPU_ABI_VERSION 3  /* 2: pgpu_query.end_time_ms, PGPU_ERR_TIMEOUT; 3: pgpu_comm, pgpu_plan_combine */
 
 /* ---- status codes (BaseCombineOperator.java:101-107 maps failures to ProcessingException; the Java shim maps
  * these codes the same way and keeps Pinot's CPU operator for PGPU_ERR_UNSUPPORTED). */
@@ -258,6 +258,52 @@ int pgpu_plan_exchange_export(pgpu_plan plan, void* stream, int32_t nparts, cons
                               int64_t cap);
 /* Replaces the plan's table by the merge of n received records (device); pgpu_plan_finalize then returns them. */
 int pgpu_plan_exchange_merge(pgpu_plan plan, void* stream, const int32_t* kinds, const void* d_records, int64_t n);
+
+/* ---- communicator and the one-call cross-GPU combine (what a Pinot server calls instead of the combine merge when
+ * its segments are spread over the GPUs of a node; GroupByCombineOperator.java:113-160 /
+ * GroupByOrderByCombineOperator.java:170-181).  One process (or thread) per GPU; every rank issues the same
+ * combine calls in the same order, as with any RCCL communicator.
+ *   PGPU_COMM_RCCL  RCCL over xGMI, one rank per GPU; collectives run on the caller's stream.  librccl.so.1 is opened
+ *                   on first use (the copy already in the process if there is one).
+ *   PGPU_COMM_HOST  processes of one machine exchanging through /dev/shm: the same combine with several ranks on one
+ *                   GPU (RCCL refuses two ranks per device).  Synchronous, staged through host memory; for
+ *                   rehearsals and tests, never the measured path.
+ * The unique id (PGPU_COMM_ID_BYTES) is made by one rank and handed to the others out of band (the JVM's own
+ * cluster channel, torch's TCPStore, ...), as ncclUniqueId is. */
+typedef struct pgpu_comm_s* pgpu_comm;
+#define PGPU_COMM_RCCL 0
+#define PGPU_COMM_HOST 1
+#define PGPU_COMM_ID_BYTES 128
+int pgpu_comm_unique_id(int32_t kind, void* id /* PGPU_COMM_ID_BYTES */);
+int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, pgpu_comm* out);
+int pgpu_comm_destroy(pgpu_comm comm);
+int pgpu_comm_rank(pgpu_comm comm, int32_t* rank, int32_t* nranks);
+/* Host memory, blocking: recv[nranks * bytes] = every rank's `bytes` bytes in rank order (dictionary unions, the
+ * mode agreement, timing barriers -- the small control exchanges of a multi-GPU query). */
+int pgpu_comm_allgather(pgpu_comm comm, const void* send, int64_t bytes, void* recv);
+
+/* How the ranks' partial results of one query merge. */
+#define PGPU_COMBINE_LOCAL 0          /* one rank: nothing to merge */
+#define PGPU_COMBINE_ALL_REDUCE 1     /* dense tables, element-wise, every rank ends with the merged table */
+#define PGPU_COMBINE_REDUCE_SCATTER 2 /* dense tables >= shard_bytes: rank r ends with keys [r*chunk, (r+1)*chunk) */
+#define PGPU_COMBINE_HASH 3           /* hash-mode tables: groups hashed to an owner rank, all-to-all, owner merges */
+#define PGPU_COMBINE_ROWS 4           /* numGroupsLimit plans / ARRAY_MAP key stages: finalized rows, by owner */
+/* Collective: the mode every rank agrees on for this query (a plan, executed or not, of the query over the rank's
+ * segments), and in kinds[num_slots] the slot kinds the merge runs in (an int64 SUM travels as float64 when another
+ * rank's sum of the slot is float64).  Modes that differ between ranks fall back to ROWS, which merges any plan
+ * kind.  PGPU_ERR_INVALID_ARGUMENT when the ranks' group-by dictionaries differ (pgpu_table_add_dictionary_values
+ * with the union first).  The caller may reuse the answer for every later query of the same shape. */
+int pgpu_plan_combine_mode(pgpu_plan plan, pgpu_comm comm, int64_t shard_bytes, int32_t* mode, int32_t* kinds);
+/* Collective, ordered on `stream`: merges the executed plan's table (d_table as given to execute, NULL = the plan's
+ * own) with the other ranks' in `mode` (ALL_REDUCE, REDUCE_SCATTER or HASH).  For REDUCE_SCATTER, d_shard (NULL = the
+ * plan's scratch) receives [num_slots][key_count] words, key_begin / key_count say which keys; they are 0 / num_keys
+ * otherwise.  pgpu_plan_finalize(plan, stream, d_table) then returns this rank's share of the merged groups (all of
+ * them for ALL_REDUCE; disjoint shares otherwise). */
+int pgpu_plan_combine(pgpu_plan plan, pgpu_comm comm, void* stream, void* d_table, int32_t mode, const int32_t* kinds,
+                      void* d_shard, int64_t* key_begin, int64_t* key_count);
+/* Collective, ROWS mode: the finalized result's rows split by owner, exchanged, merged by the owner as the broker
+ * merges server responses.  *out = this rank's disjoint share. */
+int pgpu_result_combine_rows(pgpu_result r, pgpu_comm comm, pgpu_result* out);
 
 /* One-call form: plan + execute + finalize (the whole per-server query path). */
 int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32_t num_segments, const pgpu_query* q,

@@ -37,6 +37,11 @@ OP_PRED, OP_AND, OP_OR, OP_NOT = 0, 1, 2, 3
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 SLOT_COUNT, SLOT_SUM_I64, SLOT_SUM_F64, SLOT_MIN_KEY, SLOT_MAX_KEY = 0, 1, 2, 3, 4
 GEN_UNIFORM, GEN_ZIPF, GEN_TABLE = 0, 1, 2
+COMM_RCCL, COMM_HOST = 0, 1
+COMM_ID_BYTES = 128
+COMBINE_LOCAL, COMBINE_ALL_REDUCE, COMBINE_REDUCE_SCATTER, COMBINE_HASH, COMBINE_ROWS = 0, 1, 2, 3, 4
+COMBINE_NAMES = {COMBINE_LOCAL: "local", COMBINE_ALL_REDUCE: "all_reduce", COMBINE_REDUCE_SCATTER: "reduce_scatter",
+                 COMBINE_HASH: "hash", COMBINE_ROWS: "rows"}
 
 
 class ColumnBuffers(ctypes.Structure):
@@ -186,6 +191,14 @@ _PROTOS = {
     "pgpu_result_exchange_rows": (c_int, [c_voidp, c_i32, c_i32p, c_i64p, c_i64p]),
     "pgpu_result_merge_rows": (c_int, [c_voidp, c_i64p, c_i64, c_i32p, ctypes.POINTER(c_voidp)]),
     "pgpu_result_destroy": (c_int, [c_voidp]),
+    "pgpu_comm_unique_id": (c_int, [c_i32, c_voidp]),
+    "pgpu_comm_create": (c_int, [c_i32, c_voidp, c_i32, c_i32, c_i32, ctypes.POINTER(c_voidp)]),
+    "pgpu_comm_destroy": (c_int, [c_voidp]),
+    "pgpu_comm_rank": (c_int, [c_voidp, c_i32p, c_i32p]),
+    "pgpu_comm_allgather": (c_int, [c_voidp, c_voidp, c_i64, c_voidp]),
+    "pgpu_plan_combine_mode": (c_int, [c_voidp, c_voidp, c_i64, c_i32p, c_i32p]),
+    "pgpu_plan_combine": (c_int, [c_voidp, c_voidp, c_voidp, c_voidp, c_i32, c_i32p, c_voidp, c_i64p, c_i64p]),
+    "pgpu_result_combine_rows": (c_int, [c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
     "pgpu_free_result": (c_int, [c_voidp]),
     "pgpu_filter_bitmap": (c_int, [c_voidp, c_i64, ctypes.POINTER(QueryC), c_u64p]),
     "pgpu_result_trim_sql": (c_int, [c_voidp, ctypes.POINTER(SqlTrimC), ctypes.POINTER(c_voidp)]),
@@ -227,7 +240,7 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.pgpu_abi_version() != 2:
+    if lib.pgpu_abi_version() != 3:
         raise ImportError("libpinotgpu.so ABI mismatch")
     if path is None:
         _lib = lib

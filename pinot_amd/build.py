@@ -11,12 +11,12 @@ LIB_PATH = os.path.join(HERE, "libpinotgpu.so")
 # (source, extra flags, object name): the scan kernels are compiled once per accumulator mode so the objects
 # build in parallel.
 SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime"), ("startree.cpp", [], "startree"),
-           ("filter_stats.cpp", [], "filter_stats"), ("server_response.cpp", [], "server_response"),
+           ("filter_stats.cpp", [], "filter_stats"), ("comm.cpp", [], "comm"), ("server_response.cpp", [], "server_response"),
            ("k_partition.hip", [], "k_partition")] + \
     [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
     [("k_startree.hip", ["-DPGPU_MODE=%d" % m], "k_startree_%d" % m) for m in range(3)]
 HEADERS = ["internal.h", "device.h", "scan_direct.h", "host_common.h", "startree_kernels.h",
-           "partition.h", "filter_stats.h", "host_result.h"]
+           "partition.h", "filter_stats.h", "host_result.h", "comm.h"]
 ARCH = os.environ.get("PGPU_OFFLOAD_ARCH", "gfx950")
 
 
@@ -71,7 +71,7 @@ def build(force=False, verbose=False, defines=(), out=None):
             errors.append("%s:\n%s" % (src, out[-8000:]))
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
-    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs + ["-ldl"]
     res = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc link failed:\n" + res.stdout[-8000:])

@@ -12,6 +12,9 @@ table-global key space, so the merge is element-wise: COUNT and integer SUM rows
 SUM rows add as float64, MIN / MAX rows (order-preserving int64 keys) take min / max.  Rows of one kind are
 reduced by a single collective.
 """
+import ctypes
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -169,10 +172,6 @@ def exchange_result(table, res, group=None):
     """Cross-rank merge of finalized results of any plan kind (numGroupsLimit plans, ARRAY_MAP key stages): the rows
     [dictIds, slot words] are split by owner on the host, exchanged with all_to_all, and merged by the owner
     (pgpu_result_merge_rows).  Returns this rank's disjoint share of the merged groups as a GroupByResult."""
-    import ctypes
-
-    import numpy as np
-
     from .executor import _decode_result, _ResultHolder
     lib = table.lib
     world = dist.get_world_size(group)
@@ -182,16 +181,16 @@ def exchange_result(table, res, group=None):
     L.check(lib.pgpu_result_slot_kinds(r, ctypes.byref(ns), kinds))
     mine = [kinds[i] for i in range(ns.value)]
     agreed = np.asarray(agreed_slot_kinds(mine, group), dtype=np.int32)
-    # group ids index the ranks' dictionary snapshots: they must be the same (union_dictionaries before the query)
-    sizes = []
-    for j in range(len(res._query.group_by)):
-        n = ctypes.c_int64()
-        L.check(lib.pgpu_result_key_dictionary(r, j, None, ctypes.byref(n)))
-        sizes.append(n.value)
+    # group ids index the ranks' dictionary snapshots: they must be the same (union_dictionaries before the query) --
+    # compared by content, not only by size
+    import hashlib
+    digest = hashlib.sha256()
+    for j, c in enumerate(res._query.group_by):
+        digest.update(repr(list(table.result_dictionary(r, j, c))).encode())
     gathered = [None] * world
-    dist.all_gather_object(gathered, sizes, group=group)
-    if any(g != sizes for g in gathered):
-        raise ValueError("ranks' group-by dictionaries differ (%s): union them before the query" % gathered)
+    dist.all_gather_object(gathered, digest.hexdigest(), group=group)
+    if any(g != gathered[0] for g in gathered):
+        raise ValueError("ranks' group-by dictionaries differ: union them before the query")
     nk = len(res._query.group_by)
     n = len(res)
     rows = np.empty((max(n, 1), nk + ns.value), dtype=np.int64)
@@ -235,7 +234,119 @@ def plan_combine_mode(table, handles, query, group=None):
         probe.close()
     gathered = [None] * world
     dist.all_gather_object(gathered, mode, group=group)
-    for m in ("rows", "hash"):
-        if m in gathered:
-            return m
-    return "dense"
+    # one mode on every rank, or the row exchange, which merges plans of any kind (a dense rank could not take part
+    # in a hash exchange: its collectives would not pair up)
+    return gathered[0] if len(set(gathered)) == 1 else "rows"
+
+
+# ------------------------------------------------------------------------------------- the C ABI combine (pgpu_comm)
+# The same merges as above, issued by libpinotgpu itself (include/pinotgpu.h, "communicator and the one-call
+# cross-GPU combine"): what a Java server calls through JNI, with no torch in the process.  RCCL over xGMI on a node;
+# the host transport runs the identical combine code with several ranks on one GPU (tests, rehearsals).
+
+class Communicator:
+    """pgpu_comm: one rank of a group of GPUs (RCCL) or of processes sharing a GPU (host transport)."""
+
+    def __init__(self, kind, uid, nranks, rank, device):
+        self.lib = L.load()
+        self.kind = kind
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), L.COMM_ID_BYTES)
+        L.check(self.lib.pgpu_comm_create(kind, buf, nranks, rank, device, ctypes.byref(h)))
+        self.handle = h
+        self.rank, self.nranks, self.device = rank, nranks, device
+
+    @staticmethod
+    def unique_id(kind=L.COMM_RCCL):
+        buf = ctypes.create_string_buffer(L.COMM_ID_BYTES)
+        L.check(L.load().pgpu_comm_unique_id(kind, buf))
+        return buf.raw
+
+    @classmethod
+    def from_process_group(cls, kind, device, group=None):
+        """Rank 0 makes the id, the process group (any backend: gloo is enough) hands it to the others."""
+        box = [cls.unique_id(kind) if dist.get_rank(group) == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls(kind, box[0], dist.get_world_size(group), dist.get_rank(group), device)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.pgpu_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def allgather(self, data):
+        """Every rank's `data` (bytes of one length on every rank), in rank order."""
+        data = bytes(data)
+        out = ctypes.create_string_buffer(max(1, len(data) * self.nranks))
+        L.check(self.lib.pgpu_comm_allgather(self.handle, data, len(data), out))
+        return [out.raw[i * len(data):(i + 1) * len(data)] for i in range(self.nranks)]
+
+    def allgather_var(self, data):
+        """Every rank's `data` (bytes of any length), in rank order."""
+        import struct
+        sizes = [struct.unpack("<q", b)[0] for b in self.allgather(struct.pack("<q", len(data)))]
+        width = max(sizes)
+        padded = self.allgather(bytes(data) + b"\0" * (width - len(data)))
+        return [p[:n] for p, n in zip(padded, sizes)]
+
+    def barrier(self):
+        self.allgather(b"\0")
+
+    def max(self, x):
+        import struct
+        return max(struct.unpack("<d", b)[0] for b in self.allgather(struct.pack("<d", float(x))))
+
+    def sum_int(self, x):
+        import struct
+        return sum(struct.unpack("<q", b)[0] for b in self.allgather(struct.pack("<q", int(x))))
+
+
+def union_dictionaries_comm(table, columns, comm):
+    """union_dictionaries over a pgpu_comm (values travel as JSON: exact for ints, floats via repr, and strings)."""
+    import json
+    for col in columns:
+        mine = json.dumps(list(table.dictionary(col))).encode()
+        union = sorted(set(v for b in comm.allgather_var(mine) for v in json.loads(b.decode())))
+        table.add_dictionary_values(col, union)
+
+
+def combine_mode(plan, comm, shard_bytes):
+    """(mode, kinds) every rank agrees on for this query (pgpu_plan_combine_mode, a collective)."""
+    mode = ctypes.c_int32()
+    kinds = (ctypes.c_int32 * 32)()
+    L.check(plan.lib.pgpu_plan_combine_mode(plan.handle, comm.handle, int(shard_bytes), ctypes.byref(mode), kinds))
+    ns = _num_slots(plan)
+    return mode.value, [kinds[i] for i in range(ns)]
+
+
+def _num_slots(plan):
+    try:
+        return plan.layout()[0]
+    except L.PinotGpuError:  # numGroupsLimit plan: the kinds come with the rows
+        return 0
+
+
+def combine_plan(plan, comm, stream, mode, kinds=None, d_table=None, d_shard=None):
+    """pgpu_plan_combine on the executed plan (ordered on `stream`); plan.finalize(stream, d_table) then returns this
+    rank's share.  Returns (key_begin, key_count)."""
+    k = np.ascontiguousarray(kinds, dtype=np.int32) if kinds else None
+    kb, kc = ctypes.c_int64(), ctypes.c_int64()
+    L.check(plan.lib.pgpu_plan_combine(plan.handle, comm.handle, ctypes.c_void_p(stream or 0),
+                                       ctypes.c_void_p(d_table or 0), mode,
+                                       L.ptr(k, ctypes.c_int32) if k is not None else None,
+                                       ctypes.c_void_p(d_shard or 0), ctypes.byref(kb), ctypes.byref(kc)))
+    return kb.value, kc.value
+
+
+def combine_result_rows(table, res, comm):
+    """pgpu_result_combine_rows: this rank's disjoint share of the merged finalized rows (ROWS mode)."""
+    from .executor import _decode_result, _ResultHolder
+    out = ctypes.c_void_p()
+    L.check(table.lib.pgpu_result_combine_rows(res._holder.r, comm.handle, ctypes.byref(out)))
+    return _decode_result(table, res._query, _ResultHolder(table.lib, out))

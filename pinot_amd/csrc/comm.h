@@ -1,0 +1,48 @@
+// comm.h — the communicator behind pgpu_comm (comm.cpp): the collectives the cross-GPU combine issues.  Not part of
+// the ABI.
+//
+// Two transports, one interface:
+//   RCCL  one rank per GPU, collectives over xGMI on the caller's stream (librccl is opened at the first
+//         pgpu_comm_unique_id / pgpu_comm_create, preferring the copy already in the process, e.g. torch's);
+//   HOST  processes of one machine exchange through files in /dev/shm with a shared-memory barrier: the same combine
+//         code with several ranks on one GPU, where RCCL refuses two ranks per device.  Every call synchronises the
+//         stream and stages through host memory -- a rehearsal transport, never the measured one.
+// Collectives must be issued in the same order on every rank (as with RCCL); a communicator serialises its callers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/pinotgpu.h"
+
+namespace pgpu {
+
+enum CommDtype { CDT_I64 = 0, CDT_F64 = 1 };
+enum CommOp { COP_SUM = 0, COP_MIN = 1, COP_MAX = 2 };
+
+struct Comm {
+  virtual ~Comm() {}
+  int nranks = 1, rank = 0, device = 0;
+  // In place on the device, ordered on `s`.
+  virtual int allreduce(void* d, size_t count, CommDtype t, CommOp op, hipStream_t s) = 0;
+  // send: nranks x count elements; rank r receives the reduction of block r into recv (count elements).
+  virtual int reduce_scatter(const void* dsend, void* drecv, size_t count, CommDtype t, CommOp op, hipStream_t s) = 0;
+  // send holds scount[p] records of `rec` bytes for rank p back to back (rank order); recv gets rcount[p] records from
+  // rank p back to back.  rec is a multiple of 8.
+  virtual int alltoallv(const void* dsend, const int64_t* scount, void* drecv, const int64_t* rcount, size_t rec,
+                        hipStream_t s) = 0;
+  // alltoallv over host buffers, blocking (finalized result rows).
+  virtual int alltoallv_host(const void* send, const int64_t* scount, void* recv, const int64_t* rcount, size_t rec) = 0;
+  // Host memory, blocking: recv = every rank's `bytes` bytes, in rank order.
+  virtual int allgather_host(const void* send, size_t bytes, void* recv) = 0;
+};
+
+int comm_unique_id(int32_t kind, void* id);
+int comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, Comm** out);
+
+}  // namespace pgpu
+
+struct pgpu_comm_s {
+  pgpu::Comm* impl = nullptr;
+};

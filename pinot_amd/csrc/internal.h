@@ -303,6 +303,7 @@ int launch_exchange_count(const uint64_t* table, const unsigned long long* hash_
 int launch_exchange_scatter(const uint64_t* table, const unsigned long long* hash_keys, int64_t num_keys,
                             int32_t num_slots, int32_t nparts, uint32_t conv, unsigned long long* cursor, uint64_t* out,
                             void* stream);
+int launch_i64_to_f64(uint64_t* p, int64_t n, void* stream);
 int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
                          unsigned long long* hash_keys, int64_t num_keys, void* stream);
 // Compact form of a large dense table: counts per chunk + exclusive scan (total into *total) + each slot's range over

@@ -803,6 +803,21 @@ int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, cons
   return PGPU_HIP_OK(hipGetLastError());
 }
 
+// Cross-GPU combine: an int64 SUM row of a dense table rewritten as float64 words in place, when another rank's sum of
+// the same slot is float64 (the ranks' overflow guards differ); grid-stride, one word per lane.
+__global__ void i64_to_f64_kernel(uint64_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = (uint64_t)__double_as_longlong((double)(long long)p[i]);
+}
+
+int launch_i64_to_f64(uint64_t* p, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  int64_t grid = (n + 255) / 256;
+  grid = grid > 4096 ? 4096 : grid;
+  hipLaunchKernelGGL(i64_to_f64_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), p, n);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
 int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream) {
   if (n < 1) return 0;
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), data, n,

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/pinotgpu.h"
+#include "comm.h"
 #include "filter_stats.h"
 #include "host_common.h"
 #include "host_result.h"
@@ -395,6 +396,7 @@ std::atomic<uint64_t> g_dict_ids{1};
 struct Dict {
   int type = PGPU_INT;
   uint64_t id = 0;
+  uint64_t digest = 0;           // content hash, computed on first use (dict_digest; 0 = not yet)
   std::vector<int64_t> iv;       // INT / LONG
   std::vector<double> dv;        // FLOAT / DOUBLE
   std::vector<std::string> sv;   // STRING (unpadded)
@@ -526,6 +528,7 @@ struct Scratch {
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
   DevBuf xcursor;                       // cross-GPU exchange: per-owner record cursors
+  DevBuf xsend, xrecv, xshard;          // pgpu_plan_combine: exported / received records, the reduce-scattered shard
   HostPinned xstage;                    // their initial values (pinned: the upload is asynchronous)
   // Pinned staging: `stage` is the source of the execution's asynchronous uploads (records, bitsets); `readback`
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
@@ -553,7 +556,7 @@ struct Scratch {
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release(); stage_keys.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
-    xcursor.release(); xstage.release();
+    xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -923,10 +926,22 @@ int decode_raw_forward_index(int type, const uint8_t* b, int64_t n, int32_t num_
   const int64_t data = (int64_t)header_start + (int64_t)num_chunks * entry;
   if (header_start < 28 || data > n || (compression == 0 && data + (int64_t)num_docs * size > n))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw forward index too short for %d docs", c, num_docs);
-  out->key.assign(std::max<int32_t>(num_docs, 1), 0);
-  out->val.assign(std::max<int32_t>(num_docs, 1), 0.0);
+  // A chunk decodes to at most min(numDocsPerChunk, totalDocs) entries, and an LZ4 block expands at most ~255x
+  // (each sequence byte of a match length stands for <= 255 output bytes): a header claiming more is rejected
+  // before anything is allocated.
+  const int64_t chunk_bytes = compression ? std::min<int64_t>(per_chunk, total) * size : 0;
+  if (compression && chunk_bytes > (n - data) * 256 + 64)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: raw chunk of %d docs cannot come from a %lld-byte index", c,
+                per_chunk, (long long)n);
+  std::vector<uint8_t> chunk;
+  try {
+    out->key.assign(std::max<int32_t>(num_docs, 1), 0);
+    out->val.assign(std::max<int32_t>(num_docs, 1), 0.0);
+    chunk.resize((size_t)chunk_bytes);
+  } catch (const std::bad_alloc&) {
+    return fail(PGPU_ERR_OUT_OF_MEMORY, "column %d: host memory for %d raw values", c, num_docs);
+  }
   int64_t lo = INT64_MAX, hi = INT64_MIN;
-  std::vector<uint8_t> chunk(compression ? (size_t)per_chunk * size : 0);
   for (int64_t k = 0, d0 = 0; d0 < num_docs; ++k, d0 += per_chunk) {
     const int64_t nd = std::min<int64_t>(per_chunk, num_docs - d0);
     const uint8_t* v = b + data + d0 * size;
@@ -1121,6 +1136,10 @@ struct pgpu_plan_s {
   // the records merged into the owner's table (-1: the table holds the local groups)
   std::vector<int64_t> xchg_counts;
   int64_t merged_records = -1;
+  // pgpu_plan_combine REDUCE_SCATTER: this rank's merged key range [shard_begin, shard_begin + shard_count), slot rows
+  // of shard_count words at `shard`; pgpu_plan_finalize reads it
+  const void* shard = nullptr;
+  int64_t shard_begin = 0, shard_count = 0;
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -3775,6 +3794,7 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     P->d_table_used = nullptr;
     P->last_stream = nullptr;
     P->star_docs_read = 0;
+    P->shard = nullptr;
     return true;
   }
   return false;
@@ -3797,6 +3817,12 @@ void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
   auto img = std::make_shared<pgpu_plan_s>(P);
   img->scratch = nullptr;
   std::lock_guard<std::mutex> g(t->cache_mu);
+  // The key was taken before planning.  Every change of pinned state bumps the version before it clears the cache:
+  // a plan built across such a change carries the old version in its key and may reference state of that time
+  // (an unpinned segment, an old dictionary snapshot), so it is not stored.
+  uint64_t v;
+  memcpy(&v, key.data(), 8);
+  if (v != t->version.load()) return;
   t->plan_cache.emplace_front(key, std::move(img));
   while (t->plan_cache.size() > kPlanCacheEntries) t->plan_cache.pop_back();
 }
@@ -4570,7 +4596,8 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   // A cached plan is never a numGroupsLimit split (composite plans are not cached) and the split decision is a
   // function of the cache key (query, segments, pinned-state version): a hit skips it.
   const bool cache = plan_cache_enabled(q);
-  if (!cache || !plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get())) {
+  const std::string key = cache ? plan_cache_key(t, handles, nsegs, q) : std::string();
+  if (!cache || !plan_cache_get(t, key, P.get())) {
     bool composite = false;
     TRY(split_for_groups_limit(t, handles, nsegs, q, P.get(), &composite));
     if (composite) {
@@ -4578,7 +4605,7 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
       return 0;
     }
     TRY(plan_create_impl(t, handles, nsegs, q, P.get()));
-    if (cache) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
+    if (cache) plan_cache_put(t, key, *P);
   }
   P->end_time_ms = q->end_time_ms;
   P->scratch = acquire_scratch(t);
@@ -4614,7 +4641,8 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   auto P = std::make_unique<pgpu_plan_s>();
   // a cache hit skips the numGroupsLimit split decision (pgpu_plan_create)
   const bool cache = plan_cache_enabled(q);
-  const bool hit = cache && plan_cache_get(t, plan_cache_key(t, handles, nsegs, q), P.get());
+  const std::string key = cache ? plan_cache_key(t, handles, nsegs, q) : std::string();  // before planning
+  const bool hit = cache && plan_cache_get(t, key, P.get());
   const double tt1 = trace_on() ? now_us() : 0;
   if (!hit) {
     bool composite = false;
@@ -4636,7 +4664,7 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   int rc = 0;
   if (!hit) {
     rc = plan_create_impl(t, handles, nsegs, q, P.get(), &se);
-    if (!rc && cache && !P->executed) plan_cache_put(t, plan_cache_key(t, handles, nsegs, q), *P);
+    if (!rc && cache && !P->executed) plan_cache_put(t, key, *P);
   }
   if (!rc && !P->executed) {
     if (P->hash && d_table) rc = fail(PGPU_ERR_UNSUPPORTED, "external table with a hash-mode plan");
@@ -4684,6 +4712,8 @@ int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_resu
     if (!P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
     if (d_table) return fail(PGPU_ERR_UNSUPPORTED, "external table with a numGroupsLimit plan");
     TRY(composite_finalize(P, s, R.get()));
+  } else if (P->shard) {  // reduce-scattered by pgpu_plan_combine: this rank's key range
+    TRY(plan_finalize_impl(P, s, P->shard, P->shard_begin, P->shard_count, R.get()));
   } else {
     TRY(plan_finalize_impl(P, s, d_table, 0, P->num_keys, R.get()));
   }
@@ -4956,6 +4986,324 @@ int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, con
   R->groups_limit_reached = tmpl->groups_limit_reached;
   *out = R.release();
   return 0;
+}
+
+// ---- communicator and the one-call cross-GPU combine (comm.h / comm.cpp)
+int pgpu_comm_unique_id(int32_t kind, void* id) {
+  PGPU_ABI_GUARD;
+  if (!id) return fail(PGPU_ERR_INVALID_ARGUMENT, "null id");
+  return pgpu::comm_unique_id(kind, id);
+}
+
+int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, pgpu_comm* out) {
+  PGPU_ABI_GUARD;
+  if (!out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null out");
+  pgpu::Comm* c = nullptr;
+  TRY(pgpu::comm_create(kind, id, nranks, rank, device, &c));
+  auto h = new pgpu_comm_s();
+  h->impl = c;
+  *out = h;
+  return 0;
+}
+
+int pgpu_comm_destroy(pgpu_comm c) {
+  PGPU_ABI_GUARD;
+  if (!c) return 0;
+  delete c->impl;
+  delete c;
+  return 0;
+}
+
+int pgpu_comm_rank(pgpu_comm c, int32_t* rank, int32_t* nranks) {
+  PGPU_ABI_GUARD;
+  if (!c) return fail(PGPU_ERR_INVALID_ARGUMENT, "null communicator");
+  if (rank) *rank = c->impl->rank;
+  if (nranks) *nranks = c->impl->nranks;
+  return 0;
+}
+
+int pgpu_comm_allgather(pgpu_comm c, const void* send, int64_t bytes, void* recv) {
+  PGPU_ABI_GUARD;
+  if (!c || bytes < 0 || (bytes > 0 && (!send || !recv))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard g(c->impl->device);
+  return c->impl->allgather_host(send, (size_t)bytes, recv);
+}
+
+namespace {
+// Content hash of a dictionary snapshot (computed once per snapshot): ranks compare their key spaces with it.
+uint64_t dict_digest(const Dict& d) {
+  uint64_t h = __atomic_load_n(&d.digest, __ATOMIC_RELAXED);
+  if (h) return h;
+  h = 0xcbf29ce484222325ull ^ (uint64_t)d.type;
+  auto mix = [&h](uint64_t v) {
+    h = (h ^ v) * 0x100000001b3ull;
+    h ^= h >> 31;
+  };
+  mix(d.size());
+  if (is_int_type(d.type)) {
+    for (int64_t v : d.iv) mix((uint64_t)v);
+  } else if (is_fp_type(d.type)) {
+    for (double v : d.dv) {
+      uint64_t u;
+      memcpy(&u, &v, 8);
+      mix(u);
+    }
+  } else {
+    for (const std::string& v : d.sv) {
+      mix(v.size());
+      for (size_t i = 0; i < v.size(); i += 8) {
+        uint64_t u = 0;
+        memcpy(&u, v.data() + i, std::min<size_t>(8, v.size() - i));
+        mix(u);
+      }
+    }
+  }
+  if (!h) h = 1;
+  __atomic_store_n(const_cast<uint64_t*>(&d.digest), h, __ATOMIC_RELAXED);
+  return h;
+}
+
+// The group-key space of a plan: dictionaries of the group-by columns and, for table-keyed modes, the composite key
+// layout.  Equal on every rank after a dictionary union.
+uint64_t key_space_digest(const pgpu_plan_s* P, bool layout) {
+  uint64_t h = 0x84222325cbf29ce4ull;
+  auto mix = [&h](uint64_t v) { h = (h ^ v) * 0x9E3779B97F4A7C15ull; h ^= h >> 29; };
+  mix(P->key_dicts.size());
+  for (const auto& d : P->key_dicts) mix(d ? dict_digest(*d) : 0);
+  if (layout) {
+    for (int64_t v : P->key_card) mix((uint64_t)v);
+    for (int64_t v : P->key_off) mix((uint64_t)v);
+    for (int64_t v : P->key_stride) mix((uint64_t)v);
+  }
+  return h;
+}
+
+// One rank's part of the mode agreement (int64 words).
+enum { CI_MODE = 0, CI_KEYS, CI_SLOTS, CI_DIGEST, CI_KINDS, CI_WORDS = CI_KINDS + kMaxSlots };
+
+// Agreed kinds of ranks' slots: equal, or int64 / float64 sums of one slot meeting as float64.
+int agree_kinds(const std::vector<int64_t>& all, int nranks, int ns, int32_t* kinds) {
+  for (int s = 0; s < ns; ++s) {
+    bool i64 = false, f64 = false, other = false;
+    int32_t k0 = (int32_t)all[CI_KINDS + s];
+    for (int r = 0; r < nranks; ++r) {
+      const int32_t k = (int32_t)all[(size_t)r * CI_WORDS + CI_KINDS + s];
+      i64 |= k == SLOT_SUM_I64;
+      f64 |= k == SLOT_SUM_F64;
+      if (k != SLOT_SUM_I64 && k != SLOT_SUM_F64) other = true;
+      if (other && k != k0) return fail(PGPU_ERR_INVALID_ARGUMENT, "ranks disagree on slot %d (kinds %d, %d)", s, k0, k);
+    }
+    kinds[s] = other ? k0 : f64 ? SLOT_SUM_F64 : SLOT_SUM_I64;
+    (void)i64;
+  }
+  return 0;
+}
+}  // namespace
+
+int pgpu_plan_combine_mode(pgpu_plan P, pgpu_comm c, int64_t shard_bytes, int32_t* mode, int32_t* kinds) {
+  PGPU_ABI_GUARD;
+  if (!P || !c || !mode) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  const int N = c->impl->nranks;
+  int local;
+  const pgpu_plan_s* K = P;  // the plan whose key space and slots describe the query on this rank
+  if (P->composite) {
+    local = PGPU_COMBINE_ROWS;
+    if (!P->parts.empty()) K = P->parts[0].plan.get();
+  } else if (P->hash) {
+    local = P->stage_end.empty() ? PGPU_COMBINE_HASH : PGPU_COMBINE_ROWS;  // ARRAY_MAP stages: rank-local keys
+  } else {
+    local = (int64_t)P->slot_kind.size() * P->num_keys * 8 >= shard_bytes ? PGPU_COMBINE_REDUCE_SCATTER
+                                                                           : PGPU_COMBINE_ALL_REDUCE;
+  }
+  std::vector<int64_t> mine(CI_WORDS, 0), all((size_t)N * CI_WORDS, 0);
+  mine[CI_MODE] = local;
+  mine[CI_KEYS] = local == PGPU_COMBINE_ALL_REDUCE || local == PGPU_COMBINE_REDUCE_SCATTER ? P->num_keys : 0;
+  mine[CI_SLOTS] = (int64_t)K->slot_kind.size();
+  mine[CI_DIGEST] = (int64_t)key_space_digest(K, local != PGPU_COMBINE_ROWS);
+  for (size_t s = 0; s < K->slot_kind.size() && s < (size_t)kMaxSlots; ++s) mine[CI_KINDS + s] = K->slot_kind[s];
+  {
+    DeviceGuard g(c->impl->device);
+    TRY(c->impl->allgather_host(mine.data(), mine.size() * 8, all.data()));
+  }
+  bool same = true, any_rows = false;
+  for (int r = 0; r < N; ++r) {
+    const int64_t* w = all.data() + (size_t)r * CI_WORDS;
+    same &= w[CI_MODE] == local && w[CI_KEYS] == mine[CI_KEYS];
+    any_rows |= w[CI_MODE] == PGPU_COMBINE_ROWS;
+  }
+  const int agreed = same ? local : PGPU_COMBINE_ROWS;  // rows merge any plan kind
+  // the key spaces must match: the row and table digests both carry the group-by dictionaries
+  for (int r = 0; r < N; ++r) {
+    const int64_t* w = all.data() + (size_t)r * CI_WORDS;
+    if (w[CI_SLOTS] != mine[CI_SLOTS])
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "ranks disagree on the number of accumulators (%lld, %lld)",
+                  (long long)w[CI_SLOTS], (long long)mine[CI_SLOTS]);
+    if (same && w[CI_DIGEST] != mine[CI_DIGEST])
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "rank %d's group-key space differs from rank %d's: union the group-by "
+                  "dictionaries (pgpu_table_add_dictionary_values) before the query", r, c->impl->rank);
+  }
+  (void)any_rows;
+  if (!same) {
+    // plans of different kinds meet as rows; their dictionaries must still agree
+    std::vector<int64_t> d(1, (int64_t)key_space_digest(K, false)), alld(N);
+    DeviceGuard g(c->impl->device);
+    TRY(c->impl->allgather_host(d.data(), 8, alld.data()));
+    for (int r = 0; r < N; ++r)
+      if (alld[r] != d[0])
+        return fail(PGPU_ERR_INVALID_ARGUMENT, "rank %d's group-by dictionaries differ from rank %d's: union them "
+                    "(pgpu_table_add_dictionary_values) before the query", r, c->impl->rank);
+  }
+  if (kinds) TRY(agree_kinds(all, N, (int)mine[CI_SLOTS], kinds));
+  *mode = agreed;
+  return 0;
+}
+
+int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int32_t mode, const int32_t* kinds,
+                      void* d_shard, int64_t* key_begin, int64_t* key_count) {
+  PGPU_ABI_GUARD;
+  if (!P || !c) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (mode == PGPU_COMBINE_LOCAL) {
+    if (key_begin) *key_begin = 0;
+    if (key_count) *key_count = P->num_keys;
+    return 0;
+  }
+  if (mode == PGPU_COMBINE_ROWS)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "PGPU_COMBINE_ROWS: finalize the plan, then pgpu_result_combine_rows");
+  if (mode != PGPU_COMBINE_ALL_REDUCE && mode != PGPU_COMBINE_REDUCE_SCATTER && mode != PGPU_COMBINE_HASH)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "combine mode %d", mode);
+  if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: combine its finalized rows (ROWS)");
+  if (!P->executed || !P->scratch) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  if (P->shard) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan already combined");
+  pgpu::Comm* C = c->impl;
+  const int N = C->nranks, me = C->rank;
+  if (C->device != P->table->device)
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "communicator on device %d, table on %d", C->device, P->table->device);
+  DeviceGuard g(P->table->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  Scratch* sc = P->scratch;
+  const int ns = (int)P->slot_kind.size();
+  uint32_t conv = 0;
+  TRY(check_kinds(P->slot_kind, kinds, &conv));
+  if (mode == PGPU_COMBINE_HASH) {
+    if (!P->hash) return fail(PGPU_ERR_UNSUPPORTED, "dense group tables merge element-wise (ALL_REDUCE / REDUCE_SCATTER)");
+    std::vector<int64_t> counts(N), all((size_t)N * N), rcount(N);
+    TRY(pgpu_plan_exchange_counts(P, s, N, counts.data()));
+    TRY(C->allgather_host(counts.data(), (size_t)N * 8, all.data()));
+    int64_t total = 0, nrecv = 0;
+    for (int p = 0; p < N; ++p) {
+      total += counts[p];
+      rcount[p] = all[(size_t)p * N + me];
+      nrecv += rcount[p];
+    }
+    const size_t rec = (size_t)(1 + ns) * 8;
+    TRY(sc->xsend.ensure((size_t)std::max<int64_t>(total, 1) * rec));
+    TRY(pgpu_plan_exchange_export(P, s, N, kinds, sc->xsend.p, total));
+    TRY(sc->xrecv.ensure((size_t)std::max<int64_t>(nrecv, 1) * rec));
+    TRY(C->alltoallv(sc->xsend.p, counts.data(), sc->xrecv.p, rcount.data(), rec, s));
+    TRY(pgpu_plan_exchange_merge(P, s, kinds, nrecv ? sc->xrecv.p : nullptr, nrecv));
+    if (key_begin) *key_begin = 0;
+    if (key_count) *key_count = P->num_keys;
+    return 0;
+  }
+  if (P->hash) return fail(PGPU_ERR_UNSUPPORTED, "hash-mode tables merge with PGPU_COMBINE_HASH");
+  uint64_t* table = reinterpret_cast<uint64_t*>(d_table ? d_table : const_cast<void*>(P->d_table_used));
+  if (!table) return fail(PGPU_ERR_INVALID_ARGUMENT, "no group table");
+  const int64_t G = P->num_keys;
+  for (int k = 0; k < ns; ++k)
+    if ((conv >> k) & 1u)
+      if (launch_i64_to_f64(table + (size_t)k * G, G, s))
+        return fail(PGPU_ERR_DEVICE, "slot conversion launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (kinds) P->slot_kind.assign(kinds, kinds + ns);
+  auto dtype = [&](int k) { return P->slot_kind[k] == SLOT_SUM_F64 ? pgpu::CDT_F64 : pgpu::CDT_I64; };
+  auto op = [&](int k) {
+    return P->slot_kind[k] == SLOT_MIN_KEY ? pgpu::COP_MIN : P->slot_kind[k] == SLOT_MAX_KEY ? pgpu::COP_MAX : pgpu::COP_SUM;
+  };
+  if (mode == PGPU_COMBINE_ALL_REDUCE) {
+    // consecutive rows of one element type and op in one collective
+    for (int k0 = 0; k0 < ns;) {
+      int k1 = k0 + 1;
+      while (k1 < ns && dtype(k1) == dtype(k0) && op(k1) == op(k0)) ++k1;
+      TRY(C->allreduce(table + (size_t)k0 * G, (size_t)(k1 - k0) * G, dtype(k0), op(k0), s));
+      k0 = k1;
+    }
+    if (key_begin) *key_begin = 0;
+    if (key_count) *key_count = G;
+    return 0;
+  }
+  // REDUCE_SCATTER: rank r keeps keys [r*chunk, (r+1)*chunk) -- half an all-reduce's link bytes, 1/N of the finalize
+  const int64_t chunk = (G + N - 1) / N;
+  const int64_t begin = std::min<int64_t>(G, (int64_t)me * chunk);
+  const int64_t count = std::min<int64_t>(G, begin + chunk) - begin;
+  uint64_t* shard = reinterpret_cast<uint64_t*>(d_shard);
+  if (!shard) {
+    TRY(sc->xshard.ensure((size_t)ns * std::max<int64_t>(chunk, 1) * 8 + 64));
+    shard = sc->xshard.as<uint64_t>();
+  }
+  if (G % N == 0) {
+    for (int k = 0; k < ns; ++k)
+      TRY(C->reduce_scatter(table + (size_t)k * G, shard + (size_t)k * chunk, (size_t)chunk, dtype(k), op(k), s));
+  } else {
+    // rows padded to N x chunk (the padded keys have COUNT 0 and are never finalized), then the rank's rows moved
+    // to a count-word stride
+    TRY(sc->xsend.ensure((size_t)ns * N * chunk * 8));
+    TRY(sc->xrecv.ensure((size_t)ns * chunk * 8));
+    uint64_t* pad = sc->xsend.as<uint64_t>();
+    uint64_t* part = sc->xrecv.as<uint64_t>();
+    HIP_TRY(hipMemsetAsync(pad, 0, (size_t)ns * N * chunk * 8, s));
+    HIP_TRY(hipMemcpy2DAsync(pad, (size_t)N * chunk * 8, table, (size_t)G * 8, (size_t)G * 8, (size_t)ns,
+                             hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < ns; ++k)
+      TRY(C->reduce_scatter(pad + (size_t)k * N * chunk, part + (size_t)k * chunk, (size_t)chunk, dtype(k), op(k), s));
+    if (count > 0)
+      HIP_TRY(hipMemcpy2DAsync(shard, (size_t)count * 8, part, (size_t)chunk * 8, (size_t)count * 8, (size_t)ns,
+                               hipMemcpyDeviceToDevice, s));
+  }
+  P->shard = shard;
+  P->shard_begin = begin;
+  P->shard_count = count;
+  if (key_begin) *key_begin = begin;
+  if (key_count) *key_count = count;
+  return 0;
+}
+
+int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) {
+  PGPU_ABI_GUARD;
+  if (!r || !c || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
+  pgpu::Comm* C = c->impl;
+  const int N = C->nranks, me = C->rank;
+  TRY(pgpu::result_expand(r));
+  // agree on the slot kinds; the group ids index the ranks' dictionary snapshots, which must be the same
+  std::vector<int64_t> mine(CI_WORDS, 0), all((size_t)N * CI_WORDS, 0);
+  uint64_t h = 0x84222325cbf29ce4ull;
+  auto mix = [&h](uint64_t v) { h = (h ^ v) * 0x9E3779B97F4A7C15ull; h ^= h >> 29; };
+  mix(r->key_dicts.size());
+  for (const auto& d : r->key_dicts) mix(d ? dict_digest(*static_cast<const Dict*>(d.get())) : 0);
+  mine[CI_KEYS] = r->num_keys;
+  mine[CI_SLOTS] = r->num_slots;
+  mine[CI_DIGEST] = (int64_t)h;
+  for (int s = 0; s < r->num_slots && s < kMaxSlots; ++s) mine[CI_KINDS + s] = r->slot_kind[s];
+  DeviceGuard g(C->device);
+  TRY(C->allgather_host(mine.data(), mine.size() * 8, all.data()));
+  for (int p = 0; p < N; ++p) {
+    const int64_t* w = all.data() + (size_t)p * CI_WORDS;
+    if (w[CI_KEYS] != mine[CI_KEYS] || w[CI_SLOTS] != mine[CI_SLOTS])
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "rank %d's result has another shape", p);
+    if (w[CI_DIGEST] != mine[CI_DIGEST])
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "rank %d's group-by dictionaries differ from rank %d's: union them "
+                  "(pgpu_table_add_dictionary_values) before the query", p, me);
+  }
+  std::vector<int32_t> kinds(std::max(r->num_slots, 1));
+  TRY(agree_kinds(all, N, r->num_slots, kinds.data()));
+  const int w = r->num_keys + r->num_slots;
+  std::vector<int64_t> rows((size_t)std::max<int64_t>(r->n, 1) * w), counts(N), cm((size_t)N * N), rcount(N);
+  TRY(pgpu_result_exchange_rows(r, N, kinds.data(), rows.data(), counts.data()));
+  TRY(C->allgather_host(counts.data(), (size_t)N * 8, cm.data()));
+  int64_t nrecv = 0;
+  for (int p = 0; p < N; ++p) nrecv += rcount[p] = cm[(size_t)p * N + me];
+  std::vector<int64_t> recv((size_t)std::max<int64_t>(nrecv, 1) * w);
+  TRY(C->alltoallv_host(rows.data(), counts.data(), recv.data(), rcount.data(), (size_t)w * 8));
+  return pgpu_result_merge_rows(r, nrecv ? recv.data() : nullptr, nrecv, kinds.data(), out);
 }
 
 int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,

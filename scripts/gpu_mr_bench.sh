@@ -1,9 +1,10 @@
 #!/bin/bash
-# Rehearsal of bench.py's multi-rank step on one GPU (2 ranks, gloo staging): dense all-reduce (C2), hash-mode
-# all-to-all (C5 key + m: 10^10 keys), numGroupsLimit row exchange (C1 by filt, metric: 10^7 keys per segment).
+# Rehearsal of bench.py's multi-rank step on one GPU (2 ranks, the C ABI combine over the host transport):
+# dense all-reduce (C2), reduce-scatter (C5), hash-mode all-to-all (C5 key + m: 10^10 keys), numGroupsLimit row
+# exchange (C1 by filt, metric: 10^7 keys per segment).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-export PGPU_BENCH_BACKEND=gloo
+export PGPU_BENCH_BACKEND=host
 run() {  # name, args...
   local name=$1; shift
   timeout -k 10 240 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -14,6 +15,7 @@ run() {  # name, args...
   return $rc
 }
 run dense --workload c2 --rows-total 4000000 &&
+run rs --workload c5 --rows-total 2000000 &&
 run hash --workload c5 --rows-total 2000000 --num-groups-limit 1000000000 --sql "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k3, m" &&
 run limit --workload c5 --rows-total 2000000 --sql "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3, m" &&
 run rows --workload c1 --rows-total 2000000 --sql "SELECT SUM(metric), COUNT(*) FROM t GROUP BY filt, metric"

@@ -21,7 +21,7 @@ def test_library_builds_and_loads():
     build()
     assert os.path.exists(LIB_PATH)
     lib = L.load()
-    assert lib.pgpu_abi_version() == 2
+    assert lib.pgpu_abi_version() == 3
 
 
 def test_every_declared_symbol_is_exported_and_bound():

@@ -1,0 +1,60 @@
+"""The host transport of pgpu_comm (comm.cpp) between processes, on the CPU: ids, the all-gather every combine mode's
+agreement runs on, variable-length gathers (dictionary unions), and argument checks.  The device collectives of both
+transports run in tests/test_multi_rank_gpu.py (host, two ranks on one GPU) and tests/test_combine_gpu.py (RCCL, one
+rank)."""
+import multiprocessing as mp
+import struct
+
+import pytest
+
+from pinot_amd import _lib as L
+
+
+def _rank(uid, rank, world, q):
+    try:
+        from pinot_amd.combine import Communicator
+        c = Communicator(L.COMM_HOST, uid, world, rank, 0)
+        got = c.allgather(struct.pack("<q", 100 + rank))
+        var = c.allgather_var(b"x" * (rank * 3 + 1))
+        c.barrier()
+        mx = c.max(rank * 1.5)
+        tot = c.sum_int(rank + 1)
+        c.close()
+        q.put((rank, [struct.unpack("<q", g)[0] for g in got], [len(v) for v in var], mx, tot))
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, "error: %r" % e))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_host_comm_allgather(world):
+    uid = __import__("pinot_amd.combine", fromlist=["Communicator"]).Communicator.unique_id(L.COMM_HOST)
+    assert uid.startswith(b"pgpu-comm-")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(uid, r, world, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict()
+    for _ in range(world):
+        item = q.get(timeout=60)
+        out[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(world):
+        assert not isinstance(out[r][0], str), out[r]
+        gathered, lens, mx, tot = out[r]
+        assert gathered == [100 + i for i in range(world)]
+        assert lens == [i * 3 + 1 for i in range(world)]
+        assert mx == (world - 1) * 1.5
+        assert tot == world * (world + 1) // 2
+
+
+def test_comm_bad_arguments():
+    import ctypes
+    lib = L.load()
+    h = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(b"not-an-id", L.COMM_ID_BYTES)
+    assert lib.pgpu_comm_create(L.COMM_HOST, uid, 2, 0, 0, ctypes.byref(h)) == L.PGPU_ERR_INVALID_ARGUMENT
+    assert lib.pgpu_comm_create(L.COMM_HOST, uid, 2, 2, 0, ctypes.byref(h)) == L.PGPU_ERR_INVALID_ARGUMENT
+    assert lib.pgpu_comm_create(7, uid, 1, 0, 0, ctypes.byref(h)) == L.PGPU_ERR_INVALID_ARGUMENT
+    assert lib.pgpu_comm_unique_id(7, uid) == L.PGPU_ERR_INVALID_ARGUMENT

@@ -181,3 +181,15 @@ def test_oracle_raw_filter_reference_case(oracle):
         o = oracle.run_groupby(schema, [seg], parse_query("SELECT COUNT(*) FROM t WHERE " + where))
         got = list(o.groups.values())[0][0] if o.groups else 0
         assert got == int(mask.sum()), where
+
+
+@pytest.mark.parametrize("per_chunk", [2**31 - 1, 1 << 28])
+def test_corrupted_chunk_header_is_rejected_before_allocating(per_chunk):
+    """A header claiming an absurd numDocsPerChunk (and totalDocs) must fail as INVALID_ARGUMENT, not allocate a
+    chunk buffer of per_chunk x entry bytes (INT32_MAX docs per chunk asked for ~17 GB)."""
+    vals = np.arange(100, dtype=np.int64)
+    raw = bytearray(raw_forward_index_bytes(L.LONG, vals, 3, 64, compression="LZ4"))
+    struct.pack_into(">i", raw, 8, per_chunk)   # numDocsPerChunk
+    struct.pack_into(">i", raw, 16, per_chunk)  # totalDocs
+    rc, _, _ = _product_values(bytes(raw), L.LONG, 100)
+    assert rc == L.PGPU_ERR_INVALID_ARGUMENT

@@ -34,10 +34,14 @@ WORLD = 2
 SEGS_PER_RANK = 3
 DOCS = 20000
 LIMIT = 5000
+SHARDED = ("large", "odd")  # dense cases merged by reduce-scatter (disjoint key ranges per rank)
 # name -> (sql, numGroupsLimit, expected combine mode)
 CASES = {
     "small": ("SELECT COUNT(*), SUM(mi), MIN(mi), MAX(mi), SUM(md) FROM t WHERE f < 40 GROUP BY d", 10 ** 9, "dense"),
     "large": ("SELECT SUM(mi), COUNT(*) FROM t GROUP BY d, e", 10 ** 9, "dense"),
+    # reduce-scattered over a key space of 41 x 27 = 1107 keys: not a multiple of the ranks (padded rows)
+    "odd": ("SELECT COUNT(*), SUM(mi), MIN(mi), MAX(md), SUM(md) FROM t WHERE f BETWEEN 10 AND 50 AND d BETWEEN 3 AND 29 "
+            "GROUP BY f, d", 10 ** 9, "dense"),
     "hash": ("SELECT COUNT(*), SUM(mi), MIN(md), MAX(mi) FROM t WHERE f >= 10 GROUP BY e, mi", 10 ** 9, "hash"),
     "limit": ("SELECT COUNT(*), SUM(mi), MAX(md) FROM t GROUP BY e, f", LIMIT, "rows"),
 }
@@ -79,11 +83,99 @@ def _run_dense(table, handles, q, stream, shard):
     return res
 
 
-def _worker(rank, port, out_dir):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    # a rank that fails must not leave the other waiting in a collective forever
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=90))
+def _run_dense_comm(table, handles, q, stream, shard, comm):
+    """The same merge through the C ABI (pgpu_plan_combine_mode / pgpu_plan_combine): all-reduce into a caller
+    table, or reduce-scatter of the plan's own table (finalize then reads this rank's key range)."""
+    from pinot_amd import _lib as L
+    from pinot_amd.combine import combine_mode, combine_plan
+    probe = table.plan(handles, q)
+    nslots, nkeys, _ = probe.layout()
+    mode, kinds = combine_mode(probe, comm, 0 if shard else 1 << 62)
+    probe.close()
+    assert mode == (L.COMBINE_REDUCE_SCATTER if shard else L.COMBINE_ALL_REDUCE), mode
+    d_table = None if shard else torch.empty((nslots, nkeys), dtype=torch.int64, device="cuda")
+    ptr = d_table.data_ptr() if d_table is not None else None
+    plan = table.plan_execute(handles, q, stream, ptr)
+    k0, kn = combine_plan(plan, comm, stream, mode, kinds, d_table=ptr)
+    if shard:
+        chunk = -(-nkeys // WORLD)
+        assert (k0, kn) == (min(nkeys, comm.rank * chunk), min(nkeys, (comm.rank + 1) * chunk) - min(nkeys, comm.rank * chunk))
+    res = plan.finalize(stream, ptr)
+    plan.close()
+    return res
+
+
+class _TorchMerge:
+    """Collectives through torch.distributed (gloo here, RCCL on a node): pinot_amd.combine's torch functions."""
+
+    def __init__(self, rank, port):
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        # a rank that fails must not leave the other waiting in a collective forever
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=90))
+
+    def union(self, table, cols):
+        union_dictionaries(table, cols)
+
+    def query(self, table, handles, q, stream, name):
+        mode = plan_combine_mode(table, handles, q)
+        if mode == "dense":
+            res = _run_dense(table, handles, q, stream, shard=name in SHARDED)
+        elif mode == "hash":
+            plan = table.plan_execute(handles, q, stream)
+            exchange_hash_table(plan)
+            res = plan.finalize(stream)
+            plan.close()
+        else:
+            res = exchange_result(table, table.execute_groupby(handles, q, stream))
+        return mode, res
+
+    def dense(self, table, handles, q, stream, shard):
+        return _run_dense(table, handles, q, stream, shard)
+
+    def close(self):
+        dist.destroy_process_group()
+
+
+class _CommMerge:
+    """Collectives issued by libpinotgpu (pgpu_comm, host transport: two ranks on one GPU) -- the path a JNI server
+    takes, with the combine in the C ABI."""
+
+    def __init__(self, rank, uid):
+        from pinot_amd import _lib as L
+        from pinot_amd.combine import Communicator
+        self.comm = Communicator(L.COMM_HOST, uid, WORLD, rank, 0)
+
+    def union(self, table, cols):
+        from pinot_amd.combine import union_dictionaries_comm
+        union_dictionaries_comm(table, cols, self.comm)
+
+    def query(self, table, handles, q, stream, name):
+        from pinot_amd import _lib as L
+        from pinot_amd.combine import combine_mode, combine_plan, combine_result_rows
+        probe = table.plan(handles, q)
+        mode, kinds = combine_mode(probe, self.comm, 0 if name in SHARDED else 1 << 62)
+        probe.close()
+        if mode in (L.COMBINE_ALL_REDUCE, L.COMBINE_REDUCE_SCATTER):
+            return "dense", _run_dense_comm(table, handles, q, stream, mode == L.COMBINE_REDUCE_SCATTER, self.comm)
+        if mode == L.COMBINE_HASH:
+            plan = table.plan_execute(handles, q, stream)
+            combine_plan(plan, self.comm, stream, mode, kinds)
+            res = plan.finalize(stream)
+            plan.close()
+            return "hash", res
+        assert mode == L.COMBINE_ROWS, mode
+        return "rows", combine_result_rows(table, table.execute_groupby(handles, q, stream), self.comm)
+
+    def dense(self, table, handles, q, stream, shard):
+        return _run_dense_comm(table, handles, q, stream, shard, self.comm)
+
+    def close(self):
+        self.comm.close()
+
+
+def _worker(rank, port, out_dir, transport="torch", uid=None):
+    merge = _TorchMerge(rank, port) if transport == "torch" else _CommMerge(rank, uid)
     try:
         import _oracle
         from bench import attach_star_trees
@@ -98,20 +190,11 @@ def _worker(rank, port, out_dir):
         table = GpuTable(SCHEMA, device=0)
         mine = [rank * SEGS_PER_RANK + i for i in range(SEGS_PER_RANK)]
         handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(s))) for s in mine]
-        union_dictionaries(table, ["d", "e", "f", "mi"])
+        merge.union(table, ["d", "e", "f", "mi"])
         modes = {}
         for name, (sql, limit, _) in CASES.items():
             q = parse_query(sql, num_groups_limit=limit)
-            mode = modes[name] = plan_combine_mode(table, handles, q)
-            if mode == "dense":
-                res = _run_dense(table, handles, q, stream, shard=name == "large")
-            elif mode == "hash":
-                plan = table.plan_execute(handles, q, stream)
-                exchange_hash_table(plan)
-                res = plan.finalize(stream)
-                plan.close()
-            else:
-                res = exchange_result(table, table.execute_groupby(handles, q, stream))
+            modes[name], res = merge.query(table, handles, q, stream, name)
             _dump(os.path.join(out_dir, "%s_%d.npz" % (name, rank)), table, res, q)
         table.close()
         with open(os.path.join(out_dir, "modes_%d.txt" % rank), "w") as f:
@@ -121,9 +204,9 @@ def _worker(rank, port, out_dir):
         w = WORKLOADS["c5"]()
         t5 = GpuTable(w.schema, device=0)
         h5 = [t5.generate_segment(w.gen, row0=rank * C5_DOCS, num_docs=C5_DOCS)]
-        union_dictionaries(t5, ["k1", "k2", "k3"])
+        merge.union(t5, ["k1", "k2", "k3"])
         q5 = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
-        _dump(os.path.join(out_dir, "c5_%d.npz" % rank), t5, _run_dense(t5, h5, q5, stream, shard=True), q5)
+        _dump(os.path.join(out_dir, "c5_%d.npz" % rank), t5, merge.dense(t5, h5, q5, stream, shard=True), q5)
         t5.close()
 
         # star-tree: one C4 segment per rank with its star-tree, into the caller table, all-reduced
@@ -131,17 +214,17 @@ def _worker(rank, port, out_dir):
         t4 = GpuTable(w.schema, device=0)
         h4 = [t4.generate_segment(w.gen, row0=rank * C4_DOCS, num_docs=C4_DOCS)]
         attach_star_trees(t4, h4, w, C4_DOCS)
-        union_dictionaries(t4, ["d1", "d2"])
+        merge.union(t4, ["d1", "d2"])
         q4 = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
         probe = t4.plan(h4, q4)
         star_segments = probe.star_work()  # segments the plan answers from their star-trees
         probe.close()
-        _dump(os.path.join(out_dir, "c4_%d.npz" % rank), t4, _run_dense(t4, h4, q4, stream, shard=False), q4)
+        _dump(os.path.join(out_dir, "c4_%d.npz" % rank), t4, merge.dense(t4, h4, q4, stream, shard=False), q4)
         with open(os.path.join(out_dir, "c4_star_%d.txt" % rank), "w") as f:
             f.write(str(star_segments[0]))
         t4.close()
     finally:
-        dist.destroy_process_group()
+        merge.close()
 
 
 def _free_port():
@@ -152,8 +235,13 @@ def _free_port():
     return p
 
 
-def _run_ranks(tmp_path, limit_s=200):
-    ctx = mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=False)
+def _run_ranks(tmp_path, limit_s=200, transport="torch"):
+    uid = None
+    if transport == "comm":
+        from pinot_amd.combine import Communicator
+        from pinot_amd import _lib as L
+        uid = Communicator.unique_id(L.COMM_HOST)
+    ctx = mp.spawn(_worker, args=(_free_port(), str(tmp_path), transport, uid), nprocs=WORLD, join=False)
     t0 = time.time()
     while not ctx.join(timeout=5):
         if time.time() - t0 > limit_s:
@@ -206,8 +294,11 @@ def _compare(name, got, exp, q, fp_cols):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path):
-    _run_ranks(tmp_path)
+@pytest.mark.parametrize("transport", ["torch", "comm"])
+def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path, transport):
+    """transport "torch": the collectives in pinot_amd.combine over torch.distributed (gloo); "comm": the combine
+    inside the C ABI (pgpu_plan_combine / pgpu_result_combine_rows over the host transport)."""
+    _run_ranks(tmp_path, transport=transport)
     for r in range(WORLD):
         modes = dict(kv.split("=") for kv in open(tmp_path / ("modes_%d.txt" % r)).read().split())
         assert modes == {name: c[2] for name, c in CASES.items()}, modes

@@ -54,6 +54,8 @@ def parse_args():
     p.add_argument("--cpu-sample-segments", type=int, default=None, help="default: the workload's sample size")
     p.add_argument("--cpu-target-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--parity-segments", type=int, default=None,
+                   help="segments of the full-size parity check against the oracle (default: all; 0 = skip)")
     p.add_argument("--no-bytes", action="store_true", help="skip the bytes_alg measurement pass")
     p.add_argument("--verify", action="store_true", help="check every step's result equals the first")
     p.add_argument("--host-profile", action="store_true", help="report host time per phase of a step")
@@ -232,24 +234,53 @@ def attach_inverted_indexes(table, handles, workload, docs):
                 table.attach_inverted_index(h, name, inv)
 
 
+def host_segments(table, handles, workload, docs):
+    """Each segment's Pinot bytes pulled back from HBM (what the oracle reads)."""
+    from pinot_amd import _lib as L
+    from pinot_amd.segment import ColumnData, SegmentBuffers
+    segs = []
+    for h in handles:
+        cols = {}
+        for name, typ in workload.schema:
+            card, bits, d, f = table.segment_column_bytes(int(h), name)
+            tcode = L.TYPE_NAMES[typ]
+            cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
+        segs.append(SegmentBuffers(docs, cols))
+    return segs
+
+
+def full_parity(table, handles, query, workload, docs, args):
+    """The GPU answer of the benchmarked query over the first --parity-segments segments (default: all of this
+    rank's) against the oracle's over the same bytes (pulled back from HBM): bit-exact for integer / count / dictId
+    work, 1e-9 relative for FLOAT / DOUBLE sums (BASELINE north_star).  Star-tree plans are checked against the
+    oracle's scan (BaseStarTreeV2Test's star-tree == scan rule); inverted-index plans compare numDocsScanned only
+    (the oracle restates the scan operator, whose numEntriesScannedInFilter differs by design)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    n = len(handles) if args.parity_segments is None else max(0, min(args.parity_segments, len(handles)))
+    if n == 0:
+        return None
+    t0 = time.perf_counter()
+    hs = np.ascontiguousarray(handles[:n], dtype=np.int64)
+    segs = host_segments(table, hs, workload, docs)
+    orc = _oracle.run_groupby_arrays(workload.schema, segs, query, nthreads=host_cores())
+    del segs
+    r = table.execute_groupby(hs, query)
+    cmp = _oracle.compare_result_arrays(table, r, orc, query, workload.schema,
+                                        check_stats=not workload.inverted_columns and not workload.star_tree)
+    cmp.update({"segments": n, "rows": n * docs, "seconds": round(time.perf_counter() - t0, 1),
+                "against": "oracle/oracle.c over the same segment bytes"})
+    return cmp
+
+
 def cpu_baseline(table, handles, query, workload, docs, args):
     """The oracle (C restatement of Pinot's per-segment operator + combine, one task per segment) timed on the
     host cores over a bounded sample of the same segments (bytes pulled back from HBM)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
-    from pinot_amd.segment import ColumnData, SegmentBuffers
-    types = dict(workload.schema)
     nsample = args.cpu_sample_segments or max(workload.cpu_sample_segments, 2 * host_cores())
     sample = handles[:max(1, min(nsample, len(handles)))]
-    segs = []
-    from pinot_amd import _lib as L
-    for h in sample:
-        cols = {}
-        for name, typ in workload.schema:
-            card, bits, d, f = table.segment_column_bytes(h, name)
-            tcode = L.TYPE_NAMES[typ]
-            cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
-        segs.append(SegmentBuffers(docs, cols))
+    segs = host_segments(table, sample, workload, docs)
     threads = host_cores()
     _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False)  # warm-up
     reps, elapsed = 0, 0.0
@@ -261,7 +292,6 @@ def cpu_baseline(table, handles, query, workload, docs, args):
         if elapsed >= args.cpu_target_seconds or reps >= 1000:
             break
     rows = reps * len(segs) * docs
-    _ = types
     return {"value": rows / elapsed, "unit": "rows/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "sample": "%d segments x %d rows, %d repetitions, %.1f s, %d worker threads = every core this process may "
@@ -545,9 +575,11 @@ def main():
         if pmc:
             roofline["traffic"] = round(pmc["traffic"], 0)
             roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("bytes_alg pass done; CPU baseline")
+        log("bytes_alg pass done; full-size parity")
+        parity = full_parity(table, handles, q, w, docs, args)
+        log("parity %s; CPU baseline" % (parity and parity["ok"]))
         cpu = cpu_baseline(table, handles, q, w, docs, args)
 
     if rank == 0:
@@ -571,6 +603,7 @@ def main():
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line), flush=True)
     table.close()

@@ -50,6 +50,9 @@ extern "C" {
                                         timeout (BaseCombineOperator.java:193-203 EXECUTION_TIMEOUT_ERROR for
                                         aggregation-only, GroupByCombineOperator.java:193-203 QUERY_EXECUTION_ERROR
                                         wrapping a TimeoutException for group-by); no partial result is returned */
+#define PGPU_ERR_CANCELLED (-8)      /* pgpu_plan_cancel: the caller abandoned the query (BaseOperator.nextBlock's
+                                        EarlyTerminationException after Future.cancel(true), BaseOperator.java:37-39,
+                                        BaseCombineOperator.java:124-130); no partial result is returned */
 
 /* FieldSpec.DataType subset of dictionary-encoded single-value columns. */
 enum pgpu_data_type { PGPU_INT = 0, PGPU_LONG = 1, PGPU_FLOAT = 2, PGPU_DOUBLE = 3, PGPU_STRING = 4 };
@@ -221,6 +224,18 @@ int pgpu_plan_destroy(pgpu_plan plan);
 enum pgpu_slot_kind { PGPU_SLOT_COUNT = 0, PGPU_SLOT_SUM_I64 = 1, PGPU_SLOT_SUM_F64 = 2, PGPU_SLOT_MIN_KEY = 3,
                       PGPU_SLOT_MAX_KEY = 4 };
 int pgpu_plan_layout(pgpu_plan plan, int32_t* num_slots, int64_t* num_keys, int32_t* slot_kinds /* >= 32 */);
+
+/* Cancels the plan's query from any thread (the broker abandoned it; Pinot's BaseCombineOperator cancels the
+ * segment tasks' futures, whose operators stop at the next block, BaseOperator.java:37-39).  A finalize waiting for
+ * the plan's device work -- or any later one -- returns PGPU_ERR_CANCELLED at once; launches the plan has not
+ * issued yet are not issued, and the device work already queued runs out while the plan's scratch stays out of the
+ * pool until it has (as for a timeout).  The table and its other queries are unaffected.  Idempotent. */
+int pgpu_plan_cancel(pgpu_plan plan);
+
+/* Diagnostics: how the plan's leaves run in the kernels, as (segment, leaf) pairs of the scanned segments per kernel
+ * leaf kind (counts[9]: NONE, ALL, RANGE, SET, DOCRANGE, BITMAP (a docId bitmap materialised per query),
+ * RAW_RANGE, RAW_IN, BITDIR (inverted-index containers read in place)). */
+int pgpu_plan_leaf_kinds(pgpu_plan plan, int64_t* counts);
 
 /* Runs the plan on `stream` (hipStream_t; NULL = the table's stream): predicate translation results are
  * uploaded, the fused filter/group/aggregate kernel runs over every segment, and the dense group table is

@@ -28,12 +28,14 @@ PGPU_ERR_DEVICE = -4
 PGPU_ERR_OUT_OF_MEMORY = -5
 PGPU_ERR_NOT_FOUND = -6
 PGPU_ERR_TIMEOUT = -7
+PGPU_ERR_CANCELLED = -8
 
 INT, LONG, FLOAT, DOUBLE, STRING = 0, 1, 2, 3, 4
 TYPE_NAMES = {"INT": INT, "LONG": LONG, "FLOAT": FLOAT, "DOUBLE": DOUBLE, "STRING": STRING}
 FWD_FIXED_BIT, FWD_SORTED_PAIRS, FWD_RAW_FIXED = 0, 1, 2
 PRED_EQ, PRED_NOT_EQ, PRED_IN, PRED_NOT_IN, PRED_RANGE = 0, 1, 2, 3, 4
 OP_PRED, OP_AND, OP_OR, OP_NOT = 0, 1, 2, 3
+LEAF_KIND_NAMES = ("none", "all", "range", "set", "docrange", "bitmap", "raw_range", "raw_in", "bitdir")
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 SLOT_COUNT, SLOT_SUM_I64, SLOT_SUM_F64, SLOT_MIN_KEY, SLOT_MAX_KEY = 0, 1, 2, 3, 4
 GEN_UNIFORM, GEN_ZIPF, GEN_TABLE = 0, 1, 2
@@ -121,6 +123,11 @@ class UnsupportedQueryError(PinotGpuError):
     """PGPU_ERR_UNSUPPORTED: the query shape is outside the GPU path."""
 
 
+class QueryCancelledError(PinotGpuError):
+    """PGPU_ERR_CANCELLED: pgpu_plan_cancel abandoned the query (BaseOperator's EarlyTerminationException after the
+    combine cancels its futures, BaseOperator.java:37-39 / BaseCombineOperator.java:124-130)."""
+
+
 class QueryTimeoutError(PinotGpuError):
     """PGPU_ERR_TIMEOUT: the query's end time passed (the combine's TimeoutException; Pinot reports
     QueryException.EXECUTION_TIMEOUT_ERROR_CODE 250 for aggregation-only and QUERY_EXECUTION_ERROR_CODE 200 for
@@ -151,6 +158,8 @@ _PROTOS = {
     "pgpu_plan_create_execute": (c_int, [c_voidp, c_i64p, c_i32, ctypes.POINTER(QueryC), c_voidp, c_voidp,
                                          ctypes.POINTER(c_voidp)]),
     "pgpu_plan_layout": (c_int, [c_voidp, c_i32p, c_i64p, c_i32p]),
+    "pgpu_plan_leaf_kinds": (c_int, [c_voidp, c_i64p]),
+    "pgpu_plan_cancel": (c_int, [c_voidp]),
     "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
     "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
     "pgpu_plan_finalize_range": (c_int, [c_voidp, c_voidp, c_voidp, c_i64, c_i64, ctypes.POINTER(c_voidp)]),
@@ -262,6 +271,8 @@ def check(code):
         raise BadQueryRequestException(code, msg)
     if code == PGPU_ERR_UNSUPPORTED:
         raise UnsupportedQueryError(code, msg)
+    if code == PGPU_ERR_CANCELLED:
+        raise QueryCancelledError(code, msg)
     if code == PGPU_ERR_TIMEOUT:
         raise QueryTimeoutError(code, msg)
     raise PinotGpuError(code, msg)

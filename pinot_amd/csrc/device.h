@@ -178,6 +178,29 @@ __device__ __forceinline__ uint32_t docrange_mask(int64_t group, uint32_t lo, ui
   return upto_b & ~below_a;
 }
 
+// One 32-doc group of a Roaring ARRAY container read in place (LEAF_BITDIR directory entry with bit 0 set: payload
+// pointer in bits 1..47, entry count in bits 48..63): the container's sorted u16 doc offsets are binary-searched for
+// the group's first doc, then the group's entries (at most 32) set their bits.  ARRAY containers hold < 4096 docs of
+// their 65536 (RoaringBitmap's ARRAY / BITMAP threshold), e.g. the partial last block of a segment.
+__device__ __forceinline__ uint32_t array_group_mask(uint64_t e, int64_t group) {
+  gmem<uint16_t>* __restrict__ a = gp(reinterpret_cast<const uint16_t*>(e & 0x0000FFFFFFFFFFFEull));
+  const int n = (int)(e >> 48);
+  const uint32_t lo = (uint32_t)(group & 2047) << 5;
+  int l = 0, h = n;
+  while (l < h) {
+    const int mid = (l + h) >> 1;
+    if ((uint32_t)a[mid] < lo) l = mid + 1;
+    else h = mid;
+  }
+  uint32_t m = 0;
+  for (int i = l; i < n; ++i) {
+    const uint32_t v = (uint32_t)a[i] - lo;
+    if (v >= 32u) break;
+    m |= 1u << v;
+  }
+  return m;
+}
+
 __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo, uint32_t span, const uint32_t* set,
                                               const uint32_t* fwd, int bits, int64_t group) {
   if (kind == LEAF_DOCRANGE) {
@@ -189,8 +212,8 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
     return negate ? ~m : m;
   }
   if (kind == LEAF_BITDIR) {
-    const uint32_t* blk = reinterpret_cast<const uint32_t*>(gp(reinterpret_cast<const uint64_t*>(set))[group >> 11]);
-    const uint32_t m = blk ? gp(blk)[group & 2047] : 0u;
+    const uint64_t e = gp(reinterpret_cast<const uint64_t*>(set))[group >> 11];
+    const uint32_t m = (e & 1ull) ? array_group_mask(e, group) : e ? gp(reinterpret_cast<const uint32_t*>(e))[group & 2047] : 0u;
     return negate ? ~m : m;
   }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);

@@ -39,11 +39,13 @@ constexpr int kFastLeaves = 4;              // pure-AND programs up to this many
 // LEAF_RAW_RANGE / LEAF_RAW_IN: host-side kinds of a raw-value predicate on a no-dictionary column
 // (RangePredicateEvaluatorFactory / InPredicateEvaluatorFactory raw evaluators).  raw_leaf_bitmap_kernel evaluates
 // them per query into a docId bitmap (KRawTask), which the scans read as a LEAF_BITMAP leaf.
-// LEAF_BITDIR: a LEAF_BITMAP of one dictId whose Roaring containers are all BITMAP containers -- read in place, as
-// BitmapBasedFilterOperator uses a single bitmap without an OR (BitmapBasedFilterOperator.java:77-79): `set` is a
-// directory of one device pointer per 65536-doc block (the container's 2048 words; null = no docs in the block).
+// LEAF_BITDIR: a LEAF_BITMAP of one dictId -- its Roaring containers read in place, as BitmapBasedFilterOperator
+// uses a single bitmap without an OR (BitmapBasedFilterOperator.java:77-79): `set` is a directory of one 64-bit entry
+// per 65536-doc block: 0 = no docs in the block; a BITMAP container's address (its 2048 words); an ARRAY container's
+// address | 1 with its entry count in bits 48..63 (array_group_mask, device.h).
 enum LeafKind : int32_t { LEAF_NONE = 0, LEAF_ALL = 1, LEAF_RANGE = 2, LEAF_SET = 3, LEAF_DOCRANGE = 4, LEAF_BITMAP = 5,
                           LEAF_RAW_RANGE = 6, LEAF_RAW_IN = 7, LEAF_BITDIR = 8 };
+constexpr int kLeafKinds = 9;
 enum OpCode : int32_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_NOT = 3 };
 enum SlotKind : int32_t { SLOT_COUNT = 0, SLOT_SUM_I64 = 1, SLOT_SUM_F64 = 2, SLOT_MIN_KEY = 3, SLOT_MAX_KEY = 4 };
 enum Mode : int32_t { MODE_LDS = 0, MODE_GLOBAL = 1, MODE_HASH = 2 };

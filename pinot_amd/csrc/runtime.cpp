@@ -1097,6 +1097,7 @@ struct pgpu_plan_s {
   std::vector<int> leaf_perm;             // evaluation position -> predicate index
   int64_t post_exempt_docs = 0;           // aggregation-only: docs of segments answered from metadata / dictionary
   int segments_matched_filter = 0;
+  int64_t leaf_kinds[kLeafKinds] = {};     // (segment, leaf) pairs of the scanned segments by kernel leaf kind
   std::vector<uint8_t> seg_scanned;       // per plan segment: 1 = scanned (filter not folded to empty)
   int grid = 0;
   size_t lds_bytes = 0;
@@ -1127,6 +1128,7 @@ struct pgpu_plan_s {
   // pgpu_query.end_time_ms (QueryContext.getEndTimeMs) of the query being run: set per query, not cached
   int64_t end_time_ms = 0;
   int64_t exec_start_ms = 0;
+  int cancel = 0;                         // pgpu_plan_cancel (__atomic_* access: another thread sets it)
   // key spaces beyond 64 bits (KParams.num_stages): per stage its end column, table slots, the next group's key
   // space; stage_space holds every group's key space (the last group's too)
   std::vector<int32_t> stage_end;
@@ -2151,6 +2153,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     int64_t docbit_words = 0;
     std::vector<uint8_t> scanned;
     int64_t tiles = 0, entries = 0, matched = 0, sel_docs = 0, exempt = 0;
+    int64_t leaf_kinds[kLeafKinds] = {};
     double sel = 1.0;
     int rc = 0;
     std::string err;
@@ -2333,18 +2336,26 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         }
         bool bitdir = false;
         if (lh.kind == LEAF_BITMAP && lh.inv_ids.size() == 1 && !getenv_flag("PGPU_NO_BITDIR")) {
-          // one dictId whose containers are all BITMAPs: the scan reads them in place through a block directory
+          // one dictId (no OR to compute): the scan reads its containers in place through a block directory --
+          // BITMAP containers word by word, ARRAY containers (< 4096 docs of a block, e.g. a segment's partial last
+          // block) by a binary search of their sorted offsets (array_group_mask); entry = payload address, | 1 and
+          // the entry count in bits 48..63 for an ARRAY
           const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
           const InvIndex::Entry& e = inv.ids[lh.inv_ids[0]];
           bitdir = true;
-          for (int32_t ci = e.begin; ci < e.begin + e.count && bitdir; ++ci) bitdir = inv.conts[ci].type == CONT_BITMAP;
+          for (int32_t ci = e.begin; ci < e.begin + e.count && bitdir; ++ci) {
+            const InvIndex::Cont& ct = inv.conts[ci];
+            const uint64_t a = reinterpret_cast<uint64_t>(reinterpret_cast<const uint32_t*>(inv.d_block) + ct.word);
+            bitdir = ct.type == CONT_BITMAP || (ct.type == CONT_ARRAY && ct.n >= 0 && ct.n < 65536 && (a >> 47) == 0);
+          }
           if (bitdir) {
             const int64_t nblk = ((int64_t)s->num_docs + 65535) >> 16;
             std::vector<uint64_t> dir((size_t)nblk, 0);
             for (int32_t ci = e.begin; ci < e.begin + e.count; ++ci) {
               const InvIndex::Cont& ct = inv.conts[ci];
-              if (ct.key >= 0 && ct.key < nblk)
-                dir[ct.key] = reinterpret_cast<uint64_t>(reinterpret_cast<const uint32_t*>(inv.d_block) + ct.word);
+              if (ct.key < 0 || ct.key >= nblk) continue;
+              const uint64_t a = reinterpret_cast<uint64_t>(reinterpret_cast<const uint32_t*>(inv.d_block) + ct.word);
+              dir[ct.key] = ct.type == CONT_BITMAP ? a : (ct.n > 0 ? (a | 1ull | ((uint64_t)ct.n << 48)) : 0);
             }
             C.inv_refs.push_back(s->cols[q->predicates[perm[k]].column].inv);
             const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
@@ -2356,6 +2367,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
             kl[k].kind = LEAF_BITDIR;
           }
         }
+        if (kl[k].kind >= 0 && kl[k].kind < kLeafKinds) C.leaf_kinds[kl[k].kind]++;
         if (lh.kind == LEAF_BITMAP && !bitdir) {  // docId bitmap region: whole 65536-doc containers
           const int64_t field = rec_off + (int64_t)((uint8_t*)&kl[k].set - rec.data());
           const InvIndex& inv = *s->cols[q->predicates[perm[k]].column].inv;
@@ -2552,6 +2564,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->segments_matched_filter += C.matched;
     P->scanned_entries_model += C.entries;
     P->post_exempt_docs += C.exempt;
+    for (int k = 0; k < kLeafKinds; ++k) P->leaf_kinds[k] += C.leaf_kinds[k];
     if (P->sel_docs == 0 && C.sel_docs) { P->sel_estimate = C.sel; P->sel_docs = C.sel_docs; }
   };
   const size_t nseg = P->segs.size();
@@ -2715,23 +2728,39 @@ int abandon_scratch(Scratch* sc, hipStream_t stream) {
 // _blockingQueue.poll(endTimeMs - now) / _operatorLatch.await(timeoutMs) do (BaseCombineOperator.java:193-203,
 // GroupByCombineOperator.java:193-203): the query returns PGPU_ERR_TIMEOUT at its deadline and the device work
 // left running keeps its scratch out of the pool until it completes.
+int cancel_fail() {
+  return fail(PGPU_ERR_CANCELLED, "QueryException 503 (QUERY_CANCELLATION_ERROR): Query was cancelled");
+}
+
+bool cancelled(const pgpu_plan_s* P) { return __atomic_load_n(&P->cancel, __ATOMIC_ACQUIRE) != 0; }
+
 int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
-  if (P->end_time_ms <= 0 || !P->scratch) {
+  if (!P->scratch) {
     HIP_TRY(hipStreamSynchronize(stream));
     return 0;
   }
   Scratch* sc = P->scratch;
+  if (cancelled(P)) return abandon_scratch(sc, stream) ? PGPU_ERR_DEVICE : cancel_fail();
   if (!sc->busy) HIP_TRY(hipEventCreateWithFlags(&sc->busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(sc->busy, stream));
+  // Polled, not a blocking synchronise: a pgpu_plan_cancel from another thread must end the wait.  Spinning (as the
+  // HIP runtime's own synchronise does) for the first ~2 ms keeps the wake-up latency of short queries at the
+  // poll interval; longer waits back off to 20 us sleeps.
+  const auto t0 = std::chrono::steady_clock::now();
   for (int spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(sc->busy);
     if (e == hipSuccess) return 0;
     if (e != hipErrorNotReady) return fail(PGPU_ERR_DEVICE, "query wait failed: %s", hipGetErrorString(e));
-    if (epoch_us() >= (double)P->end_time_ms * 1000.0) {
+    if (cancelled(P)) {
+      sc->abandoned = true;
+      return cancel_fail();
+    }
+    if (P->end_time_ms > 0 && epoch_us() >= (double)P->end_time_ms * 1000.0) {
       sc->abandoned = true;
       return timeout_fail(P);
     }
-    if (spin >= 32) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if ((spin & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
 
@@ -2766,6 +2795,7 @@ int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X) {
   X.t_start = trace_on() ? now_us() : 0;
+  if (cancelled(P)) return cancel_fail();  // nothing is launched for a cancelled query
   uint64_t deadline = 0;
   if (P->end_time_ms > 0) {  // past the end time already: nothing is launched
     P->exec_start_ms = (int64_t)(epoch_us() / 1000.0);
@@ -3795,6 +3825,7 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     P->last_stream = nullptr;
     P->star_docs_read = 0;
     P->shard = nullptr;
+    P->cancel = 0;
     return true;
   }
   return false;
@@ -4622,6 +4653,23 @@ int pgpu_plan_destroy(pgpu_plan P) {
   return 0;
 }
 
+int pgpu_plan_cancel(pgpu_plan P) {
+  // no ABI guard: the canceller must not wait behind the query thread's own entry points
+  if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
+  __atomic_store_n(&P->cancel, 1, __ATOMIC_RELEASE);
+  for (auto& part : P->parts) __atomic_store_n(&part.plan->cancel, 1, __ATOMIC_RELEASE);
+  return 0;
+}
+
+int pgpu_plan_leaf_kinds(pgpu_plan P, int64_t* counts) {
+  PGPU_ABI_GUARD;
+  if (!P || !counts) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  for (int k = 0; k < kLeafKinds; ++k) counts[k] = P->leaf_kinds[k];
+  for (const auto& part : P->parts)
+    for (int k = 0; k < kLeafKinds; ++k) counts[k] += part.plan->leaf_kinds[k];
+  return 0;
+}
+
 int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
   PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
@@ -4676,7 +4724,7 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   if (rc) {
     if (P->scratch) {
       // no launch of this plan may still use its scratch: wait, or (timeout) leave it to the queued work
-      if (rc == PGPU_ERR_TIMEOUT) abandon_scratch(P->scratch, se.stream);
+      if (rc == PGPU_ERR_TIMEOUT || rc == PGPU_ERR_CANCELLED) abandon_scratch(P->scratch, se.stream);
       else hipStreamSynchronize(se.stream);
       release_scratch(t, P->scratch);
       P->scratch = nullptr;

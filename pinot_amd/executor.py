@@ -504,6 +504,17 @@ class Plan:
         L.check(self.lib.pgpu_plan_layout(self.handle, ctypes.byref(ns), ctypes.byref(nk), kinds))
         return ns.value, nk.value, [kinds[i] for i in range(ns.value)]
 
+    def cancel(self):
+        """pgpu_plan_cancel: from any thread; a finalize waiting on this plan raises QueryCancelledError."""
+        L.check(self.lib.pgpu_plan_cancel(self.handle))
+
+    def leaf_kinds(self):
+        """{kernel leaf kind: (segment, leaf) pairs} of the scanned segments (pgpu_plan_leaf_kinds), e.g. "bitdir"
+        for inverted-index leaves read in place, "bitmap" for ones materialised per query."""
+        out = np.zeros(len(L.LEAF_KIND_NAMES), dtype=np.int64)
+        L.check(self.lib.pgpu_plan_leaf_kinds(self.handle, L.ptr(out, ctypes.c_int64)))
+        return {n: int(v) for n, v in zip(L.LEAF_KIND_NAMES, out) if v}
+
     def execute(self, stream=None, d_table=None):
         L.check(self.lib.pgpu_plan_execute(self.handle, ctypes.c_void_p(stream or 0), ctypes.c_void_p(d_table or 0)))
 

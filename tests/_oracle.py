@@ -364,3 +364,73 @@ def gen_values(spec, row0, n):
     out = np.zeros(n, dtype=np.int64)
     lib().or_gen_i64(ctypes.byref(g), row0, n, out.ctypes.data)
     return out
+
+
+# ------------------------------------------------------------------------------------------ result comparison
+def gpu_result_arrays(table, r, q):
+    """A GPU GroupByResult as (keys [n, k] in value space, values [num_aggs, n] float64, AVG counts), keys sorted."""
+    cols = r.gid_columns
+    keys = np.stack([np.asarray(table.dictionary(c))[g] for c, g in zip(q.group_by, cols)], axis=1) if cols else \
+        np.zeros((len(r), 0))
+    vals, cnts = [], []
+    for fn, v, e, c in r._col[2]:
+        vals.append(v if v is not None else e.astype(np.float64))
+        cnts.append(c if c is not None else np.zeros(len(r), dtype=np.int64))
+    return sort_by_key(keys, np.array(vals).reshape(len(q.aggregations), len(r)),
+                       np.array(cnts).reshape(len(q.aggregations), len(r)))
+
+
+def sort_by_key(keys, vals, cnts):
+    order = np.lexsort(keys.T[::-1]) if keys.shape[1] else np.arange(len(keys))
+    return keys[order], vals[:, order], cnts[:, order]
+
+
+def compare_result_arrays(table, r, orc, q, schema, rel=1e-9, check_stats=True):
+    """The parity bar of the path against run_groupby_arrays' output: same groups, bit-exact COUNT / integer SUM /
+    MIN / MAX and AVG counts, FLOAT / DOUBLE sums within `rel` relative (1e-6 absolute near zero).  Returns a dict
+    (ok, groups, max_rel_err of the FP sums, first mismatch) instead of raising: bench.py reports it in its line."""
+    types = {n: t for n, t in schema}
+    gk, gv, gc = gpu_result_arrays(table, r, q)
+    ok_, ov, oc, ostats = orc
+    ok_, ov, oc = sort_by_key(ok_.astype(gk.dtype) if len(ok_) else ok_.reshape(0, gk.shape[1]), ov, oc)
+    out = {"ok": True, "groups": int(len(gk)), "max_rel_err_fp_sum": 0.0, "mismatch": None}
+
+    def bad(msg):
+        out["ok"] = False
+        out["mismatch"] = out["mismatch"] or msg
+
+    if gk.shape != ok_.shape or not np.array_equal(gk, ok_):
+        bad("groups differ: gpu %s, oracle %s" % (gk.shape, ok_.shape))
+        return out
+    for a, (fn, col) in enumerate(q.aggregations):
+        fp = col != "*" and types[col] in ("FLOAT", "DOUBLE")
+        if fp and fn in ("SUM", "AVG"):
+            den = np.maximum(np.abs(ov[a]), 1e-300)
+            err = np.where(np.abs(gv[a] - ov[a]) <= 1e-6, 0.0, np.abs(gv[a] - ov[a]) / den)
+            e = float(err.max()) if len(err) else 0.0
+            out["max_rel_err_fp_sum"] = max(out["max_rel_err_fp_sum"], e)
+            if e > rel:
+                bad("%s(%s): relative error %.3g" % (fn, col, e))
+        elif not np.array_equal(gv[a], ov[a]):
+            i = int(np.nonzero(gv[a] != ov[a])[0][0])
+            bad("%s(%s) group %d: gpu %r, oracle %r" % (fn, col, i, gv[a][i], ov[a][i]))
+        if fn == "AVG" and not np.array_equal(gc[a], oc[a]):
+            bad("AVG(%s) counts" % col)
+    if check_stats and r.stats.as_tuple() != tuple(ostats):
+        bad("statistics: gpu %s, oracle %s" % (r.stats.as_tuple(), tuple(ostats)))
+    elif not check_stats and r.stats.as_tuple()[0] != ostats[0]:
+        bad("numDocsScanned: gpu %d, oracle %d" % (r.stats.as_tuple()[0], ostats[0]))
+    return out
+
+
+def segments_from_table(table, handles, schema, docs):
+    """Each pinned segment's Pinot bytes read back from HBM, as the oracle's input."""
+    segs = []
+    for h in handles:
+        cols = {}
+        for name, typ in schema:
+            card, bits, d, f = table.segment_column_bytes(int(h), name)
+            tcode = L.TYPE_NAMES[typ] if isinstance(typ, str) else typ
+            cols[name] = ColumnData(tcode, card, bits, 4 if tcode in (L.INT, L.FLOAT) else 8, d, f)
+        segs.append(SegmentBuffers(docs, cols))
+    return segs

@@ -727,6 +727,9 @@ INV_QUERIES = [
     "SELECT SUM(v) FROM t WHERE NOT (b IN (1, 2, 3) OR a = 0) GROUP BY g",
     "SELECT COUNT(*) FROM t WHERE a = 12345 GROUP BY g",
     "SELECT COUNT(*), SUM(v) FROM t WHERE s BETWEEN 2 AND 5 AND a IN (3, 5) GROUP BY g",
+    # one dictId: containers read in place (LEAF_BITDIR) -- ARRAY containers of the sparse column, negated too
+    "SELECT COUNT(*), SUM(v), MIN(v) FROM t WHERE b = 2999 GROUP BY g",
+    "SELECT COUNT(*), MAX(v) FROM t WHERE b <> 17 AND v < 300 GROUP BY g",
 ]
 
 
@@ -784,6 +787,15 @@ def test_inverted_index_leaves(oracle, gpu_lib, tmp_path, run_optimize):
             assert rm.stats.as_tuple() == om.stats, (sql, rm.stats, om.stats)
         r = t.execute_groupby(hs, parse_query("SELECT COUNT(*) FROM t WHERE a IN (2, 3) GROUP BY g"))
         assert r.stats.num_entries_scanned_in_filter == 0
+        # single-dictId leaves are read in place whatever their container kinds (no docId bitmap materialised):
+        # BITMAP containers of `a`, ARRAY containers of `b`, RUN containers (become ARRAY / BITMAP at attach)
+        for sql in ("SELECT COUNT(*) FROM t WHERE a = 3 GROUP BY g", "SELECT COUNT(*) FROM t WHERE b = 2999 GROUP BY g",
+                    "SELECT COUNT(*) FROM t WHERE b <> 17 GROUP BY g"):
+            with t.plan(hs, parse_query(sql)) as p:
+                kinds = p.leaf_kinds()
+            assert kinds.get("bitdir", 0) >= 1 and "bitmap" not in kinds, (sql, kinds)
+        with t.plan(hs, parse_query("SELECT COUNT(*) FROM t WHERE a IN (2, 3) GROUP BY g")) as p:
+            assert "bitmap" in p.leaf_kinds()  # an OR of dictIds is materialised
         for sql in ("SELECT COUNT(*), SUM(v), MIN(v), MAX(g) FROM t WHERE a = 3",
                     "SELECT COUNT(*), SUM(v) FROM t WHERE b NOT IN (5, 6) AND a IN (1, 3, 7)",
                     "SELECT COUNT(*) FROM t WHERE a = 3 AND a <> 3"):

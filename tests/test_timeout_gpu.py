@@ -101,3 +101,75 @@ def test_deadline_partitioned_and_streamed(table):
     q.end_time_ms = 0
     r = t.execute_groupby(handles[:2], q)
     assert len(r) > 0
+
+
+# ------------------------------------------------------------------------------------------------- cancellation
+# pgpu_plan_cancel: the broker abandoned the query; Pinot's combine cancels its futures and each segment operator
+# stops at its next block (BaseOperator.java:37-39 EarlyTerminationException, BaseCombineOperator.java:124-130).
+
+def test_cancel_from_another_thread_ends_the_wait(table):
+    import threading
+    t, handles = table
+    q = _hash_query()
+    with t.plan(handles, q) as p:
+        p.execute()
+        full_us = p.timing_us()[1]
+    assert full_us > 4_000, full_us
+    box = {}
+    with t.plan_execute(handles, q) as p:
+        def canceller():
+            time.sleep(full_us / 8 / 1e6)
+            box["t"] = time.perf_counter()
+            p.cancel()
+        th = threading.Thread(target=canceller)
+        t0 = time.perf_counter()
+        th.start()
+        with pytest.raises(L.QueryCancelledError) as e:
+            p.finalize()
+        t1 = time.perf_counter()
+        th.join()
+        assert "cancelled" in e.value.message
+        # the waiting finalize returned right after the cancel, long before the scan could have finished
+        assert (t1 - box["t"]) * 1e6 < 0.5 * full_us, (t1 - box["t"], full_us)
+        assert (t1 - t0) * 1e6 < 0.75 * full_us
+        with pytest.raises(L.QueryCancelledError):  # and so does any later finalize of the plan
+            p.finalize()
+    after = t.execute_aggregation(handles, _agg_query())
+    assert after.values == t.execute_aggregation(handles, _agg_query()).values
+
+
+def test_cancel_running_c3_scan_then_next_query_correct(oracle, gpu_lib):
+    """The README AdAnalytics query (C3) over 64 segments of 1M rows: cancelled from another thread while its scan is
+    queued / running on the GPU, the finalize reports PGPU_ERR_CANCELLED; the next query on the table -- on the plan
+    cache's image and a fresh scratch -- equals the oracle's answer."""
+    import threading
+    import _oracle
+    from pinot_amd.query import parse_query
+    from pinot_amd.workloads import WORKLOADS
+    w = WORKLOADS["adanalytics"]()
+    q = parse_query(w.sql, num_groups_limit=w.num_groups_limit)
+    t = GpuTable(w.schema, device=0)
+    try:
+        docs = 1_000_000
+        hs = [t.generate_segment(w.gen, row0=i * docs, num_docs=docs) for i in range(64)]
+        base = t.execute_groupby(hs, q)  # also fills the plan cache
+        for _ in range(3):
+            p = t.plan_execute(hs, q)
+            th = threading.Thread(target=p.cancel)
+            th.start()
+            th.join()
+            with pytest.raises(L.QueryCancelledError):
+                p.finalize()
+            p.close()
+        p = t.plan(hs, q)  # cancelled before it runs: nothing is launched
+        p.cancel()
+        with pytest.raises(L.QueryCancelledError):
+            p.execute()
+        p.close()
+        r = t.execute_groupby(hs, q)
+        assert r.as_dict() == base.as_dict() and r.stats.as_tuple() == base.stats.as_tuple()
+        r8 = t.execute_groupby(hs[:8], q)
+        assert r8.as_dict() == _oracle.run_groupby(w.schema, _oracle.segments_from_table(t, hs[:8], w.schema, docs),
+                                                   q).groups
+    finally:
+        t.close()

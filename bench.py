@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 SHARD_BYTES = 16 << 20  # group tables at least this large are reduce-scattered across ranks, not all-reduced
 # Rows of each workload's BASELINE.json configuration: the default strong-scaling total.
 DEFAULT_ROWS = {"adanalytics": 1_000_000_000, "adanalytics_inv": 1_000_000_000, "c1": 1_000_000, "c2": 100_000_000,
-                "c4": 64_000_000, "c5": 100_000_000}
+                "c4": 64_000_000, "c5": 100_000_000, "c5_hash": 100_000_000}
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
 
 
@@ -134,6 +134,7 @@ CALIB_SQL = {
     "c1": "SELECT COUNT(*) FROM t WHERE filt = 1 AND filt = 2 GROUP BY dim",
     "c2": "SELECT COUNT(*) FROM t WHERE f = 1 AND f = 2 GROUP BY d",
     "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
+    "c5_hash": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
 }
 SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel", "part_aggregate_kernel")
 # the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch)

@@ -335,11 +335,16 @@ __device__ __forceinline__ uint32_t eval_filter(const KParams& p, const SegView&
   return mask & stack[tid];
 }
 
-__device__ __forceinline__ int64_t hash_slot(unsigned long long* __restrict__ keys, int64_t cap, uint64_t key) {
+// Slot of `key` in an open-addressing table of `cap` (a power of two) slots, inserted if absent; linear probing,
+// at most `cap` probes: a full table returns -1 and sets *full (stats[4]; the host reports the error) instead of
+// spinning.  Tables are sized for a load <= 1/2 of the groups the plan can produce, so this never happens in a
+// correct plan -- it only bounds every wave's loop.
+__device__ __forceinline__ int64_t hash_slot(unsigned long long* __restrict__ keys, int64_t cap, uint64_t key,
+                                             unsigned long long* full) {
   uint64_t h = key * 0x9E3779B97F4A7C15ull;
   h ^= h >> 29;
   int64_t s = (int64_t)(h & (uint64_t)(cap - 1));
-  for (;;) {
+  for (int64_t probes = 0; probes < cap; ++probes) {
     unsigned long long k = keys[s];
     if (k == key) return s;
     if (k == ~0ull) {
@@ -348,6 +353,8 @@ __device__ __forceinline__ int64_t hash_slot(unsigned long long* __restrict__ ke
     }
     s = (s + 1) & (cap - 1);
   }
+  if (full) atomicOr(full, 1ull);
+  return -1;
 }
 
 template <int MODE>
@@ -455,8 +462,12 @@ template <int MODE, int NB>
 __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView (&S)[NB], const int64_t (&doc)[NB],
                                                 const bool (&ok)[NB], uint64_t* __restrict__ tbl, int64_t G) {
   int64_t key[NB];
+  bool live[NB];  // ok, and (hash mode) a slot was found
 #pragma unroll
-  for (int b = 0; b < NB; ++b) key[b] = -p.key_bias;  // filter-restricted key space (0 for hash / staged keys)
+  for (int b = 0; b < NB; ++b) {
+    key[b] = -p.key_bias;  // filter-restricted key space (0 for hash / staged keys)
+    live[b] = ok[b];
+  }
   int st = 0;  // MODE_HASH key stages (key spaces beyond 64 bits)
   for (int j = 0; j < p.num_keys; ++j) {
     const int kc = p.key_col[j];
@@ -477,9 +488,12 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     if (MODE == MODE_HASH && st < p.num_stages && j + 1 == p.stage_end[st]) {  // wave-uniform
       // the group's key -> its slot in stage table st (a dense id), the base of the next group's key
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
-        key[b] = ok[b] ? hash_slot(p.stage_keys + p.stage_off[st], p.stage_cap[st], (uint64_t)key[b]) * p.stage_mult[st]
-                       : 0;
+      for (int b = 0; b < NB; ++b) {
+        const int64_t slot = live[b] ? hash_slot(p.stage_keys + p.stage_off[st], p.stage_cap[st], (uint64_t)key[b],
+                                                 p.stats + 4) : 0;
+        live[b] = live[b] && slot >= 0;
+        key[b] = live[b] ? slot * p.stage_mult[st] : 0;
+      }
       ++st;
     }
   }
@@ -487,7 +501,10 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     idx[b] = key[b];
-    if (MODE == MODE_HASH && ok[b]) idx[b] = hash_slot(p.hash_keys, G, (uint64_t)key[b]);
+    if (MODE == MODE_HASH && live[b]) {
+      idx[b] = hash_slot(p.hash_keys, G, (uint64_t)key[b], p.stats + 4);
+      live[b] = idx[b] >= 0;
+    }
   }
   uint32_t id[NB];
   int prev_col = -1;
@@ -529,7 +546,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
-      if (ok[b]) accumulate<MODE>(tbl, (int64_t)s * G + idx[b], kind, ikey[b], dval[b]);
+      if (live[b]) accumulate<MODE>(tbl, (int64_t)s * G + idx[b], kind, ikey[b], dval[b]);
   }
 }
 

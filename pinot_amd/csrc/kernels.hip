@@ -459,7 +459,8 @@ __global__ __launch_bounds__(256) void merge_records_kernel(const uint64_t* __re
                                                             int64_t num_keys) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t* e = rec + r * (1 + num_slots);
-    const int64_t slot = hash_slot(hash_keys, num_keys, e[0]);
+    const int64_t slot = hash_slot(hash_keys, num_keys, e[0], nullptr);  // 2 x n slots: never full
+    if (slot < 0) continue;
     for (int s = 0; s < num_slots; ++s) {
       uint64_t* w = table + (int64_t)s * num_keys + slot;
       const uint64_t v = e[1 + s];

@@ -1138,6 +1138,10 @@ struct pgpu_plan_s {
   // the records merged into the owner's table (-1: the table holds the local groups)
   std::vector<int64_t> xchg_counts;
   int64_t merged_records = -1;
+  // hash-mode plans: the bound on their groups (table sizing), and the groups the plan's executions found (shared
+  // with the plan cache's image and every copy of it: -1 = none yet)
+  int64_t group_bound = 0;
+  std::shared_ptr<std::atomic<int64_t>> groups_seen;
   // pgpu_plan_combine REDUCE_SCATTER: this rank's merged key range [shard_begin, shard_begin + shard_count), slot rows
   // of shard_count words at `shard`; pgpu_plan_finalize reads it
   const void* shard = nullptr;
@@ -1171,6 +1175,14 @@ struct pgpu_plan_s {
 
 
 namespace {
+
+// Open-addressing table slots for at most `groups` groups: load <= 1/2, a power of two, >= 1024.
+int64_t hash_capacity(int64_t groups) {
+  const int64_t want = std::max<int64_t>(2 * std::max<int64_t>(groups, 1), 1024);
+  int64_t cap = 1;
+  while (cap < want) cap <<= 1;
+  return cap;
+}
 
 Scratch* acquire_scratch(pgpu_table_s* t) {
   std::lock_guard<std::mutex> g(t->mu);
@@ -2082,10 +2094,21 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   } else {
     P->mode = MODE_HASH;
     P->hash = true;
-    int64_t want = std::max<int64_t>(2 * std::min<int64_t>(G, std::max<int64_t>(P->total_docs, 1)), 1024);
-    int64_t cap = 1;
-    while (cap < want) cap <<= 1;
-    P->num_keys = cap;
+    // Groups are bounded by the key space and, per segment, by min(its local key space, its docs): C5-style keys of
+    // small per-segment cardinalities need far fewer slots than 2 x docs.  A cached plan re-sizes from the group
+    // count its last execution found (hash_capacity, plan_cache_get): same query, same segments, same groups.
+    int64_t bound = 0;
+    for (Segment* s : P->segs) {
+      int64_t local = 1;
+      for (int c : P->key_cols) {
+        const int64_t card = std::max<int64_t>(s->cols[c].card, 1);
+        local = local > (int64_t)s->num_docs / card ? (int64_t)s->num_docs + 1 : local * card;
+      }
+      bound += std::min<int64_t>(local, s->num_docs);
+    }
+    P->group_bound = std::max<int64_t>(1, std::min<int64_t>(G, bound));
+    P->groups_seen = std::make_shared<std::atomic<int64_t>>(-1);
+    P->num_keys = hash_capacity(P->group_bound);
     P->lds_bytes = stack_bytes;
   }
 
@@ -3376,10 +3399,14 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
+    if (st[5])  // stats[4]: a probe found no free slot (hash_slot) -- the table was sized below the plan's groups
+      return fail(PGPU_ERR_DEVICE, "group hash table of %lld slots overflowed (plan bound %lld groups)",
+                  (long long)G, (long long)P->group_bound);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
     P->star_docs_read = (int64_t)st[4];
+    if (P->groups_seen && P->merged_records < 0) P->groups_seen->store(n, std::memory_order_relaxed);
     if (n > 0) {
       TRY(sc->readback.ensure((size_t)n * rec * 8));
       st = reinterpret_cast<uint64_t*>(sc->readback.p);
@@ -3826,6 +3853,12 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     P->star_docs_read = 0;
     P->shard = nullptr;
     P->cancel = 0;
+    // a hash table sized by the groups the last execution of this plan found (deterministic for a cached plan:
+    // same query over the same pinned segments)
+    if (P->hash && P->groups_seen && P->stage_end.empty() && P->merged_records < 0) {
+      const int64_t g = P->groups_seen->load(std::memory_order_relaxed);
+      if (g >= 0) P->num_keys = hash_capacity(std::min<int64_t>(g, P->group_bound));
+    }
     return true;
   }
   return false;

@@ -170,7 +170,7 @@ template <int MODE, int H>
 __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const KStarSeg& S, int64_t g, uint32_t mask,
                                                     const int32_t* __restrict__ cache, bool cached,
                                                     uint64_t* __restrict__ tbl, int64_t G) {
-  const uint32_t m = (mask >> H) & 0xFFFFu;
+  uint32_t m = (mask >> H) & 0xFFFFu;
   // dense key spaces (MODE_LDS / MODE_GLOBAL) stay below 2^31: 32-bit keys
   using KeyT = typename std::conditional<MODE == MODE_HASH, int64_t, int32_t>::type;
   KeyT key[16];
@@ -198,7 +198,11 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
   if (MODE == MODE_HASH) {
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if ((m >> i) & 1u) key[i] = (KeyT)hash_slot(p.hash_keys, G, (uint64_t)key[i]);
+      if ((m >> i) & 1u) {
+        const int64_t slot = hash_slot(p.hash_keys, G, (uint64_t)key[i], p.stats + 4);
+        if (slot < 0) m &= ~(1u << i);
+        key[i] = (KeyT)(slot < 0 ? 0 : slot);
+      }
   }
   const int64_t d0 = g * 32 + H;
   for (int s = 0; s < p.num_slots; ++s) {

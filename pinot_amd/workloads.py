@@ -108,6 +108,23 @@ def c5():
                     cpu_sample_segments=16)
 
 
+def c5_hash():
+    """C5 through the global hash table (BASELINE configs[4] "with global-memory hash tables"): the same ~10M groups
+    of a 3-column key as C5, but k3 has 10 000 values drawn from k2's hash stream (k3 % 100 == k2), so the key space
+    is 1000 x 100 x 10 000 = 10^9 > 2^26 -- past every dense table -- while the data holds 10^7 combinations
+    (DictionaryBasedGroupKeyGenerator's LONG_MAP holder, DictionaryBasedGroupKeyGenerator.java:644-746)."""
+    schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT")]
+    gen = [
+        {"kind": "UNIFORM", "column_index": 0, "lo": 0, "hi": 1000},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 100},
+        {"kind": "UNIFORM", "column_index": 1, "lo": 0, "hi": 10_000},
+        {"kind": "UNIFORM", "column_index": 3, "lo": 0, "hi": 1000},
+    ]
+    sql = "SELECT SUM(m), COUNT(*) FROM t GROUP BY k1, k2, k3"
+    return Workload("c5_hash", schema, gen, sql, "C5 ~10M groups in a 10^9-key space: global hash table",
+                    num_groups_limit=1_000_000_000, cpu_sample_segments=16)
+
+
 def c4():
     """C4: star-tree query: per segment d1 U[0,100), d2 U[0,50), d3 U[0,20), d4 U[0,10),
     m U[0,1000); star-tree split order [d1, d2, d3, d4], pairs SUM__m and COUNT__*, maxLeafRecords 10 000."""
@@ -125,4 +142,5 @@ def c4():
     return Workload("c4", schema, gen, sql, "C4 star-tree multi-dim GROUP BY", star_tree=star)
 
 
-WORKLOADS = {"adanalytics": adanalytics, "adanalytics_inv": adanalytics_inv, "c1": c1, "c2": c2, "c4": c4, "c5": c5}
+WORKLOADS = {"adanalytics": adanalytics, "adanalytics_inv": adanalytics_inv, "c1": c1, "c2": c2, "c4": c4, "c5": c5,
+             "c5_hash": c5_hash}

@@ -88,8 +88,9 @@ def test_rccl_one_rank_combine_matches_oracle(oracle, rccl_table, name, sql, lim
 def test_combine_mode_after_combine_is_rejected(rccl_table):
     from pinot_amd.combine import combine_mode, combine_plan
     table, handles, _, comm = rccl_table
-    q = parse_query(CASES[1][1])
-    s = torch.cuda.Stream().cuda_stream
+    q = parse_query(CASES[1][1], num_groups_limit=CASES[1][2])
+    stream = torch.cuda.Stream()  # held: the C ABI keeps only its handle
+    s = stream.cuda_stream
     plan = table.plan_execute(handles, q, s)
     mode, kinds = combine_mode(plan, comm, 0)
     combine_plan(plan, comm, s, mode, kinds)
@@ -99,3 +100,4 @@ def test_combine_mode_after_combine_is_rejected(rccl_table):
         combine_plan(plan, comm, s, L.COMBINE_ROWS, kinds)
     plan.finalize(s)
     plan.close()
+    stream.synchronize()

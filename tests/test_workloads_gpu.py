@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 REL = 1e-9
 
 # workload -> segments (1M docs each) in the test
-SIZES = {"c1": 1, "c2": 4, "adanalytics": 8, "adanalytics_inv": 4, "c5": 2, "c4": 3}
+SIZES = {"c1": 1, "c2": 4, "adanalytics": 8, "adanalytics_inv": 4, "c5": 2, "c4": 3, "c5_hash": 2}
 
 
 def _oracle_segments(oracle, w, nseg, docs, table=None, handles=None):
@@ -51,7 +51,7 @@ def assert_same_arrays(table, r, orc, q, schema):
     assert res["ok"], res
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "adanalytics", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "adanalytics", "c5", "c5_hash"])
 def test_workload_generator_and_query(oracle, gpu_lib, name):
     w = WORKLOADS[name]()
     nseg, docs = SIZES[name], SEGMENT_DOCS
@@ -60,9 +60,15 @@ def test_workload_generator_and_query(oracle, gpu_lib, name):
     try:
         hs = [t.generate_segment(w.gen, row0=i * docs, num_docs=docs) for i in range(nseg)]
         segs = _oracle_segments(oracle, w, nseg, docs, t, hs)
+        if name == "c5_hash":  # the global hash table (a 10^9-key space), sized from the segments' group bound
+            with t.plan(hs, q) as p:
+                assert p.layout()[1] == 0
         r = t.execute_groupby(hs, q)
         o = oracle.run_groupby_arrays(w.schema, segs, q)
         assert len(r) == len(o[0]) > 0
+        if name == "c5_hash":  # again from the plan cache: the table re-sized by the groups found
+            r2 = t.execute_groupby(hs, q)
+            assert_same_arrays(t, r2, o, q, w.schema)
         assert_same_arrays(t, r, o, q, w.schema)
         assert r.stats.as_tuple() == o[3]  # numEntriesScannedInFilter included (C3: AndDocIdIterator leap-frog)
     finally:

@@ -267,8 +267,9 @@ def full_parity(table, handles, query, workload, docs, args):
     orc = _oracle.run_groupby_arrays(workload.schema, segs, query, nthreads=host_cores())
     del segs
     r = table.execute_groupby(hs, query)
+    star = workload.star_tree and query.use_star_tree
     cmp = _oracle.compare_result_arrays(table, r, orc, query, workload.schema,
-                                        check_stats=not workload.inverted_columns and not workload.star_tree)
+                                        check_stats=False if star else "docs" if workload.inverted_columns else True)
     cmp.update({"segments": n, "rows": n * docs, "seconds": round(time.perf_counter() - t0, 1),
                 "against": "oracle/oracle.c over the same segment bytes"})
     return cmp

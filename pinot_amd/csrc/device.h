@@ -24,6 +24,25 @@ __device__ __forceinline__ gmem<T>* gp(const T* p) { return (gmem<T>*)p; }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// PGPU_SADDR (default on): gathers from a wave-uniform base take a 32-bit byte offset, so they compile to the
+// global_load SADDR form (base in SGPRs, one offset VGPR per load instead of a 64-bit VGPR address pair) -- the
+// dense path keeps 16 lookups in flight per lane, and their address registers were a third of its footprint.
+#ifndef PGPU_SADDR
+#define PGPU_SADDR 1
+#endif
+template <typename T>
+__device__ __forceinline__ const T* wave_uniform(const T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+}
+template <typename T>
+__device__ __forceinline__ T load_off(const T* ubase, uint32_t byte_off) {
+  using GC = const __attribute__((address_space(1))) char;
+  return *reinterpret_cast<gmem<T>*>(reinterpret_cast<GC*>(gp(ubase)) + byte_off);
+}
+
 // The query's end time (KParams.deadline: a wall_clock64() value, 0 = none) has passed.  wall_clock64 is a scalar
 // read of the constant-rate device clock, so the answer is uniform across a wave.
 __device__ __forceinline__ bool past_deadline(uint64_t deadline) {
@@ -567,16 +586,32 @@ __device__ __forceinline__ void decode_group_b(const uint32_t* __restrict__ word
   load_group<B, true>(words, w);
   decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
 }
+// The same from a wave-uniform column base and the group's byte offset (PGPU_SADDR).
+template <int B, int H>
+__device__ __forceinline__ void decode_group_ob(const uint32_t* __restrict__ ubase, uint32_t off, uint32_t (&ids)[16]) {
+  uint32_t w[B + 1];
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(load_off(ubase, off + 4u * k));
+  w[B] = 0;
+  decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
+}
 
 // dictIds of docs [32*group + H, 32*group + H + 16) (PinotDataBitSet.readInt).
 template <int H>
 __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, int bits, int64_t group,
                                              uint32_t (&ids)[16]) {
+#if PGPU_SADDR
+  const uint32_t* ubase = wave_uniform(fwd);
+  const uint32_t off = (uint32_t)group * (uint32_t)bits * 4u;  // a segment's forward index is < 4 GB
+#define PGPU_DECODE(B) decode_group_ob<B, H>(ubase, off, ids)
+#else
   const uint32_t* words = fwd + group * (int64_t)bits;
+#define PGPU_DECODE(B) decode_group_b<B, H>(words, ids)
+#endif
   switch (bits) {
 #define PGPU_CASE(B) \
   case B:            \
-    decode_group_b<B, H>(words, ids); \
+    PGPU_DECODE(B); \
     break;
     PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
     PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
@@ -584,6 +619,7 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
     PGPU_CASE(23) PGPU_CASE(24) PGPU_CASE(25) PGPU_CASE(26) PGPU_CASE(27) PGPU_CASE(28) PGPU_CASE(29)
     PGPU_CASE(30) PGPU_CASE(31)
 #undef PGPU_CASE
+#undef PGPU_DECODE
     default:
 #pragma unroll
       for (int i = 0; i < 16; ++i) ids[i] = 0;
@@ -666,10 +702,16 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     decode_group<H>(c.fwd, c.bits, group, ids);
     const int32_t stride = (int32_t)p.key_stride[j];
     if (c.lut) {  // segment-uniform: the whole wave reads one segment here
-      gmem<int32_t>* __restrict__ lut = gp(c.lut);
       int32_t g[16];
+#if PGPU_SADDR
+      const int32_t* lut = wave_uniform(c.lut);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[i] = load_off(lut, ids[i] << 2);
+#else
+      gmem<int32_t>* __restrict__ lut = gp(c.lut);
 #pragma unroll
       for (int i = 0; i < 16; ++i) g[i] = lut[ids[i]];
+#endif
 #pragma unroll
       for (int i = 0; i < 16; ++i) key[i] += g[i] * stride;
     } else {
@@ -700,9 +742,15 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
       int64_t v[16];
       if (c.dkey) {
+#if PGPU_SADDR
+        const int64_t* dk = wave_uniform(c.dkey);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? load_off(dk, ids[i] << 3) : 0;
+#else
         gmem<int64_t>* __restrict__ dk = gp(c.dkey);
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : 0;
+#endif
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? c.key_base + (int64_t)ids[i] : 0;
@@ -723,10 +771,16 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       }
     }
     if (need_f) {
-      gmem<double>* __restrict__ dv = gp(c.dval);
       double v[16];
+#if PGPU_SADDR
+      const double* dv = wave_uniform(c.dval);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? load_off(dv, ids[i] << 3) : 0.0;
+#else
+      gmem<double>* __restrict__ dv = gp(c.dval);
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;
+#endif
       for (int r = s; r < e; ++r) {
         if (p.slot_kind[r] != SLOT_SUM_F64) continue;
         uint64_t* __restrict__ row = tbl + (int64_t)r * G;

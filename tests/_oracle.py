@@ -387,8 +387,10 @@ def sort_by_key(keys, vals, cnts):
 
 def compare_result_arrays(table, r, orc, q, schema, rel=1e-9, check_stats=True):
     """The parity bar of the path against run_groupby_arrays' output: same groups, bit-exact COUNT / integer SUM /
-    MIN / MAX and AVG counts, FLOAT / DOUBLE sums within `rel` relative (1e-6 absolute near zero).  Returns a dict
-    (ok, groups, max_rel_err of the FP sums, first mismatch) instead of raising: bench.py reports it in its line."""
+    MIN / MAX and AVG counts, FLOAT / DOUBLE sums within `rel` relative (1e-6 absolute near zero).  check_stats: True
+    = every statistic, "docs" = numDocsScanned only (index-backed leaves scan no entries), False = none (star-tree
+    plans scan pre-aggregated documents).  Returns a dict (ok, groups, max_rel_err of the FP sums, first mismatch)
+    instead of raising: bench.py reports it in its line."""
     types = {n: t for n, t in schema}
     gk, gv, gc = gpu_result_arrays(table, r, q)
     ok_, ov, oc, ostats = orc
@@ -416,9 +418,9 @@ def compare_result_arrays(table, r, orc, q, schema, rel=1e-9, check_stats=True):
             bad("%s(%s) group %d: gpu %r, oracle %r" % (fn, col, i, gv[a][i], ov[a][i]))
         if fn == "AVG" and not np.array_equal(gc[a], oc[a]):
             bad("AVG(%s) counts" % col)
-    if check_stats and r.stats.as_tuple() != tuple(ostats):
+    if check_stats is True and r.stats.as_tuple() != tuple(ostats):
         bad("statistics: gpu %s, oracle %s" % (r.stats.as_tuple(), tuple(ostats)))
-    elif not check_stats and r.stats.as_tuple()[0] != ostats[0]:
+    elif check_stats == "docs" and r.stats.as_tuple()[0] != ostats[0]:
         bad("numDocsScanned: gpu %d, oracle %d" % (r.stats.as_tuple()[0], ostats[0]))
     return out
 

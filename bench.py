@@ -284,11 +284,26 @@ def cpu_baseline(table, handles, query, workload, docs, args):
     sample = handles[:max(1, min(nsample, len(handles)))]
     segs = host_segments(table, sample, workload, docs)
     threads = host_cores()
-    _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False)  # warm-up
+    star = bool(workload.star_tree) and query.use_star_tree
+    if star:  # the path Pinot's plan picks (StarTreeUtils.isFitForStarTree): the oracle's star-tree operator
+        from concurrent.futures import ThreadPoolExecutor
+        from pinot_amd.startree import StarTree
+        spec = workload.star_tree
+
+        def tree(seg):
+            st = StarTree.build(workload.schema, seg, spec["split_order"], spec["pairs"], spec["max_leaf_records"])
+            a = st.arrays()
+            st.close()
+            return a
+        with ThreadPoolExecutor(8) as ex:
+            for seg, a in zip(segs, ex.map(tree, segs)):
+                seg.star_arrays = a
+    _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False,
+                        use_star_tree=star)  # warm-up
     reps, elapsed = 0, 0.0
     t0 = time.perf_counter()
     while True:
-        _oracle.run_groupby(workload.schema, segs, query, nthreads=threads, decode=False)
+        _oracle.run_groupby(workload.schema, segs, query, nthreads=threads, decode=False, use_star_tree=star)
         reps += 1
         elapsed = time.perf_counter() - t0
         if elapsed >= args.cpu_target_seconds or reps >= 1000:
@@ -299,8 +314,9 @@ def cpu_baseline(table, handles, query, workload, docs, args):
             "sample": "%d segments x %d rows, %d repetitions, %.1f s, %d worker threads = every core this process may "
                       "run on (sched_getaffinity; the machine has %s) (oracle/oracle.c, one task per segment as "
                       "GroupByCombineOperator%s)" % (len(segs), docs, reps, elapsed, threads, os.cpu_count(),
-                                                     "; scan path: the star-tree operator is not restated in C"
-                                                     if workload.star_tree else "")}
+                                                     "; star-tree path: StarTreeFilterOperator + "
+                                                     "StarTreeGroupByExecutor over each segment's star-tree"
+                                                     if star else "")}
 
 
 def host_cores():

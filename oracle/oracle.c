@@ -1293,6 +1293,8 @@ static int num_projected(const or_query* q) {
 
 /* AggregationGroupByOperator.getNextBlock (core/operator/query/AggregationGroupByOperator.java:62-79) on one
  * segment: DocIdSetOperator blocks of <= 10000 docIds, DefaultGroupByExecutor.process (:117-147). */
+static int run_star_segment(const or_segment* seg, const or_query* q, const pred_eval* evals, seg_result* r);
+
 static void run_segment(const or_segment* seg, const or_query* q, seg_result* r) {
   memset(r, 0, sizeof *r);
   r->total_docs = seg->num_docs;
@@ -1301,6 +1303,11 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   for (int i = 0; i < np; i++) {
     int st = build_pred_eval(seg, &q->predicates[i], &evals[i], r->msg, sizeof r->msg);
     if (st) { r->status = st; for (int j = 0; j < i; j++) pred_eval_free(&evals[j]); free(evals); return; }
+  }
+  if (q->use_star_tree && seg->star_tree && run_star_segment(seg, q, evals, r)) {
+    for (int j = 0; j < np; j++) pred_eval_free(&evals[j]);
+    free(evals);
+    return;
   }
   fnode* root = build_filter_tree(seg, q, evals, r->msg, sizeof r->msg);
   if (!root) { r->status = -1; for (int j = 0; j < np; j++) pred_eval_free(&evals[j]); free(evals); return; }
@@ -1506,6 +1513,322 @@ static void run_segment(const or_segment* seg, const or_query* q, seg_result* r)
   fn_free(root);
   for (int j = 0; j < np; j++) pred_eval_free(&evals[j]);
   free(evals);
+}
+
+/* ======================================================================================= star-tree */
+
+/* The filter program as a tree (FilterContext): AND / OR / PREDICATE / NOT nodes over predicate indexes. */
+typedef struct qnode { int op; int pred; int n; struct qnode** kid; } qnode;
+static void qn_free(qnode* n) {
+  if (!n) return;
+  for (int i = 0; i < n->n; i++) qn_free(n->kid[i]);
+  free(n->kid); free(n);
+}
+static qnode* qn_build(const or_query* q) {
+  qnode** st = calloc((size_t)q->num_filter_ops + 1, sizeof(qnode*));
+  int sp = 0;
+  for (int i = 0; i < q->num_filter_ops; i++) {
+    const or_filter_op* o = &q->filter[i];
+    qnode* n = calloc(1, sizeof(qnode));
+    n->op = o->op;
+    if (o->op == OR_OP_PRED) n->pred = o->arg;
+    else {
+      n->n = o->op == OR_OP_NOT ? 1 : o->arg;
+      n->kid = calloc((size_t)n->n, sizeof(qnode*));
+      for (int k = n->n - 1; k >= 0; k--) n->kid[k] = st[--sp];
+    }
+    st[sp++] = n;
+  }
+  qnode* root = sp ? st[0] : NULL;
+  free(st);
+  return root;
+}
+
+/* Per star-tree dimension: the composite predicate evaluators on it (StarTreeUtils.extractPredicateEvaluatorsMap,
+ * core/startree/StarTreeUtils.java:95-138): a list, ANDed, of predicate-index lists, ORed. */
+typedef struct { int ncomp; int* comp_off; int* preds; int npreds; } dim_preds;
+
+static void dp_add(dim_preds* d, const int* p, int n) {
+  d->comp_off = realloc(d->comp_off, sizeof(int) * (size_t)(d->ncomp + 2));
+  if (d->ncomp == 0) d->comp_off[0] = 0;
+  d->preds = realloc(d->preds, sizeof(int) * (size_t)(d->npreds + n + 1));
+  memcpy(d->preds + d->npreds, p, sizeof(int) * (size_t)n);
+  d->npreds += n;
+  d->ncomp++;
+  d->comp_off[d->ncomp] = d->npreds;
+}
+
+static int star_dim_of(const or_star_tree* st, int column) {
+  for (int k = 0; k < st->num_dims; k++) if (st->dim_columns[k] == column) return k;
+  return -1;
+}
+
+/* isOrClauseValidForStarTree (:180-219) over extractOrClausePredicates (:222-244): the predicates under an OR; returns
+ * 0 when the clause cannot be solved with the star-tree. */
+static int or_preds(const qnode* n, int* out, int* nout) {
+  for (int i = 0; i < n->n; i++) {
+    const qnode* c = n->kid[i];
+    if (c->op == OR_OP_PRED) out[(*nout)++] = c->pred;
+    else if (c->op == OR_OP_OR) { if (!or_preds(c, out, nout)) return 0; }
+    else return 0; /* AND / NOT under OR */
+  }
+  return 1;
+}
+
+/* extractPredicateEvaluatorsMap + isFitForStarTree: fills dp[dim]; returns 0 when the filter does not fit. */
+static int star_filter_fit(const or_segment* seg, const or_query* q, const pred_eval* ev, const qnode* root,
+                           dim_preds* dp) {
+  const or_star_tree* st = seg->star_tree;
+  if (!root) return 1;
+  const qnode** queue = malloc(sizeof(qnode*) * (size_t)(q->num_filter_ops + 1));
+  int head = 0, tail = 0, ok = 1;
+  int* buf = malloc(sizeof(int) * (size_t)(q->num_predicates + 1));
+  queue[tail++] = root;
+  while (ok && head < tail) {
+    const qnode* n = queue[head++];
+    if (n->op == OR_OP_AND) {
+      for (int i = 0; i < n->n; i++) queue[tail++] = n->kid[i];
+    } else if (n->op == OR_OP_PRED) {
+      const int col = q->predicates[n->pred].column, d = star_dim_of(st, col);
+      if (d < 0 || seg->columns[col].raw) { ok = 0; break; }        /* not a star-tree dimension */
+      if (!ev[n->pred].always_true) dp_add(&dp[d], &n->pred, 1);
+    } else if (n->op == OR_OP_OR) {
+      int np = 0;
+      if (!or_preds(n, buf, &np)) { ok = 0; break; }
+      int col = -1, keep = 0, always_true = 0;
+      for (int i = 0; i < np && ok; i++) {
+        const int c = q->predicates[buf[i]].column;
+        if (star_dim_of(st, c) < 0 || seg->columns[c].raw) { ok = 0; break; }
+        if (ev[buf[i]].always_true) { always_true = 1; break; }     /* the whole clause is always true */
+        if (ev[buf[i]].always_false) continue;
+        if (col >= 0 && col != c) { ok = 0; break; }                /* predicates on several columns */
+        col = c;
+        buf[keep++] = buf[i];
+      }
+      if (ok && !always_true && keep > 0) dp_add(&dp[star_dim_of(st, col)], buf, keep);
+      /* NOTE (reference): an OR whose predicates are all always-false yields an empty list, read as always-true */
+    } else {
+      ok = 0; /* NOT */
+    }
+  }
+  free(queue); free(buf);
+  return ok;
+}
+
+/* StarTreeFilterOperator.getMatchingDictIds (:353-423) as flags over the dimension's dictIds: the AND of the
+ * composites, each the OR of its predicates. */
+static uint8_t* dim_match(const dim_preds* d, const pred_eval* ev, int card, int* any) {
+  uint8_t* m = malloc((size_t)(card ? card : 1));
+  *any = 0;
+  for (int id = 0; id < card; id++) {
+    int v = 1;
+    for (int c = 0; c < d->ncomp && v; c++) {
+      int o = 0;
+      for (int i = d->comp_off[c]; i < d->comp_off[c + 1] && !o; i++) o = pred_apply(&ev[d->preds[i]], id);
+      v = o;
+    }
+    m[id] = (uint8_t)v;
+    *any |= v;
+  }
+  return m;
+}
+
+static int composite_apply(const dim_preds* d, const pred_eval* ev, int c, int id) {
+  for (int i = d->comp_off[c]; i < d->comp_off[c + 1]; i++) if (pred_apply(&ev[d->preds[i]], id)) return 1;
+  return 0;
+}
+
+/* StarTreeFilterOperator + StarTreeGroupByExecutor over one segment's star-tree (core/startree/operator/
+ * StarTreeFilterOperator.java:185-338, core/startree/executor/StarTreeGroupByExecutor.java:60-71).  Returns 0 when
+ * the query does not fit the tree (StarTreeUtils.isFitForStarTree, :151-176): the caller then scans. */
+static int run_star_segment(const or_segment* seg, const or_query* q, const pred_eval* ev, seg_result* r) {
+  const or_star_tree* st = seg->star_tree;
+  const int nd = st->num_dims, na = q->num_aggs, nk = q->num_group_by;
+  if (nd > 30 || nk > 16) return 0;
+  /* function-column pairs (extractAggregationFunctionPairs + containsFunctionColumnPair) */
+  int* metric_of = malloc(sizeof(int) * (size_t)(na ? na : 1));
+  for (int a = 0; a < na; a++) {
+    metric_of[a] = -1;
+    for (int m = 0; m < st->num_metrics; m++)
+      if (st->metric_fn[m] == q->aggs[a].fn && st->metric_column[m] == q->aggs[a].column) { metric_of[a] = m; break; }
+    if (metric_of[a] < 0) { free(metric_of); return 0; }
+  }
+  int gdim[16];
+  uint32_t group_mask = 0;
+  for (int j = 0; j < nk; j++) {
+    gdim[j] = star_dim_of(st, q->group_by[j]);
+    if (gdim[j] < 0) { free(metric_of); return 0; }
+  }
+  qnode* root = qn_build(q);
+  dim_preds* dp = calloc((size_t)nd, sizeof(dim_preds));
+  if (!star_filter_fit(seg, q, ev, root, dp)) {
+    for (int k = 0; k < nd; k++) { free(dp[k].comp_off); free(dp[k].preds); }
+    free(dp); qn_free(root); free(metric_of);
+    return 0;
+  }
+  uint32_t pred_mask = 0;
+  for (int k = 0; k < nd; k++) if (dp[k].ncomp) pred_mask |= 1u << k;
+  for (int j = 0; j < nk; j++) if (!((pred_mask >> gdim[j]) & 1u)) group_mask |= 1u << gdim[j];
+  /* _groupByColumns are the group-by columns without a predicate (StarTreeFilterOperator ctor, :150-160) */
+
+  /* traverseStarTree (:234-338): BFS; matching dictIds computed on first use, an empty set empties the result */
+  uint8_t** match = calloc((size_t)nd, sizeof(uint8_t*));
+  const int32_t* N = st->nodes;
+  uint8_t* docs = calloc((size_t)(st->num_docs ? st->num_docs : 1), 1);
+  uint32_t remaining = 0;
+  int empty = 0;
+  typedef struct { int node; uint32_t rp, rg; } entry;
+  int64_t qcap = 1024, qh = 0, qt = 0;
+  entry* queue = malloc(sizeof(entry) * (size_t)qcap);
+  queue[qt++] = (entry){0, pred_mask, group_mask};
+  while (qh < qt && !empty) {
+    const entry e = queue[qh++];
+    const int32_t* n = N + (int64_t)e.node * 7;
+    const int first = n[5], last = n[6];
+#define PUSH(nd_, rp_, rg_)                                                              \
+    do {                                                                                 \
+      if (qt == qcap) { qcap *= 2; queue = realloc(queue, sizeof(entry) * (size_t)qcap); } \
+      queue[qt++] = (entry){(nd_), (rp_), (rg_)};                                        \
+    } while (0)
+    if (!e.rp && !e.rg) { docs[n[4]] = 1; continue; }              /* the node's aggregated document */
+    if (first < 0) {                                               /* leaf: its documents, predicates remain */
+      for (int d = n[2]; d < n[3]; d++) docs[d] = 1;
+      remaining |= e.rp;
+      continue;
+    }
+    const int cd = N[(int64_t)first * 7];                          /* the children's dimension */
+    if ((e.rp >> cd) & 1u) {
+      if (!match[cd]) {
+        int any = 0;
+        match[cd] = dim_match(&dp[cd], ev, seg->columns[st->dim_columns[cd]].cardinality, &any);
+        if (!any) { empty = 1; break; }
+      }
+      for (int c = first; c <= last; c++) {
+        const int v = N[(int64_t)c * 7 + 1];
+        if (v != -1 && match[cd][v]) PUSH(c, e.rp & ~(1u << cd), e.rg);
+      }
+    } else {
+      uint32_t rg = e.rg;
+      if (!((e.rg >> cd) & 1u)) {
+        if (N[(int64_t)first * 7 + 1] == -1) { PUSH(first, e.rp, e.rg); continue; } /* the star node */
+      } else {
+        rg &= ~(1u << cd);
+      }
+      for (int c = first; c <= last; c++) if (N[(int64_t)c * 7 + 1] != -1) PUSH(c, e.rp, rg);
+    }
+#undef PUSH
+  }
+  free(queue);
+
+  /* residual filter (:185-226): the remaining predicate columns' composites ANDed with the traversal's documents */
+  int64_t bitmap_docs = 0, matched = 0;
+  int nrem = 0;
+  for (int k = 0; k < nd; k++) nrem += (remaining >> k) & 1u;
+  int32_t** dimids = calloc((size_t)nd, sizeof(int32_t*));
+  /* a remaining composite that can match nothing is an EmptyFilterOperator leaf, which empties the AND
+   * (FilterOperatorUtils.getLeafFilterOperator / getAndFilterOperator): no document is read */
+  for (int k = 0; k < nd && !empty; k++)
+    if ((remaining >> k) & 1u)
+      for (int c = 0; c < dp[k].ncomp && !empty; c++) {
+        int all_false = 1;
+        for (int i = dp[k].comp_off[c]; i < dp[k].comp_off[c + 1]; i++) all_false &= ev[dp[k].preds[i]].always_false;
+        empty = all_false;
+      }
+  if (!empty) {
+    for (int k = 0; k < nd; k++) {
+      const int used = ((remaining >> k) & 1u) != 0;
+      int grouped = 0;
+      for (int j = 0; j < nk; j++) grouped |= gdim[j] == k;
+      if (!used && !grouped) continue;
+      dimids[k] = malloc(sizeof(int32_t) * (size_t)(st->num_docs ? st->num_docs : 1));
+      const int bits = seg->columns[st->dim_columns[k]].bits;
+      for (int d = 0; d < st->num_docs; d++) dimids[k][d] = fixedbit_read(st->dim_fwd[k], d, bits);
+    }
+    for (int d = 0; d < st->num_docs; d++) {
+      if (!docs[d]) continue;
+      bitmap_docs++;
+      int keep = 1;
+      for (int k = 0; k < nd && keep; k++)
+        if ((remaining >> k) & 1u)
+          for (int c = 0; c < dp[k].ncomp && keep; c++) keep = composite_apply(&dp[k], ev, c, dimids[k][d]);
+      docs[d] = (uint8_t)keep;
+      matched += keep;
+    }
+  }
+
+  /* StarTreeGroupByExecutor: DictionaryBasedGroupKeyGenerator over the star-tree's dimensions (mixed radix of the
+   * segment dictionaries' cardinalities, first column fastest) and the function-column pairs' pre-aggregated values
+   * (COUNT adds count__*, CountAggregationFunction.java:97-104; SUM / MIN / MAX / AVG their pairs), in ascending
+   * star-tree docId order. */
+  int64_t card[16], stride[16], space = 1;
+  for (int j = 0; j < nk; j++) {
+    card[j] = seg->columns[q->group_by[j]].cardinality > 0 ? seg->columns[q->group_by[j]].cardinality : 1;
+    stride[j] = space;
+    space = space > INT64_MAX / card[j] ? INT64_MAX : space * card[j];
+  }
+  gen_map gm;
+  gm_init(&gm, 1);
+  int64_t ng = 0, vcap = 0;
+  double* vals = NULL;
+  int64_t* cnts = NULL;
+  int64_t* raw_of = NULL;
+  if (!empty && matched) {
+    for (int d = 0; d < st->num_docs; d++) {
+      if (!docs[d]) continue;
+      uint64_t raw = 0;
+      for (int j = 0; j < nk; j++) raw += (uint64_t)dimids[gdim[j]][d] * (uint64_t)stride[j];
+      const int gid = gm_get_group_id(&gm, &raw, INT32_MAX);
+      if (gid >= ng) {
+        if (gid >= vcap) {
+          vcap = vcap ? vcap * 2 : 1024;
+          vals = realloc(vals, sizeof(double) * (size_t)(vcap * (na ? na : 1)));
+          cnts = realloc(cnts, sizeof(int64_t) * (size_t)(vcap * (na ? na : 1)));
+          raw_of = realloc(raw_of, sizeof(int64_t) * (size_t)vcap);
+        }
+        for (; ng <= gid; ng++) {
+          raw_of[ng] = (int64_t)raw;
+          for (int a = 0; a < na; a++) {
+            vals[ng * na + a] = q->aggs[a].fn == OR_AGG_MIN ? INFINITY : q->aggs[a].fn == OR_AGG_MAX ? -INFINITY : 0.0;
+            cnts[ng * na + a] = 0;
+          }
+        }
+      }
+      for (int a = 0; a < na; a++) {
+        const int m = metric_of[a];
+        double* v = &vals[(int64_t)gid * na + a];
+        switch (q->aggs[a].fn) {
+          case OR_AGG_COUNT: *v += (double)st->metric_i64[m][d]; break;
+          case OR_AGG_SUM: *v += st->metric_f64[m][d]; break;
+          case OR_AGG_MIN: if (st->metric_f64[m][d] < *v) *v = st->metric_f64[m][d]; break;
+          case OR_AGG_MAX: if (st->metric_f64[m][d] > *v) *v = st->metric_f64[m][d]; break;
+          default: *v += st->metric_f64[m][d]; cnts[(int64_t)gid * na + a] += st->metric_i64[m][d]; break;
+        }
+      }
+    }
+  }
+  r->holder = OR_HOLDER_LONG_MAP;
+  r->docs_scanned = matched;
+  r->in_filter = bitmap_docs * nrem;  /* the residual scan leaves read each traversal document once per column */
+  r->post_filter = matched * num_projected(q);
+  bbuf* kb = &r->keys;
+  for (int64_t g = 0; g < ng; g++) {
+    sr_add_group(r, na);
+    r->koff[r->ngroups] = kb->n;
+    for (int j = 0; j < nk; j++)
+      key_append_value(kb, &seg->columns[q->group_by[j]], (int)((raw_of[g] / stride[j]) % card[j]));
+    for (int a = 0; a < na; a++) {
+      r->vals[r->ngroups * na + a] = vals[g * na + a];
+      r->cnts[r->ngroups * na + a] = cnts[g * na + a];
+    }
+    r->ngroups++;
+  }
+  if (r->koff) r->koff[r->ngroups] = kb->n;
+  gm_free(&gm);
+  free(vals); free(cnts); free(raw_of);
+  for (int k = 0; k < nd; k++) { free(dimids[k]); free(match[k]); free(dp[k].comp_off); free(dp[k].preds); }
+  free(dimids); free(match); free(dp); free(docs);
+  qn_free(root); free(metric_of);
+  return 1;
 }
 
 /* ======================================================================================= combine */

@@ -68,10 +68,30 @@ int64_t or_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t c
  * 0, -1 malformed, -2 unsupported codec. */
 int or_raw_decode(const or_column* c, const uint8_t* fwd, int64_t len, int num_docs, int64_t* ival, double* dval);
 
+/* A star-tree of a segment (StarTreeV2: OffHeapStarTree + its documents; seglocal/startree/OffHeapStarTree.java:45-80,
+ * seglocal/startree/v2/store/StarTreeDataSource): nodes as OffHeapStarTreeNode records, the star-tree documents'
+ * dimension dictIds (the segment's dictionaries, the segment column's bitsPerElement, MSB-first) and the
+ * pre-aggregated function-column pairs. */
+typedef struct {
+  int32_t num_nodes;
+  const int32_t* nodes;           /* [num_nodes][7]: dimension id, value (-1 = ALL), start doc, end doc, aggregated doc,
+                                     first child, last child (-1: leaf) */
+  int32_t num_docs;               /* star-tree documents */
+  int32_t num_dims;
+  const int32_t* dim_columns;     /* split order: segment column of each dimension */
+  const uint8_t* const* dim_fwd;  /* per dimension: packed dictIds of the star-tree documents */
+  int32_t num_metrics;
+  const int32_t* metric_fn;       /* per function-column pair: OR_AGG_* */
+  const int32_t* metric_column;   /* -1 for COUNT(*) */
+  const double* const* metric_f64;  /* SUM / MIN / MAX values, AVG sums (NULL for COUNT) */
+  const int64_t* const* metric_i64; /* COUNT counts, AVG counts (NULL otherwise) */
+} or_star_tree;
+
 typedef struct {
   int32_t num_docs;
   int32_t num_columns;
   const or_column* columns;
+  const or_star_tree* star_tree;  /* NULL: none (queries use_star_tree run on it when they fit, see or_query) */
 } or_segment;
 
 /* Dictionary + forward index creation, as SegmentDictionaryCreator / SegmentColumnarIndexCreator produce them
@@ -127,6 +147,8 @@ typedef struct {
   int32_t num_groups_limit;      /* InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000 (:70) */
   int32_t max_initial_result_holder_capacity; /* DEFAULT_MAX_INITIAL_RESULT_HOLDER_CAPACITY = 10000 (:66) */
   int32_t combine;               /* 1: GroupByCombineOperator merge (PQL) across segments; 0: single segment */
+  int32_t use_star_tree;         /* 1: segments with a star-tree the query fits run StarTreeFilterOperator +
+                                    StarTreeGroupByExecutor (AggregationGroupByPlanNode.java:67-92) */
 } or_query;
 
 /* Holder kinds chosen by DictionaryBasedGroupKeyGenerator (:110-160). */

@@ -32,8 +32,17 @@ class OrColumn(ctypes.Structure):
                 ("raw", ctypes.c_int32), ("fwd_len", ctypes.c_int64)]
 
 
+class OrStarTree(ctypes.Structure):
+    _fields_ = [("num_nodes", ctypes.c_int32), ("nodes", ctypes.POINTER(ctypes.c_int32)), ("num_docs", ctypes.c_int32),
+                ("num_dims", ctypes.c_int32), ("dim_columns", ctypes.POINTER(ctypes.c_int32)),
+                ("dim_fwd", ctypes.POINTER(ctypes.c_void_p)), ("num_metrics", ctypes.c_int32),
+                ("metric_fn", ctypes.POINTER(ctypes.c_int32)), ("metric_column", ctypes.POINTER(ctypes.c_int32)),
+                ("metric_f64", ctypes.POINTER(ctypes.c_void_p)), ("metric_i64", ctypes.POINTER(ctypes.c_void_p))]
+
+
 class OrSegment(ctypes.Structure):
-    _fields_ = [("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32), ("columns", ctypes.POINTER(OrColumn))]
+    _fields_ = [("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32), ("columns", ctypes.POINTER(OrColumn)),
+                ("star_tree", ctypes.POINTER(OrStarTree))]
 
 
 class OrPredicate(ctypes.Structure):
@@ -56,7 +65,7 @@ class OrQuery(ctypes.Structure):
                 ("num_group_by", ctypes.c_int32), ("group_by", ctypes.POINTER(ctypes.c_int32)),
                 ("num_aggs", ctypes.c_int32), ("aggs", ctypes.POINTER(OrAgg)),
                 ("num_groups_limit", ctypes.c_int32), ("max_initial_result_holder_capacity", ctypes.c_int32),
-                ("combine", ctypes.c_int32)]
+                ("combine", ctypes.c_int32), ("use_star_tree", ctypes.c_int32)]
 
 
 class OrResult(ctypes.Structure):
@@ -181,9 +190,32 @@ class _OrSeg:
                                int(c.fwd_format == L.FWD_RAW_FIXED), len(c.fwd_bytes))
         self.keep.append(cols)
         self.seg = OrSegment(seg.num_docs, len(schema), cols)
+        star = getattr(seg, "star_arrays", None)  # StarTree.arrays() of the segment's star-tree, if any
+        if star is not None:
+            self.seg.star_tree = ctypes.pointer(self._star(star))
+
+    def _star(self, a):
+        keep = self.keep
+        nodes = np.ascontiguousarray(a["nodes"], dtype=np.int32)
+        dims = np.ascontiguousarray(a["dim_columns"], dtype=np.int32)
+        fwd = [ctypes.create_string_buffer(bytes(f) + b"\0" * 16, len(f) + 16) for f in a["dim_fwd"]]
+        fwd_p = (ctypes.c_void_p * max(len(fwd), 1))(*[ctypes.cast(f, ctypes.c_void_p) for f in fwd])
+        fns = np.ascontiguousarray([m[0] for m in a["metrics"]], dtype=np.int32)
+        mcols = np.ascontiguousarray([m[1] for m in a["metrics"]], dtype=np.int32)
+        f64 = [None if x is None else np.ascontiguousarray(x, dtype=np.float64) for x in a["metric_f64"]]
+        i64 = [None if x is None else np.ascontiguousarray(x, dtype=np.int64) for x in a["metric_i64"]]
+        f_p = (ctypes.c_void_p * max(len(f64), 1))(*[None if x is None else x.ctypes.data for x in f64])
+        i_p = (ctypes.c_void_p * max(len(i64), 1))(*[None if x is None else x.ctypes.data for x in i64])
+        keep += [nodes, dims, fwd, fwd_p, fns, mcols, f64, i64, f_p, i_p]
+        st = OrStarTree(len(nodes), nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(a["num_docs"]), len(dims),
+                        dims.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fwd_p, len(fns),
+                        fns.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                        mcols.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), f_p, i_p)
+        keep.append(st)
+        return st
 
 
-def _or_query(schema, q, combine=True, max_initial_capacity=10000):
+def _or_query(schema, q, combine=True, max_initial_capacity=10000, use_star_tree=False):
     idx = {n: i for i, (n, _) in enumerate(schema)}
     keep = []
     preds, ops = [], []
@@ -202,7 +234,7 @@ def _or_query(schema, q, combine=True, max_initial_capacity=10000):
     ac = (OrAgg * max(len(q.aggregations), 1))(*[OrAgg(fns[f], -1 if c == "*" else idx[c]) for f, c in q.aggregations])
     keep += [pc, oc, gb, ac]
     oq = OrQuery(len(preds), pc, len(ops), oc, len(q.group_by), gb, len(q.aggregations), ac, q.num_groups_limit,
-                 max_initial_capacity, int(combine))
+                 max_initial_capacity, int(combine), int(use_star_tree))
     return oq, keep
 
 
@@ -230,12 +262,13 @@ def _decode_key(blob, types):
     return tuple(out)
 
 
-def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000, decode=True):
+def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000, decode=True,
+                use_star_tree=False):
     """decode=False: run the operator + combine only and return the group count (bench timing leg)."""
     o = lib()
     segs = [_OrSeg(schema, s) for s in segments]
     arr = (OrSegment * max(len(segs), 1))(*[s.seg for s in segs])
-    oq, keep = _or_query(schema, q, combine, max_initial_capacity)
+    oq, keep = _or_query(schema, q, combine, max_initial_capacity, use_star_tree)
     res = OrResult()
     msg = ctypes.create_string_buffer(512)
     rc = o.or_execute_groupby(arr, len(segs), ctypes.byref(oq), nthreads, ctypes.byref(res), msg, 512)
@@ -269,7 +302,7 @@ def run_groupby(schema, segments, q, nthreads=8, combine=True, max_initial_capac
         o.or_free_result(ctypes.byref(res))
 
 
-def run_groupby_arrays(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000):
+def run_groupby_arrays(schema, segments, q, nthreads=8, combine=True, max_initial_capacity=10000, use_star_tree=False):
     """run_groupby for numeric group-by keys, returned as numpy arrays (large results: millions of groups):
     (keys [n, num_group_by] int64 / float64, values [num_aggs, n] float64, avg_counts [num_aggs, n] int64, stats)."""
     o = lib()
@@ -278,7 +311,7 @@ def run_groupby_arrays(schema, segments, q, nthreads=8, combine=True, max_initia
     assert all(t != L.STRING for t in ktypes), "numeric group-by keys only"
     segs = [_OrSeg(schema, s) for s in segments]
     arr = (OrSegment * max(len(segs), 1))(*[s.seg for s in segs])
-    oq, keep = _or_query(schema, q, combine, max_initial_capacity)
+    oq, keep = _or_query(schema, q, combine, max_initial_capacity, use_star_tree)
     res = OrResult()
     msg = ctypes.create_string_buffer(512)
     rc = o.or_execute_groupby(arr, len(segs), ctypes.byref(oq), nthreads, ctypes.byref(res), msg, 512)

@@ -76,3 +76,33 @@ def test_skip_star_node_dimension(oracle):
     q = parse_query("SELECT SUM(m), COUNT(*) FROM t WHERE d3 = 2 GROUP BY d1", num_groups_limit=10 ** 9)
     got, _, _ = SC.startree_answer(oracle, seg, SC.C4_SCHEMA, a, q, SC.C4_SPLIT, SC.C4_PAIRS)
     assert got == oracle.run_groupby(SC.C4_SCHEMA, [seg], q).groups
+
+
+@pytest.mark.parametrize("sql", SC.C4_QUERIES)
+def test_c_startree_operator_matches(oracle, c4, sql):
+    """The C oracle's StarTreeFilterOperator + StarTreeGroupByExecutor restatement (run_star_segment, the CPU
+    baseline of bench.py's C4 line) against the Python restatement (same documents read) and the scan."""
+    from dataclasses import replace
+    seg, st, a, cols = c4
+    q = parse_query(sql, num_groups_limit=10 ** 9)
+    star_seg = replace(seg)
+    star_seg.star_arrays = a
+    got = oracle.run_groupby(SC.C4_SCHEMA, [star_seg], q, use_star_tree=True)
+    exp_star, docs, scanned = SC.startree_answer(oracle, seg, SC.C4_SCHEMA, a, q, SC.C4_SPLIT, SC.C4_PAIRS)
+    scan = oracle.run_groupby(SC.C4_SCHEMA, [seg], q)
+    assert got.stats[0] == docs and got.stats[1] == scanned  # same documents and residual entries
+    assert got.stats[3] == seg.num_docs
+    for exp in (exp_star, scan.groups):
+        assert set(got.groups) == set(exp)
+        for k, ev in exp.items():
+            for (fn, col), g, e in zip(q.aggregations, got.groups[k], ev):
+                if fn == "AVG":
+                    assert g.count == e.count and g.sum == pytest.approx(e.sum, rel=1e-12)
+                elif col == "md" or fn == "SUM":
+                    assert g == pytest.approx(e, rel=1e-9, abs=1e-6)
+                else:
+                    assert g == e, (k, fn)
+    # a query the tree does not fit (no min__md pair) runs the scan
+    q2 = parse_query("SELECT MIN(md) FROM t GROUP BY d1", num_groups_limit=10 ** 9)
+    assert oracle.run_groupby(SC.C4_SCHEMA, [star_seg], q2, use_star_tree=True).stats == \
+        oracle.run_groupby(SC.C4_SCHEMA, [seg], q2).stats

@@ -487,16 +487,16 @@ def main():
         phases["decode"] += dec_us * 1e-6
         return res, k_us
 
-    def run(n, depth, keep_all=False):
+    def run(n, depth, keep=1):
         """n queries, at most `depth` in flight; returns (results, kernel timings) in query order.  Only the first
-        result is kept unless keep_all (--verify): a server hands each result on and frees it, and holding hundreds
-        of them (C5: 51 MB of pinned host memory each) would starve the result buffer pool."""
+        `keep` results are kept (all with --verify): a server hands each result on and frees it, and holding more of
+        them (C5: 51 MB of pinned host memory each) would grow the result buffer pool inside the timed region."""
         from collections import deque
         pending, res, kus = deque(), [], []
 
         def done(item):
             r, k = complete(item)
-            if keep_all or not res:
+            if keep is None or len(res) < keep:
                 res.append(r)
             kus.append(k)
 
@@ -508,28 +508,35 @@ def main():
             done(pending.popleft())
         return res, kus
 
+    import gc
+    # as timeit does: a collector pass inside a sub-millisecond step is the harness's cost, not the query's.  Collected
+    # before the warm-up, so the GPU does not sit idle between the warm-up and the timed region (an idle gap lets the
+    # clocks drop, and the first timed queries pay the ramp).
+    gc.collect()
+    gc.disable()
     first = None
+    ngroups = 0
     if args.warmup:
         first = run(args.warmup, inflight)[0][0]
+        ngroups = len(first)
+        if not args.verify:
+            first = None  # its pinned buffer back to the pool: the timed region holds no result
     for k in phases:
         phases[k] = 0.0
-    import gc
-    gc.collect()
-    gc.disable()  # as timeit does: a collector pass inside a sub-millisecond step is the harness's cost, not the query's
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     del trace[:]
     t0 = time.perf_counter()
-    timed, _ = run(args.steps, inflight, keep_all=args.verify)
-    timed_trace = [[r[0]] + [round((x - t0) * 1e6, 1) for x in r[1:]] for r in trace]
+    timed, _ = run(args.steps, inflight, keep=None if args.verify else (0 if args.warmup else 1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    timed_trace = [[r[0]] + [round((x - t0) * 1e6, 1) for x in r[1:]] for r in trace[:args.steps]]
     if args.step_trace and rank == 0:
         with open(args.step_trace, "w") as f:
             json.dump({"elapsed_us": elapsed * 1e6, "queries": timed_trace,
@@ -541,13 +548,13 @@ def main():
             assert got.keys() == ref.keys(), "groups differ between steps"
             for k, v in got.items():
                 assert all(x == y or abs(x - y) <= 1e-9 * max(abs(x), abs(y)) for x, y in zip(v, ref[k])), k
-    if first is None and timed:
-        first = timed[0]
+    if not args.warmup and timed:
+        ngroups = len(timed[0])
+    del timed, first
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    ngroups = len(first) if first is not None else 0
     if sharded:  # disjoint per-rank shards: the query's groups are their sum
         g = torch.tensor([ngroups], dtype=torch.int64)
         dist.all_reduce(g)

@@ -4955,6 +4955,7 @@ int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kind
   if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
   uint32_t conv = 0;
   TRY(check_kinds(r->slot_kind, kinds, &conv));
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));
   const int nk = r->num_keys, ns = r->num_slots, w = nk + ns;
   std::vector<int32_t> owner((size_t)r->n);
   std::vector<int64_t> off(nparts + 1, 0), ids(std::max(nk, 1));
@@ -5353,7 +5354,7 @@ int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) {
   if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
   pgpu::Comm* C = c->impl;
   const int N = C->nranks, me = C->rank;
-  TRY(pgpu::result_expand(r));
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));
   // agree on the slot kinds; the group ids index the ranks' dictionary snapshots, which must be the same
   std::vector<int64_t> mine(CI_WORDS, 0), all((size_t)N * CI_WORDS, 0);
   uint64_t h = 0x84222325cbf29ce4ull;
@@ -5491,6 +5492,7 @@ int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_
 int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
   PGPU_ABI_GUARD;
   if (!r || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   const int nk = r->num_keys;
   for (int j = 0; j < nk; ++j) {
     const int32_t* g = r->gid(j);
@@ -5501,18 +5503,21 @@ int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
 int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out) {
   PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->n) memcpy(out, r->gid(key), (size_t)r->n * 4);
   return 0;
 }
 int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out) {
   PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   *out = r->gid(key);
   return 0;
 }
 int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form) {
   PGPU_ABI_GUARD;
   if (!r || agg < -1 || agg >= r->num_aggs || !out || !form) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (agg == -1) {  // the COUNT slot (AvgPair.count of every AVG)
     *out = r->slot(0);
     *form = RCONV_I64;
@@ -5525,6 +5530,7 @@ int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t
 int pgpu_result_values(pgpu_result r, int agg, double* out) {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   const uint64_t* w = r->slot(r->agg_slot[agg]);
   switch (r->agg_conv[agg]) {
     case RCONV_I64: for (int64_t i = 0; i < r->n; ++i) out[i] = (double)(int64_t)w[i]; break;
@@ -5536,12 +5542,14 @@ int pgpu_result_values(pgpu_result r, int agg, double* out) {
 int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->n) memcpy(out, r->slot(0), (size_t)r->n * 8);  // slot 0 = COUNT = AvgPair.count
   return 0;
 }
 int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->agg_conv[agg] != RCONV_I64) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
   if (r->n) memcpy(out, r->slot(r->agg_slot[agg]), (size_t)r->n * 8);
   return 0;

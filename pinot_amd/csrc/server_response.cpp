@@ -329,6 +329,8 @@ extern "C" {
 int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* out) {
   if (!r || !spec || !out || spec->num_order_by < 0 || (spec->num_order_by && !spec->order_by) || spec->limit < 0)
     return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire))
+    if (const int rc = pgpu::result_expand(r)) return rc;  // compact results: columnar form first
   for (int i = 0; i < spec->num_order_by; ++i) {
     const pgpu_order_by& o = spec->order_by[i];
     const int lim = o.kind == PGPU_ORDER_GROUP_BY ? r->num_keys : r->num_aggs;
@@ -359,6 +361,8 @@ int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* 
 int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, int64_t* rows, int64_t cap,
                          int64_t* counts) {
   if (!r || !counts || limit <= 0) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire))
+    if (const int rc = pgpu::result_expand(r)) return rc;  // compact results: columnar form first
   // AggregationGroupByTrimmingService: trimSize = max(limit * 5, 5000), applied past 4 x trimSize groups;
   // trimFinalResults (broker): the top `limit` of each function
   const int64_t trim = final_results ? limit : std::max<int64_t>((int64_t)limit * 5, 5000);
@@ -383,6 +387,8 @@ int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, in
 
 int pgpu_result_datatable(pgpu_result r, pgpu_table t, void* out, int64_t cap, int64_t* len) {
   if (!r || !t || !len) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (r->compact.load(std::memory_order_acquire))
+    if (const int rc = pgpu::result_expand(r)) return rc;  // compact results: columnar form first
   const int nk = r->num_keys, na = r->num_aggs, nc = nk + na;
   std::vector<DictView> dv(nk);
   std::vector<std::string> names, types;

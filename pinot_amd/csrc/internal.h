@@ -222,6 +222,10 @@ struct KPartParams {
   // cshift + pshift bits (pack_bits of them) and writes no mid_val; K8e unpacks -- 4 bytes per record instead of 8
   int32_t pack_bits;
   int64_t pack_min;
+  // 1 (pack_bits > 0 and pshift + pack_bits <= 32): K8e writes the final records packed the same way -- the key
+  // within its partition in the low pshift bits, (value - pack_min) above -- as u32 words at rec_val, and K8d
+  // unpacks them: 4 bytes per record instead of 6 (u16 key + u32 value) in K8e's write and K8d's read
+  int32_t fine_pack;
 };
 
 // K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).

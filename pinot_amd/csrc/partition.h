@@ -311,6 +311,12 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
                                                : pp.mid_val[s * pp.rec_cap + r];
     }
     __syncthreads();
+    if (pp.fine_pack) {  // one u32 per record: key | (value - pack_min) << pshift
+      uint32_t* __restrict__ r32 = reinterpret_cast<uint32_t*>(pp.rec_val);
+      for (uint32_t i = tid; i < n; i += kBlock)
+        r32[spos[i]] = (uint32_t)skey[i] | ((uint32_t)((int64_t)sval[i] - pp.pack_min) << pp.pshift);
+      continue;
+    }
     for (uint32_t i = tid; i < n; i += kBlock) {  // in bucket order: runs of consecutive positions
       const uint32_t pos = spos[i];
       pp.rec_key[pos] = skey[i];
@@ -345,8 +351,22 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
       const uint32_t r = base + b * kBlock;
       ri[b] = r < r1 ? r : r0;
     }
+    int64_t pv[NB];  // fine_pack: the records' values
+    if (pp.fine_pack) {
+      const uint32_t* __restrict__ r32 = reinterpret_cast<const uint32_t*>(pp.rec_val);
+      const uint32_t low = (1u << pp.pshift) - 1u;
+      uint32_t wr[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) k[b] = pp.rec_key[ri[b]];
+      for (int b = 0; b < NB; ++b) wr[b] = r32[ri[b]];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        k[b] = (int)(wr[b] & low);
+        pv[b] = pp.pack_min + (int64_t)(wr[b] >> pp.pshift);
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) k[b] = pp.rec_key[ri[b]];
+    }
     for (int s = 0; s < ns; ++s) {
       const int kind = p.slot_kind[s];
       const int st = pp.slot_stream[s];
@@ -354,6 +374,9 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
       if (st < 0) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) w[b] = 0ull;
+      } else if (pp.fine_pack) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) w[b] = (uint64_t)pv[b];
       } else if (pp.val32) {
         const int32_t* __restrict__ r32 = reinterpret_cast<const int32_t*>(pp.rec_val) + (int64_t)st * pp.rec_cap;
 #pragma unroll

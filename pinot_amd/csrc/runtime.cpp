@@ -3117,6 +3117,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       if ((P->part_pack_range >> vb) == 0) {
         pp.pack_bits = std::max(vb, 1);
         pp.pack_min = P->part_pack_min;
+        static const bool no_fine = getenv_flag("PGPU_NO_FINE_PACK");  // A/B: 6-byte final records
+        pp.fine_pack = !no_fine && pp.pshift + pp.pack_bits <= 32 && pp.num_streams == 1 ? 1 : 0;
       }
     }
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))

@@ -226,6 +226,11 @@ struct KPartParams {
   // within its partition in the low pshift bits, (value - pack_min) above -- as u32 words at rec_val, and K8d
   // unpacks them: 4 bytes per record instead of 6 (u16 key + u32 value) in K8e's write and K8d's read
   int32_t fine_pack;
+  // 1 (fine_pack, slots exactly COUNT + integer SUM of the stream): K8d adds (1 << 40) | (value - pack_min) into one
+  // LDS word per key instead of two atomics, where the partition's records bound both halves (count < 2^24, the
+  // sum of offsets < 2^40: pack_range x records); the word is split when the slice is stored
+  int32_t cs_pack;
+  int64_t pack_range;
 };
 
 // K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).

@@ -340,6 +340,35 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   for (int i = tid; i < ns * PR; i += kBlock) lds[i] = slot_init(p.slot_kind[i / PR]);
   __syncthreads();
   const uint32_t r0 = pp.part_start[blockIdx.x], r1 = pp.part_start[blockIdx.x + 1];
+  // COUNT + SUM in one LDS word per key when this partition's records bound both halves (uniform per workgroup)
+  if (pp.cs_pack && (r1 - r0) < (1u << 24) && (uint64_t)(r1 - r0) * (uint64_t)pp.pack_range < (1ull << 40)) {
+    constexpr int NB = 16;
+    const uint32_t* __restrict__ r32 = reinterpret_cast<const uint32_t*>(pp.rec_val);
+    const uint32_t low = (1u << pp.pshift) - 1u;
+    unsigned long long* w64 = reinterpret_cast<unsigned long long*>(lds);  // slot 0's words
+    for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
+      uint32_t wr[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t r = base + b * kBlock;
+        wr[b] = r32[r < r1 ? r : r0];
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (base + b * kBlock < r1) atomicAdd(w64 + (wr[b] & low), (1ull << 40) | (unsigned long long)(wr[b] >> pp.pshift));
+    }
+    __syncthreads();
+    const int64_t G = p.num_keys_total;
+    const int64_t k0 = (int64_t)blockIdx.x * PR;
+    const int n = (int)(G - k0 < PR ? G - k0 : PR);
+    for (int i = tid; i < n; i += kBlock) {
+      const uint64_t w = lds[i];
+      const uint64_t cnt = w >> 40;
+      p.table[k0 + i] = cnt;                                                              // COUNT (slot 0)
+      p.table[G + k0 + i] = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)cnt * pp.pack_min);  // SUM
+    }
+    return;
+  }
   // Two workgroups per CU (the LDS table), so latency is hidden by loads in flight per lane: NB records per lane
   // per step, every load issued unconditionally (records past r1 re-read record r0 and are not accumulated).
   constexpr int NB = 16;

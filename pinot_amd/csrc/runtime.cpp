@@ -3119,6 +3119,10 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
         pp.pack_min = P->part_pack_min;
         static const bool no_fine = getenv_flag("PGPU_NO_FINE_PACK");  // A/B: 6-byte final records
         pp.fine_pack = !no_fine && pp.pshift + pp.pack_bits <= 32 && pp.num_streams == 1 ? 1 : 0;
+        static const bool no_cs = getenv_flag("PGPU_NO_CS_PACK");  // A/B: two LDS atomics per record
+        pp.cs_pack = pp.fine_pack && !no_cs && nslots == 2 && P->slot_kind[0] == SLOT_COUNT &&
+                     P->slot_kind[1] == SLOT_SUM_I64 && P->slot_stream[1] == 0 ? 1 : 0;
+        pp.pack_range = P->part_pack_range;
       }
     }
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))

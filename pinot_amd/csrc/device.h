@@ -293,6 +293,11 @@ __device__ __forceinline__ uint64_t slot_init(int kind) {
   if (kind == SLOT_MAX_KEY) return (uint64_t)INT64_MIN;
   return 0ull;
 }
+// An LDS table word's start value (KParams.narrow: 32-bit min / max on the low half).
+__device__ __forceinline__ uint64_t slot_init_lds(int kind, bool narrow) {
+  if (narrow) return kind == SLOT_MIN_KEY ? 0xFFFFFFFFull : 0ull;
+  return slot_init(kind);
+}
 
 // Leaf descriptors of the current segment held in registers (reloaded only when the segment changes).
 struct LeafReg {
@@ -633,25 +638,39 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
 // same with 32 or 64 lanes active.  Global tables keep the branches (a neutral global atomic is real traffic).
 template <int MODE>
 __device__ __forceinline__ void accumulate16_i(uint64_t* __restrict__ row, const int32_t (&key)[16], uint32_t m,
-                                               int kind, const int64_t (&v)[16]) {
+                                               int kind, const int64_t (&v)[16], bool narrow = false,
+                                               uint64_t addend = 0) {
   if (MODE == MODE_LDS) {
     unsigned long long* u = reinterpret_cast<unsigned long long*>(row);
     long long* l = reinterpret_cast<long long*>(row);
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(row);  // narrow: the word's low half (little-endian)
     switch (kind) {
       case SLOT_SUM_I64:
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) atomicAdd(u + key[i], (unsigned long long)v[i]);
+          if ((m >> i) & 1u) atomicAdd(u + key[i], (unsigned long long)v[i] + addend);
         break;
       case SLOT_MIN_KEY:
+        if (narrow) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) atomicMin(l + key[i], (long long)v[i]);
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) atomicMin(w32 + 2 * key[i], (uint32_t)v[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) atomicMin(l + key[i], (long long)v[i]);
+        }
         break;
       default:
+        if (narrow) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((m >> i) & 1u) atomicMax(l + key[i], (long long)v[i]);
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) atomicMax(w32 + 2 * key[i], (uint32_t)v[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u) atomicMax(l + key[i], (long long)v[i]);
+        }
         break;
     }
   } else {
@@ -725,7 +744,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     if (kind == SLOT_COUNT) {
       uint64_t* __restrict__ row = tbl + (int64_t)s * G;
       if (G == 1) accumulate_wave(row, SLOT_COUNT, __popc(m), 0, 0.0);
-      else accumulate16_count<MODE>(row, key, m);
+      else if (MODE != MODE_LDS || p.pack_slot < 0) accumulate16_count<MODE>(row, key, m);  // else: with the sum
       ++s;
       continue;
     }
@@ -767,7 +786,9 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
           accumulate_wave(row, kr, __popc(m), acc, 0.0);
           continue;
         }
-        accumulate16_i<MODE>(row, key, m, kr, v);
+        // KParams.pack_slot: the COUNT rides in the high bits of the sum; narrow: 32-bit min / max
+        accumulate16_i<MODE>(row, key, m, kr, v, MODE == MODE_LDS && ((p.narrow >> r) & 1u),
+                             MODE == MODE_LDS && r == p.pack_slot ? (1ull << 40) : 0ull);
       }
     }
     if (need_f) {

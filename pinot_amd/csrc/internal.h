@@ -108,6 +108,15 @@ struct KParams {
   int32_t num_slots;
   int32_t slot_kind[kMaxSlots];
   int32_t slot_col[kMaxSlots];
+  // Dense LDS tables (MODE_LDS, dense instance), set at plan time where the plan's value ranges allow:
+  // pack_slot >= 0: an integer SUM slot whose whole-group adds carry the COUNT too -- (1 << 40) | value in one LDS
+  //   atomic (values >= 0, a workgroup's docs < 2^24 and their sum < 2^40); the kernel splits the word into the COUNT
+  //   row (slot 0) and the sum before it stores its slab.
+  // narrow (bit s): MIN / MAX slot s of an integer column with values in [0, 2^32 - 1): the whole-group path takes
+  //   32-bit LDS min / max on the word's low half (the word starts at 2^32 - 1 / 0, so the 64-bit atomics of the
+  //   per-doc path see the same order).
+  int32_t pack_slot;
+  uint32_t narrow;
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
   unsigned long long* hash_keys;  // [num_keys_total] (MODE_HASH), empty = ~0

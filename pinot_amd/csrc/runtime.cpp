@@ -2816,6 +2816,38 @@ int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
 // ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
 // (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
+// KParams.pack_slot / narrow of a dense LDS plan, from the value ranges of its integer columns in every segment
+// (sorted dictionaries: first and last entries; raw columns: their decoded range) and a bound on the docs one
+// workgroup of the launch can aggregate (its tiles under either tile order).  PGPU_NO_DENSE_NARROW=1: neither (A/B).
+void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow) {
+  *pack_slot = -1;
+  *narrow = 0;
+  static const bool off = getenv_flag("PGPU_NO_DENSE_NARROW");
+  if (off || !P->dense || P->mode != MODE_LDS || P->num_keys <= 1 || !P->star.empty() || P->grid <= 0) return;
+  const int64_t tiles = std::max<int64_t>(P->num_tiles, P->tile_bound);
+  const int64_t wg_docs = ((tiles + P->grid - 1) / P->grid + 2) * kTileDocs;
+  for (size_t s = 0; s < P->slot_kind.size() && s < 32; ++s) {
+    const int kind = P->slot_kind[s], c = P->slot_tcol[s];
+    if ((kind != SLOT_SUM_I64 && kind != SLOT_MIN_KEY && kind != SLOT_MAX_KEY) || c < 0 || c == kDocIdColumn) continue;
+    if (!is_int_type(P->table->types[c])) continue;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    bool known = true;
+    for (const Segment* seg : P->segs) {
+      const Column& col = seg->cols[c];
+      if (col.raw) { lo = std::min(lo, col.raw_min); hi = std::max(hi, col.raw_max); }
+      else if (!col.dict.iv.empty()) { lo = std::min(lo, col.dict.iv.front()); hi = std::max(hi, col.dict.iv.back()); }
+      else if (col.dict.size() != 0) { known = false; break; }
+    }
+    if (!known || lo > hi || lo < 0) continue;
+    if (kind != SLOT_SUM_I64) {
+      if (hi < INT64_C(0xFFFFFFFF)) *narrow |= 1u << s;
+    } else if (*pack_slot < 0 && P->slot_kind[0] == SLOT_COUNT && wg_docs < (INT64_C(1) << 24) &&
+               (long double)wg_docs * (long double)hi < 0x1p40L) {
+      *pack_slot = (int32_t)s;
+    }
+  }
+}
+
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X) {
   X.t_start = trace_on() ? now_us() : 0;
   if (cancelled(P)) return cancel_fail();  // nothing is launched for a cancelled query
@@ -2917,6 +2949,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   P->d_table_used = table;
   KParams& kp = X.kp;
   memset(&kp, 0, sizeof kp);
+  kp.pack_slot = -1;
   kp.deadline = deadline;
   kp.seg_stride = P->seg_stride;
   kp.num_cols = (int)P->query_cols.size();
@@ -2944,6 +2977,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   }
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
+  dense_lds_forms(P, &kp.pack_slot, &kp.narrow);
   kp.stats = stats;
   if (P->leap_reserved) {  // one byte per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
     TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *
@@ -5624,6 +5658,7 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
       hipMemcpyAsync(sc->sets.p, P->set_words.data(), P->set_words.size() * 4, hipMemcpyHostToDevice, t->stream);
     KParams kp;
     memset(&kp, 0, sizeof kp);
+    kp.pack_slot = -1;
     kp.segs = sc->segrec.as<uint8_t>();
     kp.seg_stride = P->seg_stride;
     kp.num_cols = (int)P->query_cols.size();

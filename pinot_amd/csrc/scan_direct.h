@@ -76,7 +76,10 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
   if (p.deadline && p.stats[5]) return;
 
   if (MODE == MODE_LDS) {
-    for (int64_t i = tid; i < table_words; i += kBlock) lds[i] = slot_init(p.slot_kind[i / G]);
+    for (int64_t i = tid; i < table_words; i += kBlock) {
+      const int s = (int)(i / G);
+      lds[i] = slot_init_lds(p.slot_kind[s], DENSE && ((p.narrow >> s) & 1u));
+    }
     __syncthreads();
   }
   uint64_t* tbl = (MODE == MODE_LDS) ? lds : p.table;
@@ -233,6 +236,16 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
 #endif
 
   if (MODE == MODE_LDS) {
+    if (DENSE && p.pack_slot >= 0) {  // split the packed words: COUNT (slot 0) += high bits, the sum keeps the low
+      __syncthreads();
+      uint64_t* ps = lds + (int64_t)p.pack_slot * G;
+      for (int64_t k = tid; k < G; k += kBlock) {
+        const uint64_t w = ps[k];
+        lds[k] += w >> 40;
+        ps[k] = w & ((1ull << 40) - 1);
+      }
+      __syncthreads();
+    }
     uint64_t* out = p.slab + (int64_t)blockIdx.x * table_words;
     for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
   }

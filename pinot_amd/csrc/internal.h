@@ -324,6 +324,12 @@ int launch_exchange_scatter(const uint64_t* table, const unsigned long long* has
                             int32_t num_slots, int32_t nparts, uint32_t conv, unsigned long long* cursor, uint64_t* out,
                             void* stream);
 int launch_i64_to_f64(uint64_t* p, int64_t n, void* stream);
+// k_hashsort.hip: hash-mode finalize on the device (radix sort of the compacted records by key, decode to columns).
+int hash_sort_temp_bytes(int64_t n, int key_bits, size_t* bytes);
+int launch_hash_sort_decode(const uint64_t* rec, int64_t n, int32_t num_slots, int32_t num_keys, const int64_t* stride,
+                            const int64_t* card, const int64_t* off, int key_bits, void* tmp, size_t temp_bytes,
+                            uint64_t* keys_a, uint64_t* keys_b, uint32_t* idx_a, uint32_t* idx_b, uint8_t* out,
+                            size_t slot_off, void* stream);
 int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
                          unsigned long long* hash_keys, int64_t num_keys, void* stream);
 // Compact form of a large dense table: counts per chunk + exclusive scan (total into *total) + each slot's range over

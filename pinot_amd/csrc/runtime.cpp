@@ -529,6 +529,7 @@ struct Scratch {
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
   DevBuf xcursor;                       // cross-GPU exchange: per-owner record cursors
   DevBuf xsend, xrecv, xshard;          // pgpu_plan_combine: exported / received records, the reduce-scattered shard
+  DevBuf hsort;                         // hash-mode finalize: sort keys / indexes, decoded columns, sort temp
   HostPinned xstage;                    // their initial values (pinned: the upload is asynchronous)
   // Pinned staging: `stage` is the source of the execution's asynchronous uploads (records, bitsets); `readback`
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
@@ -556,7 +557,7 @@ struct Scratch {
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release(); stage_keys.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
-    xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release();
+    xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release(); hsort.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -3447,12 +3448,45 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     star_scanned = st[2] + st[3];
     P->star_docs_read = (int64_t)st[4];
     if (P->groups_seen && P->merged_records < 0) P->groups_seen->store(n, std::memory_order_relaxed);
-    if (n > 0) {
+    static const bool host_sort = getenv_flag("PGPU_HASH_HOST_SORT");  // A/B: sort and decode on the host
+    if (n >= 4096 && P->stage_end.empty() && !host_sort) {
+      // sorted by key and decoded into the columnar result on the device (k_hashsort.hip): one copy back
+      int key_bits = 1;
+      {
+        const long double space = (long double)P->key_stride[nk - 1] * (long double)P->key_card[nk - 1];
+        while (key_bits < 64 && (long double)(INT64_C(1) << key_bits) < space) ++key_bits;
+      }
+      size_t tmp_bytes = 0;
+      if (hash_sort_temp_bytes(n, key_bits, &tmp_bytes))
+        return fail(PGPU_ERR_DEVICE, "hash sort sizing failed: %s", hipGetErrorString(hipGetLastError()));
+      const size_t slot_off = pgpu_result_s::slot_offset(nk, n);
+      const size_t out_bytes = slot_off + (size_t)nslots * n * 8;
+      const size_t a = ((size_t)n * 8 + 255) & ~size_t(255), b = ((size_t)n * 4 + 255) & ~size_t(255);
+      const size_t ob = (out_bytes + 255) & ~size_t(255);
+      TRY(sc->hsort.ensure(2 * a + 2 * b + ob + tmp_bytes + 256));
+      uint8_t* base = sc->hsort.as<uint8_t>();
+      uint64_t* keys_a = reinterpret_cast<uint64_t*>(base);
+      uint64_t* keys_b = reinterpret_cast<uint64_t*>(base + a);
+      uint32_t* idx_a = reinterpret_cast<uint32_t*>(base + 2 * a);
+      uint32_t* idx_b = reinterpret_cast<uint32_t*>(base + 2 * a + b);
+      uint8_t* out = base + 2 * a + 2 * b;
+      if (launch_hash_sort_decode(sc->ckeys.as<uint64_t>(), n, nslots, nk, P->key_stride.data(), P->key_card.data(),
+                                  P->key_off.data(), key_bits, out + ob, tmp_bytes, keys_a, keys_b, idx_a, idx_b, out,
+                                  slot_off, stream))
+        return fail(PGPU_ERR_DEVICE, "hash sort / decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+      TRY(R->alloc(nk, nslots, n));
+      HIP_TRY(hipMemcpyAsync(R->buf.p, out, out_bytes, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      n = -1;  // decoded
+    } else if (n > 0) {
       TRY(sc->readback.ensure((size_t)n * rec * 8));
       st = reinterpret_cast<uint64_t*>(sc->readback.p);
       HIP_TRY(hipMemcpyAsync(st, sc->ckeys.p, (size_t)n * rec * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
     }
+    if (n < 0) {
+      n = R->n;
+    } else {
     std::vector<uint64_t> stages;  // ARRAY_MAP: the stage tables (slot -> that group's key), back to back
     std::vector<int64_t> stage_off;
     if (!P->stage_end.empty() && n > 0) {
@@ -3484,6 +3518,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
         decode_keys(P, R, r, e[0]);
       }
       for (int s = 0; s < nslots; ++s) R->slot(s)[r] = e[1 + s];
+    }
     }
   }
   const double t_sync2 = trace_on() ? now_us() : 0;

@@ -412,7 +412,13 @@ def main():
         log("rank %d: inverted indexes built and pinned in %.1f s" % (rank, time.perf_counter() - t_inv))
     comm = None
     if world > 1:
-        comm = Communicator.from_process_group(L.COMM_HOST if backend == "host" else L.COMM_RCCL, device)
+        kind = L.COMM_HOST if backend == "host" else L.COMM_RCCL
+        try:
+            comm = Communicator.from_process_group(kind, device)
+        except L.PinotGpuError as e:  # every rank fails alike (RCCL missing / bootstrap refused): same transport
+            log("rank %d: RCCL communicator failed (%s); combining over the host transport" % (rank, e))
+            backend = "host (RCCL failed)"
+            comm = Communicator.from_process_group(L.COMM_HOST, device)
         union_dictionaries_comm(table, q.group_by, comm)
     handles = np.array(handles, dtype=np.int64)
 

@@ -264,10 +264,30 @@ class Communicator:
 
     @classmethod
     def from_process_group(cls, kind, device, group=None):
-        """Rank 0 makes the id, the process group (any backend: gloo is enough) hands it to the others."""
-        box = [cls.unique_id(kind) if dist.get_rank(group) == 0 else None]
+        """Rank 0 makes the id, the process group (any backend: gloo is enough) hands it to the others.  A failure
+        on any rank raises PinotGpuError on every rank (no rank is left waiting in a collective)."""
+        rank = dist.get_rank(group)
+        box = [None]
+        if rank == 0:
+            try:
+                box[0] = cls.unique_id(kind)
+            except L.PinotGpuError as e:
+                box[0] = ("error", str(e))
         dist.broadcast_object_list(box, src=0, group=group)
-        return cls(kind, box[0], dist.get_world_size(group), dist.get_rank(group), device)
+        if isinstance(box[0], tuple):
+            raise L.PinotGpuError(L.PGPU_ERR_DEVICE, "communicator id: " + box[0][1])
+        comm, err = None, None
+        try:
+            comm = cls(kind, box[0], dist.get_world_size(group), rank, device)
+        except L.PinotGpuError as e:
+            err = str(e)
+        errs = [None] * dist.get_world_size(group)
+        dist.all_gather_object(errs, err, group=group)
+        if any(errs):
+            if comm is not None:
+                comm.close()
+            raise L.PinotGpuError(L.PGPU_ERR_DEVICE, "communicator: " + "; ".join(e for e in errs if e))
+        return comm
 
     def close(self):
         if getattr(self, "handle", None):

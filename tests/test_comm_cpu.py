@@ -58,3 +58,56 @@ def test_comm_bad_arguments():
     assert lib.pgpu_comm_create(L.COMM_HOST, uid, 2, 2, 0, ctypes.byref(h)) == L.PGPU_ERR_INVALID_ARGUMENT
     assert lib.pgpu_comm_create(7, uid, 1, 0, 0, ctypes.byref(h)) == L.PGPU_ERR_INVALID_ARGUMENT
     assert lib.pgpu_comm_unique_id(7, uid) == L.PGPU_ERR_INVALID_ARGUMENT
+
+
+def _pg_rank(rank, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from pinot_amd.combine import Communicator, union_dictionaries_comm
+        c = Communicator.from_process_group(L.COMM_HOST, 0)
+
+        class T:  # the two table methods union_dictionaries_comm uses
+            def __init__(self, vals):
+                self.vals = vals
+
+            def dictionary(self, col):
+                return list(self.vals)
+
+            def add_dictionary_values(self, col, values):
+                self.vals = sorted(set(self.vals) | set(values))
+        t = T([3, 1, 7] if rank == 0 else [2, 7, 11])
+        union_dictionaries_comm(t, ["k"], c)
+        c.close()
+        try:  # an unknown transport fails on every rank (no rank left waiting in a collective)
+            Communicator.from_process_group(7, 0)
+            bad = "no error"
+        except L.PinotGpuError as e:
+            bad = e.message
+        q.put((rank, t.vals, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_communicator_from_process_group():
+    """bench.py's bootstrap: rank 0's id through a gloo process group, dictionary union over the communicator."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pg_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(2):
+        vals, bad = out[r]
+        assert vals == [1, 2, 3, 7, 11]
+        assert "communicator" in bad

@@ -444,6 +444,7 @@ def main():
     d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
     sharded = mode in (L.COMBINE_REDUCE_SCATTER, L.COMBINE_HASH, L.COMBINE_ROWS)  # disjoint per-rank results
 
+    trace = []  # per query: [k, launch start, launch end, finalize start, complete end] (perf_counter)
     phases = {"plan": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0, "decode": 0.0}
     star_work = [0, 0, 0]
 

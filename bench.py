@@ -441,7 +441,8 @@ def main():
     probe.close()
     # PGPU_BENCH_CALLER_TABLE=1: plans write into caller-owned device tables instead of their scratch tables
     caller_table = nkeys > 0 and os.environ.get("PGPU_BENCH_CALLER_TABLE") == "1"
-    d_tables = [torch.empty((nslots, max(nkeys, 1)), dtype=torch.int64, device="cuda") for _ in range(inflight)]
+    d_tables = [torch.empty((nslots, max(nkeys, 1)) if caller_table else (1,), dtype=torch.int64, device="cuda")
+                for _ in range(inflight)]
     sharded = mode in (L.COMBINE_REDUCE_SCATTER, L.COMBINE_HASH, L.COMBINE_ROWS)  # disjoint per-rank results
 
     trace = []  # per query: [k, launch start, launch end, finalize start, complete end] (perf_counter)

@@ -568,6 +568,17 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       accumulate_wave(tbl + s, kind, cnt, iacc, facc);
       continue;
     }
+    if (MODE == MODE_LDS && p.pack_slot >= 0) {  // KParams.pack_slot: no COUNT row; the pack slot adds both
+      if (kind == SLOT_COUNT) continue;
+      if (s == p.pack_slot) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          if (live[b])
+            atomicAdd(reinterpret_cast<unsigned long long*>(tbl + (int64_t)s * G + idx[b]),
+                      (1ull << 40) | (unsigned long long)ikey[b]);
+        continue;
+      }
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
       if (live[b]) accumulate<MODE>(tbl, (int64_t)s * G + idx[b], kind, ikey[b], dval[b]);

@@ -1143,6 +1143,8 @@ struct pgpu_plan_s {
   // with the plan cache's image and every copy of it: -1 = none yet)
   int64_t group_bound = 0;
   std::shared_ptr<std::atomic<int64_t>> groups_seen;
+  // MODE_LDS plans: KParams.pack_slot (the COUNT rides in an integer SUM's LDS word; the table has no COUNT row)
+  int32_t pack_slot = -1;
   // pgpu_plan_combine REDUCE_SCATTER: this rank's merged key range [shard_begin, shard_begin + shard_count), slot rows
   // of shard_count words at `shard`; pgpu_plan_finalize reads it
   const void* shard = nullptr;
@@ -1775,6 +1777,38 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, cons
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 
+// The slot whose LDS word also carries the COUNT (KParams.pack_slot) in an LDS-table plan, or -1: the first integer
+// SUM over a column whose values are >= 0 in every segment, when every workgroup's docs bound both halves of the word
+// (count < 2^24, sum < 2^40).  A workgroup scans at most ceil(tiles / grid) + 2 tiles under either tile order, and the
+// grid is at least min(tiles, CUs).  Not with star-tree segments (K6 keeps its own table layout).  PGPU_NO_PACK_COUNT=1:
+// never (A/B).
+int32_t lds_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int64_t G) {
+  static const bool off = getenv_flag("PGPU_NO_PACK_COUNT");
+  if (off || G <= 1 || P->slot_kind.empty() || P->slot_kind[0] != SLOT_COUNT) return -1;
+  int64_t tiles = 0;
+  for (const Segment* s : P->segs) {
+    if (s->star && !(q->options & PGPU_OPT_NO_STAR_TREE)) return -1;
+    tiles += ((int64_t)s->num_docs + kTileDocs - 1) / kTileDocs;
+  }
+  const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(tiles, t->num_cus));
+  const int64_t wg_docs = ((tiles + min_grid - 1) / min_grid + 2) * kTileDocs;
+  if (wg_docs >= (INT64_C(1) << 24)) return -1;
+  for (size_t sl = 1; sl < P->slot_kind.size(); ++sl) {
+    const int c = P->slot_tcol[sl];
+    if (P->slot_kind[sl] != SLOT_SUM_I64 || c < 0 || c == kDocIdColumn || !is_int_type(t->types[c])) continue;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    bool known = true;
+    for (const Segment* seg : P->segs) {
+      const Column& col = seg->cols[c];
+      if (col.raw) { lo = std::min(lo, col.raw_min); hi = std::max(hi, col.raw_max); }
+      else if (!col.dict.iv.empty()) { lo = std::min(lo, col.dict.iv.front()); hi = std::max(hi, col.dict.iv.back()); }
+      else if (col.dict.size() != 0) { known = false; break; }
+    }
+    if (known && lo <= hi && lo >= 0 && (long double)wg_docs * (long double)hi < 0x1p40L) return (int32_t)sl;
+  }
+  return -1;
+}
+
 // A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
 bool dict_gathers_forced() {
   static const bool on = getenv("PGPU_DICT_GATHERS") && getenv("PGPU_DICT_GATHERS")[0] == '1';
@@ -2084,15 +2118,19 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // direct kernel LDS: [table (MODE_LDS)] [filter stack (general programs)] [per-wave match queues]
   const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * 2 * kWaveQ * 4;
   for (Segment* s : P->segs) P->total_docs += s->num_docs;
-  if ((int64_t)nslots * G * 8 <= kLdsBudget) {
+  P->pack_slot = lds_pack_slot(t, P, q, G);
+  const int lds_rows = nslots - (P->pack_slot >= 0 ? 1 : 0);
+  if ((int64_t)lds_rows * G * 8 <= kLdsBudget) {
     P->mode = MODE_LDS;
     P->num_keys = G;
-    P->lds_bytes = (size_t)nslots * G * 8 + stack_bytes;
+    P->lds_bytes = (size_t)lds_rows * G * 8 + stack_bytes;
   } else if (G <= kDenseGlobalMax) {
+    P->pack_slot = -1;
     P->mode = MODE_GLOBAL;
     P->num_keys = G;
     P->lds_bytes = stack_bytes;
   } else {
+    P->pack_slot = -1;
     P->mode = MODE_HASH;
     P->hash = true;
     // Groups are bounded by the key space and, per segment, by min(its local key space, its docs): C5-style keys of
@@ -2817,19 +2855,17 @@ int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
 // ---- execution, in three phases so that plan_create can launch segment chunks while it still plans the rest
 // (streamed plans): prologue (buffers, table init, stats), one launch per chunk of segment records, epilogue
 // (star-tree kernels, slab reduce).  A plan that is not streamed is one chunk.
-// KParams.pack_slot / narrow of a dense LDS plan, from the value ranges of its integer columns in every segment
-// (sorted dictionaries: first and last entries; raw columns: their decoded range) and a bound on the docs one
-// workgroup of the launch can aggregate (its tiles under either tile order).  PGPU_NO_DENSE_NARROW=1: neither (A/B).
+// KParams.pack_slot (planned with the LDS table's rows, lds_pack_slot) and narrow of a dense LDS plan, from the value
+// ranges of its integer columns in every segment (sorted dictionaries: first and last entries; raw columns: their
+// decoded range).  PGPU_NO_DENSE_NARROW=1: no 32-bit min / max (A/B).
 void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow) {
-  *pack_slot = -1;
+  *pack_slot = P->mode == MODE_LDS ? P->pack_slot : -1;  // planned with the table layout (lds_pack_slot)
   *narrow = 0;
   static const bool off = getenv_flag("PGPU_NO_DENSE_NARROW");
   if (off || !P->dense || P->mode != MODE_LDS || P->num_keys <= 1 || !P->star.empty() || P->grid <= 0) return;
-  const int64_t tiles = std::max<int64_t>(P->num_tiles, P->tile_bound);
-  const int64_t wg_docs = ((tiles + P->grid - 1) / P->grid + 2) * kTileDocs;
   for (size_t s = 0; s < P->slot_kind.size() && s < 32; ++s) {
     const int kind = P->slot_kind[s], c = P->slot_tcol[s];
-    if ((kind != SLOT_SUM_I64 && kind != SLOT_MIN_KEY && kind != SLOT_MAX_KEY) || c < 0 || c == kDocIdColumn) continue;
+    if ((kind != SLOT_MIN_KEY && kind != SLOT_MAX_KEY) || c < 0 || c == kDocIdColumn) continue;
     if (!is_int_type(P->table->types[c])) continue;
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     bool known = true;
@@ -2840,12 +2876,7 @@ void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow)
       else if (col.dict.size() != 0) { known = false; break; }
     }
     if (!known || lo > hi || lo < 0) continue;
-    if (kind != SLOT_SUM_I64) {
-      if (hi < INT64_C(0xFFFFFFFF)) *narrow |= 1u << s;
-    } else if (*pack_slot < 0 && P->slot_kind[0] == SLOT_COUNT && wg_docs < (INT64_C(1) << 24) &&
-               (long double)wg_docs * (long double)hi < 0x1p40L) {
-      *pack_slot = (int32_t)s;
-    }
+    if (hi < INT64_C(0xFFFFFFFF)) *narrow |= 1u << s;
   }
 }
 

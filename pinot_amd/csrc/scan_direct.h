@@ -60,7 +60,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t G = p.num_keys_total;
-  const int64_t table_words = (MODE == MODE_LDS) ? (int64_t)p.num_slots * G : 0;
+  // MODE_LDS with KParams.pack_slot: no COUNT row in LDS (slot s at row s - 1; the COUNT rides in the pack slot)
+  const int lds_row0 = (MODE == MODE_LDS && p.pack_slot >= 0) ? 1 : 0;
+  const int64_t table_words = (MODE == MODE_LDS) ? (int64_t)(p.num_slots - lds_row0) * G : 0;
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds + table_words);
   // per-wave queue of sparse matches ((doc, segment) pairs), after the filter stack
   uint32_t* wq = stack + (p.pure_and ? 0 : kMaxStack * kBlock) + wave * 2 * kWaveQ;
@@ -77,12 +79,13 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
 
   if (MODE == MODE_LDS) {
     for (int64_t i = tid; i < table_words; i += kBlock) {
-      const int s = (int)(i / G);
+      const int s = (int)(i / G) + lds_row0;
       lds[i] = slot_init_lds(p.slot_kind[s], DENSE && ((p.narrow >> s) & 1u));
     }
     __syncthreads();
   }
-  uint64_t* tbl = (MODE == MODE_LDS) ? lds : p.table;
+  // slot s's row at tbl + s * G; with a packed COUNT, row 0 (tbl itself) is never addressed
+  uint64_t* tbl = (MODE == MODE_LDS) ? lds - lds_row0 * G : p.table;
 
   // XCD-aware tile order: workgroups b and b+8 share an XCD (round-robin dispatch; speed only, never correctness),
   // so XCD x sweeps its own contiguous eighth of the tile space with its workgroups side by side, one tile each.
@@ -236,18 +239,25 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
 #endif
 
   if (MODE == MODE_LDS) {
-    if (DENSE && p.pack_slot >= 0) {  // split the packed words: COUNT (slot 0) += high bits, the sum keeps the low
-      __syncthreads();
-      uint64_t* ps = lds + (int64_t)p.pack_slot * G;
-      for (int64_t k = tid; k < G; k += kBlock) {
-        const uint64_t w = ps[k];
-        lds[k] += w >> 40;
-        ps[k] = w & ((1ull << 40) - 1);
+    // the slab in the plan's full layout ([num_slots][G]): a packed word splits into the COUNT row and its sum
+    __syncthreads();
+    uint64_t* out = p.slab + (int64_t)blockIdx.x * p.num_slots * G;
+    if (lds_row0) {
+      const int ps = p.pack_slot;
+      for (int64_t i = tid; i < table_words; i += kBlock) {
+        const int s = (int)(i / G) + 1;
+        const int64_t k = i - (int64_t)(s - 1) * G;
+        const uint64_t w = lds[i];
+        if (s == ps) {
+          out[k] = w >> 40;
+          out[(int64_t)s * G + k] = w & ((1ull << 40) - 1);
+        } else {
+          out[(int64_t)s * G + k] = w;
+        }
       }
-      __syncthreads();
+    } else {
+      for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
     }
-    uint64_t* out = p.slab + (int64_t)blockIdx.x * table_words;
-    for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
   }
 }
 

@@ -22,7 +22,7 @@ for spec in ${WL:-c1:1 c2:100 c4:64 c5:100}; do
   done
   (
     for e in "${envs[@]}"; do export "$e"; done
-    timeout -k 10 ${WL_TIMEOUT:-400} python -u bench.py --workload $w --segments-per-gpu $n --steps ${STEPS:-20} --warmup 3 $PMCFLAG --host-profile "${args[@]}" > $OUT/${name}_bench.log 2>&1 || { echo "$name bench failed"; tail -5 $OUT/${name}_bench.log; exit 1; }
+    timeout -k 10 ${WL_TIMEOUT:-400} python -u bench.py --workload $w --segments-per-gpu $n --steps ${STEPS:-20} --warmup ${WARMUP:-5} $PMCFLAG --host-profile "${args[@]}" > $OUT/${name}_bench.log 2>&1 || { echo "$name bench failed"; tail -5 $OUT/${name}_bench.log; exit 1; }
     tail -1 $OUT/${name}_bench.log > $OUT/${name}_bench.json
     echo "== $name $(python -c "import json; d=json.load(open('$OUT/${name}_bench.json')); r=d['roofline'] or {}; print(d['value'], d['ms_per_step'], r.get('kernel_us'), r.get('frac'), (d['cpu_baseline'] or {}).get('value'))")"
     [ -n "$NOPROF" ] && exit 0

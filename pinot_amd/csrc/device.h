@@ -568,14 +568,14 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       accumulate_wave(tbl + s, kind, cnt, iacc, facc);
       continue;
     }
-    if (MODE == MODE_LDS && p.pack_slot >= 0) {  // KParams.pack_slot: no COUNT row; the pack slot adds both
+    if ((MODE == MODE_LDS || MODE == MODE_HASH) && p.pack_slot >= 0) {  // KParams.pack_slot: the pack slot adds both
       if (kind == SLOT_COUNT) continue;
       if (s == p.pack_slot) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
           if (live[b])
             atomicAdd(reinterpret_cast<unsigned long long*>(tbl + (int64_t)s * G + idx[b]),
-                      (1ull << 40) | (unsigned long long)ikey[b]);
+                      (1ull << p.pack_shift) | (unsigned long long)ikey[b]);
         continue;
       }
     }
@@ -799,7 +799,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
         }
         // KParams.pack_slot: the COUNT rides in the high bits of the sum; narrow: 32-bit min / max
         accumulate16_i<MODE>(row, key, m, kr, v, MODE == MODE_LDS && ((p.narrow >> r) & 1u),
-                             MODE == MODE_LDS && r == p.pack_slot ? (1ull << 40) : 0ull);
+                             MODE == MODE_LDS && r == p.pack_slot ? (1ull << kLdsPackShift) : 0ull);
       }
     }
     if (need_f) {

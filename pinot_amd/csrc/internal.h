@@ -19,6 +19,7 @@ namespace pgpu {
 constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
 constexpr int kDocsPerLane = 32;            // one lane owns a 32-doc group = `bits` u32 words
 constexpr int kTileDocs = kBlock * kDocsPerLane;  // 8192 docs per tile
+constexpr int kLdsPackShift = 40;           // KParams.pack_shift of an LDS table (COUNT < 2^24, SUM < 2^40)
 constexpr int kMaxQueryCols = 16;           // distinct columns referenced by one query
 constexpr int kMaxLeaves = 16;              // predicate leaves
 constexpr int kMaxOps = 48;                 // postfix filter program length
@@ -111,11 +112,13 @@ struct KParams {
   // Dense LDS tables (MODE_LDS, dense instance), set at plan time where the plan's value ranges allow:
   // pack_slot >= 0: an integer SUM slot whose whole-group adds carry the COUNT too -- (1 << 40) | value in one LDS
   //   atomic (values >= 0, a workgroup's docs < 2^24 and their sum < 2^40); the kernel splits the word into the COUNT
-  //   row (slot 0) and the sum before it stores its slab.
+  //   row (slot 0) and the sum before it stores its slab.  MODE_HASH: the same add, (1 << pack_shift) | value, into the
+  //   global table word (pack_shift = 64 - bits(plan docs)); hash_unpack_kernel splits the occupied words afterwards.
   // narrow (bit s): MIN / MAX slot s of an integer column with values in [0, 2^32 - 1): the whole-group path takes
   //   32-bit LDS min / max on the word's low half (the word starts at 2^32 - 1 / 0, so the 64-bit atomics of the
   //   per-doc path see the same order).
   int32_t pack_slot;
+  int32_t pack_shift;      // the COUNT's low bit in the pack slot's word (kLdsPackShift for MODE_LDS)
   uint32_t narrow;
   uint64_t* table;         // [num_slots][num_keys_total] (MODE_GLOBAL / MODE_HASH), init by table_init_kernel
   uint64_t* slab;          // [gridDim][num_slots][num_keys_total] (MODE_LDS)
@@ -293,6 +296,8 @@ struct KRawJob {
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
+int launch_hash_unpack(uint64_t* table, const unsigned long long* hash_keys, int64_t cap, int32_t pack_slot,
+                       int32_t shift, void* stream);
 int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                       unsigned long long* hash_keys, void* stream);
 // Also the deadline gate of the scan launch that follows it: sets stats[5] when `deadline` (wall_clock64 ticks,

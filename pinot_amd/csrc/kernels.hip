@@ -699,6 +699,31 @@ int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slo
   return PGPU_HIP_OK(hipGetLastError());
 }
 
+// KParams.pack_slot of a hash plan: every occupied slot's pack word holds (count << shift) | sum; split it into the
+// COUNT row (slot 0) and the SUM row so finalize, combine and compaction read the plain table layout.
+__global__ __launch_bounds__(256) void hash_unpack_kernel(uint64_t* __restrict__ table,
+                                                          const unsigned long long* __restrict__ keys, int64_t cap,
+                                                          int32_t pack_slot, int32_t shift) {
+  const uint64_t mask = (1ull << shift) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    if (keys[i] == ~0ull) continue;
+    const uint64_t w = table[(int64_t)pack_slot * cap + i];
+    table[i] = w >> shift;
+    table[(int64_t)pack_slot * cap + i] = w & mask;
+  }
+}
+
+int launch_hash_unpack(uint64_t* table, const unsigned long long* hash_keys, int64_t cap, int32_t pack_slot,
+                       int32_t shift, void* stream) {
+  if (cap <= 0) return 0;
+  if (pack_slot <= 0 || pack_slot >= kMaxSlots || shift <= 0 || shift >= 64) return -1;
+  int64_t grid = (cap + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(hash_unpack_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, cap,
+                     pack_slot, shift);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
 // One object per (kernel family, mode): k_direct.hip / k_startree.hip compiled with -DPGPU_MODE=0,1,2.
 int launch_direct_mode0(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
 int launch_direct_mode1(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);

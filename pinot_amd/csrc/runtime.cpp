@@ -1143,8 +1143,10 @@ struct pgpu_plan_s {
   // with the plan cache's image and every copy of it: -1 = none yet)
   int64_t group_bound = 0;
   std::shared_ptr<std::atomic<int64_t>> groups_seen;
-  // MODE_LDS plans: KParams.pack_slot (the COUNT rides in an integer SUM's LDS word; the table has no COUNT row)
+  // MODE_LDS / MODE_HASH plans: KParams.pack_slot (the COUNT rides in an integer SUM's word; an LDS table has no
+  // COUNT row, a hash table's is filled by hash_unpack after the scan)
   int32_t pack_slot = -1;
+  int pack_shift = kLdsPackShift;   // the COUNT's bits start here (MODE_HASH: 64 - bits(total docs))
   // pgpu_plan_combine REDUCE_SCATTER: this rank's merged key range [shard_begin, shard_begin + shard_count), slot rows
   // of shard_count words at `shard`; pgpu_plan_finalize reads it
   const void* shard = nullptr;
@@ -1777,22 +1779,17 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, cons
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 
-// The slot whose LDS word also carries the COUNT (KParams.pack_slot) in an LDS-table plan, or -1: the first integer
-// SUM over a column whose values are >= 0 in every segment, when every workgroup's docs bound both halves of the word
-// (count < 2^24, sum < 2^40).  A workgroup scans at most ceil(tiles / grid) + 2 tiles under either tile order, and the
-// grid is at least min(tiles, CUs).  Not with star-tree segments (K6 keeps its own table layout).  PGPU_NO_PACK_COUNT=1:
-// never (A/B).
-int32_t lds_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int64_t G) {
+// The slot whose table word also carries the COUNT (KParams.pack_slot), or -1: the first integer SUM over a column
+// whose values are >= 0 in every segment, when `max_count` (the most docs one word can see) bounds both halves of the
+// word -- count < 2^(64 - shift), sum < 2^shift.  Not with star-tree segments (K6 keeps its own table layout).
+// PGPU_NO_PACK_COUNT=1: never (A/B).
+int32_t pack_slot_for(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int64_t max_count,
+                      int shift) {
   static const bool off = getenv_flag("PGPU_NO_PACK_COUNT");
-  if (off || G <= 1 || P->slot_kind.empty() || P->slot_kind[0] != SLOT_COUNT) return -1;
-  int64_t tiles = 0;
-  for (const Segment* s : P->segs) {
+  if (off || P->slot_kind.empty() || P->slot_kind[0] != SLOT_COUNT || shift <= 0 || shift >= 64) return -1;
+  if (max_count >= (INT64_C(1) << (64 - shift))) return -1;
+  for (const Segment* s : P->segs)
     if (s->star && !(q->options & PGPU_OPT_NO_STAR_TREE)) return -1;
-    tiles += ((int64_t)s->num_docs + kTileDocs - 1) / kTileDocs;
-  }
-  const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(tiles, t->num_cus));
-  const int64_t wg_docs = ((tiles + min_grid - 1) / min_grid + 2) * kTileDocs;
-  if (wg_docs >= (INT64_C(1) << 24)) return -1;
   for (size_t sl = 1; sl < P->slot_kind.size(); ++sl) {
     const int c = P->slot_tcol[sl];
     if (P->slot_kind[sl] != SLOT_SUM_I64 || c < 0 || c == kDocIdColumn || !is_int_type(t->types[c])) continue;
@@ -1804,9 +1801,31 @@ int32_t lds_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_qu
       else if (!col.dict.iv.empty()) { lo = std::min(lo, col.dict.iv.front()); hi = std::max(hi, col.dict.iv.back()); }
       else if (col.dict.size() != 0) { known = false; break; }
     }
-    if (known && lo <= hi && lo >= 0 && (long double)wg_docs * (long double)hi < 0x1p40L) return (int32_t)sl;
+    if (known && lo <= hi && lo >= 0 && (long double)max_count * (long double)hi < ldexpl(1.0L, shift))
+      return (int32_t)sl;
   }
   return -1;
+}
+
+// LDS-table plans (shift 40): a workgroup scans at most ceil(tiles / grid) + 2 tiles under either tile order, and the
+// grid is at least min(tiles, CUs).
+int32_t lds_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int64_t G) {
+  if (G <= 1) return -1;
+  int64_t tiles = 0;
+  for (const Segment* s : P->segs) tiles += ((int64_t)s->num_docs + kTileDocs - 1) / kTileDocs;
+  const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(tiles, t->num_cus));
+  const int64_t wg_docs = ((tiles + min_grid - 1) / min_grid + 2) * kTileDocs;
+  return pack_slot_for(t, P, q, wg_docs, kLdsPackShift);
+}
+
+// Hash-table plans: one word sees at most every doc of the plan, so the COUNT takes bits(total_docs) high bits; the
+// scan's adds stay packed and hash_unpack splits the occupied words after it (exec_epilogue).  Single-stage keys only.
+int32_t hash_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int* shift) {
+  if (!P->stage_end.empty() || P->total_docs <= 0) return -1;
+  int bits = 0;
+  while (bits < 63 && (INT64_C(1) << bits) <= P->total_docs) ++bits;
+  *shift = 64 - bits;
+  return pack_slot_for(t, P, q, P->total_docs, *shift);
 }
 
 // A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
@@ -2130,9 +2149,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     P->num_keys = G;
     P->lds_bytes = stack_bytes;
   } else {
-    P->pack_slot = -1;
     P->mode = MODE_HASH;
     P->hash = true;
+    P->pack_slot = hash_pack_slot(t, P, q, &P->pack_shift);
     // Groups are bounded by the key space and, per segment, by min(its local key space, its docs): C5-style keys of
     // small per-segment cardinalities need far fewer slots than 2 x docs.  A cached plan re-sizes from the group
     // count its last execution found (hash_capacity, plan_cache_get): same query, same segments, same groups.
@@ -2859,7 +2878,7 @@ int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
 // ranges of its integer columns in every segment (sorted dictionaries: first and last entries; raw columns: their
 // decoded range).  PGPU_NO_DENSE_NARROW=1: no 32-bit min / max (A/B).
 void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow) {
-  *pack_slot = P->mode == MODE_LDS ? P->pack_slot : -1;  // planned with the table layout (lds_pack_slot)
+  *pack_slot = P->mode == MODE_LDS || P->mode == MODE_HASH ? P->pack_slot : -1;  // planned with the table layout
   *narrow = 0;
   static const bool off = getenv_flag("PGPU_NO_DENSE_NARROW");
   if (off || !P->dense || P->mode != MODE_LDS || P->num_keys <= 1 || !P->star.empty() || P->grid <= 0) return;
@@ -3010,6 +3029,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   dense_lds_forms(P, &kp.pack_slot, &kp.narrow);
+  kp.pack_shift = P->pack_shift;
   kp.stats = stats;
   if (P->leap_reserved) {  // one byte per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
     TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *
@@ -3303,6 +3323,9 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     }
     X.leap_nsegs = 0;
   }
+  if (P->mode == MODE_HASH && kp.pack_slot >= 0 &&
+      launch_hash_unpack(X.table, kp.hash_keys, P->num_keys, kp.pack_slot, kp.pack_shift, stream))
+    return fail(PGPU_ERR_DEVICE, "hash unpack launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (X.leap_nsegs > 0 &&  // deferred but no fold ran (cannot happen for a plan with scan tiles; kept exact)
       launch_leap2_compose(X.leap_segs, P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream))
     return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));

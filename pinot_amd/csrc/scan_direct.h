@@ -249,8 +249,8 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
         const int64_t k = i - (int64_t)(s - 1) * G;
         const uint64_t w = lds[i];
         if (s == ps) {
-          out[k] = w >> 40;
-          out[(int64_t)s * G + k] = w & ((1ull << 40) - 1);
+          out[k] = w >> kLdsPackShift;
+          out[(int64_t)s * G + k] = w & ((1ull << kLdsPackShift) - 1);
         } else {
           out[(int64_t)s * G + k] = w;
         }

@@ -1,0 +1,4 @@
+#!/bin/bash
+# r04 profiles, part 2: C4 (star-tree and scan paths), C5 (partitioned), C5 through the hash table.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+WL="${WL:-c4:64 c4:64:scan:--no-star-tree c5:100 c5_hash:100}" PMC=1 WL_TIMEOUT=600 bash scripts/gpu_profiles.sh

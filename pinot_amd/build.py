@@ -91,5 +91,45 @@ def build_tools():
     return out
 
 
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-Xarch_host",
+             "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer"]
+FUZZ_PATH = os.path.join(ROOT, "build", "host_fuzz")
+
+
+def build_host_fuzz(force=False):
+    """build/host_fuzz: tools/host_fuzz.cpp linked with every library source compiled for the host only under
+    AddressSanitizer + UndefinedBehaviorSanitizer (host-only flags: the device code is compiled as usual, and the
+    harness calls pure host entry points, never a kernel).  Rebuilt when a source is newer than the binary."""
+    src = os.path.join(ROOT, "tools", "host_fuzz.cpp")
+    if not force and os.path.exists(FUZZ_PATH) and \
+            all(os.path.getmtime(f) <= os.path.getmtime(FUZZ_PATH) for f in _inputs() + [src]):
+        return FUZZ_PATH
+    hipcc = _hipcc()
+    flags = ["--offload-arch=" + ARCH, "-O1", "-g", "-std=c++17", "-fPIC",
+             "-I" + os.path.join(ROOT, "include")] + SAN_FLAGS
+    objdir = os.path.join(ROOT, "build", "obj_san")
+    os.makedirs(objdir, exist_ok=True)
+    jobs = [(os.path.join(CSRC, s), extra, os.path.join(objdir, name + ".o")) for s, extra, name in SOURCES]
+    jobs.append((src, [], os.path.join(objdir, "host_fuzz_main.o")))
+    hdr_t = max(os.path.getmtime(f) for f in _inputs() if not f.endswith((".cpp", ".hip")))
+    procs = [(s, subprocess.Popen([hipcc] + flags + extra + ["-c", s, "-o", o], cwd=ROOT, stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT, text=True)) for s, extra, o in jobs
+             if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t)]
+    errors = []
+    for s, pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            errors.append("%s:\n%s" % (s, out[-6000:]))
+    if errors:
+        raise RuntimeError("hipcc (host sanitizers) failed:\n" + "\n".join(errors))
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-fsanitize=address", "-fsanitize=undefined", "-o", FUZZ_PATH + ".tmp"] + \
+        [o for _, _, o in jobs] + ["-ldl", "-lpthread"]
+    res = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc (host sanitizers) link failed:\n" + res.stdout[-6000:])
+    os.replace(FUZZ_PATH + ".tmp", FUZZ_PATH)
+    return FUZZ_PATH
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))

@@ -146,7 +146,13 @@ struct In {
   int64_t i64() { if (!need(8)) return 0; uint64_t v = 0; for (int k = 0; k < 8; ++k) v = v << 8 | p[pos++]; return (int64_t)v; }
   double f64() { int64_t v = i64(); double d; memcpy(&d, &v, 8); return d; }
   std::string str() { int32_t l = i32(); if (!need(l)) return std::string(); std::string s((const char*)p + pos, l); pos += l; return s; }
+  // a wire count of entries of at least `each` bytes: no larger than what is left (a corrupt count must not size an
+  // allocation before the reads behind it fail)
+  bool count(int32_t c, int64_t each) { if (c < 0 || (int64_t)c * each > n - pos) ok = false; return ok; }
 };
+
+// Java long addition (two's complement wrap-around): CountAggregationFunction.merge and the broker's statistics sums.
+inline int64_t java_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
 // java.lang.String.hashCode over UTF-16 units (the names here are ASCII) and java.util.HashMap's iteration order
 // (bucket (h ^ h >>> 16) & (capacity - 1), insertion order within a bucket, capacity 16 doubling past 0.75 load):
@@ -252,9 +258,11 @@ bool parse_table(const uint8_t* p, int64_t n, Table* T, std::string* err) {
   if (sec[3]) {
     In d = section(1);
     const int32_t nd = d.i32();
+    d.count(nd, 8);
     for (int i = 0; i < nd && d.ok; ++i) {
       const std::string col = d.str();
       const int32_t sz = d.i32();
+      if (!d.count(sz, 8)) break;
       auto& m = T->dict[col];
       for (int j = 0; j < sz && d.ok; ++j) { const int32_t key = d.i32(); m[key] = d.str(); }
     }
@@ -263,8 +271,9 @@ bool parse_table(const uint8_t* p, int64_t n, Table* T, std::string* err) {
   if (sec[5]) {
     In s = section(2);
     const int32_t nc = s.i32();
-    for (int i = 0; i < nc; ++i) T->names.push_back(s.str());
-    for (int i = 0; i < nc; ++i) T->types.push_back(s.str());
+    s.count(nc, 8);
+    for (int i = 0; i < nc && s.ok; ++i) T->names.push_back(s.str());
+    for (int i = 0; i < nc && s.ok; ++i) T->types.push_back(s.str());
     if (!s.ok || nc != ncols) { *err = "bad data schema"; return false; }
   }
   for (const auto& t : T->types) { T->offsets.push_back(T->row_size); T->row_size += type_size(t); }
@@ -283,6 +292,7 @@ bool parse_table(const uint8_t* p, int64_t n, Table* T, std::string* err) {
   if (!m.ok || ml < 0 || m.pos + (int64_t)ml > n) { *err = "bad metadata"; return false; }
   In md{p + m.pos, ml};
   const int32_t ne = md.i32();
+  md.count(ne, 8);
   for (int i = 0; i < ne && md.ok; ++i) {
     const int32_t ord = md.i32();
     const MetaKey* k = meta_by_ordinal(ord);
@@ -597,7 +607,7 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
       std::vector<Cell>& dst = rows[it->second];
       for (int c = nk; c < nc; ++c) {
         switch (fn[c]) {
-          case PGPU_AGG_COUNT: dst[c].i += cells[c].i; break;
+          case PGPU_AGG_COUNT: dst[c].i = java_add(dst[c].i, cells[c].i); break;
           case PGPU_AGG_SUM: dst[c].d += cells[c].d; break;
           case PGPU_AGG_MIN: dst[c].d = std::min(dst[c].d, cells[c].d); break;
           case PGPU_AGG_MAX: dst[c].d = std::max(dst[c].d, cells[c].d); break;
@@ -681,7 +691,7 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
   for (const Table& t : T) {
     for (int k = 0; k < 6; ++k) {
       auto it = t.meta.find(stat_names[k]);
-      if (it != t.meta.end()) sums[k] += std::stoll(it->second);
+      if (it != t.meta.end()) sums[k] = java_add(sums[k], std::stoll(it->second));
     }
     limit_reached |= t.meta.count("numGroupsLimitReached") > 0;
   }

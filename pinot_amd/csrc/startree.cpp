@@ -54,6 +54,12 @@ int32_t read_bits(const uint8_t* buf, int64_t index, int bits) {
   return (int32_t)v;
 }
 
+// A fixed-bit forward index of N docs that read_bits may read: 1..31 bits per value, the bytes present, a dictionary.
+bool fixed_bit_ok(const pgpu_column_buffers& cb, int64_t N) {
+  return cb.bits_per_element >= 1 && cb.bits_per_element <= 31 && cb.cardinality >= 1 && cb.fwd != nullptr &&
+         (N * cb.bits_per_element + 7) / 8 <= cb.fwd_len;
+}
+
 // PinotDataBitSet.writeInt (:138-165), into a zeroed buffer.
 void write_bits(uint8_t* buf, int64_t index, int bits, uint32_t value) {
   int64_t bit = index * bits;
@@ -573,9 +579,12 @@ int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_type
     const pgpu_column_buffers& cb = seg->columns[c];
     if (cb.fwd_format != PGPU_FWD_FIXED_BIT)
       return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree dimension must be a fixed-bit column");
-    if ((int64_t)(((int64_t)N * cb.bits_per_element + 7) / 8) > cb.fwd_len)
-      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "forward index too short");
-    for (int i = 0; i < N; ++i) raw_dims[(size_t)i * num_dims + d] = read_bits(cb.fwd, i, cb.bits_per_element);
+    if (!fixed_bit_ok(cb, N)) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad dimension forward index");
+    for (int i = 0; i < N; ++i) {
+      const int32_t id = read_bits(cb.fwd, i, cb.bits_per_element);
+      if (id < 0 || id >= cb.cardinality) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "dictId past the dictionary");
+      raw_dims[(size_t)i * num_dims + d] = id;
+    }
     st->dim_columns.push_back(c);
     st->dim_bits.push_back(bits_for(cb.cardinality));
   }
@@ -590,6 +599,12 @@ int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_type
     const pgpu_column_buffers& cb = seg->columns[c];
     const int t = column_types[c];
     if (t == PGPU_STRING) return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "numeric star-tree metric required");
+    if (cb.fwd_format != PGPU_FWD_FIXED_BIT)
+      return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree metric must be a fixed-bit column");
+    const int width = t == PGPU_INT || t == PGPU_FLOAT ? 4 : 8;
+    if (!fixed_bit_ok(cb, N) || cb.entry_width < width || !cb.dict ||
+        (int64_t)cb.cardinality * cb.entry_width > cb.dict_len)
+      return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad metric column buffers");
     std::vector<double> dv(cb.cardinality);
     for (int i = 0; i < cb.cardinality; ++i) {
       const uint8_t* p = cb.dict + (int64_t)i * cb.entry_width;
@@ -599,9 +614,11 @@ int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_type
       else { uint64_t u = rd_be64(p); memcpy(&dv[i], &u, 8); }
     }
     raw[m].resize(N);
-    if (cb.fwd_format != PGPU_FWD_FIXED_BIT)
-      return pgpu::host_fail(PGPU_ERR_UNSUPPORTED, "star-tree metric must be a fixed-bit column");
-    for (int i = 0; i < N; ++i) raw[m][i] = dv[read_bits(cb.fwd, i, cb.bits_per_element)];
+    for (int i = 0; i < N; ++i) {
+      const int32_t id = read_bits(cb.fwd, i, cb.bits_per_element);
+      if (id < 0 || id >= cb.cardinality) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "dictId past the dictionary");
+      raw[m][i] = dv[id];
+    }
   }
   // sortAndAggregateSegmentRecords: stable sort by dimensions in split order, merge equal rows in doc order
   std::vector<int> order(N);

@@ -505,6 +505,12 @@ int pgpu_attach_startree(pgpu_table table, int64_t segment_handle, const pgpu_st
  * plans created before a re-attach (or an unpin) keep the index they were planned on alive until destroyed. */
 int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
                                int64_t num_bytes);
+/* The same file checked on the host without a device or a table (a loader can reject a bad index before it pins
+ * the segment): the offsets and every Roaring bitmap are validated exactly as pgpu_attach_inverted_index does for a
+ * column of `cardinality` values in a segment of num_docs documents; *total_docs (may be NULL) = the summed bitmap
+ * cardinalities (num_docs for a single-value column's complete index). */
+int pgpu_inverted_index_check(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
+                              int64_t* total_docs);
 
 /* Host-side reader of a raw forward index (PGPU_FWD_RAW_FIXED bytes; FixedByteChunkSVForwardIndexReader.readValuesSV
  * over every chunk, LZ4 chunks decompressed as LZ4Decompressor / LZ4WithLengthDecompressor do): num_docs values of a

@@ -173,6 +173,7 @@ _PROTOS = {
     "pgpu_plan_scanned_segments": (c_int, [c_voidp, c_u8p]),
     "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_attach_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),
+    "pgpu_inverted_index_check": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_voidp]),
     "pgpu_build_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32, c_voidp, c_i64, c_i64p]),
     "pgpu_raw_forward_index_values": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i64p, c_f64p]),
     "pgpu_startree_build": (c_int, [ctypes.POINTER(SegmentDesc), c_i32p, c_i32p, c_i32, c_i32p, c_i32,

@@ -4366,6 +4366,34 @@ bool parse_roaring(const uint8_t* b, int64_t n, int32_t num_docs, std::vector<ui
   }
   return pos <= n;
 }
+
+// A `<column>.bitmap.inv` file (BitmapInvertedIndexReader.java:40-70): (card + 1) big-endian int32 bitmap offsets,
+// then one portable Roaring bitmap per dictId, parsed into `inv`'s per-dictId container lists and the device
+// payload `words`.  Pure host code (pgpu_attach_inverted_index, pgpu_inverted_index_check).
+int parse_inverted_index(const uint8_t* b, int64_t num_bytes, int64_t card, int32_t num_docs, int column,
+                         InvIndex* inv, std::vector<uint32_t>& words) {
+  if (card < 0 || num_docs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad cardinality / document count");
+  const int64_t hdr = (card + 1) * 4;
+  if (!b || num_bytes < hdr) return fail(PGPU_ERR_INVALID_ARGUMENT, "inverted index shorter than its offset header");
+  auto be32 = [&](int64_t o) {
+    return (int64_t)(int32_t)(((uint32_t)b[o] << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) | b[o + 3]);
+  };
+  inv->ids.assign(card, InvIndex::Entry{0, 0, 0});
+  const int64_t first = be32(0);
+  for (int64_t id = 0; id < card; ++id) {
+    const int64_t off = be32(id * 4) - first, end = be32((id + 1) * 4) - first;
+    inv->ids[id].begin = (int32_t)inv->conts.size();
+    if (off < 0 || end < off || hdr + end > num_bytes)
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "bitmap %lld of column %d overruns the index", (long long)id, column);
+    if (!parse_roaring(b + hdr + off, end - off, num_docs, words, inv->conts, &inv->ids[id].docs))
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed Roaring bitmap for dictId %lld of column %d", (long long)id,
+                  column);
+  }
+  for (int64_t id = 0; id < card; ++id)
+    inv->ids[id].count = (int32_t)((id + 1 < card ? inv->ids[id + 1].begin : (int32_t)inv->conts.size()) -
+                                   inv->ids[id].begin);
+  return 0;
+}
 }  // namespace
 
 namespace {
@@ -4470,6 +4498,21 @@ int pgpu_raw_forward_index_values(const void* fwd, int64_t fwd_len, int32_t data
   return 0;
 }
 
+int pgpu_inverted_index_check(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
+                              int64_t* total_docs) {
+  PGPU_ABI_GUARD;
+  if (!bytes && num_bytes) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
+  InvIndex inv;
+  std::vector<uint32_t> words;
+  TRY(parse_inverted_index(reinterpret_cast<const uint8_t*>(bytes), num_bytes, cardinality, num_docs, -1, &inv,
+                           words));
+  if (total_docs) {
+    *total_docs = 0;
+    for (const auto& e : inv.ids) *total_docs += e.docs;
+  }
+  return 0;
+}
+
 int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
   PGPU_ABI_GUARD;
   if (t) t->version++;
@@ -4482,28 +4525,10 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
   Segment& seg = *it->second;
   if (column < 0 || column >= (int)seg.cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column %d", column);
   Column& col = seg.cols[column];
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(bytes);
-  const int64_t card = col.card, hdr = (card + 1) * 4;
-  if (num_bytes < hdr) return fail(PGPU_ERR_INVALID_ARGUMENT, "inverted index shorter than its offset header");
-  auto be32 = [&](int64_t o) {
-    return (int64_t)(int32_t)(((uint32_t)b[o] << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) | b[o + 3]);
-  };
   auto inv = std::make_shared<InvIndex>();
-  inv->ids.assign(card, InvIndex::Entry{0, 0, 0});
   std::vector<uint32_t> words;
-  const int64_t first = be32(0);
-  for (int64_t id = 0; id < card; ++id) {
-    const int64_t off = be32(id * 4) - first, end = be32((id + 1) * 4) - first;
-    inv->ids[id].begin = (int32_t)inv->conts.size();
-    if (off < 0 || end < off || hdr + end > num_bytes)
-      return fail(PGPU_ERR_INVALID_ARGUMENT, "bitmap %lld of column %d overruns the index", (long long)id, column);
-    if (!parse_roaring(b + hdr + off, end - off, seg.num_docs, words, inv->conts, &inv->ids[id].docs))
-      return fail(PGPU_ERR_INVALID_ARGUMENT, "malformed Roaring bitmap for dictId %lld of column %d", (long long)id,
-                  column);
-  }
-  for (int64_t id = 0; id < card; ++id)
-    inv->ids[id].count = (int32_t)((id + 1 < card ? inv->ids[id + 1].begin : (int32_t)inv->conts.size()) -
-                                   inv->ids[id].begin);
+  TRY(parse_inverted_index(reinterpret_cast<const uint8_t*>(bytes), num_bytes, col.card, seg.num_docs, column,
+                           inv.get(), words));
   inv->bytes = (int64_t)std::max<size_t>(words.size(), 1) * 4;
   HIP_TRY(hipMalloc(&inv->d_block, inv->bytes));
   if (!words.empty()) HIP_TRY(hipMemcpy(inv->d_block, words.data(), words.size() * 4, hipMemcpyHostToDevice));

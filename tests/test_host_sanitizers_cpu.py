@@ -3,7 +3,8 @@
 Every library source is compiled with host-only sanitizer flags into build/host_fuzz (pinot_amd.build.
 build_host_fuzz); this test writes a seed corpus with the product's own writers -- raw forward indexes
 (FixedByteChunkSVForwardIndexWriter layout, PASS_THROUGH / LZ4 / LZ4_LENGTH_PREFIXED, versions 2 and 3), DataTable V3
-responses (DataTableImplV3.toBytes layout) and star-tree files (star_tree_index + star_tree_index_map) -- and runs the
+responses (DataTableImplV3.toBytes layout), bitmap inverted indexes (BitmapInvertedIndexWriter + portable Roaring,
+with and without run containers) and star-tree files (star_tree_index + star_tree_index_map) -- and runs the
 harness, which mutates each seed a few thousand times and also drives the inverted-index creator, the star-tree
 builder and the filter-statistics replay with random inputs.  Pass = no sanitizer report (the harness exits non-zero
 on the first one, and its output names the read).  No GPU is touched.
@@ -17,6 +18,7 @@ import pytest
 
 import startree_common as SC
 from pinot_amd import _lib as L
+from pinot_amd import segment_files as SF
 from pinot_amd.segment import raw_forward_index_bytes
 from pinot_amd.startree import StarTree, star_tree_files
 from test_broker_reduce_cpu import _meta, datatable
@@ -56,6 +58,13 @@ def _corpus(oracle, d):
     for i, b in enumerate(tables):
         with open(os.path.join(d, "dt.%d.bin" % i), "wb") as f:
             f.write(b)
+    for i, (card, docs, sort, runs) in enumerate(((7, 5000, False, False), (3, 140000, True, True),
+                                                  (40, 70000, False, True), (1, 10, False, False))):
+        ids = rng.integers(0, card, docs)
+        if sort:
+            ids = np.sort(ids)
+        with open(os.path.join(d, "inv.%d.%d.%d.bin" % (card, docs, i)), "wb") as f:
+            f.write(SF.build_inverted_index(ids, card, run_optimize=runs))
     cols = SC.c4_columns(rng, 3000, cards=(9, 5, 4, 3))
     seg = oracle.make_segment(SC.C4_SCHEMA, cols)
     st = StarTree.build(SC.C4_SCHEMA, seg, SC.C4_SPLIT, SC.C4_PAIRS, max_leaf_records=40)

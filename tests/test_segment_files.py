@@ -242,3 +242,29 @@ def test_native_inverted_index_builder_matches_writer():
         ids = _unpack(c.fwd_bytes, c.bits_per_element, n)
         native = build_inverted_index_native(c.fwd_bytes, c.bits_per_element, n, c.cardinality)
         assert native == build_inverted_index(ids, c.cardinality)
+
+
+def test_inverted_index_host_check():
+    """pgpu_inverted_index_check: the attach-time validation of a bitmap.inv file, on the host (no device)."""
+    import ctypes
+    from pinot_amd.segment_files import build_inverted_index
+    lib = L.load()
+    rng = np.random.default_rng(8)
+
+    def check(b, card, n):
+        total = ctypes.c_int64(-1)
+        buf = ctypes.create_string_buffer(bytes(b), max(len(b), 1))
+        rc = lib.pgpu_inverted_index_check(ctypes.cast(buf, ctypes.c_void_p), len(b), card, n, ctypes.byref(total))
+        return rc, total.value
+
+    for n, card, runs in ((5000, 7, False), (140000, 3, True), (1, 1, False)):
+        ids = np.sort(rng.integers(0, card, n)) if runs else rng.integers(0, card, n)
+        b = build_inverted_index(ids, card, run_optimize=runs)
+        assert check(b, card, n) == (0, n)
+        assert check(b, card, n - 1)[0] == L.PGPU_ERR_INVALID_ARGUMENT or n == 1  # a docId past numDocs
+        assert check(b[:-1], card, n)[0] == L.PGPU_ERR_INVALID_ARGUMENT           # truncated last bitmap
+        assert check(b[:4 * card], card, n)[0] == L.PGPU_ERR_INVALID_ARGUMENT     # shorter than its offset header
+        bad = bytearray(b)
+        off = struct.unpack(">i", bytes(b[:4]))[0]
+        bad[off:off + 4] = struct.pack("<I", 99)  # not a Roaring cookie
+        assert check(bytes(bad), card, n)[0] == L.PGPU_ERR_INVALID_ARGUMENT

@@ -7,6 +7,7 @@
 //   raw   pgpu_raw_forward_index_values  FixedByteChunkSVForwardIndexReader chunks, PASS_THROUGH / LZ4 / LZ4_LENGTH
 //   dt    pgpu_broker_reduce_sql         DataTable V3 bytes from servers (DataTableImplV3(ByteBuffer))
 //   st    pgpu_startree_load             star_tree_index + star_tree_index_map files (StarTreeLoaderUtils)
+//   invf  pgpu_inverted_index_check      bitmap.inv files (BitmapInvertedIndexReader + portable RoaringBitmap)
 //   inv   pgpu_build_inverted_index      fixed-bit forward index -> bitmap.inv bytes
 //   stb   pgpu_startree_build            segment buffers -> star-tree (OnHeapSingleTreeBuilder)
 //   flt   pgpu_filter_entries_scanned    postfix filter programs + per-leaf doc sets
@@ -136,6 +137,29 @@ long fuzz_raw(const std::string& dir, long iters, Rng& r) {
       std::vector<int64_t> oi((size_t)n + 1);
       std::vector<double> of((size_t)n + 1);
       pgpu_raw_forward_index_values(b.p, (int64_t)b.n, type, n, r.below(2) ? oi.data() : nullptr, of.data());
+      ++calls;
+    }
+  }
+  return calls;
+}
+
+// ---- inv.<cardinality>.<num_docs>.<k>.bin
+long fuzz_invfile(const std::string& dir, long iters, Rng& r) {
+  long calls = 0;
+  for (const std::string& name : list_dir(dir)) {
+    int card = 0, docs = 0, k = 0;
+    if (sscanf(name.c_str(), "inv.%d.%d.%d.bin", &card, &docs, &k) != 3) continue;
+    const Bytes seed = read_file(dir + "/" + name);
+    for (long it = 0; it < iters; ++it) {
+      Exact b(it == 0 ? seed : mutate(seed, r));
+      int64_t total = 0;
+      const int c = it > 0 && r.below(10) == 0 ? card + (int)r.below(3) - 1 : card;
+      const int n = it > 0 && r.below(10) == 0 ? docs - (int)r.below(70000) : docs;
+      const int rc = pgpu_inverted_index_check(b.p, (int64_t)b.n, c, n, &total);
+      if (it == 0 && (rc != 0 || total != docs)) {
+        fprintf(stderr, "seed %s rejected (rc %d, %lld docs)\n", name.c_str(), rc, (long long)total);
+        exit(4);
+      }
       ++calls;
     }
   }
@@ -381,9 +405,11 @@ int main(int argc, char** argv) {
   const long raw = timed("raw", [&] { return fuzz_raw(dir, iters, r); });
   const long dt = timed("dt", [&] { return fuzz_dt(dir, iters, r); });
   const long st = timed("st", [&] { return fuzz_st(dir, iters, r); });
+  const long invf = timed("invf", [&] { return fuzz_invfile(dir, iters, r); });
   const long inv = timed("inv", [&] { return fuzz_inv(iters, r); });
   const long stb = timed("stb", [&] { return fuzz_startree_build(iters / 4 + 1, r); });
   const long flt = timed("flt", [&] { return fuzz_filter(iters, r); });
-  printf("host_fuzz calls: raw %ld dt %ld st %ld inv %ld stb %ld flt %ld\n", raw, dt, st, inv, stb, flt);
-  return (raw > 0 && dt > 0 && st > 0) ? 0 : 3;  // 3: a seed family is missing from the corpus
+  printf("host_fuzz calls: raw %ld dt %ld st %ld invf %ld inv %ld stb %ld flt %ld\n", raw, dt, st, invf, inv, stb,
+         flt);
+  return (raw > 0 && dt > 0 && st > 0 && invf > 0) ? 0 : 3;  // 3: a seed family is missing from the corpus
 }

@@ -296,6 +296,7 @@ struct KRawJob {
 // Host-callable launchers (kernels.hip).
 int launch_unpack(const uint32_t* fwd, int32_t bits, int64_t start, int64_t n, int32_t* out, void* stream);
 int launch_gather_ids(const uint32_t* fwd, int32_t bits, const int32_t* docs, int32_t n, int32_t* out, void* stream);
+int launch_fwd_max(const void* d_fwd, int64_t n, int32_t bits, unsigned int* d_out, void* stream);
 int launch_hash_unpack(uint64_t* table, const unsigned long long* hash_keys, int64_t cap, int32_t pack_slot,
                        int32_t shift, void* stream);
 int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,

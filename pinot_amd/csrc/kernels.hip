@@ -699,6 +699,39 @@ int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slo
   return PGPU_HIP_OK(hipGetLastError());
 }
 
+// Largest dictId of a pinned fixed-bit forward index (pgpu_pin_segment): a value >= the column's cardinality would
+// index past its dictionary / translation arrays in every later scan, so the pin rejects it (Pinot's reader would
+// throw ArrayIndexOutOfBoundsException on the first such doc).  Byte reads of the big-endian bit stream; pin-time only.
+__global__ __launch_bounds__(256) void fwd_max_kernel(const uint8_t* __restrict__ fwd, int64_t n, int32_t bits,
+                                                      unsigned int* __restrict__ out) {
+  uint32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t bit = (uint64_t)i * (uint64_t)bits;
+    const int64_t byte = (int64_t)(bit >> 3);
+    const int sh = (int)(bit & 7);
+    const int nb = (sh + bits + 7) >> 3;
+    uint64_t w = 0;
+    for (int k = 0; k < nb; ++k) w = (w << 8) | fwd[byte + k];
+    const uint32_t v = (uint32_t)((w >> (nb * 8 - sh - bits)) & ((1ull << bits) - 1));
+    m = v > m ? v : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = (uint32_t)__shfl_xor((int)m, o);
+    m = x > m ? x : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+int launch_fwd_max(const void* d_fwd, int64_t n, int32_t bits, unsigned int* d_out, void* stream) {
+  if (n <= 0) return 0;
+  if (bits < 1 || bits > 31) return -1;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(fwd_max_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream),
+                     reinterpret_cast<const uint8_t*>(d_fwd), n, bits, d_out);
+  return PGPU_HIP_OK(hipGetLastError());
+}
+
 // KParams.pack_slot of a hash plan: every occupied slot's pack word holds (count << shift) | sum; split it into the
 // COUNT row (slot 0) and the SUM row so finalize, combine and compaction read the plain table layout.
 __global__ __launch_bounds__(256) void hash_unpack_kernel(uint64_t* __restrict__ table,

@@ -4245,7 +4245,31 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
     }
     off += (col.fwd_words + 63) & ~int64_t(63);
   }
+  // dictIds within the dictionary (fwd_max_kernel): only columns whose bit width can hold values >= cardinality
+  std::vector<int> check;
+  for (int c = 0; c < d->num_columns; ++c) {
+    const Column& col = seg->cols[c];
+    if (!col.raw && !col.sorted && d->num_docs > 0 && (int64_t)col.card < (INT64_C(1) << col.bits)) check.push_back(c);
+  }
+  DevBuf dmax;
+  struct Release { DevBuf& b; ~Release() { b.release(); } } release_dmax{dmax};
+  std::vector<uint32_t> hmax(check.size(), 0);
+  if (!check.empty()) {
+    TRY(dmax.ensure(check.size() * 4));
+    HIP_TRY(hipMemsetAsync(dmax.p, 0, check.size() * 4, t->stream));
+    for (size_t i = 0; i < check.size(); ++i)
+      if (launch_fwd_max(seg->cols[check[i]].d_fwd, d->num_docs, seg->cols[check[i]].bits,
+                         dmax.as<unsigned int>() + i, t->stream))
+        return fail(PGPU_ERR_DEVICE, "forward-index check launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipMemcpyAsync(hmax.data(), dmax.p, check.size() * 4, hipMemcpyDeviceToHost, t->stream));
+  }
   HIP_TRY(hipStreamSynchronize(t->stream));
+  for (size_t i = 0; i < check.size(); ++i)
+    if ((int64_t)hmax[i] >= seg->cols[check[i]].card) {
+      account_unpin(t, seg.get());
+      return fail(PGPU_ERR_INVALID_ARGUMENT, "column %d: forward index holds dictId %u, cardinality is %d", check[i],
+                  hmax[i], seg->cols[check[i]].card);
+    }
   std::lock_guard<std::mutex> lk(t->mu);
   if (any_raw) TRY(ensure_docid(t, d->num_docs, t->stream));
   *handle = register_segment(t, std::move(seg));

@@ -844,6 +844,31 @@ def test_inverted_index_malformed(gpu_lib):
         t.close()
 
 
+def test_pin_rejects_dict_ids_past_the_dictionary(gpu_lib):
+    """A fixed-bit forward index holding a dictId >= cardinality (2 bits, cardinality 3, a stored 3) is refused at pin
+    (fwd_max_kernel's pin-time check): every later scan would index past the column's dictionary arrays.  The table
+    stays usable and its byte accounting unchanged."""
+    from dataclasses import replace
+    from pinot_amd.segment import SegmentBuffers
+    from pinot_amd.segment_files import build_column, pack_msb_first
+    t = GpuTable([("a", "INT")])
+    try:
+        c = build_column(L.INT, [0, 1, 2, 1, 0, 2], is_sorted=False)
+        assert c.bits_per_element == 2 and c.cardinality == 3
+        before = t.device_bytes()
+        for ids in ([0, 1, 3, 1, 0, 2], [0] * 5 + [3]):
+            bad = replace(c, fwd_bytes=pack_msb_first(ids, 2), fwd_format=L.FWD_FIXED_BIT)
+            with pytest.raises(L.PinotGpuError) as e:
+                t.pin_segment(SegmentBuffers(6, {"a": bad}))
+            assert "dictId 3" in e.value.message
+        assert t.device_bytes() == before
+        h = t.pin_segment(SegmentBuffers(6, {"a": c}))
+        r = t.execute_groupby([h], parse_query("SELECT COUNT(*) FROM t GROUP BY a"))
+        assert {k: v[0] for k, v in r.as_dict().items()} == {(0,): 2, (1,): 2, (2,): 2}
+    finally:
+        t.close()
+
+
 def test_long_literals_beyond_double_precision(oracle, gpu_lib):
     """Dictionary lookups of LONG literals that differ by less than one double ulp (values around 2^60, where
     interpolation in double precision degenerates) find the exact dictId (BaseImmutableDictionary.insertionIndexOf)."""

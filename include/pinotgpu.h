@@ -237,6 +237,14 @@ int pgpu_plan_cancel(pgpu_plan plan);
  * RAW_RANGE, RAW_IN, BITDIR (inverted-index containers read in place)). */
 int pgpu_plan_leaf_kinds(pgpu_plan plan, int64_t* counts);
 
+/* Diagnostics: the group-by path the plan's scan takes (a numGroupsLimit plan: its first part's).  LDS: tables
+ * privatised per workgroup in LDS; GLOBAL: a dense table with global atomics; HASH: the global open-addressing hash
+ * table (sparse key spaces); PARTITIONED: radix-partitioned dense keys aggregated per partition in LDS; HASH_PARTITIONED:
+ * hash-partitioned sparse keys aggregated per partition in LDS hash tables. */
+enum pgpu_group_path { PGPU_PATH_LDS = 0, PGPU_PATH_GLOBAL = 1, PGPU_PATH_HASH = 2, PGPU_PATH_PARTITIONED = 3,
+                       PGPU_PATH_HASH_PARTITIONED = 4 };
+int pgpu_plan_group_path(pgpu_plan plan, int32_t* path);
+
 /* Runs the plan on `stream` (hipStream_t; NULL = the table's stream): predicate translation results are
  * uploaded, the fused filter/group/aggregate kernel runs over every segment, and the dense group table is
  * written to d_table (device pointer, num_slots * num_keys * 8 bytes, caller-owned; may be NULL to use an

@@ -36,6 +36,7 @@ FWD_FIXED_BIT, FWD_SORTED_PAIRS, FWD_RAW_FIXED = 0, 1, 2
 PRED_EQ, PRED_NOT_EQ, PRED_IN, PRED_NOT_IN, PRED_RANGE = 0, 1, 2, 3, 4
 OP_PRED, OP_AND, OP_OR, OP_NOT = 0, 1, 2, 3
 LEAF_KIND_NAMES = ("none", "all", "range", "set", "docrange", "bitmap", "raw_range", "raw_in", "bitdir")
+GROUP_PATH_NAMES = ("lds", "global", "hash", "partitioned", "hash_partitioned")  # enum pgpu_group_path
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 SLOT_COUNT, SLOT_SUM_I64, SLOT_SUM_F64, SLOT_MIN_KEY, SLOT_MAX_KEY = 0, 1, 2, 3, 4
 GEN_UNIFORM, GEN_ZIPF, GEN_TABLE = 0, 1, 2
@@ -159,6 +160,7 @@ _PROTOS = {
                                          ctypes.POINTER(c_voidp)]),
     "pgpu_plan_layout": (c_int, [c_voidp, c_i32p, c_i64p, c_i32p]),
     "pgpu_plan_leaf_kinds": (c_int, [c_voidp, c_i64p]),
+    "pgpu_plan_group_path": (c_int, [c_voidp, c_i32p]),
     "pgpu_plan_cancel": (c_int, [c_voidp]),
     "pgpu_plan_execute": (c_int, [c_voidp, c_voidp, c_voidp]),
     "pgpu_plan_finalize": (c_int, [c_voidp, c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),

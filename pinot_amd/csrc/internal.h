@@ -243,13 +243,31 @@ struct KPartParams {
   // sum of offsets < 2^40: pack_range x records); the word is split when the slice is stored
   int32_t cs_pack;
   int64_t pack_range;
+  // Hashed partitions (MODE_HASH key spaces < 2^31, partition.h K8h): a record's partition is the top pbits of
+  // part_hash(key), its key is stored whole (mid_key / rec_key32), and K8h aggregates each partition in an LDS hash
+  // table of 2^sbits entries, appending (key, slot words) records at out_rec / out_count (the compacted form of a
+  // hash table, finalized as one).  pshift is 0 and pack_bits / fine_pack / cs_pack are off.
+  int32_t hashed;
+  int32_t pbits;
+  int32_t sbits;
+  uint32_t* rec_key32;                // [rec_cap] final layout: the whole key
+  uint64_t* out_rec;                  // [rec_cap][1 + num_slots]
+  unsigned long long* out_count;
 };
+// K8h: value streams a record carries in registers (plans with more use the global hash table).
+constexpr int kHashPartStreams = 4;
+// K8h: linear probes of the LDS hash table before a record is left for the partition's next round.
+constexpr int kHashPartProbes = 128;
 
 // K8e batch: records sorted by partition in LDS per step (at most kSplitBatch; fewer with many value streams).
 constexpr int kSplitBatch = 2048;
 // LDS bytes of part_split_kernel: 2^cshift partitions per coarse run, `streams` value streams, `batch` records.
-constexpr size_t part_split_lds(int cshift, int streams, int batch) {
-  return (size_t)3 * ((size_t)1 << cshift) * 4 + 8 + (size_t)streams * batch * 8 + (size_t)batch * (4 + 2) + 16;
+constexpr size_t part_split_lds(int cshift, int streams, int batch, int key_bytes = 2) {
+  return (size_t)3 * ((size_t)1 << cshift) * 4 + 8 + (size_t)streams * batch * 8 + (size_t)batch * (4 + key_bytes) + 16;
+}
+// LDS bytes of part_hash_aggregate_kernel: 2^sbits entries of a u32 key and num_slots u64 words.
+constexpr size_t part_hash_lds(int sbits, int num_slots) {
+  return ((size_t)1 << sbits) * ((size_t)num_slots * 8 + 4);
 }
 
 // ---------------------------------------------------------------------------------------------- inverted index

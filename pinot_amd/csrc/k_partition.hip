@@ -20,7 +20,13 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
   if (pp.cshift > 0) {
     if (hipMemsetAsync(pp.fine_fill, 0, (size_t)pp.num_parts * 4, s) != hipSuccess) return -1;
     hipLaunchKernelGGL(part_split_kernel, dim3(pp.num_coarse * pp.chunks_per_coarse), dim3(kBlock),
-                       part_split_lds(pp.cshift, pp.num_streams, pp.split_batch), s, pp);
+                       part_split_lds(pp.cshift, pp.num_streams, pp.split_batch, pp.hashed ? 4 : 2), s, pp);
+  }
+  if (pp.hashed) {
+    if (pp.num_streams > kHashPartStreams || pp.sbits < 1 || pp.sbits > 16) return -1;
+    hipLaunchKernelGGL(part_hash_aggregate_kernel, dim3(pp.num_parts), dim3(kBlock),
+                       part_hash_lds(pp.sbits, pp.base.num_slots), s, pp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   const size_t agg_lds = (size_t)pp.base.num_slots * ((size_t)1 << pp.pshift) * 8;
   hipLaunchKernelGGL(part_aggregate_kernel, dim3(pp.num_parts), dim3(kBlock), agg_lds, s, pp);

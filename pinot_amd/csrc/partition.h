@@ -20,6 +20,15 @@
 //   K8d part_aggregate: one workgroup per partition: LDS table, LDS atomics over its records, then the
 //                       partition's slice of every table row stored whole (no table init, no global atomics).
 //
+// Hashed partitions (KPartParams.hashed; sparse key spaces of MODE_HASH plans, e.g. 10^7 groups in a 10^9-key
+// space): the same passes with the partition taken from the top bits of a multiplicative hash of the key and the
+// whole key carried in the records; instead of K8d,
+//   K8h part_hash_aggregate: one workgroup per partition: an LDS hash table (keys + slot words) over its records;
+//                       records whose key finds no slot within kHashPartProbes probes are compacted in place and
+//                       aggregated by the next round; each round appends its (key, slot words) records to out_rec
+//                       (the compacted form of the global hash table, DictionaryBasedGroupKeyGenerator's LONG_MAP
+//                       holder at :644-746) -- no table init, no random global atomics.
+//
 // Replaces the same reference code as the direct kernel (DictionaryBasedGroupKeyGenerator INT_MAP holder +
 // aggregateGroupBySV + GroupByCombineOperator merge); results are identical (integer
 // accumulators exact; double sums within the path's 1e-9 relative bound — their order is not fixed).
@@ -34,6 +43,13 @@ namespace pgpu {
 __device__ __forceinline__ void part_tiles(int64_t T, int64_t& t0, int64_t& t1) {
   t0 = (int64_t)blockIdx.x * T / gridDim.x;
   t1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+}
+
+// Hashed partitions: Fibonacci hash of a key; its top pbits name the partition, the next sbits the LDS slot.
+__device__ __forceinline__ uint32_t part_hash(uint32_t key) { return key * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t part_of(const KPartParams& pp, int32_t key) {
+  if (pp.hashed) return pp.pbits ? part_hash((uint32_t)key) >> (32 - pp.pbits) : 0u;
+  return (uint32_t)key >> pp.pshift;
 }
 
 // Composite keys of docs [32*group + H, +16) of segment S.
@@ -90,13 +106,25 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     return;
   }
   uint32_t pos[16];
+  if (pp.hashed) {  // the coarse run of the key's hashed partition; the whole key stored
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    pos[i] = 0;
-    if ((m >> i) & 1u) {
-      pos[i] = atomicAdd(&cursor[key[i] >> cbits], 1u);
-      if (two) pp.mid_key[pos[i]] = (uint32_t)(key[i] & ((1 << cbits) - 1));
-      else pp.rec_key[pos[i]] = (uint16_t)(key[i] & ((1 << pp.pshift) - 1));
+    for (int i = 0; i < 16; ++i) {
+      pos[i] = 0;
+      if ((m >> i) & 1u) {
+        pos[i] = atomicAdd(&cursor[part_of(pp, key[i]) >> pp.cshift], 1u);
+        if (two) pp.mid_key[pos[i]] = (uint32_t)key[i];
+        else pp.rec_key32[pos[i]] = (uint32_t)key[i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      pos[i] = 0;
+      if ((m >> i) & 1u) {
+        pos[i] = atomicAdd(&cursor[key[i] >> cbits], 1u);
+        if (two) pp.mid_key[pos[i]] = (uint32_t)(key[i] & ((1 << cbits) - 1));
+        else pp.rec_key[pos[i]] = (uint16_t)(key[i] & ((1 << pp.pshift) - 1));
+      }
     }
   }
   uint32_t ids[16];
@@ -143,7 +171,7 @@ __device__ __forceinline__ void part_count_half(const KPartParams& pp, const Seg
   part_keys<H>(pp.base, S, group, key);
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    if ((m >> i) & 1u) atomicAdd(&hist[key[i] >> pp.pshift], 1u);
+    if ((m >> i) & 1u) atomicAdd(&hist[part_of(pp, key[i])], 1u);
 }
 
 // K8a (SCATTER = false) / K8c (SCATTER = true).  LDS: [num_parts u32 histogram / cursors] [filter stack].
@@ -237,6 +265,7 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   uint64_t* sval = reinterpret_cast<uint64_t*>(bstart + NP + (NP & 1));
   uint32_t* spos = reinterpret_cast<uint32_t*>(sval + (size_t)pp.num_streams * batch);
   uint16_t* skey = reinterpret_cast<uint16_t*>(spos + batch);
+  uint32_t* skey32 = reinterpret_cast<uint32_t*>(spos + batch);  // hashed: whole keys (part_split_lds key_bytes 4)
   __shared__ uint32_t wtot[kBlock / 64];
   const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
   const uint32_t r0 = cs + (uint32_t)((uint64_t)(ce - cs) * j / pp.chunks_per_coarse);
@@ -272,8 +301,12 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
                                     : pp.mid_val[r];
       }
     }
+    uint32_t part[NB];  // the record's partition within this coarse run
 #pragma unroll
-    for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[k[b] >> pp.pshift], 1u) : 0u;
+    for (int b = 0; b < NB; ++b)
+      part[b] = pp.hashed ? part_of(pp, (int32_t)k[b]) & (uint32_t)(NP - 1) : k[b] >> pp.pshift;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[part[b]], 1u) : 0u;
     __syncthreads();
     {  // exclusive prefix of the batch histogram: slices, wave scan of the slice sums, wave totals
       const int lane = tid & 63, w = tid >> 6;
@@ -300,10 +333,10 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       if (k[b] == ~0u) continue;
-      const uint32_t part = k[b] >> pp.pshift;
-      const uint32_t l = bstart[part] + rank[b];
-      spos[l] = cnt[part] + rank[b];
-      skey[l] = (uint16_t)(k[b] & low);
+      const uint32_t l = bstart[part[b]] + rank[b];
+      spos[l] = cnt[part[b]] + rank[b];
+      if (pp.hashed) skey32[l] = k[b];
+      else skey[l] = (uint16_t)(k[b] & low);
       const int64_t r = b0 + tid + b * kBlock;
       if (pp.num_streams > 0) sval[l] = v0[b];
       for (int s = 1; s < pp.num_streams; ++s)
@@ -319,7 +352,8 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     }
     for (uint32_t i = tid; i < n; i += kBlock) {  // in bucket order: runs of consecutive positions
       const uint32_t pos = spos[i];
-      pp.rec_key[pos] = skey[i];
+      if (pp.hashed) pp.rec_key32[pos] = skey32[i];
+      else pp.rec_key[pos] = skey[i];
       if (pp.val32)
         for (int s = 0; s < pp.num_streams; ++s)
           reinterpret_cast<uint32_t*>(pp.rec_val)[(int64_t)s * pp.rec_cap + pos] = (uint32_t)sval[(size_t)s * batch + i];
@@ -427,6 +461,112 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   const int n = (int)(G - k0 < PR ? G - k0 : PR);
   for (int s = 0; s < ns; ++s)
     for (int i = tid; i < n; i += kBlock) p.table[(int64_t)s * G + k0 + i] = lds[(int64_t)s * PR + i];
+}
+
+// Slot of `key` in an LDS hash table of 2^sbits u32 keys (empty = ~0u), inserted if absent, or -1 after
+// kHashPartProbes probes.  Start slot: the sbits of part_hash(key) below the partition's pbits.
+__device__ __forceinline__ int lds_hash_slot(uint32_t* keys, uint32_t key, int pbits, int sbits) {
+  const uint32_t mask = (1u << sbits) - 1u;
+  uint32_t s = (part_hash(key) << pbits) >> (32 - sbits);
+  const int probes = kHashPartProbes < (1 << sbits) ? kHashPartProbes : (1 << sbits);
+  for (int i = 0; i < probes; ++i) {
+    const uint32_t k = keys[s];
+    if (k == key) return (int)s;
+    if (k == ~0u) {
+      const uint32_t prev = atomicCAS(&keys[s], ~0u, key);
+      if (prev == ~0u || prev == key) return (int)s;
+    }
+    s = (s + 1u) & mask;
+  }
+  return -1;
+}
+
+// K8h: partition blockIdx.x -> its groups' compacted records.  LDS: [num_slots][2^sbits] u64 words, then
+// [2^sbits] u32 keys.  Each round aggregates the partition's pending records (those of round 0: its whole run);
+// a record whose key finds no slot is written back at the front of the run (in place: every record of a batch is
+// loaded before any of the batch is written, and the write position never passes the records read) and waits for
+// the next round, so every round places at least one new key and the loop ends.
+__global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPartParams pp) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const KParams& p = pp.base;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (p.deadline && p.stats[5]) return;
+  const int S = 1 << pp.sbits;
+  const int ns = p.num_slots, nst = pp.num_streams;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(lds + (size_t)ns * S);
+  __shared__ uint32_t pending;
+  const uint32_t r0 = pp.part_start[blockIdx.x];
+  uint32_t n = pp.part_start[blockIdx.x + 1] - r0;
+  const int64_t cap = pp.rec_cap;
+  constexpr int NB = 8;
+  while (n > 0) {
+    for (int i = tid; i < S; i += kBlock) keys[i] = ~0u;
+    for (int i = tid; i < ns * S; i += kBlock) lds[i] = slot_init(p.slot_kind[i >> pp.sbits]);
+    if (tid == 0) pending = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += NB * kBlock) {
+      uint32_t key[NB];
+      uint64_t v[NB][kHashPartStreams];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t i = base + b * kBlock + tid;
+        const uint32_t r = r0 + (i < n ? i : 0u);
+        key[b] = i < n ? pp.rec_key32[r] : ~0u;
+#pragma unroll
+        for (int st = 0; st < kHashPartStreams; ++st)
+          v[b][st] = st >= nst ? 0ull
+                     : pp.val32 ? (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(pp.rec_val)[st * cap + r]
+                                : pp.rec_val[st * cap + r];
+      }
+      __syncthreads();  // the batch is in registers before any record of it is overwritten by a pending one
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if (key[b] == ~0u) continue;
+        const int slot = lds_hash_slot(keys, key[b], pp.pbits, pp.sbits);
+        if (slot < 0) {
+          const uint32_t at = r0 + atomicAdd(&pending, 1u);
+          pp.rec_key32[at] = key[b];
+#pragma unroll
+          for (int st = 0; st < kHashPartStreams; ++st)
+            if (st < nst) {
+              if (pp.val32) reinterpret_cast<uint32_t*>(pp.rec_val)[st * cap + at] = (uint32_t)v[b][st];
+              else pp.rec_val[st * cap + at] = v[b][st];
+            }
+          continue;
+        }
+        for (int s = 0; s < ns; ++s) {
+          const int st = pp.slot_stream[s];
+          uint64_t w = 0;
+#pragma unroll
+          for (int j = 0; j < kHashPartStreams; ++j)
+            if (j == st) w = v[b][j];
+          accumulate<MODE_LDS>(lds + (int64_t)s * S, slot, p.slot_kind[s], (int64_t)w,
+                               __longlong_as_double((long long)w));
+        }
+      }
+    }
+    __syncthreads();
+    // append this round's groups: one reservation per wave
+    for (int i0 = 0; i0 < S; i0 += kBlock) {
+      const int i = i0 + tid;
+      const bool occ = i < S && keys[i] != ~0u;
+      const uint64_t bal = __ballot(occ);
+      unsigned long long at = 0;
+      if (lane == 0 && bal) at = atomicAdd(pp.out_count, (unsigned long long)__popcll(bal));
+      at = (unsigned long long)__shfl((long long)at, 0);
+      if (occ) {
+        const uint64_t r = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (r < (uint64_t)cap) {
+          uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
+          o[0] = (uint64_t)keys[i];
+          for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
+        }
+      }
+    }
+    __syncthreads();
+    n = pending;
+    __syncthreads();
+  }
 }
 
 }  // namespace pgpu

@@ -339,6 +339,7 @@ constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large 
 #endif
 constexpr int64_t kPartLds = PGPU_PART_LDS_KB * 1024;  // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
+constexpr int64_t kHashPartLds = 48 * 1024;          // K8h LDS hash table per partition (three workgroups per CU)
 constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
 constexpr int kDocIdColumn = -2;                     // query column of the virtual $docId (hidden first-doc slot)
 
@@ -524,6 +525,7 @@ struct Scratch {
   HostPinned rawstage;
   DevBuf segrec, sets, slab, table, hash_keys, stats, ckeys, cslots, counter, bitmap, tile_seg, starrec, starwork;
   DevBuf part_start, block_off, rec_key, rec_val;  // partitioned group-by (large dense key spaces)
+  DevBuf rec_key32;                                // hashed partitions: whole record keys
   DevBuf stage_keys;  // ARRAY_MAP key spaces: the prefix hash table
   DevBuf coarse_fill, fine_fill, mid_key, mid_val;
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
@@ -1112,6 +1114,11 @@ struct pgpu_plan_s {
   size_t part_lds = 0;
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
   bool part_val32 = false;  // KPartParams.val32
+  // MODE_HASH plans over key spaces < 2^31: hashed partitions (KPartParams.hashed, K8h) instead of the global hash
+  // table.  part_hash_live: the last execution's groups are the compacted records in Scratch::ckeys (count in
+  // Scratch::counter) and no table was built; finalize reads them as is, an exchange first materialises the table.
+  bool part_hash = false, part_hash_live = false;
+  int part_pbits = 0, part_sbits = 0;
   int64_t part_pack_min = 0, part_pack_range = -1;  // the single stream's value range (-1: none)
   double sel_estimate = 1.0;              // estimated filter selectivity (uniform dictIds)
   int64_t sel_docs = 0;
@@ -1826,6 +1833,18 @@ int32_t hash_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_q
   while (bits < 63 && (INT64_C(1) << bits) <= P->total_docs) ++bits;
   *shift = 64 - bits;
   return pack_slot_for(t, P, q, P->total_docs, *shift);
+}
+
+// Hashed partitions (KPartParams.hashed) for a MODE_HASH plan: single-stage keys whose composite key fits int32
+// (part_keys' arithmetic and the records' u32 keys).  PGPU_NO_PART_HASH=1: the global hash table (A/B).
+bool part_hash_eligible(const pgpu_plan_s* P, int64_t G) {
+  static const bool off = getenv_flag("PGPU_NO_PART_HASH");
+  return !off && P->mode == MODE_HASH && P->stage_end.empty() && G > 0 && G < (INT64_C(1) << 31) && P->key_bias == 0;
+}
+
+// Records K8h may append (the groups): as finalize's compaction of a hash table sizes its output.
+int64_t part_hash_out_cap(const pgpu_plan_s* P) {
+  return std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
 }
 
 // A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
@@ -2544,12 +2563,28 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       const int64_t per_wg = (tile_base + P->grid - 1) / std::max(P->grid, 1) + 3;
       P->lds_bytes += (size_t)((per_wg * (kBlock / 64) + 15) & ~int64_t(15));
     }
-    // Large dense tables: partitioned group-by (partition.h) instead of random global atomics.
-    if (P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes && P->star.empty() && tile_base > 0 &&
-        P->total_docs < (int64_t)UINT32_MAX && !getenv_flag("PGPU_NO_PARTITION")) {
+    // Large dense tables: partitioned group-by (partition.h) instead of random global atomics; sparse hash key
+    // spaces below 2^31: the same passes over hashed partitions (K8h) instead of the global hash table.
+    const bool dense_part = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes;
+    const bool hash_part = part_hash_eligible(P, G);
+    if ((dense_part || hash_part) && P->star.empty() && tile_base > 0 && P->total_docs < (int64_t)UINT32_MAX &&
+        !getenv_flag("PGPU_NO_PARTITION")) {
       int shift = 16;
       while (shift > 8 && ((int64_t)nslots << shift) * 8 > kPartLds) --shift;
-      const int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
+      int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
+      int pbits = 0, sbits = 0;
+      if (hash_part) {
+        // LDS table of 2^sbits entries within kHashPartLds; partitions: the plan's group bound at <= half load,
+        // at most kMaxParts (more groups than that holds take further K8h rounds)
+        sbits = 12;
+        while (sbits > 8 && (int64_t)part_hash_lds(sbits, nslots) > kHashPartLds) --sbits;
+        // PGPU_PART_HASH_PBITS: at most that many partition bits (read per plan; tests force K8h's extra rounds)
+        const char* pb = getenv("PGPU_PART_HASH_PBITS");
+        const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 14;
+        while (pbits < max_pbits && (int64_t(1) << (pbits + sbits - 1)) < P->group_bound) ++pbits;
+        shift = 0;
+        parts = int64_t(1) << pbits;
+      }
       std::vector<int32_t> scol, sf64, sstream(nslots, -1);
       for (int sl = 1; sl < nslots; ++sl) {
         const int f64 = P->slot_kind[sl] == SLOT_SUM_F64 ? 1 : 0;
@@ -2559,10 +2594,15 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         if (k < 0) { scol.push_back(P->slot_col[sl]); sf64.push_back(f64); k = (int)scol.size() - 1; }
         sstream[sl] = k;
       }
-      const int64_t rec_bytes = P->total_docs * (2 + 8 * (int64_t)scol.size());
+      const int64_t rec_bytes = P->total_docs * ((hash_part ? 4 : 2) + 8 * (int64_t)scol.size());
       const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
-      if (parts <= kMaxParts && rec_bytes <= kPartMaxRecordBytes && pass_lds <= 96 * 1024) {
+      if (parts <= kMaxParts && rec_bytes <= kPartMaxRecordBytes && pass_lds <= 96 * 1024 &&
+          (!hash_part || (int)scol.size() <= kHashPartStreams)) {
         P->partitioned = true;
+        P->part_hash = hash_part;
+        if (hash_part) P->pack_slot = -1;  // K8h accumulates every slot itself (no packed global words)
+        P->part_pbits = pbits;
+        P->part_sbits = sbits;
         P->part_shift = shift;
         P->num_parts = (int)parts;
         P->stream_col = scol;
@@ -2588,7 +2628,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->part_val32 = v32;
         // one integer stream: its value range, for packing values into the coarse records (KPartParams.pack_bits)
         P->part_pack_range = -1;
-        if (v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn && !getenv_flag("PGPU_NO_PACK")) {
+        if (!hash_part && v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn &&
+            !getenv_flag("PGPU_NO_PACK")) {
           int64_t lo = INT64_MAX, hi = INT64_MIN;
           for (const Segment* s : P->segs) {
             const Column& col = s->cols[P->query_cols[scol[0]]];
@@ -2652,7 +2693,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // Streamed plan (pgpu_plan_create_execute): equal chunks of segments, each launched as soon as it is planned,
   // so the GPU scans chunk c while the host translates chunk c + 1 (Pinot plans and runs each segment's
   // operator on its own worker thread, BaseCombineOperator.java:85-115).
-  const bool part_eligible = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes &&
+  const bool part_eligible = ((P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes) ||
+                              part_hash_eligible(P, G)) &&
                              !getenv_flag("PGPU_NO_PARTITION");
   // CHAIN / LEAP2 statistics need the direct kernel's register fast path (a pure AND of <= kFastLeaves leaves)
   P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !part_eligible;
@@ -2911,7 +2953,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   Scratch* sc = P->scratch;
   X.nslots = (int)P->slot_kind.size();
   const int nslots = X.nslots;
-  X.words = (int64_t)nslots * P->num_keys;
+  X.words = P->part_hash ? 0 : (int64_t)nslots * P->num_keys;  // hashed partitions: records, no table
   for (auto& e : sc->ev)
     if (!e) HIP_TRY(hipEventCreate(&e));
   if ((int)sc->cev.size() < 2 * max_chunks) {
@@ -3041,7 +3083,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     TRY(sc->slab.ensure((size_t)std::max(max_chunks * P->grid + star_blocks, 1) * X.words * 8));
     kp.slab = sc->slab.as<uint64_t>();
   } else {
-    if (P->mode == MODE_HASH) {
+    if (P->mode == MODE_HASH && !P->part_hash) {
       TRY(sc->hash_keys.ensure((size_t)P->num_keys * 8));
       kp.hash_keys = sc->hash_keys.as<unsigned long long>();
       if (!P->stage_end.empty()) {
@@ -3173,8 +3215,9 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.num_coarse = (P->num_parts + (1 << cshift) - 1) >> cshift;
     pp.chunks_per_coarse = std::max(1, 1024 / pp.num_coarse);
     {  // K8e batch: as many records as fit 96 KB of LDS beside the per-partition counters, a multiple of kBlock
-      const int64_t fixed = (int64_t)part_split_lds(cshift, pp.num_streams, 0);
-      const int64_t b = (96 * 1024 - fixed) / (8 * pp.num_streams + 6) / kBlock * kBlock;
+      const int kb = P->part_hash ? 4 : 2;  // staged key bytes
+      const int64_t fixed = (int64_t)part_split_lds(cshift, pp.num_streams, 0, kb);
+      const int64_t b = (96 * 1024 - fixed) / (8 * pp.num_streams + 4 + kb) / kBlock * kBlock;
       pp.split_batch = (int)std::max<int64_t>(kBlock, std::min<int64_t>(kSplitBatch, b));
     }
     TRY(sc->block_off.ensure((size_t)P->part_grid * pp.num_coarse * 4));
@@ -3188,7 +3231,23 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     }
     pp.coarse_fill = sc->coarse_fill.as<uint32_t>();
     pp.fine_fill = sc->fine_fill.as<uint32_t>();
-    TRY(sc->rec_key.ensure((size_t)cap * 2));
+    if (P->part_hash) {
+      pp.hashed = 1;
+      pp.pbits = P->part_pbits;
+      pp.sbits = P->part_sbits;
+      TRY(sc->rec_key32.ensure((size_t)cap * 4));
+      pp.rec_key32 = sc->rec_key32.as<uint32_t>();
+      // the groups' compacted records, where finalize's compaction of a hash table would put them
+      const int64_t ocap = part_hash_out_cap(P);
+      TRY(sc->ckeys.ensure((size_t)ocap * 8 * (1 + nslots)));
+      TRY(sc->counter.ensure(64));
+      HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
+      pp.out_rec = sc->ckeys.as<uint64_t>();
+      pp.out_count = sc->counter.as<unsigned long long>();
+      P->part_hash_live = true;
+    } else {
+      TRY(sc->rec_key.ensure((size_t)cap * 2));
+    }
     TRY(sc->rec_val.ensure(std::max<size_t>((size_t)cap * 8 * pp.num_streams, 8)));
     pp.part_start = sc->part_start.as<uint32_t>();
     pp.block_off = sc->block_off.as<uint32_t>();
@@ -3323,7 +3382,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     }
     X.leap_nsegs = 0;
   }
-  if (P->mode == MODE_HASH && kp.pack_slot >= 0 &&
+  if (P->mode == MODE_HASH && !P->part_hash && kp.pack_slot >= 0 &&
       launch_hash_unpack(X.table, kp.hash_keys, P->num_keys, kp.pack_slot, kp.pack_shift, stream))
     return fail(PGPU_ERR_DEVICE, "hash unpack launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (X.leap_nsegs > 0 &&  // deferred but no fold ran (cannot happen for a plan with scan tiles; kept exact)
@@ -3478,15 +3537,20 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     }
   } else {
     // hash table: unordered compaction, then key order on the host
-    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0 ? P->merged_records
-                                                                                         : std::max<int64_t>(P->total_docs, 1)));
     const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
-    TRY(sc->counter.ensure(64));
-    TRY(sc->ckeys.ensure((size_t)cap * 8 * rec));
-    HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
-    if (launch_compact(table, sc->hash_keys.as<unsigned long long>(), nslots, G, sc->counter.as<unsigned long long>(),
-                       sc->ckeys.as<uint64_t>(), cap, stream))
-      return fail(PGPU_ERR_DEVICE, "compact launch failed");
+    int64_t cap;
+    if (P->part_hash_live) {  // K8h wrote the compacted records and their count at execute
+      cap = part_hash_out_cap(P);
+    } else {
+      cap = std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0 ? P->merged_records
+                                                                            : std::max<int64_t>(P->total_docs, 1)));
+      TRY(sc->counter.ensure(64));
+      TRY(sc->ckeys.ensure((size_t)cap * 8 * rec));
+      HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
+      if (launch_compact(table, sc->hash_keys.as<unsigned long long>(), nslots, G, sc->counter.as<unsigned long long>(),
+                         sc->ckeys.as<uint64_t>(), cap, stream))
+        return fail(PGPU_ERR_DEVICE, "compact launch failed");
+    }
     TRY(sc->readback.ensure(64));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
@@ -4881,6 +4945,18 @@ int pgpu_plan_leaf_kinds(pgpu_plan P, int64_t* counts) {
   return 0;
 }
 
+int pgpu_plan_group_path(pgpu_plan P, int32_t* path) {
+  PGPU_ABI_GUARD;
+  if (!P || !path) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  const pgpu_plan_s* K = P->composite && !P->parts.empty() ? P->parts[0].plan.get() : P;
+  *path = K->part_hash     ? PGPU_PATH_HASH_PARTITIONED
+          : K->partitioned ? PGPU_PATH_PARTITIONED
+          : K->mode == MODE_HASH ? PGPU_PATH_HASH
+          : K->mode == MODE_GLOBAL ? PGPU_PATH_GLOBAL
+                                   : PGPU_PATH_LDS;
+  return 0;
+}
+
 int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
   PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
@@ -5028,6 +5104,52 @@ int32_t row_owner(const int64_t* ids, int nk, int32_t nparts) {
 }
 }  // namespace
 
+}  // extern "C"
+
+namespace {
+// A fresh hash table of >= 2n slots holding n (key, slot words) records (merged per slot kind): the owner's merge of
+// an exchange, and the materialised table of a K8h plan.
+int build_hash_table(pgpu_plan_s* P, hipStream_t s, const uint64_t* d_records, int64_t n) {
+  Scratch* sc = P->scratch;
+  const int nslots = (int)P->slot_kind.size();
+  int64_t G = 1024;
+  while (G < 2 * n) G <<= 1;
+  // DevBuf growth frees the old buffer with hipFree, which waits for the device: nothing queued still reads it
+  TRY(sc->table.ensure((size_t)nslots * G * 8 + 64));
+  TRY(sc->hash_keys.ensure((size_t)G * 8));
+  P->num_keys = G;
+  P->d_table_used = sc->table.p;
+  if (launch_table_init(sc->table.as<uint64_t>(), P->slot_kind.data(), nslots, G, sc->hash_keys.as<unsigned long long>(), s))
+    return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (launch_merge_records(d_records, n, nslots, P->slot_kind.data(), sc->table.as<uint64_t>(),
+                           sc->hash_keys.as<unsigned long long>(), G, s))
+    return fail(PGPU_ERR_DEVICE, "merge launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+// A K8h plan's groups as the hash table the exchange entries read (pgpu_plan_exchange_counts / _export): the
+// statistics words move out of the (record-less) table buffer first, then the records are inserted.
+int part_hash_materialize(pgpu_plan_s* P, hipStream_t s) {
+  if (!P->part_hash_live) return 0;
+  Scratch* sc = P->scratch;
+  TRY(sc->stats.ensure(64));
+  if (P->d_stats != sc->stats.as<unsigned long long>()) {
+    HIP_TRY(hipMemcpyAsync(sc->stats.p, P->d_stats, 64, hipMemcpyDeviceToDevice, s));
+    P->d_stats = sc->stats.as<unsigned long long>();
+  }
+  TRY(sc->xstage.ensure(64));
+  uint64_t* st = reinterpret_cast<uint64_t*>(sc->xstage.p);
+  HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, s));
+  TRY(wait_plan(P, s));
+  const int64_t n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)part_hash_out_cap(P));
+  TRY(build_hash_table(P, s, sc->ckeys.as<uint64_t>(), n));
+  P->part_hash_live = false;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t* counts) {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
@@ -5035,6 +5157,7 @@ int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t
   if (P->merged_records >= 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "the table already holds merged records");
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
+  TRY(part_hash_materialize(P, s));
   Scratch* sc = P->scratch;
   TRY(sc->counter.ensure((size_t)nparts * 8 + 64));
   HIP_TRY(hipMemsetAsync(sc->counter.p, 0, (size_t)nparts * 8, s));
@@ -5101,19 +5224,9 @@ int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, co
     HIP_TRY(hipMemcpyAsync(sc->stats.p, P->d_stats, 64, hipMemcpyDeviceToDevice, s));
     P->d_stats = sc->stats.as<unsigned long long>();
   }
-  int64_t G = 1024;
-  while (G < 2 * n) G <<= 1;
-  // DevBuf growth frees the old buffer with hipFree, which waits for the device: nothing queued still reads it
-  TRY(sc->table.ensure((size_t)nslots * G * 8 + 64));
-  TRY(sc->hash_keys.ensure((size_t)G * 8));
-  P->num_keys = G;
-  P->d_table_used = sc->table.p;
+  TRY(build_hash_table(P, s, reinterpret_cast<const uint64_t*>(d_records), n));
   P->merged_records = n;
-  if (launch_table_init(sc->table.as<uint64_t>(), P->slot_kind.data(), nslots, G, sc->hash_keys.as<unsigned long long>(), s))
-    return fail(PGPU_ERR_DEVICE, "table init launch failed: %s", hipGetErrorString(hipGetLastError()));
-  if (launch_merge_records(reinterpret_cast<const uint64_t*>(d_records), n, nslots, P->slot_kind.data(),
-                           sc->table.as<uint64_t>(), sc->hash_keys.as<unsigned long long>(), G, s))
-    return fail(PGPU_ERR_DEVICE, "merge launch failed: %s", hipGetErrorString(hipGetLastError()));
+  P->part_hash_live = false;  // the merged table replaces this rank's K8h records
   return 0;
 }
 

@@ -515,6 +515,13 @@ class Plan:
         L.check(self.lib.pgpu_plan_leaf_kinds(self.handle, L.ptr(out, ctypes.c_int64)))
         return {n: int(v) for n, v in zip(L.LEAF_KIND_NAMES, out) if v}
 
+    def group_path(self):
+        """The group-by path of the plan's scan (pgpu_plan_group_path): "lds", "global", "hash", "partitioned" or
+        "hash_partitioned"."""
+        out = ctypes.c_int32(-1)
+        L.check(self.lib.pgpu_plan_group_path(self.handle, ctypes.byref(out)))
+        return L.GROUP_PATH_NAMES[out.value]
+
     def execute(self, stream=None, d_table=None):
         L.check(self.lib.pgpu_plan_execute(self.handle, ctypes.c_void_p(stream or 0), ctypes.c_void_p(d_table or 0)))
 

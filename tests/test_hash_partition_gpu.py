@@ -1,0 +1,82 @@
+"""Hashed partitions (partition.h K8h): sparse group-key spaces (past every dense table, below 2^31) aggregated per
+hash partition in LDS hash tables instead of the global hash table -- against the oracle's LONG_MAP restatement
+(DictionaryBasedGroupKeyGenerator.java:644-746), including partitions that need several K8h rounds, the
+global-hash-table path beside it, a filter, every accumulator kind and the exchange (materialised table)."""
+import numpy as np
+import pytest
+
+from pinot_amd import _lib as L
+from pinot_amd.query import parse_query
+from test_gpu_parity import assert_same, gpu_table
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = [("a", "INT"), ("b", "INT"), ("c", "INT"), ("m", "INT"), ("x", "DOUBLE")]
+DOCS = 120000
+
+
+def _columns(seed):
+    rng = np.random.default_rng(seed)
+    return {"a": rng.integers(0, 3000, DOCS).astype(np.int64), "b": rng.integers(0, 3000, DOCS).astype(np.int64),
+            "c": rng.integers(0, 30, DOCS).astype(np.int64), "m": rng.integers(-400, 900, DOCS).astype(np.int64),
+            "x": np.round(rng.uniform(-1e4, 1e4, DOCS), 3)}
+
+
+@pytest.fixture(scope="module")
+def sparse(oracle, gpu_lib):
+    segs = [oracle.make_segment(SCHEMA, _columns(41 + s)) for s in range(2)]
+    t, hs = gpu_table(SCHEMA, segs)
+    yield t, hs, segs
+    t.close()
+
+
+QUERIES = [
+    "SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c",
+    "SELECT MIN(m), MAX(x), SUM(x), AVG(m), COUNT(*) FROM t WHERE c < 20 GROUP BY a, b, c",
+    "SELECT SUM(m), MAX(m) FROM t WHERE m > 0 AND c IN (1, 3, 5, 7) GROUP BY c, a, b",
+]
+
+
+@pytest.mark.parametrize("sql", QUERIES)
+def test_hash_partitions_match_oracle(oracle, sparse, sql):
+    t, hs, segs = sparse
+    q = parse_query(sql, num_groups_limit=10 ** 9)
+    with t.plan(hs, q) as p:
+        assert p.group_path() == "hash_partitioned"
+    assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+
+
+def test_hash_partition_rounds(oracle, sparse, monkeypatch):
+    """One partition of 2^sbits LDS slots for ~2e5 groups: K8h loops over rounds, each placing the keys that find a
+    slot and compacting the rest in place."""
+    t, hs, segs = sparse
+    monkeypatch.setenv("PGPU_PART_HASH_PBITS", "0")
+    for sql in QUERIES[:2]:
+        q = parse_query(sql, num_groups_limit=10 ** 9)
+        q.no_plan_cache = True  # planned afresh under the knob
+        with t.plan(hs, q) as p:
+            assert p.group_path() == "hash_partitioned"
+        assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+
+
+def test_hash_partitions_exchange_materialises_table(oracle, sparse):
+    """pgpu_plan_exchange_counts / _export / _merge on a hashed-partition plan: its records become a hash table
+    first; one part exported and merged back gives the plan's own groups."""
+    import ctypes
+    t, hs, segs = sparse
+    q = parse_query(QUERIES[0], num_groups_limit=10 ** 9)
+    plan = t.plan_execute(hs, q)
+    try:
+        lib = plan.lib
+        counts = (ctypes.c_int64 * 1)()
+        L.check(lib.pgpu_plan_exchange_counts(plan.handle, None, 1, counts))
+        exp = oracle.run_groupby(SCHEMA, segs, q)
+        assert counts[0] == len(exp.groups)
+        import torch
+        out = torch.empty((counts[0], 3), dtype=torch.int64, device="cuda")
+        L.check(lib.pgpu_plan_exchange_export(plan.handle, None, 1, None, ctypes.c_void_p(out.data_ptr()),
+                                              counts[0]))
+        L.check(lib.pgpu_plan_exchange_merge(plan.handle, None, None, ctypes.c_void_p(out.data_ptr()), counts[0]))
+        assert_same(plan.finalize(), exp, q, SCHEMA)
+    finally:
+        plan.close()

@@ -136,7 +136,8 @@ CALIB_SQL = {
     "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
     "c5_hash": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
 }
-SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel", "part_aggregate_kernel")
+SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel", "part_aggregate_kernel",
+                "part_hash_aggregate_kernel")
 # the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch)
 LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false>")
 

@@ -368,7 +368,7 @@ int64_t simulate_entries_scanned(const StatTree& t, const std::vector<const uint
 // ================================================================================================ C ABI
 extern "C" int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t num_filter_ops,
                                            const int32_t* leaf_types, const uint32_t* const* leaf_masks,
-                                           int32_t num_leaves, int32_t num_docs, int64_t* out) {
+                                           int32_t num_leaves, int32_t num_docs, int64_t* out) try {
   using namespace pgpu;
   if (!out || num_leaves < 0 || num_filter_ops < 0 || num_docs < 0 || (num_filter_ops && !filter) ||
       (num_leaves && !leaf_types))
@@ -403,4 +403,4 @@ extern "C" int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t
   }
   *out = simulate_entries_scanned(build_stat_tree(ops, types), masks, num_docs);
   return 0;
-}
+} PGPU_ABI_CATCH

@@ -141,6 +141,19 @@ int pgpu::host_fail(int code, const char* fmt, ...) {
   return code;
 }
 
+int pgpu::abi_exception() noexcept {
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return PGPU_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    return host_fail(PGPU_ERR_INVALID_ARGUMENT, "internal error: %s", e.what());
+  } catch (...) {
+    return host_fail(PGPU_ERR_INVALID_ARGUMENT, "internal error");
+  }
+}
+
 namespace {
 
 #define HIP_TRY(expr)                                                                               \
@@ -4112,7 +4125,7 @@ std::mutex g_init_mu;
 int g_init_devices = 0;
 }  // namespace
 
-int pgpu_init(int n_gpus) {
+int pgpu_init(int n_gpus) try {
   PGPU_ABI_GUARD;
   install_crash_trace();
   int count = 0;
@@ -4130,9 +4143,9 @@ int pgpu_init(int n_gpus) {
   g_init_devices = std::max(g_init_devices, n);
   host_pool();  // the planning workers start here, not inside the first query
   return n;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_shutdown(void) {
+int pgpu_shutdown(void) try {
   PGPU_ABI_GUARD;
   std::lock_guard<std::mutex> g(g_init_mu);
   int prev = 0;
@@ -4143,18 +4156,18 @@ int pgpu_shutdown(void) {
   }
   HIP_TRY(hipSetDevice(prev));
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_last_error(char* buf, size_t len) {
+int pgpu_last_error(char* buf, size_t len) try {
   if (buf && len) {
     size_t n = std::min(len - 1, g_err.size());
     memcpy(buf, g_err.data(), n);
     buf[n] = 0;
   }
   return (int)g_err.size();
-}
+} PGPU_ABI_CATCH
 
-int pgpu_device_count(int* count) {
+int pgpu_device_count(int* count) try {
   PGPU_ABI_GUARD;
   if (!count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null count");
   int n = 0;
@@ -4162,9 +4175,9 @@ int pgpu_device_count(int* count) {
   if (e != hipSuccess) { *count = 0; return fail(PGPU_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
   *count = n;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_create(int device, int num_columns, const char* const* names, const int32_t* types, pgpu_table* out) {
+int pgpu_table_create(int device, int num_columns, const char* const* names, const int32_t* types, pgpu_table* out) try {
   PGPU_ABI_GUARD;
   install_crash_trace();
   if (!out || num_columns <= 0 || !types) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad table arguments");
@@ -4191,9 +4204,9 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
     t->num_cus = cus;
   *out = t.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_destroy(pgpu_table t) {
+int pgpu_table_destroy(pgpu_table t) try {
   PGPU_ABI_GUARD;
   if (!t) return 0;
   DeviceGuard g(t->device);
@@ -4212,9 +4225,9 @@ int pgpu_table_destroy(pgpu_table t) {
   hipStreamDestroy(t->stream);
   delete t;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) {
+int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) try {
   PGPU_ABI_GUARD;
   if (!t || !d || !handle) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (d->num_columns != (int)t->names.size())
@@ -4338,9 +4351,9 @@ int pgpu_pin_segment(pgpu_table t, const pgpu_segment_desc* d, int64_t* handle) 
   if (any_raw) TRY(ensure_docid(t, d->num_docs, t->stream));
   *handle = register_segment(t, std::move(seg));
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_unpin_segment(pgpu_table t, int64_t h) {
+int pgpu_unpin_segment(pgpu_table t, int64_t h) try {
   PGPU_ABI_GUARD;
   if (t) t->version++;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
@@ -4358,7 +4371,7 @@ int pgpu_unpin_segment(pgpu_table t, int64_t h) {
   plan_cache_clear(t);  // cached plans reference the segment set of their time
   hipStreamSynchronize(t->stream);  // work queued on the table's own stream (pins, reads) is done with it
   return 0;
-}
+} PGPU_ABI_CATCH
 
 namespace {
 // Portable RoaringBitmap deserialisation (RoaringBitmap 0.9.x RoaringArray.deserialize, little-endian): cookie
@@ -4527,7 +4540,7 @@ void serialize_roaring_plain(const int32_t* docs, int64_t n, std::vector<uint8_t
 // seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:60-78): dictIds of the MSB-first fixed-bit
 // forward index -> per dictId the sorted docIds -> (card + 1) BE offsets + serialised bitmaps.
 int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, int32_t num_docs, int32_t cardinality,
-                              void* out, int64_t out_cap, int64_t* out_len) {
+                              void* out, int64_t out_cap, int64_t* out_len) try {
   PGPU_ABI_GUARD;
   if (!fwd || !out_len || bits < 1 || bits > 31 || num_docs < 0 || cardinality < 1 ||
       fwd_len < ((int64_t)num_docs * bits + 7) / 8)
@@ -4570,10 +4583,10 @@ int pgpu_build_inverted_index(const void* fwd, int64_t fwd_len, int32_t bits, in
   }
   memcpy(o + hdr, body.data(), body.size());
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_raw_forward_index_values(const void* fwd, int64_t fwd_len, int32_t data_type, int32_t num_docs,
-                                  int64_t* out_i64, double* out_f64) {
+                                  int64_t* out_i64, double* out_f64) try {
   PGPU_ABI_GUARD;
   if (!fwd || num_docs < 0 || data_type < PGPU_INT || data_type > PGPU_STRING)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -4584,10 +4597,10 @@ int pgpu_raw_forward_index_values(const void* fwd, int64_t fwd_len, int32_t data
     if (out_f64) out_f64[i] = v.val[i];
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_inverted_index_check(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
-                              int64_t* total_docs) {
+                              int64_t* total_docs) try {
   PGPU_ABI_GUARD;
   if (!bytes && num_bytes) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   InvIndex inv;
@@ -4599,9 +4612,9 @@ int pgpu_inverted_index_check(const void* bytes, int64_t num_bytes, int32_t card
     for (const auto& e : inv.ids) *total_docs += e.docs;
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) {
+int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) try {
   PGPU_ABI_GUARD;
   if (t) t->version++;
   if (t) plan_cache_clear(t);
@@ -4624,7 +4637,7 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
   t->device_bytes += inv->bytes;
   col.inv = inv;
   return 0;
-}
+} PGPU_ABI_CATCH
 
 }  // extern "C"
 
@@ -4681,7 +4694,7 @@ int validate_startree(const pgpu_startree_desc* d, const std::vector<int32_t>& d
 
 extern "C" {
 
-int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
+int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) try {
   PGPU_ABI_GUARD;
   if (t) t->version++;
   if (t) plan_cache_clear(t);
@@ -4768,20 +4781,20 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) {
   t->device_bytes += bytes;
   seg.star = std::move(st);
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_num_segments(pgpu_table t, int32_t* count) {
+int pgpu_table_num_segments(pgpu_table t, int32_t* count) try {
   PGPU_ABI_GUARD;
   if (!t || !count) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(t->mu);
   *count = (int32_t)t->segments.size();
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int64_t pgpu_table_device_bytes(pgpu_table t) { return t ? t->device_bytes : 0; }
 
 int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int64_t* vi, const double* vd,
-                                     const uint8_t* blob, const int64_t* offsets) {
+                                     const uint8_t* blob, const int64_t* offsets) try {
   PGPU_ABI_GUARD;
   if (t) t->version++;
   if (t) plan_cache_clear(t);
@@ -4805,35 +4818,35 @@ int pgpu_table_add_dictionary_values(pgpu_table t, int col, int64_t n, const int
   std::lock_guard<std::mutex> lk(t->mu);
   if (merge_dict(t->global[col], d)) t->global_version[col]++;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_dictionary_size(pgpu_table t, int col, int64_t* size) {
+int pgpu_table_dictionary_size(pgpu_table t, int col, int64_t* size) try {
   PGPU_ABI_GUARD;
   if (!t || !size || col < 0 || col >= (int)t->names.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
   *size = (int64_t)t->global[col]->size();
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_dictionary_i64(pgpu_table t, int col, int64_t* out) {
+int pgpu_table_dictionary_i64(pgpu_table t, int col, int64_t* out) try {
   PGPU_ABI_GUARD;
   if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_int_type(t->types[col]))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
   std::copy(t->global[col]->iv.begin(), t->global[col]->iv.end(), out);
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_dictionary_f64(pgpu_table t, int col, double* out) {
+int pgpu_table_dictionary_f64(pgpu_table t, int col, double* out) try {
   PGPU_ABI_GUARD;
   if (!t || !out || col < 0 || col >= (int)t->names.size() || !is_fp_type(t->types[col]))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::lock_guard<std::mutex> lk(t->mu);
   std::copy(t->global[col]->dv.begin(), t->global[col]->dv.end(), out);
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap, int64_t* offsets) {
+int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap, int64_t* offsets) try {
   PGPU_ABI_GUARD;
   if (!t || !offsets || col < 0 || col >= (int)t->names.size() || t->types[col] != PGPU_STRING)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -4850,9 +4863,9 @@ int pgpu_table_dictionary_str(pgpu_table t, int col, uint8_t* blob, int64_t cap,
     offsets[i + 1] = off;
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, int32_t n, int32_t* out) {
+int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, int32_t n, int32_t* out) try {
   PGPU_ABI_GUARD;
   if (!t || (n > 0 && (!docs || !out))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
@@ -4878,10 +4891,10 @@ int pgpu_read_dict_ids(pgpu_table t, int64_t h, int col, const int32_t* docs, in
   HIP_TRY(hipFreeAsync(d_out, t->stream));
   HIP_TRY(hipStreamSynchronize(t->stream));
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bits, int64_t start, int64_t n,
-                                 int32_t* d_out, void* stream) {
+                                 int32_t* d_out, void* stream) try {
   PGPU_ABI_GUARD;
   if (bits < 1 || bits > 31 || start < 0 || n < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   // the two-word gather reads up to word ((start+n-1)*bits >> 5) + 1
@@ -4892,9 +4905,9 @@ int pgpu_unpack_fixed_bit_device(const void* d_fwd, int64_t fwd_len, int32_t bit
   if (launch_unpack(reinterpret_cast<const uint32_t*>(d_fwd), bits, start, n, d_out, stream))
     return fail(PGPU_ERR_DEVICE, "unpack launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan* out) {
+int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan* out) try {
   PGPU_ABI_GUARD;
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
@@ -4917,35 +4930,35 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   P->scratch = acquire_scratch(t);
   *out = P.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_destroy(pgpu_plan P) {
+int pgpu_plan_destroy(pgpu_plan P) try {
   PGPU_ABI_GUARD;
   if (!P) return 0;
   for (auto& part : P->parts) release_scratch(P->table, part.plan->scratch);
   release_scratch(P->table, P->scratch);
   delete P;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_cancel(pgpu_plan P) {
+int pgpu_plan_cancel(pgpu_plan P) try {
   // no ABI guard: the canceller must not wait behind the query thread's own entry points
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   __atomic_store_n(&P->cancel, 1, __ATOMIC_RELEASE);
   for (auto& part : P->parts) __atomic_store_n(&part.plan->cancel, 1, __ATOMIC_RELEASE);
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_leaf_kinds(pgpu_plan P, int64_t* counts) {
+int pgpu_plan_leaf_kinds(pgpu_plan P, int64_t* counts) try {
   PGPU_ABI_GUARD;
   if (!P || !counts) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   for (int k = 0; k < kLeafKinds; ++k) counts[k] = P->leaf_kinds[k];
   for (const auto& part : P->parts)
     for (int k = 0; k < kLeafKinds; ++k) counts[k] += part.plan->leaf_kinds[k];
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_group_path(pgpu_plan P, int32_t* path) {
+int pgpu_plan_group_path(pgpu_plan P, int32_t* path) try {
   PGPU_ABI_GUARD;
   if (!P || !path) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const pgpu_plan_s* K = P->composite && !P->parts.empty() ? P->parts[0].plan.get() : P;
@@ -4955,9 +4968,9 @@ int pgpu_plan_group_path(pgpu_plan P, int32_t* path) {
           : K->mode == MODE_GLOBAL ? PGPU_PATH_GLOBAL
                                    : PGPU_PATH_LDS;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) {
+int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t* kinds) try {
   PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: its parts have their own group tables");
@@ -4965,10 +4978,10 @@ int pgpu_plan_layout(pgpu_plan P, int32_t* num_slots, int64_t* num_keys, int32_t
   if (num_keys) *num_keys = P->hash ? 0 : P->num_keys;
   if (kinds) for (size_t i = 0; i < P->slot_kind.size(); ++i) kinds[i] = P->slot_kind[i];
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
-                             void* d_table, pgpu_plan* out) {
+                             void* d_table, pgpu_plan* out) try {
   PGPU_ABI_GUARD;
   if (!t || !out || (nsegs > 0 && !handles) || nsegs < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const double tt0 = trace_on() ? now_us() : 0;
@@ -5020,9 +5033,9 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   }
   *out = P.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
+int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) try {
   PGPU_ABI_GUARD;
   if (!P) return fail(PGPU_ERR_INVALID_ARGUMENT, "null plan");
   if (P->composite) {
@@ -5035,9 +5048,9 @@ int pgpu_plan_execute(pgpu_plan P, void* stream, void* d_table) {
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   return plan_execute_impl(P, s, d_table);
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_result* out) {
+int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(P->table->device);
@@ -5054,10 +5067,10 @@ int pgpu_plan_finalize(pgpu_plan P, void* stream, const void* d_table, pgpu_resu
   }
   *out = R.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shard, int64_t key_begin,
-                             int64_t key_count, pgpu_result* out) {
+                             int64_t key_count, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!P || !out || !d_table_shard || key_begin < 0 || key_count < 0 || key_begin + key_count > P->num_keys)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -5070,7 +5083,7 @@ int pgpu_plan_finalize_range(pgpu_plan P, void* stream, const void* d_table_shar
   TRY(plan_finalize_impl(P, s, d_table_shard, key_begin, key_count, R.get()));
   *out = R.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
 // ---- cross-GPU combine of hash-mode tables (device records) and of any finalized result (host rows)
 namespace {
@@ -5150,7 +5163,7 @@ int part_hash_materialize(pgpu_plan_s* P, hipStream_t s) {
 
 extern "C" {
 
-int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t* counts) {
+int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t* counts) try {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
   if (nparts < 1 || nparts > 64 || !counts) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -5173,10 +5186,10 @@ int pgpu_plan_exchange_counts(pgpu_plan P, void* stream, int32_t nparts, int64_t
   P->xchg_counts.assign(nparts, 0);
   for (int p = 0; p < nparts; ++p) counts[p] = P->xchg_counts[p] = (int64_t)st[p];
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_plan_exchange_export(pgpu_plan P, void* stream, int32_t nparts, const int32_t* kinds, void* d_out,
-                              int64_t cap) {
+                              int64_t cap) try {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
   if ((int32_t)P->xchg_counts.size() != nparts || nparts < 1)
@@ -5204,9 +5217,9 @@ int pgpu_plan_exchange_export(pgpu_plan P, void* stream, int32_t nparts, const i
   // the staged cursors must stay put until the upload ran: the next use of xstage waits for this stream
   HIP_TRY(hipStreamSynchronize(s));
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, const void* d_records, int64_t n) {
+int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, const void* d_records, int64_t n) try {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
   if (n < 0 || (n > 0 && !d_records) || n > (INT64_C(1) << 40))  // the table below holds >= 2n slots
@@ -5228,18 +5241,18 @@ int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, co
   P->merged_records = n;
   P->part_hash_live = false;  // the merged table replaces this rank's K8h records
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_slot_kinds(pgpu_result r, int32_t* num_slots, int32_t* kinds) {
+int pgpu_result_slot_kinds(pgpu_result r, int32_t* num_slots, int32_t* kinds) try {
   PGPU_ABI_GUARD;
   if (!r) return fail(PGPU_ERR_INVALID_ARGUMENT, "null result");
   if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
   if (num_slots) *num_slots = r->num_slots;
   if (kinds) for (int i = 0; i < r->num_slots; ++i) kinds[i] = r->slot_kind[i];
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kinds, int64_t* rows, int64_t* counts) {
+int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kinds, int64_t* rows, int64_t* counts) try {
   PGPU_ABI_GUARD;
   if (!r || nparts < 1 || nparts > (1 << 20) || !counts || (r->n > 0 && !rows))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -5269,9 +5282,9 @@ int pgpu_result_exchange_rows(pgpu_result r, int32_t nparts, const int32_t* kind
     }
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, const int32_t* kinds, pgpu_result* out) {
+int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, const int32_t* kinds, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!tmpl || !out || n < 0 || (n > 0 && !rows)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if ((int)tmpl->slot_kind.size() != tmpl->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
@@ -5359,16 +5372,16 @@ int pgpu_result_merge_rows(pgpu_result tmpl, const int64_t* rows, int64_t n, con
   R->groups_limit_reached = tmpl->groups_limit_reached;
   *out = R.release();
   return 0;
-}
+} PGPU_ABI_CATCH
 
 // ---- communicator and the one-call cross-GPU combine (comm.h / comm.cpp)
-int pgpu_comm_unique_id(int32_t kind, void* id) {
+int pgpu_comm_unique_id(int32_t kind, void* id) try {
   PGPU_ABI_GUARD;
   if (!id) return fail(PGPU_ERR_INVALID_ARGUMENT, "null id");
   return pgpu::comm_unique_id(kind, id);
-}
+} PGPU_ABI_CATCH
 
-int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, pgpu_comm* out) {
+int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, pgpu_comm* out) try {
   PGPU_ABI_GUARD;
   if (!out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null out");
   pgpu::Comm* c = nullptr;
@@ -5377,30 +5390,30 @@ int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank,
   h->impl = c;
   *out = h;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_comm_destroy(pgpu_comm c) {
+int pgpu_comm_destroy(pgpu_comm c) try {
   PGPU_ABI_GUARD;
   if (!c) return 0;
   delete c->impl;
   delete c;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_comm_rank(pgpu_comm c, int32_t* rank, int32_t* nranks) {
+int pgpu_comm_rank(pgpu_comm c, int32_t* rank, int32_t* nranks) try {
   PGPU_ABI_GUARD;
   if (!c) return fail(PGPU_ERR_INVALID_ARGUMENT, "null communicator");
   if (rank) *rank = c->impl->rank;
   if (nranks) *nranks = c->impl->nranks;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_comm_allgather(pgpu_comm c, const void* send, int64_t bytes, void* recv) {
+int pgpu_comm_allgather(pgpu_comm c, const void* send, int64_t bytes, void* recv) try {
   PGPU_ABI_GUARD;
   if (!c || bytes < 0 || (bytes > 0 && (!send || !recv))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(c->impl->device);
   return c->impl->allgather_host(send, (size_t)bytes, recv);
-}
+} PGPU_ABI_CATCH
 
 namespace {
 // Content hash of a dictionary snapshot (computed once per snapshot): ranks compare their key spaces with it.
@@ -5473,7 +5486,7 @@ int agree_kinds(const std::vector<int64_t>& all, int nranks, int ns, int32_t* ki
 }
 }  // namespace
 
-int pgpu_plan_combine_mode(pgpu_plan P, pgpu_comm c, int64_t shard_bytes, int32_t* mode, int32_t* kinds) {
+int pgpu_plan_combine_mode(pgpu_plan P, pgpu_comm c, int64_t shard_bytes, int32_t* mode, int32_t* kinds) try {
   PGPU_ABI_GUARD;
   if (!P || !c || !mode) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   const int N = c->impl->nranks;
@@ -5529,10 +5542,10 @@ int pgpu_plan_combine_mode(pgpu_plan P, pgpu_comm c, int64_t shard_bytes, int32_
   if (kinds) TRY(agree_kinds(all, N, (int)mine[CI_SLOTS], kinds));
   *mode = agreed;
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int32_t mode, const int32_t* kinds,
-                      void* d_shard, int64_t* key_begin, int64_t* key_count) {
+                      void* d_shard, int64_t* key_begin, int64_t* key_count) try {
   PGPU_ABI_GUARD;
   if (!P || !c) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (mode == PGPU_COMBINE_LOCAL) {
@@ -5637,9 +5650,9 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
   if (key_begin) *key_begin = begin;
   if (key_count) *key_count = count;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) {
+int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!r || !c || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
@@ -5677,10 +5690,10 @@ int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) {
   std::vector<int64_t> recv((size_t)std::max<int64_t>(nrecv, 1) * w);
   TRY(C->alltoallv_host(rows.data(), counts.data(), recv.data(), rcount.data(), (size_t)w * 8));
   return pgpu_result_merge_rows(r, nrecv ? recv.data() : nullptr, nrecv, kinds.data(), out);
-}
+} PGPU_ABI_CATCH
 
 int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, void* stream,
-                         pgpu_result* out) {
+                         pgpu_result* out) try {
   PGPU_ABI_GUARD;
   pgpu_plan P = nullptr;
   TRY(pgpu_plan_create_execute(t, handles, nsegs, q, stream, nullptr, &P));
@@ -5689,16 +5702,16 @@ int pgpu_execute_groupby(pgpu_table t, const int64_t* handles, int32_t nsegs, co
   pgpu_plan_destroy(P);
   g_err = keep;
   return rc;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_scanned_segments(pgpu_plan P, uint8_t* out) {
+int pgpu_plan_scanned_segments(pgpu_plan P, uint8_t* out) try {
   PGPU_ABI_GUARD;
   if (!P || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null argument");
   if (!P->seg_scanned.empty()) memcpy(out, P->seg_scanned.data(), P->seg_scanned.size());
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
+int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) try {
   PGPU_ABI_GUARD;
   if (!P || !out3) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   int64_t nodes = 0;
@@ -5707,9 +5720,9 @@ int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) {
   out3[1] = nodes;
   out3[2] = P->star_docs_read;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_plan_timing(pgpu_plan P, double* out3) {
+int pgpu_plan_timing(pgpu_plan P, double* out3) try {
   PGPU_ABI_GUARD;
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: timing is per part");
@@ -5730,41 +5743,41 @@ int pgpu_plan_timing(pgpu_plan P, double* out3) {
   out3[2] = P->num_tiles > 0 ? (double)P->launches_done : 0.0;
   out3[3] = st * 1000.0;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_num_groups(pgpu_result r, int64_t* n) {
+int pgpu_result_num_groups(pgpu_result r, int64_t* n) try {
   PGPU_ABI_GUARD;
   if (!r || !n) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   *n = r->n;
   return 0;
-}
+} PGPU_ABI_CATCH
 static const Dict* result_dict(pgpu_result r, int key) {
   if (!r || key < 0 || key >= r->num_keys || key >= (int)r->key_dicts.size() || !r->key_dicts[key]) return nullptr;
   return static_cast<const Dict*>(r->key_dicts[key].get());
 }
-int pgpu_result_key_dictionary(pgpu_result r, int key, uint64_t* snapshot_id, int64_t* size) {
+int pgpu_result_key_dictionary(pgpu_result r, int key, uint64_t* snapshot_id, int64_t* size) try {
   PGPU_ABI_GUARD;
   const Dict* d = result_dict(r, key);
   if (!d) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad group-by key %d", key);
   if (snapshot_id) *snapshot_id = d->id;
   if (size) *size = (int64_t)d->size();
   return 0;
-}
-int pgpu_result_key_dictionary_i64(pgpu_result r, int key, int64_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_key_dictionary_i64(pgpu_result r, int key, int64_t* out) try {
   PGPU_ABI_GUARD;
   const Dict* d = result_dict(r, key);
   if (!d || !out || !is_int_type(d->type)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::copy(d->iv.begin(), d->iv.end(), out);
   return 0;
-}
-int pgpu_result_key_dictionary_f64(pgpu_result r, int key, double* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_key_dictionary_f64(pgpu_result r, int key, double* out) try {
   PGPU_ABI_GUARD;
   const Dict* d = result_dict(r, key);
   if (!d || !out || !is_fp_type(d->type)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::copy(d->dv.begin(), d->dv.end(), out);
   return 0;
-}
-int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_t cap, int64_t* offsets) {
+} PGPU_ABI_CATCH
+int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_t cap, int64_t* offsets) try {
   PGPU_ABI_GUARD;
   const Dict* d = result_dict(r, key);
   if (!d || !offsets || d->type != PGPU_STRING) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -5779,8 +5792,8 @@ int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_
     offsets[i + 1] = off;
   }
   return 0;
-}
-int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_group_ids(pgpu_result r, int32_t* out) try {
   PGPU_ABI_GUARD;
   if (!r || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
@@ -5790,22 +5803,22 @@ int pgpu_result_group_ids(pgpu_result r, int32_t* out) {
     for (int64_t i = 0; i < r->n; ++i) out[i * nk + j] = g[i];
   }
   return 0;
-}
-int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out) try {
   PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->n) memcpy(out, r->gid(key), (size_t)r->n * 4);
   return 0;
-}
-int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out) {
+} PGPU_ABI_CATCH
+int pgpu_result_group_ids_view(pgpu_result r, int key, const int32_t** out) try {
   PGPU_ABI_GUARD;
   if (!r || key < 0 || key >= r->num_keys || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   *out = r->gid(key);
   return 0;
-}
-int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form) {
+} PGPU_ABI_CATCH
+int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t* form) try {
   PGPU_ABI_GUARD;
   if (!r || agg < -1 || agg >= r->num_aggs || !out || !form) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
@@ -5817,8 +5830,8 @@ int pgpu_result_words_view(pgpu_result r, int agg, const uint64_t** out, int32_t
   *out = r->slot(r->agg_slot[agg]);
   *form = r->agg_conv[agg];
   return 0;
-}
-int pgpu_result_values(pgpu_result r, int agg, double* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_values(pgpu_result r, int agg, double* out) try {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
@@ -5829,42 +5842,42 @@ int pgpu_result_values(pgpu_result r, int agg, double* out) {
     default: for (int64_t i = 0; i < r->n; ++i) out[i] = key_double((int64_t)w[i]); break;
   }
   return 0;
-}
-int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_avg_counts(pgpu_result r, int agg, int64_t* out) try {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->n) memcpy(out, r->slot(0), (size_t)r->n * 8);  // slot 0 = COUNT = AvgPair.count
   return 0;
-}
-int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_values_i64(pgpu_result r, int agg, int64_t* out) try {
   PGPU_ABI_GUARD;
   if (!r || agg < 0 || agg >= r->num_aggs || (!out && r->n)) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));  // compact: columnar form first
   if (r->agg_conv[agg] != RCONV_I64) return fail(PGPU_ERR_INVALID_ARGUMENT, "aggregation %d is floating point", agg);
   if (r->n) memcpy(out, r->slot(r->agg_slot[agg]), (size_t)r->n * 8);
   return 0;
-}
-int pgpu_result_stats(pgpu_result r, int64_t* out6) {
+} PGPU_ABI_CATCH
+int pgpu_result_stats(pgpu_result r, int64_t* out6) try {
   PGPU_ABI_GUARD;
   if (!r || !out6) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   memcpy(out6, r->stats, sizeof r->stats);
   return 0;
-}
-int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out) {
+} PGPU_ABI_CATCH
+int pgpu_result_groups_limit_reached(pgpu_result r, int32_t* out) try {
   PGPU_ABI_GUARD;
   if (!r || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   *out = r->groups_limit_reached ? 1 : 0;
   return 0;
-}
-int pgpu_result_destroy(pgpu_result r) {
+} PGPU_ABI_CATCH
+int pgpu_result_destroy(pgpu_result r) try {
   PGPU_ABI_GUARD;
   delete r;
   return 0;
-}
+} PGPU_ABI_CATCH
 int pgpu_free_result(pgpu_result r) { return pgpu_result_destroy(r); }
 
-int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* out_words) {
+int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* out_words) try {
   PGPU_ABI_GUARD;
   if (!t || !q || !out_words) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   DeviceGuard g(t->device);
@@ -5930,10 +5943,10 @@ int pgpu_filter_bitmap(pgpu_table t, int64_t h, const pgpu_query* q, uint64_t* o
   } while (0);
   release_scratch(t, sc);
   return rc;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_generate_segment(pgpu_table t, const pgpu_gen_column* gc, int32_t ncols, int64_t row0, int32_t num_docs,
-                          int64_t* handle) {
+                          int64_t* handle) try {
   PGPU_ABI_GUARD;
   if (!t || !gc || !handle || ncols != (int)t->names.size() || num_docs < 0)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -6063,10 +6076,10 @@ int pgpu_generate_segment(pgpu_table t, const pgpu_gen_column* gc, int32_t ncols
   std::lock_guard<std::mutex> lk(t->mu);
   *handle = register_segment(t, std::move(seg));
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_segment_column_info(pgpu_table t, int64_t h, int col, int32_t* card, int32_t* bits, int64_t* dict_len,
-                             int64_t* fwd_len) {
+                             int64_t* fwd_len) try {
   PGPU_ABI_GUARD;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   std::lock_guard<std::mutex> lk(t->mu);
@@ -6079,9 +6092,9 @@ int pgpu_segment_column_info(pgpu_table t, int64_t h, int col, int32_t* card, in
   if (dict_len) *dict_len = (int64_t)c.raw_dict.size();
   if (fwd_len) *fwd_len = c.fwd_bytes;
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_segment_column_bytes(pgpu_table t, int64_t h, int col, uint8_t* dict_out, uint8_t* fwd_out) {
+int pgpu_segment_column_bytes(pgpu_table t, int64_t h, int col, uint8_t* dict_out, uint8_t* fwd_out) try {
   PGPU_ABI_GUARD;
   if (!t) return fail(PGPU_ERR_INVALID_ARGUMENT, "null table");
   DeviceGuard g(t->device);
@@ -6100,6 +6113,6 @@ int pgpu_segment_column_bytes(pgpu_table t, int64_t h, int col, uint8_t* dict_ou
     HIP_TRY(hipStreamSynchronize(t->stream));
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
 }  // extern "C"

@@ -336,7 +336,7 @@ void json_str(std::string& o, const std::string& s) {
 // ================================================================================================ C ABI
 extern "C" {
 
-int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* out) {
+int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* out) try {
   if (!r || !spec || !out || spec->num_order_by < 0 || (spec->num_order_by && !spec->order_by) || spec->limit < 0)
     return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire))
@@ -366,10 +366,10 @@ int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* 
     std::iota(rows.begin(), rows.end(), 0);
   }
   return copy_rows(r, rows, out);
-}
+} PGPU_ABI_CATCH
 
 int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, int64_t* rows, int64_t cap,
-                         int64_t* counts) {
+                         int64_t* counts) try {
   if (!r || !counts || limit <= 0) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire))
     if (const int rc = pgpu::result_expand(r)) return rc;  // compact results: columnar form first
@@ -393,9 +393,9 @@ int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, in
     std::copy(top.begin(), top.end(), rows + (int64_t)a * cap);
   }
   return 0;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_result_datatable(pgpu_result r, pgpu_table t, void* out, int64_t cap, int64_t* len) {
+int pgpu_result_datatable(pgpu_result r, pgpu_table t, void* out, int64_t cap, int64_t* len) try {
   if (!r || !t || !len) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   if (r->compact.load(std::memory_order_acquire))
     if (const int rc = pgpu::result_expand(r)) return rc;  // compact results: columnar form first
@@ -514,10 +514,10 @@ int pgpu_result_datatable(pgpu_result r, pgpu_table t, void* out, int64_t cap, i
   if (cap < *len) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "output buffer too small");
   memcpy(out, o.b.data(), o.b.size());
   return 0;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32_t num_tables,
-                           const pgpu_sql_trim* spec, char* json, int64_t cap, int64_t* len) {
+                           const pgpu_sql_trim* spec, char* json, int64_t cap, int64_t* len) try {
   if (!tables || !lens || num_tables < 0 || !spec || !len) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   std::vector<Table> T(num_tables);
   std::string err;
@@ -704,6 +704,6 @@ int pgpu_broker_reduce_sql(const void* const* tables, const int64_t* lens, int32
   if (cap < *len + 1) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "output buffer too small");
   memcpy(json, o.c_str(), o.size() + 1);
   return 0;
-}
+} PGPU_ABI_CATCH
 
 }  // extern "C"

@@ -437,7 +437,7 @@ extern "C" {
 
 int pgpu_startree_load(const void* index, int64_t index_len, const char* index_map, int64_t index_map_len,
                        int32_t star_tree_id, int32_t num_docs, int32_t num_columns, const char* const* column_names,
-                       const int32_t* bits_per_element, pgpu_startree* out) {
+                       const int32_t* bits_per_element, pgpu_startree* out) try {
   if (!index || index_len < 0 || !index_map || index_map_len < 0 || num_docs < 0 || num_columns < 1 || !column_names ||
       !bits_per_element || !out)
     return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree load arguments");
@@ -554,11 +554,11 @@ int pgpu_startree_load(const void* index, int64_t index_len, const char* index_m
   st->num_raw_records = -1;  // not recorded in the files
   *out = st.release();
   return PGPU_OK;
-}
+} PGPU_ABI_CATCH
 
 int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_types, const int32_t* split_order,
                         int32_t num_dims, const int32_t* skip_star_dims, int32_t num_skip, const pgpu_agg* pairs,
-                        int32_t num_pairs, int32_t max_leaf_records, pgpu_startree* out) {
+                        int32_t num_pairs, int32_t max_leaf_records, pgpu_startree* out) try {
   if (!seg || !column_types || !split_order || num_dims < 1 || num_pairs < 1 || !pairs || !out)
     return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree build arguments");
   const int N = seg->num_docs;
@@ -721,9 +721,9 @@ int pgpu_startree_build(const pgpu_segment_desc* seg, const int32_t* column_type
   }
   *out = st.release();
   return PGPU_OK;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_startree_get_desc(pgpu_startree st, pgpu_startree_desc* d) {
+int pgpu_startree_get_desc(pgpu_startree st, pgpu_startree_desc* d) try {
   if (!st || !d) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "null star-tree");
   d->num_dims = (int32_t)st->dim_columns.size();
   d->num_metrics = (int32_t)st->metrics.size();
@@ -737,17 +737,17 @@ int pgpu_startree_get_desc(pgpu_startree st, pgpu_startree_desc* d) {
   d->metric_f64 = st->f_ptrs.data();
   d->metric_i64 = st->c_ptrs.data();
   return PGPU_OK;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_startree_num_raw_records(pgpu_startree st, int32_t* n) {
+int pgpu_startree_num_raw_records(pgpu_startree st, int32_t* n) try {
   if (!st || !n) return pgpu::host_fail(PGPU_ERR_INVALID_ARGUMENT, "null star-tree");
   *n = st->num_raw_records;
   return PGPU_OK;
-}
+} PGPU_ABI_CATCH
 
-int pgpu_startree_destroy(pgpu_startree st) {
+int pgpu_startree_destroy(pgpu_startree st) try {
   delete st;
   return PGPU_OK;
-}
+} PGPU_ABI_CATCH
 
 }  // extern "C"

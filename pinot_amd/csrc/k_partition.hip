@@ -23,7 +23,7 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
                        part_split_lds(pp.cshift, pp.num_streams, pp.split_batch, pp.hashed ? 4 : 2), s, pp);
   }
   if (pp.hashed) {
-    if (pp.num_streams > kHashPartStreams || pp.sbits < 1 || pp.sbits > 16) return -1;
+    if (pp.num_streams > kHashPartStreams || pp.sbits < 8 || pp.sbits > 14) return -1;
     hipLaunchKernelGGL(part_hash_aggregate_kernel, dim3(pp.num_parts), dim3(kBlock),
                        part_hash_lds(pp.sbits, pp.base.num_slots), s, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;

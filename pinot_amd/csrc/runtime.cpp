@@ -352,7 +352,7 @@ constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large 
 #endif
 constexpr int64_t kPartLds = PGPU_PART_LDS_KB * 1024;  // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
-constexpr int64_t kHashPartLds = 48 * 1024;          // K8h LDS hash table per partition (three workgroups per CU)
+constexpr int64_t kHashPartLds = 80 * 1024;          // K8h LDS hash table per partition (two workgroups per CU)
 constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
 constexpr int kDocIdColumn = -2;                     // query column of the virtual $docId (hidden first-doc slot)
 
@@ -2589,11 +2589,15 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       if (hash_part) {
         // LDS table of 2^sbits entries within kHashPartLds; partitions: the plan's group bound at <= half load,
         // at most kMaxParts (more groups than that holds take further K8h rounds)
-        sbits = 12;
-        while (sbits > 8 && (int64_t)part_hash_lds(sbits, nslots) > kHashPartLds) --sbits;
-        // PGPU_PART_HASH_PBITS: at most that many partition bits (read per plan; tests force K8h's extra rounds)
+        // PGPU_PART_HASH_LDS_KB / PGPU_PART_HASH_PBITS (read per plan: A/B, and tests that force K8h's extra rounds)
+        // override the LDS budget and the partition-bit cap.  13 bits keep K8a / K8c's LDS histogram at 32 KB (three
+        // workgroups per CU at their VGPR count); 8 192 tables of 4 096 entries hold 16.7 M groups at half load.
+        const char* lk = getenv("PGPU_PART_HASH_LDS_KB");
+        const int64_t lds_budget = lk && atoi(lk) > 0 ? std::min<int64_t>((int64_t)atoi(lk) * 1024, 128 * 1024) : kHashPartLds;
+        sbits = 13;
+        while (sbits > 8 && (int64_t)part_hash_lds(sbits, nslots) > lds_budget) --sbits;
         const char* pb = getenv("PGPU_PART_HASH_PBITS");
-        const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 14;
+        const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 13;
         while (pbits < max_pbits && (int64_t(1) << (pbits + sbits - 1)) < P->group_bound) ++pbits;
         shift = 0;
         parts = int64_t(1) << pbits;

@@ -45,11 +45,13 @@ __device__ __forceinline__ void part_tiles(int64_t T, int64_t& t0, int64_t& t1) 
   t1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
 }
 
-// Hashed partitions: Fibonacci hash of a key; its top pbits name the partition, the next sbits the LDS slot.
-__device__ __forceinline__ uint32_t part_hash(uint32_t key) { return key * 0x9E3779B1u; }
-__device__ __forceinline__ uint32_t part_of(const KPartParams& pp, int32_t key) {
-  if (pp.hashed) return pp.pbits ? part_hash((uint32_t)key) >> (32 - pp.pbits) : 0u;
-  return (uint32_t)key >> pp.pshift;
+// Hashed partitions: records carry hk = part_hash(key), a bijection of u32 (the constant is odd), so the key comes
+// back as hk * kHashInv.  hk's top pbits name the partition, the next sbits the start slot of the LDS table; since
+// keys are < 2^31, hk is never ~0u (the preimage of ~0u is 0xF174D0AF), which stays free as the empty / padding mark.
+constexpr uint32_t kHashMul = 0x9E3779B1u, kHashInv = 0x0E8B2F51u;
+__device__ __forceinline__ uint32_t part_hash(uint32_t key) { return key * kHashMul; }
+__device__ __forceinline__ uint32_t hpart(const KPartParams& pp, uint32_t hk) {
+  return pp.pbits ? hk >> (32 - pp.pbits) : 0u;
 }
 
 // Composite keys of docs [32*group + H, +16) of segment S.
@@ -106,14 +108,15 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     return;
   }
   uint32_t pos[16];
-  if (pp.hashed) {  // the coarse run of the key's hashed partition; the whole key stored
+  if (pp.hashed) {  // the coarse run of the key's hashed partition; the whole hashed key stored
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       pos[i] = 0;
       if ((m >> i) & 1u) {
-        pos[i] = atomicAdd(&cursor[part_of(pp, key[i]) >> pp.cshift], 1u);
-        if (two) pp.mid_key[pos[i]] = (uint32_t)key[i];
-        else pp.rec_key32[pos[i]] = (uint32_t)key[i];
+        const uint32_t hk = part_hash((uint32_t)key[i]);
+        pos[i] = atomicAdd(&cursor[hpart(pp, hk) >> pp.cshift], 1u);
+        if (two) pp.mid_key[pos[i]] = hk;
+        else pp.rec_key32[pos[i]] = hk;
       }
     }
   } else {
@@ -171,7 +174,7 @@ __device__ __forceinline__ void part_count_half(const KPartParams& pp, const Seg
   part_keys<H>(pp.base, S, group, key);
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    if ((m >> i) & 1u) atomicAdd(&hist[part_of(pp, key[i])], 1u);
+    if ((m >> i) & 1u) atomicAdd(&hist[pp.hashed ? hpart(pp, part_hash((uint32_t)key[i])) : (uint32_t)key[i] >> pp.pshift], 1u);
 }
 
 // K8a (SCATTER = false) / K8c (SCATTER = true).  LDS: [num_parts u32 histogram / cursors] [filter stack].
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     uint32_t part[NB];  // the record's partition within this coarse run
 #pragma unroll
     for (int b = 0; b < NB; ++b)
-      part[b] = pp.hashed ? part_of(pp, (int32_t)k[b]) & (uint32_t)(NP - 1) : k[b] >> pp.pshift;
+      part[b] = pp.hashed ? hpart(pp, k[b]) & (uint32_t)(NP - 1) : k[b] >> pp.pshift;
 #pragma unroll
     for (int b = 0; b < NB; ++b) rank[b] = k[b] != ~0u ? atomicAdd(&hist[part[b]], 1u) : 0u;
     __syncthreads();
@@ -346,6 +349,13 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     __syncthreads();
     if (pp.fine_pack) {  // one u32 per record: key | (value - pack_min) << pshift
       uint32_t* __restrict__ r32 = reinterpret_cast<uint32_t*>(pp.rec_val);
+      if (pp.hashed) {  // hk below its partition bits | (value - pack_min) << (32 - pbits)
+        const int lb = 32 - pp.pbits;
+        const uint32_t hlow = (1u << lb) - 1u;
+        for (uint32_t i = tid; i < n; i += kBlock)
+          r32[spos[i]] = (skey32[i] & hlow) | ((uint32_t)((int64_t)sval[i] - pp.pack_min) << lb);
+        continue;
+      }
       for (uint32_t i = tid; i < n; i += kBlock)
         r32[spos[i]] = (uint32_t)skey[i] | ((uint32_t)((int64_t)sval[i] - pp.pack_min) << pp.pshift);
       continue;
@@ -463,11 +473,11 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
     for (int i = tid; i < n; i += kBlock) p.table[(int64_t)s * G + k0 + i] = lds[(int64_t)s * PR + i];
 }
 
-// Slot of `key` in an LDS hash table of 2^sbits u32 keys (empty = ~0u), inserted if absent, or -1 after
-// kHashPartProbes probes.  Start slot: the sbits of part_hash(key) below the partition's pbits.
+// Slot of hashed key `hk` in an LDS hash table of 2^sbits u32 entries (empty = ~0u), inserted if absent, or -1
+// after kHashPartProbes probes.  Start slot: the sbits of hk below the partition's pbits.
 __device__ __forceinline__ int lds_hash_slot(uint32_t* keys, uint32_t key, int pbits, int sbits) {
   const uint32_t mask = (1u << sbits) - 1u;
-  uint32_t s = (part_hash(key) << pbits) >> (32 - sbits);
+  uint32_t s = (key << pbits) >> (32 - sbits);
   const int probes = kHashPartProbes < (1 << sbits) ? kHashPartProbes : (1 << sbits);
   for (int i = 0; i < probes; ++i) {
     const uint32_t k = keys[s];
@@ -505,18 +515,35 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
     if (tid == 0) pending = 0;
     __syncthreads();
     for (uint32_t base = 0; base < n; base += NB * kBlock) {
-      uint32_t key[NB];
+      uint32_t key[NB];  // hashed keys
       uint64_t v[NB][kHashPartStreams];
+      uint32_t w32[NB];  // fine_pack: the packed records as read (written back as they are when left pending)
+      if (pp.fine_pack) {
+        const uint32_t* __restrict__ r32 = reinterpret_cast<const uint32_t*>(pp.rec_val);
+        const int lb = 32 - pp.pbits;
+        const uint32_t hi = (uint32_t)blockIdx.x << lb, hlow = (1u << lb) - 1u;
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const uint32_t i = base + b * kBlock + tid;
-        const uint32_t r = r0 + (i < n ? i : 0u);
-        key[b] = i < n ? pp.rec_key32[r] : ~0u;
+        for (int b = 0; b < NB; ++b) {
+          const uint32_t i = base + b * kBlock + tid;
+          w32[b] = r32[r0 + (i < n ? i : 0u)];
+          key[b] = i < n ? hi | (w32[b] & hlow) : ~0u;
+          v[b][0] = (uint64_t)(pp.pack_min + (int64_t)(w32[b] >> lb));
 #pragma unroll
-        for (int st = 0; st < kHashPartStreams; ++st)
-          v[b][st] = st >= nst ? 0ull
-                     : pp.val32 ? (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(pp.rec_val)[st * cap + r]
-                                : pp.rec_val[st * cap + r];
+          for (int st = 1; st < kHashPartStreams; ++st) v[b][st] = 0ull;
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const uint32_t i = base + b * kBlock + tid;
+          const uint32_t r = r0 + (i < n ? i : 0u);
+          w32[b] = 0;
+          key[b] = i < n ? pp.rec_key32[r] : ~0u;
+#pragma unroll
+          for (int st = 0; st < kHashPartStreams; ++st)
+            v[b][st] = st >= nst ? 0ull
+                       : pp.val32 ? (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(pp.rec_val)[st * cap + r]
+                                  : pp.rec_val[st * cap + r];
+        }
       }
       __syncthreads();  // the batch is in registers before any record of it is overwritten by a pending one
 #pragma unroll
@@ -525,6 +552,10 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
         const int slot = lds_hash_slot(keys, key[b], pp.pbits, pp.sbits);
         if (slot < 0) {
           const uint32_t at = r0 + atomicAdd(&pending, 1u);
+          if (pp.fine_pack) {
+            reinterpret_cast<uint32_t*>(pp.rec_val)[at] = w32[b];
+            continue;
+          }
           pp.rec_key32[at] = key[b];
 #pragma unroll
           for (int st = 0; st < kHashPartStreams; ++st)
@@ -558,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
         const uint64_t r = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
         if (r < (uint64_t)cap) {
           uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
-          o[0] = (uint64_t)keys[i];
+          o[0] = (uint64_t)(keys[i] * kHashInv);  // the composite key back from its hash
           for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
         }
       }

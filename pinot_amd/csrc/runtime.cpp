@@ -2645,8 +2645,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->part_val32 = v32;
         // one integer stream: its value range, for packing values into the coarse records (KPartParams.pack_bits)
         P->part_pack_range = -1;
-        if (!hash_part && v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn &&
-            !getenv_flag("PGPU_NO_PACK")) {
+        if (v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn && !getenv_flag("PGPU_NO_PACK")) {
           int64_t lo = INT64_MAX, hi = INT64_MIN;
           for (const Segment* s : P->segs) {
             const Column& col = s->cols[P->query_cols[scol[0]]];
@@ -3272,7 +3271,17 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.rec_val = sc->rec_val.as<uint64_t>();
     pp.rec_cap = cap;
     pp.val32 = P->part_val32 ? 1 : 0;
-    if (cshift > 0 && P->part_pack_range >= 0) {
+    if (P->part_hash && P->part_pack_range >= 0 && pp.num_streams == 1 && pp.val32 && P->part_pbits >= 1) {
+      // hashed partitions: K8e's records packed as hk below the partition bits | (value - pack_min) above them
+      int vb = 0;
+      while (vb < 32 && (P->part_pack_range >> vb) != 0) ++vb;
+      static const bool no_fine = getenv_flag("PGPU_NO_FINE_PACK");
+      if (!no_fine && vb <= P->part_pbits) {
+        pp.fine_pack = 1;
+        pp.pack_min = P->part_pack_min;
+        pp.pack_range = P->part_pack_range;
+      }
+    } else if (!P->part_hash && cshift > 0 && P->part_pack_range >= 0) {
       const int free_bits = 32 - (pp.pshift + cshift);
       int vb = 0;
       while (vb < free_bits && (P->part_pack_range >> vb) != 0) ++vb;

@@ -11,7 +11,7 @@ from test_gpu_parity import assert_same, gpu_table
 
 pytestmark = pytest.mark.gpu
 
-SCHEMA = [("a", "INT"), ("b", "INT"), ("c", "INT"), ("m", "INT"), ("x", "DOUBLE")]
+SCHEMA = [("a", "INT"), ("b", "INT"), ("c", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("s", "INT")]
 DOCS = 120000
 
 
@@ -19,7 +19,7 @@ def _columns(seed):
     rng = np.random.default_rng(seed)
     return {"a": rng.integers(0, 3000, DOCS).astype(np.int64), "b": rng.integers(0, 3000, DOCS).astype(np.int64),
             "c": rng.integers(0, 30, DOCS).astype(np.int64), "m": rng.integers(-400, 900, DOCS).astype(np.int64),
-            "x": np.round(rng.uniform(-1e4, 1e4, DOCS), 3)}
+            "x": np.round(rng.uniform(-1e4, 1e4, DOCS), 3), "s": rng.integers(0, 100, DOCS).astype(np.int64)}
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +33,9 @@ def sparse(oracle, gpu_lib):
 QUERIES = [
     "SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c",
     "SELECT MIN(m), MAX(x), SUM(x), AVG(m), COUNT(*) FROM t WHERE c < 20 GROUP BY a, b, c",
-    "SELECT SUM(m), MAX(m) FROM t WHERE m > 0 AND c IN (1, 3, 5, 7) GROUP BY c, a, b",
+    "SELECT SUM(m), MAX(m) FROM t WHERE m > 0 AND x < 5000 GROUP BY c, a, b",
+    # one stream whose range (7 bits) fits under the partition bits: K8e / K8h records packed into a u32
+    "SELECT COUNT(*), SUM(s), MAX(s) FROM t WHERE m >= 0 GROUP BY a, b, c",
 ]
 
 
@@ -57,6 +59,16 @@ def test_hash_partition_rounds(oracle, sparse, monkeypatch):
         with t.plan(hs, q) as p:
             assert p.group_path() == "hash_partitioned"
         assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+
+
+def test_hash_partition_rounds_packed(oracle, sparse, monkeypatch):
+    """Packed records (hashed key bits | value) left pending: LDS tables of 256 entries for ~1 800 groups per
+    partition, so K8h writes packed words back and re-reads them over several rounds."""
+    t, hs, segs = sparse
+    monkeypatch.setenv("PGPU_PART_HASH_LDS_KB", "4")
+    q = parse_query(QUERIES[3], num_groups_limit=10 ** 9)
+    q.no_plan_cache = True
+    assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
 
 
 def test_hash_partitions_exchange_materialises_table(oracle, sparse):

@@ -509,6 +509,9 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
   uint32_t n = pp.part_start[blockIdx.x + 1] - r0;
   const int64_t cap = pp.rec_cap;
   constexpr int NB = 8;
+  // COUNT + SUM in one LDS word (slot 0's row) when the partition's records bound both halves (uniform per
+  // workgroup): (1 << 40) | (value - pack_min) per record, split when the round's groups are written
+  const bool cs = pp.cs_pack && n < (1u << 24) && (uint64_t)n * (uint64_t)pp.pack_range < (1ull << 40);
   while (n > 0) {
     for (int i = tid; i < S; i += kBlock) keys[i] = ~0u;
     for (int i = tid; i < ns * S; i += kBlock) lds[i] = slot_init(p.slot_kind[i >> pp.sbits]);
@@ -565,6 +568,11 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
             }
           continue;
         }
+        if (cs) {
+          atomicAdd(reinterpret_cast<unsigned long long*>(lds) + slot,
+                    (1ull << 40) | (unsigned long long)((int64_t)v[b][0] - pp.pack_min));
+          continue;
+        }
         for (int s = 0; s < ns; ++s) {
           const int st = pp.slot_stream[s];
           uint64_t w = 0;
@@ -590,7 +598,13 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
         if (r < (uint64_t)cap) {
           uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
           o[0] = (uint64_t)(keys[i] * kHashInv);  // the composite key back from its hash
-          for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
+          if (cs) {
+            const uint64_t w = lds[i], c = w >> 40;
+            o[1] = c;
+            o[2] = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)c * pp.pack_min);
+          } else {
+            for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
+          }
         }
       }
     }

@@ -3280,6 +3280,9 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
         pp.fine_pack = 1;
         pp.pack_min = P->part_pack_min;
         pp.pack_range = P->part_pack_range;
+        static const bool no_cs = getenv_flag("PGPU_NO_CS_PACK");  // A/B: two LDS atomics per record
+        pp.cs_pack = !no_cs && nslots == 2 && P->slot_kind[0] == SLOT_COUNT && P->slot_kind[1] == SLOT_SUM_I64 &&
+                     P->slot_stream[1] == 0 ? 1 : 0;
       }
     } else if (!P->part_hash && cshift > 0 && P->part_pack_range >= 0) {
       const int free_bits = 32 - (pp.pshift + cshift);

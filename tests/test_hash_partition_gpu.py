@@ -36,6 +36,8 @@ QUERIES = [
     "SELECT SUM(m), MAX(m) FROM t WHERE m > 0 AND x < 5000 GROUP BY c, a, b",
     # one stream whose range (7 bits) fits under the partition bits: K8e / K8h records packed into a u32
     "SELECT COUNT(*), SUM(s), MAX(s) FROM t WHERE m >= 0 GROUP BY a, b, c",
+    # ... and exactly COUNT + SUM of it: one LDS word per group (count in the high bits)
+    "SELECT SUM(s), COUNT(*) FROM t GROUP BY b, c, a",
 ]
 
 

@@ -92,7 +92,7 @@ struct pgpu_result_s {
   // per group-by key: the table-global dictionary snapshot its group ids index (runtime.cpp's Dict)
   std::vector<std::shared_ptr<const void>> key_dicts;
   bool groups_limit_reached = false;
-  // Compact form (large dense tables, e.g. C5's 10M groups): the groups are the set bits of the bitmap at the start
+  // Compact form (large tables, e.g. C5's 10M groups): the groups are the set bits of the bitmap at the start
   // of `cbuf` over the composite keys [ckey_base, ckey_base + cbits), and slot s holds their words in key order,
   // cwidth[s] bytes each (two's complement, sign-extended) at cbuf + cslot_off[s].  The columnar form above is built
   // from it on first access to gid() / slot() (pgpu::result_expand), as Pinot's group-key iterator decodes raw keys.
@@ -100,6 +100,9 @@ struct pgpu_result_s {
   std::atomic<bool> compact{false};
   std::mutex expand_mu;
   int64_t ckey_base = 0, cbits = 0;
+  // ckey_width 4 / 8 (hash-mode results): instead of the bitmap, cbuf starts with the n groups' composite keys in
+  // ascending order at that width (8-aligned area); the slots follow as above.
+  int32_t ckey_width = 0;
   std::vector<int64_t> cstride, ccard, coff;
   std::vector<int32_t> cwidth;
   std::vector<size_t> cslot_off;

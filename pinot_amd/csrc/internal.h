@@ -350,6 +350,12 @@ int launch_exchange_scatter(const uint64_t* table, const unsigned long long* has
 int launch_i64_to_f64(uint64_t* p, int64_t n, void* stream);
 // k_hashsort.hip: hash-mode finalize on the device (radix sort of the compacted records by key, decode to columns).
 int hash_sort_temp_bytes(int64_t n, int key_bits, size_t* bytes);
+int launch_hash_minmax(const uint64_t* rec, const unsigned long long* count, int64_t cap, int32_t num_slots,
+                       unsigned long long* mm, void* stream);
+int launch_hash_sort_compact(const uint64_t* rec, int64_t n, int32_t num_slots, int key_bits, int32_t key_width,
+                             const int32_t* width, const int64_t* slot_off, void* tmp, size_t temp_bytes,
+                             uint64_t* keys_a, uint64_t* keys_b, uint32_t* idx_a, uint32_t* idx_b, uint8_t* out,
+                             void* stream);
 int launch_hash_sort_decode(const uint64_t* rec, int64_t n, int32_t num_slots, int32_t num_keys, const int64_t* stride,
                             const int64_t* card, const int64_t* off, int key_bits, void* tmp, size_t temp_bytes,
                             uint64_t* keys_a, uint64_t* keys_b, uint32_t* idx_a, uint32_t* idx_b, uint8_t* out,

@@ -3580,10 +3580,19 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
                          sc->ckeys.as<uint64_t>(), cap, stream))
         return fail(PGPU_ERR_DEVICE, "compact launch failed");
     }
-    TRY(sc->readback.ensure(64));
+    // each slot's range over the records, read back with their count (the compact form's widths, below)
+    static const bool no_compact_h = getenv_flag("PGPU_NO_COMPACT_RESULT");
+    const bool want_compact = P->stage_end.empty() && !no_compact_h;
+    TRY(sc->counter.ensure(64 + (size_t)kMaxSlots * 16));  // (no regrowth: the first allocation is 4 KB)
+    unsigned long long* d_mm = reinterpret_cast<unsigned long long*>(sc->counter.as<uint8_t>() + 64);
+    if (want_compact && launch_hash_minmax(sc->ckeys.as<uint64_t>(), sc->counter.as<unsigned long long>(), cap, nslots,
+                                           d_mm, stream))
+      return fail(PGPU_ERR_DEVICE, "slot range launch failed: %s", hipGetErrorString(hipGetLastError()));
+    TRY(sc->readback.ensure(64 + (size_t)nslots * 16));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
     HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st + 1, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+    if (want_compact) HIP_TRY(hipMemcpyAsync(st + 8, d_mm, (size_t)nslots * 16, hipMemcpyDeviceToHost, stream));
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;
     if (st[6]) return timeout_fail(P);
@@ -3597,7 +3606,58 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     if (P->groups_seen && P->merged_records < 0) P->groups_seen->store(n, std::memory_order_relaxed);
     static const bool host_sort = getenv_flag("PGPU_HASH_HOST_SORT");  // A/B: sort and decode on the host
     if (n >= 4096 && P->stage_end.empty() && !host_sort) {
-      // sorted by key and decoded into the columnar result on the device (k_hashsort.hip): one copy back
+      // sorted by key on the device (k_hashsort.hip), held in compact form when that moves fewer bytes
+      int key_bits = 1;
+      {
+        const long double space = (long double)P->key_stride[nk - 1] * (long double)P->key_card[nk - 1];
+        while (key_bits < 64 && (long double)(INT64_C(1) << key_bits) < space) ++key_bits;
+      }
+      size_t tmp_bytes = 0;
+      if (hash_sort_temp_bytes(n, key_bits, &tmp_bytes))
+        return fail(PGPU_ERR_DEVICE, "hash sort sizing failed: %s", hipGetErrorString(hipGetLastError()));
+      // Compact form when it moves fewer bytes (C5-sized results: 10M groups): sorted composite keys at 4 or 8
+      // bytes instead of the decoded dictIds, and each slot at the narrowest width of its range (as the dense
+      // compact form); the host decodes it on first access (result_expand).
+      const int32_t key_width = key_bits <= 32 ? 4 : 8;
+      std::vector<int32_t> width(nslots, 8);
+      std::vector<int64_t> woff(nslots, 0);
+      size_t cbytes = ((size_t)n * key_width + 7) & ~size_t(7);
+      for (int s2 = 0; s2 < nslots; ++s2) {
+        const long long lo = (long long)(st[8 + s2] ^ (1ull << 63)), hi = (long long)(st[8 + nslots + s2] ^ (1ull << 63));
+        width[s2] = compact_slot_width(lo, hi, P->slot_kind[s2]);
+        woff[s2] = (int64_t)cbytes;
+        cbytes += ((size_t)n * width[s2] + 7) & ~size_t(7);
+      }
+      if (want_compact && cbytes < (size_t)n * (4 * nk + 8 * nslots)) {
+        const size_t a = ((size_t)n * 8 + 255) & ~size_t(255), b = ((size_t)n * 4 + 255) & ~size_t(255);
+        const size_t ob = (cbytes + 255) & ~size_t(255);
+        TRY(sc->hsort.ensure(2 * a + 2 * b + ob + tmp_bytes + 256));
+        uint8_t* base = sc->hsort.as<uint8_t>();
+        uint8_t* out = base + 2 * a + 2 * b;
+        if (launch_hash_sort_compact(sc->ckeys.as<uint64_t>(), n, nslots, key_bits, key_width, width.data(),
+                                     woff.data(), out + ob, tmp_bytes, reinterpret_cast<uint64_t*>(base),
+                                     reinterpret_cast<uint64_t*>(base + a), reinterpret_cast<uint32_t*>(base + 2 * a),
+                                     reinterpret_cast<uint32_t*>(base + 2 * a + b), out, stream))
+          return fail(PGPU_ERR_DEVICE, "hash sort / compact launch failed: %s", hipGetErrorString(hipGetLastError()));
+        R->num_keys = nk;
+        R->num_slots = nslots;
+        R->n = n;
+        R->ckey_width = key_width;
+        R->cstride = P->key_stride;
+        R->ccard = P->key_card;
+        R->coff = P->key_off;
+        R->cwidth = width;
+        R->cslot_off.assign(woff.begin(), woff.end());
+        if (R->pool) R->cbuf = R->pool->take();
+        TRY(R->cbuf.ensure(cbytes));
+        HIP_TRY(hipMemcpyAsync(R->cbuf.p, out, cbytes, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        R->compact.store(true, std::memory_order_release);
+        n = -1;  // held compact
+      }
+    }
+    if (n >= 4096 && P->stage_end.empty() && !host_sort) {
+      // sorted by key and decoded into the columnar result on the device: one copy back
       int key_bits = 1;
       {
         const long double space = (long double)P->key_stride[nk - 1] * (long double)P->key_card[nk - 1];
@@ -3727,8 +3787,24 @@ int pgpu::result_expand(pgpu_result_s* R) {
   const int nk = R->num_keys, ns = R->num_slots;
   const int64_t n = R->n;
   TRY(R->alloc(nk, ns, n));
+  if (R->ckey_width) {  // sorted composite keys (hash-mode results): decode each row's key
+    const uint8_t* kb = reinterpret_cast<const uint8_t*>(R->cbuf.p);
+    constexpr int64_t kRowsPerTask = 1 << 20;
+    const int64_t ktasks = (n + kRowsPerTask - 1) / kRowsPerTask;
+    auto keys = [&](int t) {
+      const int64_t r0 = t * kRowsPerTask, r1 = std::min(n, r0 + kRowsPerTask);
+      for (int64_t r = r0; r < r1; ++r) {
+        const uint64_t key = R->ckey_width == 4 ? (uint64_t)reinterpret_cast<const uint32_t*>(kb)[r]
+                                                : reinterpret_cast<const uint64_t*>(kb)[r];
+        for (int j = 0; j < nk; ++j)
+          R->gid_raw(j)[r] = (int32_t)((key / (uint64_t)R->cstride[j]) % (uint64_t)R->ccard[j] + R->coff[j]);
+      }
+    };
+    if (ktasks > 1) host_pool().run((int)ktasks, keys);
+    else if (ktasks == 1) keys(0);
+  }
   const uint64_t* bm = reinterpret_cast<const uint64_t*>(R->cbuf.p);
-  const int64_t words = (R->cbits + 63) / 64;
+  const int64_t words = R->ckey_width ? 0 : (R->cbits + 63) / 64;
   constexpr int64_t kBlockWords = 4096;
   const int64_t nb = (words + kBlockWords - 1) / kBlockWords;
   std::vector<int64_t> first(nb + 1, 0);

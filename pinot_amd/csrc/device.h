@@ -24,11 +24,12 @@ __device__ __forceinline__ gmem<T>* gp(const T* p) { return (gmem<T>*)p; }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// PGPU_SADDR (default on): gathers from a wave-uniform base take a 32-bit byte offset, so they compile to the
-// global_load SADDR form (base in SGPRs, one offset VGPR per load instead of a 64-bit VGPR address pair) -- the
-// dense path keeps 16 lookups in flight per lane, and their address registers were a third of its footprint.
+// PGPU_SADDR (default off): gathers from a wave-uniform base take a 32-bit byte offset, so they compile to the
+// global_load SADDR form (base in SGPRs, one offset VGPR per load instead of a 64-bit VGPR address pair).  Measured
+// on MI355X (r04, interleaved A/B of two libraries): the dense instance keeps 168 VGPRs either way, and C2's scan
+// ran 605 / 604 us with it against 578 / 573 without (C3 and C1 flat), so it stays off.
 #ifndef PGPU_SADDR
-#define PGPU_SADDR 1
+#define PGPU_SADDR 0
 #endif
 template <typename T>
 __device__ __forceinline__ const T* wave_uniform(const T* p) {

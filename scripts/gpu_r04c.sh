@@ -5,7 +5,5 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 touch pinot_amd/libpinotgpu*.so
 export TMPDIR=/tmp
 VARIANTS="PGPU_X=0 PGPU_NO_DENSE_NARROW=1" BENCH_ARGS="--workload c2 --no-bytes" bash scripts/ab_env.sh || exit 1
-LIBS="pinot_amd/libpinotgpu.so pinot_amd/libpinotgpu_ab0.so" BENCH_ARGS="--workload c2 --no-bytes" bash scripts/ab_lib.sh || exit 1
 VARIANTS="PGPU_X=0 PGPU_NO_CS_PACK=1 PGPU_NO_FINE_PACK=1" BENCH_ARGS="--workload c5 --no-bytes" bash scripts/ab_env.sh || exit 1
-STEPS=10 VARIANTS="PGPU_X=0 PGPU_NO_PART_HASH=1 PGPU_PART_HASH_PBITS=14 PGPU_PART_HASH_LDS_KB=40" BENCH_ARGS="--workload c5_hash --no-bytes" bash scripts/ab_env.sh || exit 1
 WL="adanalytics_inv:1000 c5_hash:100" NOPROF=1 bash scripts/gpu_profiles.sh

@@ -505,6 +505,8 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
   const int ns = p.num_slots, nst = pp.num_streams;
   uint32_t* keys = reinterpret_cast<uint32_t*>(lds + (size_t)ns * S);
   __shared__ uint32_t pending;
+  __shared__ uint32_t wave_tot[kBlock / 64];
+  __shared__ unsigned long long blk_base;
   const uint32_t r0 = pp.part_start[blockIdx.x];
   uint32_t n = pp.part_start[blockIdx.x + 1] - r0;
   const int64_t cap = pp.rec_cap;
@@ -585,14 +587,28 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
       }
     }
     __syncthreads();
-    // append this round's groups: one reservation per wave
+    // append this round's groups with one reservation per workgroup (a single global counter: per-wave atomics
+    // would queue 4 x 2^sbits / 256 of them per partition at one address): waves count their entries by ballot, the
+    // workgroup reserves their sum, each wave writes a contiguous run
+    uint32_t mine = 0;
+    for (int i0 = 0; i0 < S; i0 += kBlock) {
+      const int i = i0 + tid;
+      mine += (uint32_t)__popcll(__ballot(i < S && keys[i] != ~0u));
+    }
+    if (lane == 0) wave_tot[tid >> 6] = mine;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tot = 0;
+      for (int w = 0; w < kBlock / 64; ++w) tot += wave_tot[w];
+      blk_base = tot ? atomicAdd(pp.out_count, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    uint64_t at = blk_base;
+    for (int w = 0; w < (tid >> 6); ++w) at += wave_tot[w];
     for (int i0 = 0; i0 < S; i0 += kBlock) {
       const int i = i0 + tid;
       const bool occ = i < S && keys[i] != ~0u;
       const uint64_t bal = __ballot(occ);
-      unsigned long long at = 0;
-      if (lane == 0 && bal) at = atomicAdd(pp.out_count, (unsigned long long)__popcll(bal));
-      at = (unsigned long long)__shfl((long long)at, 0);
       if (occ) {
         const uint64_t r = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
         if (r < (uint64_t)cap) {
@@ -607,6 +623,7 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
           }
         }
       }
+      at += (uint64_t)__popcll(bal);
     }
     __syncthreads();
     n = pending;

@@ -23,6 +23,14 @@ __global__ __launch_bounds__(256) void hash_keys_kernel(const uint64_t* __restri
   }
 }
 
+__global__ __launch_bounds__(256) void hash_keys32_kernel(const uint64_t* __restrict__ rec, int64_t n, int32_t rec_words,
+                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    keys[i] = (uint32_t)rec[i * rec_words];
+    idx[i] = (uint32_t)i;
+  }
+}
+
 // Row r of the sorted order: its dictIds (key / stride % card + off per column) and slot words.
 __global__ __launch_bounds__(256) void hash_decode_kernel(const uint64_t* __restrict__ rec, int64_t n, int32_t num_slots,
                                                           int32_t num_keys, const uint64_t* __restrict__ keys,
@@ -44,7 +52,9 @@ __global__ __launch_bounds__(256) void hash_decode_kernel(const uint64_t* __rest
 __global__ __launch_bounds__(256) void hash_minmax_kernel(const uint64_t* __restrict__ rec,
                                                           const unsigned long long* __restrict__ count, int64_t cap,
                                                           int32_t num_slots, unsigned long long* __restrict__ mm) {
+  __shared__ unsigned long long part[2][256 / 64];
   const int64_t n = (int64_t)(*count < (unsigned long long)cap ? *count : (unsigned long long)cap);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int s = 0; s < num_slots; ++s) {
     unsigned long long lo = ~0ull, hi = 0ull;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
@@ -58,10 +68,20 @@ __global__ __launch_bounds__(256) void hash_minmax_kernel(const uint64_t* __rest
       lo = a < lo ? a : lo;
       hi = b > hi ? b : hi;
     }
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) {
+      part[0][wave] = lo;
+      part[1][wave] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic per workgroup and bound (a few hundred at each address, not thousands)
+      for (int w = 1; w < 256 / 64; ++w) {
+        lo = part[0][w] < lo ? part[0][w] : lo;
+        hi = part[1][w] > hi ? part[1][w] : hi;
+      }
       atomicMin(&mm[s], lo);
       atomicMax(&mm[num_slots + s], hi);
     }
+    __syncthreads();
   }
 }
 
@@ -77,7 +97,7 @@ __global__ __launch_bounds__(256) void hash_compact_kernel(const uint64_t* __res
                                                            const uint32_t* __restrict__ idx, int32_t key_width,
                                                            SlotWidths sw, uint8_t* __restrict__ out) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    if (key_width == 4) reinterpret_cast<uint32_t*>(out)[r] = (uint32_t)keys[r];
+    if (key_width == 4) reinterpret_cast<uint32_t*>(out)[r] = reinterpret_cast<const uint32_t*>(keys)[r];
     else reinterpret_cast<uint64_t*>(out)[r] = keys[r];
     const uint64_t* e = rec + (int64_t)idx[r] * (1 + num_slots);
     for (int s = 0; s < num_slots; ++s) {
@@ -101,7 +121,7 @@ int launch_hash_minmax(const uint64_t* rec, const unsigned long long* count, int
   if (hipMemsetAsync(mm, 0xFF, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
   if (hipMemsetAsync(mm + num_slots, 0, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
   int64_t grid = (cap + 255) / 256;
-  grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
+  grid = grid > 512 ? 512 : (grid < 1 ? 1 : grid);
   hipLaunchKernelGGL(hash_minmax_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), rec, count, cap, num_slots, mm);
   return PGPU_HIP_OK(hipGetLastError());
 }
@@ -116,13 +136,24 @@ int launch_hash_sort_compact(const uint64_t* rec, int64_t n, int32_t num_slots, 
   if (n > INT32_MAX || num_slots > kMaxSlots || (key_width != 4 && key_width != 8)) return -1;
   int64_t grid = (n + 255) / 256;
   grid = grid > 4096 ? 4096 : grid;
-  hipLaunchKernelGGL(hash_keys_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), rec, n, 1 + num_slots, keys_a,
-                     idx_a);
-  if (hipGetLastError() != hipSuccess) return -1;
   size_t tb = temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_a, keys_b, idx_a, idx_b, (int)n, 0, key_bits, S(stream)) !=
-      hipSuccess)
-    return -1;
+  if (key_width == 4) {  // key spaces below 2^32: u32 keys (the sort moves 8 bytes per element and pass, not 12)
+    uint32_t* ka = reinterpret_cast<uint32_t*>(keys_a);
+    uint32_t* kb = reinterpret_cast<uint32_t*>(keys_b);
+    hipLaunchKernelGGL(hash_keys32_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), rec, n, 1 + num_slots, ka,
+                       idx_a);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, ka, kb, idx_a, idx_b, (int)n, 0, key_bits, S(stream)) !=
+        hipSuccess)
+      return -1;
+  } else {
+    hipLaunchKernelGGL(hash_keys_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), rec, n, 1 + num_slots, keys_a,
+                       idx_a);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_a, keys_b, idx_a, idx_b, (int)n, 0, key_bits, S(stream)) !=
+        hipSuccess)
+      return -1;
+  }
   SlotWidths sw{};
   for (int s = 0; s < num_slots; ++s) {
     sw.w[s] = width[s];
@@ -133,13 +164,22 @@ int launch_hash_sort_compact(const uint64_t* rec, int64_t n, int32_t num_slots, 
   return PGPU_HIP_OK(hipGetLastError());
 }
 
+// Temporary storage of the key sort: the larger of the u64-key and (key spaces below 2^32) u32-key sorts.
 int hash_sort_temp_bytes(int64_t n, int key_bits, size_t* bytes) {
   *bytes = 0;
   if (n <= 0) return 0;
-  return PGPU_HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, *bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0,
-                                                        key_bits));
+  size_t b64 = 0, b32 = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, b64, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, key_bits) != hipSuccess)
+    return -1;
+  if (key_bits <= 32 &&
+      hipcub::DeviceRadixSort::SortPairs(nullptr, b32, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, key_bits) != hipSuccess)
+    return -1;
+  *bytes = b64 > b32 ? b64 : b32;
+  return 0;
 }
+
 
 // rec: n records of 1 + num_slots words; work: keys_a/keys_b (u64) and idx_a/idx_b (u32), n each; tmp: temp_bytes;
 // out: [num_keys][n] int32 then, at slot_off bytes, [num_slots][n] u64.

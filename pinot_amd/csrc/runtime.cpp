@@ -352,7 +352,7 @@ constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large 
 #endif
 constexpr int64_t kPartLds = PGPU_PART_LDS_KB * 1024;  // K8d accumulators per partition (LDS)
 constexpr int64_t kMaxParts = 16384;                 // K8a/K8c LDS histogram entries
-constexpr int64_t kHashPartLds = 40 * 1024;          // K8h LDS hash table per partition (four workgroups per CU)
+constexpr int64_t kHashPartLdsMax = 64 * 1024;       // K8h LDS hash table per partition, at most
 constexpr int64_t kPartMaxRecordBytes = 32ll << 30;  // scratch for the partitioned records
 constexpr int kDocIdColumn = -2;                     // query column of the virtual $docId (hidden first-doc slot)
 
@@ -1855,6 +1855,47 @@ bool part_hash_eligible(const pgpu_plan_s* P, int64_t G) {
   return !off && P->mode == MODE_HASH && P->stage_end.empty() && G > 0 && G < (INT64_C(1) << 31) && P->key_bias == 0;
 }
 
+// Hashed partitions' shape for `groups` expected groups: 2^pbits partitions (K8a / K8c's LDS histogram: at most
+// kMaxParts) of LDS hash tables of 2^sbits entries (4 + 8 x slots bytes each).  Small tables keep more K8h
+// workgroups on a CU, so the tables are 2^10 entries at a load of at most ~0.6 and partitions are added first; past
+// kMaxParts partitions the tables grow, up to kHashPartLdsMax (more groups than that take further K8h rounds).
+// Measured on c5_hash (10^7 groups, r04, ms per query): 2^14 x 2^10 (20 KB) 3.69-3.72, 2^13 x 2^11 (40 KB)
+// 4.06-4.17, 2^13 x 2^12 (80 KB) 7.67, 2^14 x 2^12 11.7-12.7; the global hash table 14.8.  PGPU_PART_HASH_LDS_KB /
+// PGPU_PART_HASH_PBITS (read per plan: A/B, and tests that force K8h's extra rounds) cap the table bytes and the
+// partition bits.
+void hash_part_bits(int64_t groups, int nslots, int* pbits, int* sbits) {
+  const char* lk = getenv("PGPU_PART_HASH_LDS_KB");
+  const int64_t lds_cap = lk && atoi(lk) > 0 ? std::min<int64_t>((int64_t)atoi(lk) * 1024, 128 * 1024) : kHashPartLdsMax;
+  const char* pb = getenv("PGPU_PART_HASH_PBITS");
+  const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 14;
+  auto fits = [&](int p, int sb) { return (long double)groups <= 0.6L * (long double)(int64_t(1) << (p + sb)); };
+  int sb = 10;
+  while (sb > 8 && (int64_t)part_hash_lds(sb, nslots) > lds_cap) --sb;
+  int p = 0;
+  while (p < max_pbits && !fits(p, sb)) ++p;
+  while (!fits(p, sb) && sb < 14 && (int64_t)part_hash_lds(sb + 1, nslots) <= lds_cap) ++sb;
+  *pbits = p;
+  *sbits = sb;
+}
+
+// A cached hashed-partition plan re-shaped for the groups its last execution found (plan_cache_get): the partition
+// count, the pass kernels' LDS and grid follow.
+void hash_part_resize(pgpu_plan_s* P, int64_t groups) {
+  const int nslots = (int)P->slot_kind.size();
+  int pbits = 0, sbits = 0;
+  hash_part_bits(groups, nslots, &pbits, &sbits);
+  const int64_t parts = int64_t(1) << pbits;
+  const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (P->pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
+  if (pass_lds > 96 * 1024) return;
+  P->part_pbits = pbits;
+  P->part_sbits = sbits;
+  P->num_parts = (int)parts;
+  P->part_lds = pass_lds;
+  int per_cu = occupancy_part_pass(pass_lds);
+  per_cu = std::max(1, std::min(per_cu, 4));
+  P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->num_tiles, (int64_t)P->table->num_cus * per_cu));
+}
+
 // Records K8h may append (the groups): as finalize's compaction of a hash table sizes its output.
 int64_t part_hash_out_cap(const pgpu_plan_s* P) {
   return std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
@@ -2587,20 +2628,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
       int pbits = 0, sbits = 0;
       if (hash_part) {
-        // LDS table of 2^sbits entries within kHashPartLds; partitions: the plan's group bound at <= half load,
-        // at most kMaxParts (more groups than that holds take further K8h rounds)
-        // PGPU_PART_HASH_LDS_KB / PGPU_PART_HASH_PBITS (read per plan: A/B, and tests that force K8h's extra rounds)
-        // override the LDS budget and the partition-bit cap.  13 bits keep K8a / K8c's LDS histogram at 32 KB (three
-        // workgroups per CU at their VGPR count); 40 KB tables (2 048 entries of COUNT + SUM) let four K8h workgroups
-        // share a CU.  Measured on c5_hash (10^7 groups, r04): 80 KB tables 7.67 ms per query, 40 KB 5.42-5.56, 14
-        // partition bits with 80 KB 11.7-12.7, the global hash table 14.8.
-        const char* lk = getenv("PGPU_PART_HASH_LDS_KB");
-        const int64_t lds_budget = lk && atoi(lk) > 0 ? std::min<int64_t>((int64_t)atoi(lk) * 1024, 128 * 1024) : kHashPartLds;
-        sbits = 13;
-        while (sbits > 8 && (int64_t)part_hash_lds(sbits, nslots) > lds_budget) --sbits;
-        const char* pb = getenv("PGPU_PART_HASH_PBITS");
-        const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 13;
-        while (pbits < max_pbits && (int64_t(1) << (pbits + sbits - 1)) < P->group_bound) ++pbits;
+        hash_part_bits(P->group_bound, nslots, &pbits, &sbits);
         shift = 0;
         parts = int64_t(1) << pbits;
       }
@@ -4158,6 +4186,7 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     if (P->hash && P->groups_seen && P->stage_end.empty() && P->merged_records < 0) {
       const int64_t g = P->groups_seen->load(std::memory_order_relaxed);
       if (g >= 0) P->num_keys = hash_capacity(std::min<int64_t>(g, P->group_bound));
+      if (g >= 0 && P->part_hash) hash_part_resize(P, std::max<int64_t>(g, 1));
     }
     return true;
   }

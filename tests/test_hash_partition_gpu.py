@@ -64,10 +64,11 @@ def test_hash_partition_rounds(oracle, sparse, monkeypatch):
 
 
 def test_hash_partition_rounds_packed(oracle, sparse, monkeypatch):
-    """Packed records (hashed key bits | value) left pending: LDS tables of 256 entries for ~1 800 groups per
-    partition, so K8h writes packed words back and re-reads them over several rounds."""
+    """Packed records (hashed key bits | value) left pending: 128 partitions of 256-entry LDS tables for ~1 800 groups
+    each, so K8h writes packed words back and re-reads them over several rounds."""
     t, hs, segs = sparse
-    monkeypatch.setenv("PGPU_PART_HASH_LDS_KB", "4")
+    monkeypatch.setenv("PGPU_PART_HASH_LDS_KB", "4")  # 256 entries
+    monkeypatch.setenv("PGPU_PART_HASH_PBITS", "7")   # 128 partitions: 7 bits, just room for the 7-bit values
     q = parse_query(QUERIES[3], num_groups_limit=10 ** 9)
     q.no_plan_cache = True
     assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)

@@ -251,6 +251,9 @@ struct KPartParams {
   int32_t pbits;
   int32_t sbits;
   uint32_t* rec_key32;                // [rec_cap] final layout: the whole key
+  // 1 (hashed, two-level, one u32 value stream): K8c writes each record as one u64 (hk | value << 32) at mid_val
+  // instead of a u32 key and a u32 value in two arrays; K8e reads it so
+  int32_t mid_pair;
   uint64_t* out_rec;                  // [rec_cap][1 + num_slots]
   unsigned long long* out_count;
 };

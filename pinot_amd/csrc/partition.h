@@ -107,6 +107,28 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
       }
     return;
   }
+  if (pp.mid_pair) {  // hashed, one u32 value: (hk | value << 32) in one 8-byte word, one scattered store per record
+    const KCol& c = S.cols[pp.stream_col[0]];
+    uint32_t ids[16];
+    decode_group<H>(c.fwd, c.bits, group, ids);
+    uint32_t v[16];
+    if (c.dkey) {
+      gmem<int64_t>* __restrict__ dk = gp(c.dkey);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? (uint32_t)dk[ids[i]] : 0u;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = (uint32_t)(c.key_base + (int64_t)ids[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) {
+        const uint32_t hk = part_hash((uint32_t)key[i]);
+        const uint32_t at = atomicAdd(&cursor[hpart(pp, hk) >> pp.cshift], 1u);
+        pp.mid_val[at] = (uint64_t)hk | ((uint64_t)v[i] << 32);
+      }
+    return;
+  }
   uint32_t pos[16];
   if (pp.hashed) {  // the coarse run of the key's hashed partition; the whole hashed key stored
 #pragma unroll
@@ -284,10 +306,20 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
     __syncthreads();  // (also: the previous batch's write-out has read the staged arrays)
     uint32_t k[NB], rank[NB];
     uint64_t v0[NB];  // stream 0's values, loaded with the keys so they are in flight through the sort
+    if (pp.mid_pair) {  // (hashed key, u32 value) words
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const uint32_t i = tid + b * kBlock;
-      k[b] = i < n ? pp.mid_key[b0 + i] : ~0u;
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t i = tid + b * kBlock;
+        const uint64_t w = pp.mid_val[b0 + (i < n ? i : 0u)];
+        k[b] = i < n ? (uint32_t)w : ~0u;
+        v0[b] = (uint64_t)(uint32_t)(w >> 32);
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t i = tid + b * kBlock;
+        k[b] = i < n ? pp.mid_key[b0 + i] : ~0u;
+      }
     }
     if (pp.pack_bits) {
 #pragma unroll
@@ -295,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
         v0[b] = (uint64_t)(pp.pack_min + (int64_t)(k[b] >> cbits));  // as the u32 record the aggregate reads
         k[b] = tid + b * kBlock < n ? k[b] & kmask : ~0u;  // (a packed word may be all ones)
       }
-    } else {
+    } else if (!pp.mid_pair) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         const uint32_t r = b0 + min(tid + b * kBlock, n - 1u);

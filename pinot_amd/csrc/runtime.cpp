@@ -3279,6 +3279,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.fine_fill = sc->fine_fill.as<uint32_t>();
     if (P->part_hash) {
       pp.hashed = 1;
+      static const bool no_pair = getenv_flag("PGPU_NO_MID_PAIR");  // A/B: key and value arrays
+      pp.mid_pair = !no_pair && cshift > 0 && pp.num_streams == 1 && P->part_val32 && !P->stream_f64[0] ? 1 : 0;
       pp.pbits = P->part_pbits;
       pp.sbits = P->part_sbits;
       TRY(sc->rec_key32.ensure((size_t)cap * 4));

@@ -3351,28 +3351,6 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
   return 0;
 }
 
-// The buffers finalize fills before it waits for the plan's device work, grown now: growing a device buffer frees
-// the old one (hipFree waits for the device), so a growth inside finalize would block its wait -- and with it a
-// pgpu_plan_cancel from another thread -- until the scan is done.  Sizes as plan_finalize_impl takes them for the
-// plan's own table.
-int prepare_finalize(pgpu_plan_s* P) {
-  Scratch* sc = P->scratch;
-  const int nslots = (int)P->slot_kind.size();
-  const int64_t G = P->num_keys, words = (int64_t)nslots * G;
-  TRY(sc->counter.ensure(64 + (size_t)kMaxSlots * 16));
-  TRY(sc->readback.ensure(64 + (size_t)nslots * 16));
-  if (!P->hash && words * 8 <= kHostCompactBytes) {
-    TRY(sc->readback.ensure((size_t)words * 8 + 64));
-  } else if (!P->hash) {
-    TRY(sc->cslots.ensure((size_t)std::max<int64_t>(compact_ordered_chunks(G), 1) * 4));
-  } else if (!P->part_hash_live) {
-    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0 ? P->merged_records
-                                                                                     : std::max<int64_t>(P->total_docs, 1)));
-    TRY(sc->ckeys.ensure((size_t)cap * 8 * (1 + nslots)));
-  }
-  return 0;
-}
-
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   Scratch* sc = P->scratch;
   const int nslots = X.nslots;
@@ -3472,7 +3450,6 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
       launch_leap2_compose(X.leap_segs, P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream))
     return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIP_TRY(hipEventRecord(sc->ev[3], stream));
-  TRY(prepare_finalize(P));
   P->last_stream = stream;
   P->executed = true;
   if (trace_on()) fprintf(stderr, "[pgpu] execute: %.1f us host\n", now_us() - X.t_start);
@@ -3512,6 +3489,23 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   const int64_t words = (int64_t)nslots * G;
   double t_sync1 = 0;
   R->pool = P->table->result_pool;
+  {
+    // The buffers filled before the wait below: growing one frees the old one, and hipFree waits for the whole
+    // device -- it would hold the wait (and a pgpu_plan_cancel or the query's deadline) until the scan is done.  When
+    // one must grow, the plan's work is waited for first (cancel- and deadline-aware), then the buffers grow.
+    bool grow = sc->counter.cap < 64 + (size_t)kMaxSlots * 16 || sc->readback.cap < 64 + (size_t)nslots * 16;
+    if (!P->hash && words * 8 <= kHostCompactBytes) grow |= sc->readback.cap < (size_t)words * 8 + 64;
+    else if (!P->hash) grow |= sc->cslots.cap < (size_t)std::max<int64_t>(compact_ordered_chunks(G), 1) * 4;
+    else if (!P->part_hash_live)
+      grow |= sc->ckeys.cap < (size_t)std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0
+                                                                                 ? P->merged_records
+                                                                                 : std::max<int64_t>(P->total_docs, 1))) *
+                                 8 * (1 + nslots);
+    if (grow) {
+      TRY(wait_plan(P, stream));
+      TRY(sc->counter.ensure(64 + (size_t)kMaxSlots * 16));
+    }
+  }
   if (!P->hash && words * 8 <= kHostCompactBytes) {
     // small dense table: one copy (table + stats) and one sync, compacted on the host in key order
     TRY(sc->readback.ensure((size_t)words * 8 + 64));

@@ -221,13 +221,6 @@ __device__ __forceinline__ uint32_t array_group_mask(uint64_t e, int64_t group) 
   return m;
 }
 
-// One 32-doc group of a LEAF_BITDIR leaf from its block's directory entry (0: no docs; a BITMAP container's address;
-// an ARRAY container's address | 1 with its count in bits 48-63).
-__device__ __forceinline__ uint32_t bitdir_mask(uint64_t e, int negate, int64_t group) {
-  const uint32_t m = (e & 1ull) ? array_group_mask(e, group) : e ? gp(reinterpret_cast<const uint32_t*>(e))[group & 2047] : 0u;
-  return negate ? ~m : m;
-}
-
 __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo, uint32_t span, const uint32_t* set,
                                               const uint32_t* fwd, int bits, int64_t group) {
   if (kind == LEAF_DOCRANGE) {
@@ -238,7 +231,11 @@ __device__ __forceinline__ uint32_t leaf_eval(int kind, int negate, uint32_t lo,
     const uint32_t m = gp(set)[group];
     return negate ? ~m : m;
   }
-  if (kind == LEAF_BITDIR) return bitdir_mask(gp(reinterpret_cast<const uint64_t*>(set))[group >> 11], negate, group);
+  if (kind == LEAF_BITDIR) {
+    const uint64_t e = gp(reinterpret_cast<const uint64_t*>(set))[group >> 11];
+    const uint32_t m = (e & 1ull) ? array_group_mask(e, group) : e ? gp(reinterpret_cast<const uint32_t*>(e))[group & 2047] : 0u;
+    return negate ? ~m : m;
+  }
   return leaf_eval_words(kind, negate, lo, span, set, fwd + group * (int64_t)bits, bits);
 }
 

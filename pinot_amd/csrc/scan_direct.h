@@ -123,11 +123,6 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
     // named registers, not an array: a runtime-guarded array of structs lands in scratch
     LeafReg R0{}, R1{}, R2{}, R3{};
     const int nl = p.num_leaves;
-    // A LEAF_BITDIR first leaf (an inverted index read in place): the directory entry of the next tile's block is
-    // loaded a tile ahead, so a tile's chain is container word + the scan leaves' words, not directory -> container
-    // -> words (a tile's 256 groups lie in one 65 536-doc block)
-    uint64_t bd_next = 0;
-    int64_t bd_next_blk = -1;
 #define PGPU_LOAD_LEAVES()                      \
   do {                                          \
     if (nl > 0) R0 = load_leaf_reg(p, S, 0);    \
@@ -146,7 +141,6 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
         nd = S.hdr->num_docs;
         stats = S.hdr->stats;
         if (fast) PGPU_LOAD_LEAVES();
-        bd_next_blk = -1;
       }
       const int64_t lt = t - tile_base;
       const int64_t group = (lt >> p.tile_shift) * kBlock + tid;
@@ -164,24 +158,12 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;
-        const bool bd = !DENSE && nl > 0 && R0.kind == LEAF_BITDIR;  // (sparse instance: the dense one is at its limit)
-        uint64_t bd_e = 0;
-        if (bd) {
-          const int64_t blk = gclamp >> 11;
-          bd_e = blk == bd_next_blk ? bd_next : gp(reinterpret_cast<const uint64_t*>(R0.set))[blk];
-          bd_next_blk = -1;
-          if (t + t_step < t_end && next_seg == cur_seg) {
-            const int64_t ng = ((t + t_step - tile_base) >> p.tile_shift) * kBlock + tid;
-            bd_next_blk = (ng < ngroups ? ng : ngroups - 1) >> 11;
-            bd_next = gp(reinterpret_cast<const uint64_t*>(R0.set))[bd_next_blk];
-          }
-        }
         for (int l = 0; l < nl; ++l) {
           if (!leap && !__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
           // applyAnd of a scan after the index leaves (AndDocIdSet.java:124-126): its input docs are its entries
           if ((stats >> (4 + l)) & 1) in_filter += __popc(mask);
           const LeafReg& r = l == 0 ? R0 : l == 1 ? R1 : l == 2 ? R2 : R3;
-          const uint32_t m = l == 0 && bd ? bitdir_mask(bd_e, R0.negate, gclamp) : leaf_mask_reg(r, gclamp);
+          const uint32_t m = leaf_mask_reg(r, gclamp);
           ma = l == la ? m : ma;
           mb = l == lb ? m : mb;
           mask &= m;

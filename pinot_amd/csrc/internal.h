@@ -368,6 +368,8 @@ int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, cons
 // Compact form of a large dense table: counts per chunk + exclusive scan (total into *total) + each slot's range over
 // the present groups (minmax [2][num_slots]); then the presence bitmap (ceil(num_keys / 64) words) and the slots'
 // words of the present groups in key order at compact_slot_width bytes, slot s from out_slots + s * cap * 8.
+// chunk_scratch bytes launch_compact_dense_count needs (chunk counts, then per-chunk slot ranges).
+size_t compact_scratch_bytes(int64_t num_keys, int32_t num_slots);
 int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t num_keys, uint32_t* chunk_scratch,
                                unsigned long long* total, long long* minmax, void* stream);
 int launch_compact_dense_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int32_t* slot_kind,

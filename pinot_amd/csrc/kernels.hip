@@ -246,9 +246,33 @@ __global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t* __re
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  if (minmax && threadIdx.x < num_slots && smm[threadIdx.x] <= smm[num_slots + threadIdx.x]) {
-    atomicMin(minmax + threadIdx.x, smm[threadIdx.x]);
-    atomicMax(minmax + num_slots + threadIdx.x, smm[num_slots + threadIdx.x]);
+  // the chunk's ranges to its own row (reduced by compact_minmax_kernel): thousands of chunks' atomics on the same
+  // few words serialised at the memory side and took most of this kernel's time
+  if (minmax && threadIdx.x < 2 * num_slots) minmax[(int64_t)blockIdx.x * 2 * num_slots + threadIdx.x] = smm[threadIdx.x];
+}
+
+// Per slot, the min / max over the chunks' rows (compact_count_kernel) into minmax[2][num_slots].
+__global__ __launch_bounds__(256) void compact_minmax_kernel(const long long* __restrict__ rows, int64_t nch,
+                                                             int32_t num_slots, long long* __restrict__ minmax) {
+  __shared__ long long part[4];
+  for (int s = 0; s < 2 * num_slots; ++s) {
+    const bool is_min = s < num_slots;
+    long long v = is_min ? INT64_MAX : INT64_MIN;
+    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) {
+      const long long x = rows[c * 2 * num_slots + s];
+      v = is_min ? min(v, x) : max(v, x);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const long long y = __shfl_xor(v, off);
+      v = is_min ? min(v, y) : max(v, y);
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 4; ++w) v = is_min ? min(v, part[w]) : max(v, part[w]);
+      minmax[s] = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -885,6 +909,10 @@ int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream) {
 }
 
 int64_t compact_ordered_chunks(int64_t num_keys) { return (num_keys + kCompactChunk - 1) / kCompactChunk; }
+size_t compact_scratch_bytes(int64_t num_keys, int32_t num_slots) {
+  const int64_t nch = std::max<int64_t>(compact_ordered_chunks(num_keys), 1);
+  return (size_t)((nch * 4 + 7) & ~int64_t(7)) + (size_t)nch * 2 * num_slots * 8;
+}
 
 int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num_keys, int64_t key_base,
                            const int64_t* key_stride, const int64_t* key_card, const int64_t* key_off,
@@ -912,10 +940,12 @@ int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t
                                unsigned long long* total, long long* minmax, void* stream) {
   const int64_t nch = compact_ordered_chunks(num_keys);
   if (nch < 1 || nch > INT32_MAX || num_slots > kMaxSlots) return -1;
-  if (hipMemsetAsync(minmax, 0x7F, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
-  if (hipMemsetAsync(minmax + num_slots, 0x80, (size_t)num_slots * 8, S(stream)) != hipSuccess) return -1;
+  // per-chunk ranges after the counts in chunk_scratch (compact_scratch_bytes), reduced into minmax
+  long long* rows = reinterpret_cast<long long*>(reinterpret_cast<uint8_t*>(chunk_scratch) + ((nch * 4 + 7) & ~int64_t(7)));
   hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch,
-                     num_slots, minmax);
+                     num_slots, minmax ? rows : nullptr);
+  if (minmax)
+    hipLaunchKernelGGL(compact_minmax_kernel, dim3(1), dim3(256), 0, S(stream), rows, nch, num_slots, minmax);
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);
   return PGPU_HIP_OK(hipGetLastError());
 }

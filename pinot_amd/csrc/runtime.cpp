@@ -3495,7 +3495,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     // one must grow, the plan's work is waited for first (cancel- and deadline-aware), then the buffers grow.
     bool grow = sc->counter.cap < 64 + (size_t)kMaxSlots * 16 || sc->readback.cap < 64 + (size_t)nslots * 16;
     if (!P->hash && words * 8 <= kHostCompactBytes) grow |= sc->readback.cap < (size_t)words * 8 + 64;
-    else if (!P->hash) grow |= sc->cslots.cap < (size_t)std::max<int64_t>(compact_ordered_chunks(G), 1) * 4;
+    else if (!P->hash) grow |= sc->cslots.cap < compact_scratch_bytes(G, nslots);
     else if (!P->part_hash_live)
       grow |= sc->ckeys.cap < (size_t)std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0
                                                                                  ? P->merged_records
@@ -3538,7 +3538,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     // narrowest width their range allows (decoded on the host on first access).
     const int64_t nch = compact_ordered_chunks(G);
     TRY(sc->counter.ensure(64 + (size_t)nslots * 16));
-    TRY(sc->cslots.ensure((size_t)std::max<int64_t>(nch, 1) * 4));
+    TRY(sc->cslots.ensure(compact_scratch_bytes(G, nslots)));
     long long* d_minmax = reinterpret_cast<long long*>(sc->counter.as<uint8_t>() + 64);
     if (launch_compact_dense_count(table, nslots, G, sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(),
                                    d_minmax, stream))

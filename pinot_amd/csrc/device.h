@@ -483,7 +483,10 @@ __device__ __forceinline__ int64_t slot_fold(int kind, int64_t a, int64_t v) {
 // (segment record -> forward-index words -> dictId -> LUT / dictionary value) is issued for all NB docs before any
 // is consumed, so a batch pays each memory round trip once.  Docs with ok[b] == false read doc 0 of their segment
 // (always in bounds) and add nothing.
-template <int MODE, int NB>
+// SIMPLE (KParams of a "simple" dense plan, plan_create_impl): every group-by column's dictionary is a contiguous run of
+// the global one in every segment (no LUT), every aggregated column is an integer of consecutive values (no
+// dictionary lookup) and no slot sums doubles -- the gathers compile away, and with them their registers.
+template <int MODE, int NB, bool SIMPLE = false>
 __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView (&S)[NB], const int64_t (&doc)[NB],
                                                 const bool (&ok)[NB], uint64_t* __restrict__ tbl, int64_t G) {
   int64_t key[NB];
@@ -506,7 +509,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {  // the lanes' docs may come from different segments: per-lane select
       const KCol& c = S[b].cols[kc];
-      g[b] = c.lut ? gp(c.lut)[id[b]] : (int32_t)id[b] + c.lut_off;
+      g[b] = !SIMPLE && c.lut ? gp(c.lut)[id[b]] : (int32_t)id[b] + c.lut_off;
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) key[b] += (int64_t)g[b] * p.key_stride[j];
@@ -549,14 +552,14 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
         }
         prev_col = col;
       }
-      if (kind == SLOT_SUM_F64) {
+      if (!SIMPLE && kind == SLOT_SUM_F64) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) dval[b] = gp(S[b].cols[col].dval)[id[b]];
       } else {
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const KCol& c = S[b].cols[col];
-          ikey[b] = c.dkey ? gp(c.dkey)[id[b]] : c.key_base + (int64_t)id[b];
+          ikey[b] = !SIMPLE && c.dkey ? gp(c.dkey)[id[b]] : c.key_base + (int64_t)id[b];
         }
       }
     }
@@ -720,7 +723,7 @@ __device__ __forceinline__ void accumulate16_f(uint64_t* __restrict__ row, const
 }
 
 // One half (docs H..H+15 of the lane's group) of aggregate_group.
-template <int MODE, int H>
+template <int MODE, int H, bool SIMPLE = false>
 __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
                                                uint64_t* __restrict__ tbl, int64_t G) {
   const uint32_t m = (mask >> H) & 0xFFFFu;
@@ -732,7 +735,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     const KCol& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
     const int32_t stride = (int32_t)p.key_stride[j];
-    if (c.lut) {  // segment-uniform: the whole wave reads one segment here
+    if (!SIMPLE && c.lut) {  // segment-uniform: the whole wave reads one segment here
       int32_t g[16];
 #if PGPU_SADDR
       const int32_t* lut = wave_uniform(c.lut);
@@ -772,7 +775,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     decode_group<H>(c.fwd, c.bits, group, ids);
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
       int64_t v[16];
-      if (c.dkey) {
+      if (!SIMPLE && c.dkey) {
 #if PGPU_SADDR
         const int64_t* dk = wave_uniform(c.dkey);
 #pragma unroll
@@ -803,7 +806,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
                              MODE == MODE_LDS && r == p.pack_slot ? (1ull << kLdsPackShift) : 0ull);
       }
     }
-    if (need_f) {
+    if (!SIMPLE && need_f) {
       double v[16];
 #if PGPU_SADDR
       const double* dv = wave_uniform(c.dval);
@@ -835,16 +838,16 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
 // Aggregates the matched docs (bits of `mask`) of this lane's 32-doc group `group` of segment S, 16 docs at a
 // time.  Dense key spaces only (MODE_LDS / MODE_GLOBAL: composite keys < 2^31).  Docs beyond numDocs decode from
 // the zero padding to dictId 0 (in bounds) and are never in `mask`.
-template <int MODE>
+template <int MODE, bool SIMPLE = false>
 __device__ __forceinline__ void aggregate_group(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
                                                 uint64_t* __restrict__ tbl, int64_t G) {
   // wave-uniform conditions: the single-row (G == 1) fold inside uses cross-lane shuffles
-  if (__any((mask & 0xFFFFu) != 0u)) aggregate_half<MODE, 0>(p, S, group, mask, tbl, G);
-  if (__any((mask >> 16) != 0u)) aggregate_half<MODE, 16>(p, S, group, mask, tbl, G);
+  if (__any((mask & 0xFFFFu) != 0u)) aggregate_half<MODE, 0, SIMPLE>(p, S, group, mask, tbl, G);
+  if (__any((mask >> 16) != 0u)) aggregate_half<MODE, 16, SIMPLE>(p, S, group, mask, tbl, G);
 }
 
 // Drains a wave's queue of matched (segment, doc) entries: 2 per lane per batch.
-template <int MODE>
+template <int MODE, bool SIMPLE = false>
 __device__ __forceinline__ void flush_wave_queue(const KParams& p, const uint32_t* qd, const uint32_t* qs, uint32_t qn,
                                                  int lane, uint64_t* __restrict__ tbl, int64_t G) {
   for (uint32_t base = 0; base < qn; base += 128) {
@@ -856,7 +859,7 @@ __device__ __forceinline__ void flush_wave_queue(const KParams& p, const uint32_
     doc[0] = ok[0] ? qd[i0] : 0;
     doc[1] = ok[1] ? qd[i1] : 0;
     const SegView S[2] = {seg_view(p, ok[0] ? (int)qs[i0] : (int)qs[0]), seg_view(p, ok[1] ? (int)qs[i1] : (int)qs[0])};
-    aggregate_batch<MODE, 2>(p, S, doc, ok, tbl, G);
+    aggregate_batch<MODE, 2, SIMPLE>(p, S, doc, ok, tbl, G);
   }
 }
 

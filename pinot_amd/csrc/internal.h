@@ -326,9 +326,10 @@ int launch_table_init(uint64_t* table, const int32_t* slot_kind, int32_t num_slo
 // 0 = none) has passed.
 int launch_expand_tiles(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, int32_t* tile_seg,
                         uint64_t deadline, unsigned long long* stats, void* stream);
-int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream);
+// variant: 0 sparse instance, 1 dense, 2 dense "simple" (no LUT / dictionary gathers, no double sums)
+int launch_filter_groupby(const KParams& p, int mode, int variant, int grid, size_t lds_bytes, void* stream);
 // Resident workgroups per CU of the direct kernel instance (< 0: query failed).
-int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes);
+int occupancy_filter_groupby(int mode, int variant, size_t lds_bytes);
 int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind_dev, int32_t num_slots, int64_t num_keys,
                         int32_t num_blocks, uint64_t* out, void* stream);
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,

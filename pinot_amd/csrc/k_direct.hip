@@ -9,24 +9,29 @@
 
 namespace pgpu {
 
-int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream) {
-  if (dense)
-    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, true>), dim3(grid), dim3(kBlock), lds_bytes,
-                       reinterpret_cast<hipStream_t>(stream), p);
+// variant: 0 the sparse instance, 1 the dense one, 2 the dense one for "simple" plans (aggregate_batch's SIMPLE).
+int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, int variant, int grid, size_t lds_bytes, void* stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (variant == 2)
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, true, true>), dim3(grid), dim3(kBlock), lds_bytes, s, p);
+  else if (variant == 1)
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, true>), dim3(grid), dim3(kBlock), lds_bytes, s, p);
   else
-    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, false>), dim3(grid), dim3(kBlock), lds_bytes,
-                       reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, false>), dim3(grid), dim3(kBlock), lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Resident workgroups per CU of the instance (registers and LDS): the persistent grid is sized to exactly fill
 // the chip, since its tile ranges are assigned statically.
-int PGPU_CAT(occupancy_direct_mode, PGPU_MODE)(bool dense, size_t lds_bytes) {
+int PGPU_CAT(occupancy_direct_mode, PGPU_MODE)(int variant, size_t lds_bytes) {
   int n = 0;
-  const hipError_t e = dense ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                                   &n, filter_groupby_kernel<PGPU_MODE, true>, kBlock, lds_bytes)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                                   &n, filter_groupby_kernel<PGPU_MODE, false>, kBlock, lds_bytes);
+  const hipError_t e =
+      variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, filter_groupby_kernel<PGPU_MODE, true, true>, kBlock,
+                                                                   lds_bytes)
+      : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, filter_groupby_kernel<PGPU_MODE, true>, kBlock,
+                                                                     lds_bytes)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, filter_groupby_kernel<PGPU_MODE, false>, kBlock,
+                                                                    lds_bytes);
   return e == hipSuccess ? n : -1;
 }
 

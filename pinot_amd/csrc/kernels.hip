@@ -782,12 +782,12 @@ int launch_hash_unpack(uint64_t* table, const unsigned long long* hash_keys, int
 }
 
 // One object per (kernel family, mode): k_direct.hip / k_startree.hip compiled with -DPGPU_MODE=0,1,2.
-int launch_direct_mode0(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
-int launch_direct_mode1(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
-int launch_direct_mode2(const KParams& p, bool dense, int grid, size_t lds_bytes, void* stream);
-int occupancy_direct_mode0(bool dense, size_t lds_bytes);
-int occupancy_direct_mode1(bool dense, size_t lds_bytes);
-int occupancy_direct_mode2(bool dense, size_t lds_bytes);
+int launch_direct_mode0(const KParams& p, int variant, int grid, size_t lds_bytes, void* stream);
+int launch_direct_mode1(const KParams& p, int variant, int grid, size_t lds_bytes, void* stream);
+int launch_direct_mode2(const KParams& p, int variant, int grid, size_t lds_bytes, void* stream);
+int occupancy_direct_mode0(int variant, size_t lds_bytes);
+int occupancy_direct_mode1(int variant, size_t lds_bytes);
+int occupancy_direct_mode2(int variant, size_t lds_bytes);
 
 int launch_startree_scan_mode0(const KStarParams& p, size_t lds_bytes, void* stream);
 int launch_startree_scan_mode1(const KStarParams& p, size_t lds_bytes, void* stream);
@@ -801,19 +801,19 @@ int launch_startree_scan(const KStarParams& p, int mode, size_t lds_bytes, void*
   }
 }
 
-int launch_filter_groupby(const KParams& p, int mode, bool dense, int grid, size_t lds_bytes, void* stream) {
+int launch_filter_groupby(const KParams& p, int mode, int variant, int grid, size_t lds_bytes, void* stream) {
   switch (mode) {
-    case MODE_LDS: return launch_direct_mode0(p, dense, grid, lds_bytes, stream);
-    case MODE_GLOBAL: return launch_direct_mode1(p, dense, grid, lds_bytes, stream);
-    default: return launch_direct_mode2(p, dense, grid, lds_bytes, stream);
+    case MODE_LDS: return launch_direct_mode0(p, variant, grid, lds_bytes, stream);
+    case MODE_GLOBAL: return launch_direct_mode1(p, variant, grid, lds_bytes, stream);
+    default: return launch_direct_mode2(p, variant, grid, lds_bytes, stream);
   }
 }
 
-int occupancy_filter_groupby(int mode, bool dense, size_t lds_bytes) {
+int occupancy_filter_groupby(int mode, int variant, size_t lds_bytes) {
   switch (mode) {
-    case MODE_LDS: return occupancy_direct_mode0(dense, lds_bytes);
-    case MODE_GLOBAL: return occupancy_direct_mode1(dense, lds_bytes);
-    default: return occupancy_direct_mode2(dense, lds_bytes);
+    case MODE_LDS: return occupancy_direct_mode0(variant, lds_bytes);
+    case MODE_GLOBAL: return occupancy_direct_mode1(variant, lds_bytes);
+    default: return occupancy_direct_mode2(variant, lds_bytes);
   }
 }
 

@@ -1118,6 +1118,10 @@ struct pgpu_plan_s {
   int grid = 0;
   size_t lds_bytes = 0;
   bool dense = false;                     // direct kernel instance with whole-group decode (dense tiles)
+  // dense plans whose group-by columns need no LUT and whose operands no dictionary lookup in any segment, with no
+  // double sums: the dense instance compiled without those gathers (aggregate_batch's SIMPLE; fewer registers)
+  bool dense_simple = false;
+  bool gathers = false;                   // some segment's key LUT or operand dictionary is read (not simple)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
   std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
   int launches_done = 0;
@@ -2293,6 +2297,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // on the host worker pool for large segment lists; records carry chunk-relative tile / set offsets, fixed up
   // when the chunks are concatenated in segment order.
   struct Chunk {
+    bool gathers = false;  // pgpu_plan_s::gathers
     std::vector<uint8_t> rec;
     std::vector<uint32_t> set_words;
     std::vector<std::pair<int64_t, int64_t>> set_fix;
@@ -2448,6 +2453,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           kc[j].dval = c.d_val;
         }
       }
+      for (int j = 0; j < nqc; ++j)
+        C.gathers |= (qcol_key[j] >= 0 && kc[j].lut != nullptr) || (qcol_val[j] && kc[j].dkey != nullptr);
       KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
       const int64_t rec_off = (int64_t)C.rec.size();
       for (int k = 0; k < P->num_leaves; ++k) {
@@ -2586,15 +2593,23 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
     P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16 && !getenv_flag("PGPU_NO_DENSE");
+    {
+      bool f64 = false;
+      for (int k : P->slot_kind) f64 |= k == SLOT_SUM_F64;
+      static const bool no_simple = getenv_flag("PGPU_NO_SIMPLE");  // A/B
+      // (a streamed plan configures before its later chunks are planned: never simple)
+      P->dense_simple = P->dense && !P->gathers && !f64 && P->tile_bound == 0 && !no_simple;
+    }
+    const int variant = P->dense_simple ? 2 : P->dense ? 1 : 0;
     int per_cu;  // resident workgroups per CU
     {
       static std::mutex occ_mu;
       static std::map<std::tuple<int, int, int, size_t>, int> occ_cache;  // (device, mode, dense, lds) -> per CU
       {
         std::lock_guard<std::mutex> g(occ_mu);
-        const auto k = std::make_tuple(t->device, (int)P->mode, (int)P->dense, P->lds_bytes);
+        const auto k = std::make_tuple(t->device, (int)P->mode, variant, P->lds_bytes);
         auto it = occ_cache.find(k);
-        if (it == occ_cache.end()) it = occ_cache.emplace(k, occupancy_filter_groupby(P->mode, P->dense, P->lds_bytes)).first;
+        if (it == occ_cache.end()) it = occ_cache.emplace(k, occupancy_filter_groupby(P->mode, variant, P->lds_bytes)).first;
         per_cu = it->second;
       }
       if (per_cu <= 0) per_cu = 1;
@@ -2725,6 +2740,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       P->generic.push_back(std::move(g));
     }
     P->any_leap2 |= C.any_leap2;
+    P->gathers |= C.gathers;
     P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
@@ -3334,7 +3350,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
-    const int rc = launch_filter_groupby(kp, P->mode, P->dense, grid, P->lds_bytes, stream);
+    const int rc = launch_filter_groupby(kp, P->mode, P->dense_simple ? 2 : P->dense ? 1 : 0, grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));

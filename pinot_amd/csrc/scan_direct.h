@@ -49,14 +49,17 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 // DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
-template <int MODE, bool DENSE>
+template <int MODE, bool DENSE, bool SIMPLE = false>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
 #ifndef PGPU_DENSE_MIN_WAVES
 #define PGPU_DENSE_MIN_WAVES 3
 #endif
-__global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
+#ifndef PGPU_SIMPLE_MIN_WAVES
+#define PGPU_SIMPLE_MIN_WAVES 4
+#endif
+__global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : PGPU_DENSE_MIN_WAVES) : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t G = p.num_keys_total;
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
       }
       if (DENSE && MODE != MODE_HASH && wave_cnt >= (uint32_t)kDenseGroupMin) {
         // dense tile: whole-group decode of the group-by / aggregated columns
-        aggregate_group<MODE>(p, S, gclamp, mask, tbl, G);
+        aggregate_group<MODE, SIMPLE>(p, S, gclamp, mask, tbl, G);
       } else if (__any(cnt > 2u)) {
         // dense: the lane's own 32-doc group, 2 matched docs per batch (the lines are already cached)
         while (__any(mask != 0u)) {
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
             mask &= mask - 1u;
           }
           const SegView SS[2] = {S, S};
-          aggregate_batch<MODE, 2>(p, SS, doc, ok, tbl, G);
+          aggregate_batch<MODE, 2, SIMPLE>(p, SS, doc, ok, tbl, G);
         }
       } else if (__any(mask != 0u)) {
         // sparse: append to the wave's queue (<= 2 per lane, so <= 128 per tile), aggregate in batches
@@ -211,13 +214,13 @@ __global__ __launch_bounds__(kBlock, DENSE ? PGPU_DENSE_MIN_WAVES : PGPU_MIN_WAV
           qn += (uint32_t)__popcll(bal);
         }
         if (qn >= (uint32_t)kFlushAt) {
-          flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
+          flush_wave_queue<MODE, SIMPLE>(p, wq, wqs, qn, lane, tbl, G);
           qn = 0;
         }
       }
       ++kk;
     }
-    if (qn) flush_wave_queue<MODE>(p, wq, wqs, qn, lane, tbl, G);
+    if (qn) flush_wave_queue<MODE, SIMPLE>(p, wq, wqs, qn, lane, tbl, G);
     if (p.leap_maps)  // each wave stores its own bytes (tiles of other segments hold don't-care values)
       for (int k = lane; k < kk; k += 64)
         p.leap_maps[(t_begin + (int64_t)k * t_step) * (kBlock / 64) + wave] = lmaps[k * (kBlock / 64) + wave];

@@ -161,6 +161,20 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;
+        if (!DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE && p.pair_leaves) {
+          // index leaf + scan leaf (the indexed C3 shape): both requested together (bitdir_range), applied in order
+          uint32_t m0, m1;
+          bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, reinterpret_cast<const uint64_t*>(R0.set),
+                       R0.negate, gclamp, m0, m1);
+          if (__any(mask != 0u)) {
+            if ((stats >> 4) & 1) in_filter += __popc(mask);
+            mask &= m0;
+            if (__any(mask != 0u)) {
+              if ((stats >> 5) & 1) in_filter += __popc(mask);
+              mask &= m1;
+            }
+          }
+        } else
         for (int l = 0; l < nl; ++l) {
           if (!leap && !__any(mask != 0u)) break;  // AndDocIdIterator never scans past an empty child
           // applyAnd of a scan after the index leaves (AndDocIdSet.java:124-126): its input docs are its entries

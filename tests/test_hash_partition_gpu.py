@@ -95,3 +95,16 @@ def test_hash_partitions_exchange_materialises_table(oracle, sparse):
         assert_same(plan.finalize(), exp, q, SCHEMA)
     finally:
         plan.close()
+
+
+def test_group_paths(oracle, sparse):
+    """pgpu_plan_group_path across the key-space sizes of one table: an LDS table (small dense), hashed partitions
+    (sparse, < 2^31 keys), the global hash table (>= 2^31 keys) -- each against the oracle."""
+    t, hs, segs = sparse
+    for sql, path in (("SELECT COUNT(*), SUM(m) FROM t GROUP BY c", "lds"),
+                      ("SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c", "hash_partitioned"),
+                      ("SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c, s", "hash")):
+        q = parse_query(sql, num_groups_limit=10 ** 9)
+        with t.plan(hs, q) as p:
+            assert p.group_path() == path, sql
+        assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)

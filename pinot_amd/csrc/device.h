@@ -234,23 +234,24 @@ __device__ __forceinline__ uint32_t bitdir_mask(uint64_t e, int negate, int64_t 
 // them in Pinot's order (index leaf, then the scan on its survivors).
 template <int B>
 __device__ __forceinline__ void bitdir_range_b(const uint32_t* __restrict__ words, uint32_t lo, uint32_t span,
-                                               uint64_t e, int neg0, int64_t group, uint32_t& m0, uint32_t& m1) {
+                                               const uint64_t* dir, int neg0, int64_t group, uint32_t& m0,
+                                               uint32_t& m1) {
   uint32_t w[B + 1];
   load_group<B, true>(words, w);
-  m0 = bitdir_mask(e, neg0, group);
+  m0 = bitdir_mask(gp(dir)[group >> 11], neg0, group);
   m1 = span == 1 ? eq_all<B>(w, lo, std::make_integer_sequence<int, 32>{})
                  : range_all<B>(w, lo, lo + span, std::make_integer_sequence<int, 32>{});
 }
-// e: the group's block directory entry (loaded ahead by the caller).
 __device__ __forceinline__ void bitdir_range(const uint32_t* fwd, int bits, uint32_t lo, uint32_t span, int neg1,
-                                             uint64_t e, int neg0, int64_t group, uint32_t& m0, uint32_t& m1) {
+                                             const uint64_t* dir, int neg0, int64_t group, uint32_t& m0,
+                                             uint32_t& m1) {
   const uint32_t* words = fwd + group * (int64_t)bits;
   m0 = 0;
   m1 = 0;
   switch (bits) {
 #define PGPU_CASE(B)                                                 \
   case B:                                                            \
-    bitdir_range_b<B>(words, lo, span, e, neg0, group, m0, m1); \
+    bitdir_range_b<B>(words, lo, span, dir, neg0, group, m0, m1); \
     break;
     PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
     PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)

@@ -96,8 +96,7 @@ struct KParams {
   int32_t num_tiles;
   int32_t tile_shift;      // small plans: each 8192-doc tile is split into 1 << tile_shift tiles (16 / 8 docs per lane)
   int32_t tile_chunks;     // 1: each workgroup takes a contiguous run of tiles (else XCD-interleaved tiles)
-  int32_t pair_leaves;     // >= 1: an index leaf + a range scan evaluated together (bitdir_range); 2: the next
-                           // tile's directory entry loaded a tile ahead; 0: leaf by leaf (A/B)
+  int32_t pair_leaves;     // 1: an index leaf + a range scan are evaluated together (bitdir_range; 0 = A/B off)
   int32_t num_ops;         // 0 = match all
   int32_t pure_and;        // program is LEAF... AND(n): evaluate leaves with early exit, no stack
   int32_t ops[kMaxOps];    // (opcode << 16) | arg

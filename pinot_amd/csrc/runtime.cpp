@@ -3133,10 +3133,8 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   {
-    // A/B: PGPU_NO_PAIR_LEAVES=1 (leaf by leaf), PGPU_PAIR_PREFETCH=0 (no directory entry loaded a tile ahead)
-    static const bool no_pair = getenv_flag("PGPU_NO_PAIR_LEAVES");
-    static const bool no_pf = getenv("PGPU_PAIR_PREFETCH") && getenv("PGPU_PAIR_PREFETCH")[0] == '0';
-    kp.pair_leaves = no_pair ? 0 : no_pf ? 1 : 2;
+    static const bool no_pair = getenv_flag("PGPU_NO_PAIR_LEAVES");  // A/B
+    kp.pair_leaves = no_pair ? 0 : 1;
   }
   dense_lds_forms(P, &kp.pack_slot, &kp.narrow);
   kp.pack_shift = P->pack_shift;

@@ -126,10 +126,6 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
     // named registers, not an array: a runtime-guarded array of structs lands in scratch
     LeafReg R0{}, R1{}, R2{}, R3{};
     const int nl = p.num_leaves;
-    // the index + scan pair (bitdir_range): the next tile's directory entry, loaded a tile ahead (a tile's 256
-    // groups lie in one 65 536-doc block), so the container word and the scan's words are one round trip
-    uint64_t bd_next = 0;
-    int64_t bd_next_blk = -1;
 #define PGPU_LOAD_LEAVES()                      \
   do {                                          \
     if (nl > 0) R0 = load_leaf_reg(p, S, 0);    \
@@ -148,7 +144,6 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         nd = S.hdr->num_docs;
         stats = S.hdr->stats;
         if (fast) PGPU_LOAD_LEAVES();
-        bd_next_blk = -1;
       }
       const int64_t lt = t - tile_base;
       const int64_t group = (lt >> p.tile_shift) * kBlock + tid;
@@ -168,17 +163,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         uint32_t ma = 0, mb = 0;
         if (!DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE && p.pair_leaves) {
           // index leaf + scan leaf (the indexed C3 shape): both requested together (bitdir_range), applied in order
-          const uint64_t* dir = reinterpret_cast<const uint64_t*>(R0.set);
-          const int64_t blk = gclamp >> 11;
-          const uint64_t e = blk == bd_next_blk ? bd_next : gp(dir)[blk];
-          bd_next_blk = -1;
-          if (p.pair_leaves > 1 && t + t_step < t_end && next_seg == cur_seg) {
-            const int64_t ng = ((t + t_step - tile_base) >> p.tile_shift) * kBlock + tid;
-            bd_next_blk = (ng < ngroups ? ng : ngroups - 1) >> 11;
-            bd_next = gp(dir)[bd_next_blk];
-          }
           uint32_t m0, m1;
-          bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, e, R0.negate, gclamp, m0, m1);
+          bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, reinterpret_cast<const uint64_t*>(R0.set),
+                       R0.negate, gclamp, m0, m1);
           if (__any(mask != 0u)) {
             if ((stats >> 4) & 1) in_filter += __popc(mask);
             mask &= m0;

@@ -182,16 +182,46 @@ __global__ void table_init_kernel(uint64_t* __restrict__ table, SlotKinds kinds,
 }
 
 // Groups with COUNT > 0, entry-major: out[j * (1 + num_slots)] = key, then the slot words.
-__global__ void compact_kernel(const uint64_t* __restrict__ table, const unsigned long long* __restrict__ hash_keys,
-                               int32_t num_slots, int64_t num_keys, unsigned long long* __restrict__ counter,
-                               uint64_t* __restrict__ out, int64_t cap) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < num_keys; i += (int64_t)gridDim.x * blockDim.x) {
-    if (table[i] == 0) continue;  // row 0 = COUNT
-    const unsigned long long j = atomicAdd(counter, 1ull);
-    if ((int64_t)j >= cap) continue;
-    uint64_t* o = out + (int64_t)j * (1 + num_slots);
-    o[0] = hash_keys ? (uint64_t)hash_keys[i] : (uint64_t)i;
-    for (int s = 0; s < num_slots; ++s) o[1 + s] = table[(int64_t)s * num_keys + i];
+// Unordered compaction of a hash table: each workgroup takes kHashCompactChunk slots, counts its groups by ballot,
+// reserves their run with one atomic and writes it (an atomic per group -- or per wave -- on the one counter
+// serialised at the memory side: ~10^7 groups queued there).
+constexpr int kHashCompactChunk = 4096;
+__global__ __launch_bounds__(256) void compact_kernel(const uint64_t* __restrict__ table,
+                                                      const unsigned long long* __restrict__ hash_keys,
+                                                      int32_t num_slots, int64_t num_keys,
+                                                      unsigned long long* __restrict__ counter,
+                                                      uint64_t* __restrict__ out, int64_t cap) {
+  __shared__ uint32_t wave_tot[4];
+  __shared__ unsigned long long blk_base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kHashCompactChunk;
+  uint32_t mine = 0;
+  for (int r = 0; r < kHashCompactChunk / 256; ++r) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    mine += (uint32_t)__popcll(__ballot(i < num_keys && table[i] != 0));  // row 0 = COUNT
+  }
+  if (lane == 0) wave_tot[wave] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+    blk_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long at = blk_base;
+  for (int w = 0; w < wave; ++w) at += wave_tot[w];
+  for (int r = 0; r < kHashCompactChunk / 256; ++r) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const bool f = i < num_keys && table[i] != 0;
+    const uint64_t bal = __ballot(f);
+    if (f) {
+      const unsigned long long j = at + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
+      if ((int64_t)j < cap) {
+        uint64_t* o = out + (int64_t)j * (1 + num_slots);
+        o[0] = hash_keys ? (uint64_t)hash_keys[i] : (uint64_t)i;
+        for (int s = 0; s < num_slots; ++s) o[1 + s] = table[(int64_t)s * num_keys + i];
+      }
+    }
+    at += (unsigned long long)__popcll(bal);
   }
 }
 
@@ -844,9 +874,9 @@ int launch_reduce_slabs(const uint64_t* slab, const int32_t* slot_kind, int32_t 
 
 int launch_compact(const uint64_t* table, const unsigned long long* hash_keys, int32_t num_slots, int64_t num_keys,
                    unsigned long long* counter, uint64_t* out, int64_t out_cap, void* stream) {
-  int64_t grid = (num_keys + 255) / 256;
-  if (grid > 4096) grid = 4096;
+  int64_t grid = (num_keys + kHashCompactChunk - 1) / kHashCompactChunk;
   if (grid < 1) grid = 1;
+  if (grid > INT32_MAX) return -1;
   hipLaunchKernelGGL(compact_kernel, dim3((unsigned)grid), dim3(256), 0, S(stream), table, hash_keys, num_slots,
                      num_keys, counter, out, out_cap);
   return PGPU_HIP_OK(hipGetLastError());

@@ -161,7 +161,11 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;
-        if (!DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE && p.pair_leaves) {
+#ifndef PGPU_PAIR_LEAVES
+#define PGPU_PAIR_LEAVES 1
+#endif
+        if (PGPU_PAIR_LEAVES && !DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE &&
+            p.pair_leaves) {
           // index leaf + scan leaf (the indexed C3 shape): both requested together (bitdir_range), applied in order
           uint32_t m0, m1;
           bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, reinterpret_cast<const uint64_t*>(R0.set),

@@ -1122,6 +1122,7 @@ struct pgpu_plan_s {
   // double sums: the dense instance compiled without those gathers (aggregate_batch's SIMPLE; fewer registers)
   bool dense_simple = false;
   bool gathers = false;                   // some segment's key LUT or operand dictionary is read (not simple)
+  bool pair_variant = false;              // sparse instance with the index + scan pair (variant 3)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
   std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
   int launches_done = 0;
@@ -2600,7 +2601,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       // (a streamed plan configures before its later chunks are planned: never simple)
       P->dense_simple = P->dense && !P->gathers && !f64 && P->tile_bound == 0 && !no_simple;
     }
-    const int variant = P->dense_simple ? 2 : P->dense ? 1 : 0;
+    // the sparse instance with the index + scan pair: two-leaf AND plans with an in-place index leaf
+    P->pair_variant = !P->dense && P->pure_and && P->num_leaves == 2 && P->leaf_kinds[LEAF_BITDIR] > 0;
+    const int variant = P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : 0;
     int per_cu;  // resident workgroups per CU
     {
       static std::mutex occ_mu;
@@ -3354,7 +3357,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
-    const int rc = launch_filter_groupby(kp, P->mode, P->dense_simple ? 2 : P->dense ? 1 : 0, grid, P->lds_bytes, stream);
+    const int rc = launch_filter_groupby(kp, P->mode, P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : 0,
+                                         grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));

@@ -49,7 +49,7 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 // DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
-template <int MODE, bool DENSE, bool SIMPLE = false>
+template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
@@ -161,11 +161,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;
-#ifndef PGPU_PAIR_LEAVES
-#define PGPU_PAIR_LEAVES 1
-#endif
-        if (PGPU_PAIR_LEAVES && !DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE &&
-            p.pair_leaves) {
+        // (PAIR: a separate instance for plans with index leaves -- compiled into the plain sparse instance, this
+        // branch cost C3's scan 1.6 %)
+        if (PAIR && !DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE && p.pair_leaves) {
           // index leaf + scan leaf (the indexed C3 shape): both requested together (bitdir_range), applied in order
           uint32_t m0, m1;
           bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, reinterpret_cast<const uint64_t*>(R0.set),

@@ -1123,6 +1123,7 @@ struct pgpu_plan_s {
   bool dense_simple = false;
   bool gathers = false;                   // some segment's key LUT or operand dictionary is read (not simple)
   bool pair_variant = false;              // sparse instance with the index + scan pair (variant 3)
+  bool fast_variant = false;              // sparse instance for pure-AND plans of <= kFastLeaves leaves (variant 4)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
   std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
   int launches_done = 0;
@@ -2603,7 +2604,9 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     // the sparse instance with the index + scan pair: two-leaf AND plans with an in-place index leaf
     P->pair_variant = !P->dense && P->pure_and && P->num_leaves == 2 && P->leaf_kinds[LEAF_BITDIR] > 0;
-    const int variant = P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : 0;
+    static const bool no_fast = getenv_flag("PGPU_NO_FAST_INSTANCE");  // A/B
+    P->fast_variant = !P->dense && !P->pair_variant && P->pure_and && P->num_leaves <= kFastLeaves && !no_fast;
+    const int variant = P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0;
     int per_cu;  // resident workgroups per CU
     {
       static std::mutex occ_mu;
@@ -3357,7 +3360,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
-    const int rc = launch_filter_groupby(kp, P->mode, P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : 0,
+    const int rc = launch_filter_groupby(kp, P->mode,
+                                         P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0,
                                          grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
   }

@@ -49,7 +49,7 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 // DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
-template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false>
+template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAST = false>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
@@ -116,7 +116,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
     t_end = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
     t_step = 1;
   }
-  const bool fast = p.pure_and && p.num_leaves <= kFastLeaves;
+  // FAST: an instance for plans whose filter is a pure AND of at most kFastLeaves leaves (the general program
+  // evaluator compiled out)
+  const bool fast = FAST || (p.pure_and && p.num_leaves <= kFastLeaves);
   if (t_begin < t_end) {
     int seg = -1;
     SegView S{};

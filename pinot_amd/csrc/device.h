@@ -691,25 +691,19 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
 }
 
 // Staged columns (KParams.st_num): this wave's 64 lanes' 32-doc groups of every staged column into the wave's LDS
-// staging area `stg` as they lie in the forward index (lane l's words at [64 st_off + l bits, + bits)).  LDS-DMA loads (no registers held): issued
+// staging area `stg`, word k of lane l at row KCol.st_off + k, column l.  LDS-DMA loads (no registers held): issued
 // before the tile's filter loads, they share its memory round trip; the filter's first use of its own loads waits
-// for them too.  `group` is the lane's group (unclamped: words past the segment's last group read its last word).
+// for them too.  `group` is the lane's (clamped, in-bounds) group.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
 __device__ __forceinline__ void stage_columns(const KParams& p, const SegView& S, int64_t group, uint32_t* stg) {
   for (int i = 0; i < p.st_num; ++i) {
     const KCol& c = S.cols[p.st_col[i]];
     const int bits = c.bits;
-    // the wave's 64 groups are 64 * bits consecutive words: row k = words [64k, 64k + 64) of them (coalesced)
-    const int64_t g0 = group - (threadIdx.x & 63);
-    const int64_t last = (int64_t)S.hdr->num_docs <= 0 ? 0 : ((((int64_t)S.hdr->num_docs + 31) >> 5) * bits - 1);
-    const uint32_t* src = c.fwd + g0 * (int64_t)bits + (threadIdx.x & 63);
+    const uint32_t* src = c.fwd + group * (int64_t)bits;
     uint32_t* dst = stg + c.st_off * 64;
-    for (int k = 0; k < bits; ++k) {
-      const int64_t w = g0 * (int64_t)bits + k * 64 + (threadIdx.x & 63);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(w <= last ? src + k * 64 : c.fwd + last), (lds_void_t*)(dst + k * 64),
-                                       4, 0, 0);
-    }
+    for (int k = 0; k < bits; ++k)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + k), (lds_void_t*)(dst + k * 64), 4, 0, 0);
   }
 }
 
@@ -718,7 +712,7 @@ template <int B, int H>
 __device__ __forceinline__ void decode_staged_b(const uint32_t* col, int lane, uint32_t (&ids)[16]) {
   uint32_t w[B + 1];
 #pragma unroll
-  for (int k = 0; k < B; ++k) w[k] = bswap32(col[lane * B + k]);  // words no extract of this half reads are dropped
+  for (int k = 0; k < B; ++k) w[k] = bswap32(col[k * 64 + lane]);  // rows no extract of this half reads are dropped
   w[B] = 0;
   decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
 }

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         mask &= (0xFFFFFFFFu >> (32 - w)) << (w * (int)(lt & ((1 << p.tile_shift) - 1)));
       }
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
-      if (DENSE && stg) stage_columns(p, S, group, stg);  // in flight with the filter's loads
+      if (DENSE && stg) stage_columns(p, S, gclamp, stg);  // in flight with the filter's loads
       if (fast) {
         // STATS_LEAP2 (two scans in leap-frog): both masks are needed for the entry count, no early exit
         const bool leap = (stats & 3) == KSTATS_LEAP2;

@@ -690,59 +690,6 @@ __device__ __forceinline__ void decode_group(const uint32_t* __restrict__ fwd, i
   }
 }
 
-// Staged columns (KParams.st_num): this wave's 64 lanes' 32-doc groups of every staged column into the wave's LDS
-// staging area `stg`, word k of lane l at row KCol.st_off + k, column l.  LDS-DMA loads (no registers held): issued
-// before the tile's filter loads, they share its memory round trip; the filter's first use of its own loads waits
-// for them too.  `group` is the lane's (clamped, in-bounds) group.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-__device__ __forceinline__ void stage_columns(const KParams& p, const SegView& S, int64_t group, uint32_t* stg) {
-  for (int i = 0; i < p.st_num; ++i) {
-    const KCol& c = S.cols[p.st_col[i]];
-    const int bits = c.bits;
-    const uint32_t* src = c.fwd + group * (int64_t)bits;
-    uint32_t* dst = stg + c.st_off * 64;
-    for (int k = 0; k < bits; ++k)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + k), (lds_void_t*)(dst + k * 64), 4, 0, 0);
-  }
-}
-
-// decode_group from a staged column (`col` = its first row in the wave's staging area).
-template <int B, int H>
-__device__ __forceinline__ void decode_staged_b(const uint32_t* col, int lane, uint32_t (&ids)[16]) {
-  uint32_t w[B + 1];
-#pragma unroll
-  for (int k = 0; k < B; ++k) w[k] = bswap32(col[k * 64 + lane]);  // rows no extract of this half reads are dropped
-  w[B] = 0;
-  decode_half<B, H>(w, ids, std::make_integer_sequence<int, 16>{});
-}
-template <int H>
-__device__ __forceinline__ void decode_staged(const uint32_t* col, int bits, uint32_t (&ids)[16]) {
-  const int lane = threadIdx.x & 63;
-  switch (bits) {
-#define PGPU_CASE(B)                          \
-  case B:                                     \
-    decode_staged_b<B, H>(col, lane, ids);    \
-    break;
-    PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
-    PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
-    PGPU_CASE(16) PGPU_CASE(17) PGPU_CASE(18) PGPU_CASE(19) PGPU_CASE(20) PGPU_CASE(21) PGPU_CASE(22)
-    PGPU_CASE(23) PGPU_CASE(24) PGPU_CASE(25) PGPU_CASE(26) PGPU_CASE(27) PGPU_CASE(28) PGPU_CASE(29)
-    PGPU_CASE(30) PGPU_CASE(31)
-#undef PGPU_CASE
-    default:
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ids[i] = 0;
-      break;
-  }
-}
-// A column's dictIds of the half: from the staging area when the plan staged it, else from global memory.
-template <int H>
-__device__ __forceinline__ void decode_col(const KCol& c, int64_t group, const uint32_t* stg, uint32_t (&ids)[16]) {
-  if (stg) decode_staged<H>(stg + c.st_off * 64, c.bits, ids);
-  else decode_group<H>(c.fwd, c.bits, group, ids);
-}
-
 // The 16 docs of a half-group into one slot row of the table.  In LDS the atomics are issued for every doc, the
 // unmatched ones with the kind's neutral value at key 0: no per-doc exec-mask branch and no per-doc switch on the
 // slot kind (measured on C2: SALU instructions outnumbered VALU ones with the branches), and an LDS atomic costs the
@@ -821,7 +768,7 @@ __device__ __forceinline__ void accumulate16_f(uint64_t* __restrict__ row, const
 // One half (docs H..H+15 of the lane's group) of aggregate_group.
 template <int MODE, int H, bool SIMPLE = false>
 __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
-                                               uint64_t* __restrict__ tbl, int64_t G, const uint32_t* stg) {
+                                               uint64_t* __restrict__ tbl, int64_t G) {
   const uint32_t m = (mask >> H) & 0xFFFFu;
   uint32_t ids[16];
   int32_t key[16];
@@ -829,7 +776,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
   for (int i = 0; i < 16; ++i) key[i] = -(int32_t)p.key_bias;  // dense key spaces: < 2^31 after the bias
   for (int j = 0; j < p.num_keys; ++j) {
     const KCol& c = S.cols[p.key_col[j]];
-    decode_col<H>(c, group, stg, ids);
+    decode_group<H>(c.fwd, c.bits, group, ids);
     const int32_t stride = (int32_t)p.key_stride[j];
     if (!SIMPLE && c.lut) {  // segment-uniform: the whole wave reads one segment here
       int32_t g[16];
@@ -868,7 +815,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       ++e;
     }
     const KCol& c = S.cols[col];
-    decode_col<H>(c, group, stg, ids);
+    decode_group<H>(c.fwd, c.bits, group, ids);
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
       int64_t v[16];
       if (!SIMPLE && c.dkey) {
@@ -934,14 +881,12 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
 // Aggregates the matched docs (bits of `mask`) of this lane's 32-doc group `group` of segment S, 16 docs at a
 // time.  Dense key spaces only (MODE_LDS / MODE_GLOBAL: composite keys < 2^31).  Docs beyond numDocs decode from
 // the zero padding to dictId 0 (in bounds) and are never in `mask`.
-// stg: the wave's staging area when the plan staged its columns (stage_columns at the tile's start), else null.
 template <int MODE, bool SIMPLE = false>
 __device__ __forceinline__ void aggregate_group(const KParams& p, const SegView& S, int64_t group, uint32_t mask,
-                                                uint64_t* __restrict__ tbl, int64_t G, const uint32_t* stg = nullptr) {
-  if (stg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staging loads have landed
+                                                uint64_t* __restrict__ tbl, int64_t G) {
   // wave-uniform conditions: the single-row (G == 1) fold inside uses cross-lane shuffles
-  if (__any((mask & 0xFFFFu) != 0u)) aggregate_half<MODE, 0, SIMPLE>(p, S, group, mask, tbl, G, stg);
-  if (__any((mask >> 16) != 0u)) aggregate_half<MODE, 16, SIMPLE>(p, S, group, mask, tbl, G, stg);
+  if (__any((mask & 0xFFFFu) != 0u)) aggregate_half<MODE, 0, SIMPLE>(p, S, group, mask, tbl, G);
+  if (__any((mask >> 16) != 0u)) aggregate_half<MODE, 16, SIMPLE>(p, S, group, mask, tbl, G);
 }
 
 // Drains a wave's queue of matched (segment, doc) entries: 2 per lane per batch.

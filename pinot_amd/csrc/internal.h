@@ -26,8 +26,6 @@ constexpr int kMaxOps = 48;                 // postfix filter program length
 constexpr int kMaxKeys = 16;                // group-by columns handled on the GPU
 constexpr int kMaxSlots = 24;               // accumulator rows of the group table
 constexpr int kMaxStack = 8;                // filter evaluation stack depth
-constexpr int kMaxStaged = 8;               // dense instance: staged columns (KParams.st_col)
-constexpr int kStageMaxWords = 48;          // ... and their bits per doc (LDS: 1 KiB per word row and workgroup)
 constexpr int kFwdPadWords = 4;
 constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
@@ -75,8 +73,6 @@ struct KCol {
   int64_t key_base;
   int32_t bits;
   int32_t lut_off;
-  int32_t st_off;   // staged plans (KParams.st_num): the column's first word row in a wave's staging area, else -1
-  int32_t st_pad;
 };
 
 // Per-plan, per-segment record (uploaded once per plan): a KSegHdr followed by num_cols KCol and num_leaves
@@ -146,15 +142,6 @@ struct KParams {
   // scans stop taking tiles and set stats[5] (BaseCombineOperator.java:79-132 / GroupByCombineOperator.java:193-203
   // give up at the same point; the host then reports the timeout instead of a partial result)
   uint64_t deadline;
-  // Dense instance, staged columns: at each tile's start every wave copies its 64 lanes' 32-doc groups of the
-  // st_num group-by / aggregated columns st_col[] into its LDS staging area with LDS-DMA loads, issued with the
-  // filter's loads (one memory round trip per tile instead of one per column and half-group); word k of lane l of
-  // a column sits at row KCol.st_off + k, column l (conflict-free reads).  The staging areas (st_words rows of 64
-  // words per wave) come first in LDS, the kernel's other LDS st_qwords 8-byte words later.  st_num = 0: off.
-  int32_t st_num;
-  int32_t st_words;
-  int32_t st_qwords;
-  int32_t st_col[kMaxStaged];
 };
 
 // leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to

@@ -1122,11 +1122,6 @@ struct pgpu_plan_s {
   // double sums: the dense instance compiled without those gathers (aggregate_batch's SIMPLE; fewer registers)
   bool dense_simple = false;
   bool gathers = false;                   // some segment's key LUT or operand dictionary is read (not simple)
-  // dense instance, staged columns (KParams.st_num): the key / value query columns and the largest sum of their bit
-  // widths over the plan's segments (word rows per wave); staged = the launch stages them
-  std::vector<int32_t> st_cols;
-  int32_t st_words = 0;
-  bool staged = false;
   bool pair_variant = false;              // sparse instance with the index + scan pair (variant 3)
   bool fast_variant = false;              // sparse instance for pure-AND plans of <= kFastLeaves leaves (variant 4)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
@@ -2300,15 +2295,11 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     for (size_t i = 0; i < P->query_cols.size(); ++i)
       if (P->query_cols[i] == P->key_cols[j]) qcol_key[i] = (int)j;
   for (size_t k = 1; k < P->slot_col.size(); ++k) qcol_val[P->slot_col[k]] = 1;
-  P->st_cols.clear();
-  for (size_t j = 0; j < P->query_cols.size(); ++j)
-    if (qcol_key[j] >= 0 || qcol_val[j]) P->st_cols.push_back((int32_t)j);
   // Per-segment translation (PredicateEvaluatorProvider + FilterPlanNode per segment) in contiguous chunks,
   // on the host worker pool for large segment lists; records carry chunk-relative tile / set offsets, fixed up
   // when the chunks are concatenated in segment order.
   struct Chunk {
     bool gathers = false;  // pgpu_plan_s::gathers
-    int32_t st_words = 0;  // pgpu_plan_s::st_words
     std::vector<uint8_t> rec;
     std::vector<uint32_t> set_words;
     std::vector<std::pair<int64_t, int64_t>> set_fix;
@@ -2466,15 +2457,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       }
       for (int j = 0; j < nqc; ++j)
         C.gathers |= (qcol_key[j] >= 0 && kc[j].lut != nullptr) || (qcol_val[j] && kc[j].dkey != nullptr);
-      {  // staged columns: each key / value column's first word row in a wave's staging area (KCol.st_off)
-        int32_t off = 0;
-        for (int j = 0; j < nqc; ++j) {
-          const bool st = qcol_key[j] >= 0 || qcol_val[j];
-          kc[j].st_off = st ? off : -1;
-          if (st) off += std::max(kc[j].bits, 0);
-        }
-        C.st_words = std::max(C.st_words, off);
-      }
       KLeaf* kl = reinterpret_cast<KLeaf*>(rec.data() + sizeof(KSegHdr) + sizeof(KCol) * nqc);
       const int64_t rec_off = (int64_t)C.rec.size();
       for (int k = 0; k < P->num_leaves; ++k) {
@@ -2619,14 +2601,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       static const bool no_simple = getenv_flag("PGPU_NO_SIMPLE");  // A/B
       // (a streamed plan configures before its later chunks are planned: never simple)
       P->dense_simple = P->dense && !P->gathers && !f64 && P->tile_bound == 0 && !no_simple;
-    }
-    {  // dense instance: stage the key / value columns through LDS when their rows fit (kStageMaxWords)
-      static const bool no_stage = getenv_flag("PGPU_NO_STAGE");  // A/B
-      const size_t st_bytes = (size_t)P->st_words * 64 * 4 * (kBlock / 64);
-      P->staged = P->dense && P->mode != MODE_HASH && P->tile_bound == 0 && !no_stage && P->st_words > 0 &&
-                  P->st_words <= kStageMaxWords && (int)P->st_cols.size() <= kMaxStaged &&
-                  P->lds_bytes + st_bytes <= 96 * 1024;
-      if (P->staged) P->lds_bytes += st_bytes;
     }
     // the sparse instance with the index + scan pair: two-leaf AND plans with an in-place index leaf
     P->pair_variant = !P->dense && P->pure_and && P->num_leaves == 2 && P->leaf_kinds[LEAF_BITDIR] > 0;
@@ -2773,7 +2747,6 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     }
     P->any_leap2 |= C.any_leap2;
     P->gathers |= C.gathers;
-    P->st_words = std::max(P->st_words, C.st_words);
     P->docbit_words += C.docbit_words;
     P->segrec.insert(P->segrec.end(), C.rec.begin(), C.rec.end());
     P->set_words.insert(P->set_words.end(), C.set_words.begin(), C.set_words.end());
@@ -3171,12 +3144,6 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   }
   dense_lds_forms(P, &kp.pack_slot, &kp.narrow);
   kp.pack_shift = P->pack_shift;
-  if (P->staged) {
-    kp.st_num = (int)P->st_cols.size();
-    for (int i = 0; i < kp.st_num; ++i) kp.st_col[i] = P->st_cols[i];
-    kp.st_words = P->st_words;
-    kp.st_qwords = P->st_words * 64 * (kBlock / 64) / 2;
-  }
   kp.stats = stats;
   if (P->leap_reserved) {  // one byte per (tile, wave) of the plan, written by the scan kernel for LEAP2 segments
     TRY(sc->leap_maps.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) *

@@ -60,11 +60,8 @@ template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAS
 #define PGPU_SIMPLE_MIN_WAVES 4
 #endif
 __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : PGPU_DENSE_MIN_WAVES) : PGPU_MIN_WAVES) void filter_groupby_kernel(const KParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // DENSE with staged columns (KParams.st_num): the waves' staging areas first, the rest of the kernel's LDS after
-  uint64_t* const lds = DENSE ? lds_raw + p.st_qwords : lds_raw;
-  uint32_t* const stg = DENSE && p.st_num ? reinterpret_cast<uint32_t*>(lds_raw) + wave * p.st_words * 64 : nullptr;
   const int64_t G = p.num_keys_total;
   // MODE_LDS with KParams.pack_slot: no COUNT row in LDS (slot s at row s - 1; the COUNT rides in the pack slot)
   const int lds_row0 = (MODE == MODE_LDS && p.pack_slot >= 0) ? 1 : 0;
@@ -160,7 +157,6 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         mask &= (0xFFFFFFFFu >> (32 - w)) << (w * (int)(lt & ((1 << p.tile_shift) - 1)));
       }
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
-      if (DENSE && stg) stage_columns(p, S, gclamp, stg);  // in flight with the filter's loads
       if (fast) {
         // STATS_LEAP2 (two scans in leap-frog): both masks are needed for the entry count, no early exit
         const bool leap = (stats & 3) == KSTATS_LEAP2;
@@ -206,7 +202,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
       }
       if (DENSE && MODE != MODE_HASH && wave_cnt >= (uint32_t)kDenseGroupMin) {
         // dense tile: whole-group decode of the group-by / aggregated columns
-        aggregate_group<MODE, SIMPLE>(p, S, gclamp, mask, tbl, G, stg);
+        aggregate_group<MODE, SIMPLE>(p, S, gclamp, mask, tbl, G);
       } else if (__any(cnt > 2u)) {
         // dense: the lane's own 32-doc group, 2 matched docs per batch (the lines are already cached)
         while (__any(mask != 0u)) {

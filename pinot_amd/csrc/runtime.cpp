@@ -2593,8 +2593,13 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       static const int64_t want_env = getenv("PGPU_STAR_WGS") ? atol(getenv("PGPU_STAR_WGS")) : 0;  // A/B knob
       P->star_chunks = (int)(want_env > 0 ? want_env : (int64_t)t->num_cus * per_cu);
     }
-    // Dense instance when tiles are expected to hold >= 2 matches per 32-doc group on average.
-    P->dense = P->mode != MODE_HASH && P->sel_estimate >= 1.0 / 16 && !getenv_flag("PGPU_NO_DENSE");
+    // Dense instance when tiles are expected to hold >= 8 matches per 32-doc group on average: below that the sparse
+    // instance's per-match batches win (measured on MI355X, r04 session x: the C4 scan path at 15 % selectivity
+    // 195 -> 170 us with the sparse instance; C2 at 50 % 577 us dense vs 1468 sparse).  PGPU_DENSE_SEL: A/B.
+    {
+      static const double dense_sel = getenv("PGPU_DENSE_SEL") ? atof(getenv("PGPU_DENSE_SEL")) : 0.25;
+      P->dense = P->mode != MODE_HASH && P->sel_estimate >= dense_sel && !getenv_flag("PGPU_NO_DENSE");
+    }
     {
       bool f64 = false;
       for (int k : P->slot_kind) f64 |= k == SLOT_SUM_F64;

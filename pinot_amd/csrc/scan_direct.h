@@ -46,7 +46,7 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 }
 
 // ---------------------------------------------------------------------------------------------- K3 fused
-// DENSE: the plan expects dense tiles (estimated selectivity >= 1/16): wave-tiles with >= kDenseGroupMin matches
+// DENSE: the plan expects dense tiles (estimated selectivity >= 1/4, runtime.cpp): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
 template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAST = false>

@@ -99,17 +99,12 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = c.key_base + (int64_t)ids[i];
     }
-    // the 16 cursor reservations issued together (independent LDS atomics: one LDS round trip, not 16 in a row --
-    // K8c waited 85 % of its wave cycles with each store behind its own reservation), then the 16 stores
-    uint32_t rec[16], pos[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      rec[i] = (uint32_t)(key[i] & ((1 << cbits) - 1)) | ((uint32_t)(v[i] - pp.pack_min) << cbits);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) pos[i] = ((m >> i) & 1u) ? atomicAdd(&cursor[key[i] >> cbits], 1u) : 0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if ((m >> i) & 1u) pp.mid_key[pos[i]] = rec[i];
+      if ((m >> i) & 1u) {
+        const uint32_t pos = atomicAdd(&cursor[key[i] >> cbits], 1u);
+        pp.mid_key[pos] = (uint32_t)(key[i] & ((1 << cbits) - 1)) | ((uint32_t)(v[i] - pp.pack_min) << cbits);
+      }
     return;
   }
   if (pp.mid_pair) {  // hashed, one u32 value: (hk | value << 32) in one 8-byte word, one scattered store per record
@@ -125,38 +120,37 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = (uint32_t)(c.key_base + (int64_t)ids[i]);
     }
-    uint32_t hk[16], at[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) hk[i] = part_hash((uint32_t)key[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) at[i] = ((m >> i) & 1u) ? atomicAdd(&cursor[hpart(pp, hk[i]) >> pp.cshift], 1u) : 0u;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if ((m >> i) & 1u) pp.mid_val[at[i]] = (uint64_t)hk[i] | ((uint64_t)v[i] << 32);
+      if ((m >> i) & 1u) {
+        const uint32_t hk = part_hash((uint32_t)key[i]);
+        const uint32_t at = atomicAdd(&cursor[hpart(pp, hk) >> pp.cshift], 1u);
+        pp.mid_val[at] = (uint64_t)hk | ((uint64_t)v[i] << 32);
+      }
     return;
   }
   uint32_t pos[16];
   if (pp.hashed) {  // the coarse run of the key's hashed partition; the whole hashed key stored
-    uint32_t hk[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) hk[i] = part_hash((uint32_t)key[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) pos[i] = ((m >> i) & 1u) ? atomicAdd(&cursor[hpart(pp, hk[i]) >> pp.cshift], 1u) : 0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < 16; ++i) {
+      pos[i] = 0;
       if ((m >> i) & 1u) {
-        if (two) pp.mid_key[pos[i]] = hk[i];
-        else pp.rec_key32[pos[i]] = hk[i];
+        const uint32_t hk = part_hash((uint32_t)key[i]);
+        pos[i] = atomicAdd(&cursor[hpart(pp, hk) >> pp.cshift], 1u);
+        if (two) pp.mid_key[pos[i]] = hk;
+        else pp.rec_key32[pos[i]] = hk;
       }
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) pos[i] = ((m >> i) & 1u) ? atomicAdd(&cursor[key[i] >> cbits], 1u) : 0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < 16; ++i) {
+      pos[i] = 0;
       if ((m >> i) & 1u) {
+        pos[i] = atomicAdd(&cursor[key[i] >> cbits], 1u);
         if (two) pp.mid_key[pos[i]] = (uint32_t)(key[i] & ((1 << cbits) - 1));
         else pp.rec_key[pos[i]] = (uint16_t)(key[i] & ((1 << pp.pshift) - 1));
       }
+    }
   }
   uint32_t ids[16];
   for (int s = 0; s < pp.num_streams; ++s) {

@@ -4,6 +4,10 @@ pinned in HBM, one process per GPU.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|c1|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+--gpus N > 1 without a launcher starts the N rank processes itself (before this process touches the GPU) and exits
+with the first failing rank's code; under a launcher WORLD_SIZE must equal --gpus.  RCCL takes one GPU per rank, so
+more ranks than visible GPUs fail at once (PGPU_BENCH_BACKEND=host rehearses N ranks on fewer GPUs).
+
 A step is one whole query on every rank: plan (per-segment predicate translation; a plan-cache hit for a repeated
 query), the fused scan kernel over all local segments, the dense group-table merge across ranks (RCCL all-reduce
 over xGMI) and the compacted result copied back to the host.  By default the workload's BASELINE row count is split
@@ -140,11 +144,19 @@ CALIB_SQL = {
     "c2": "SELECT COUNT(*) FROM t WHERE f = 1 AND f = 2 GROUP BY d",
     "c5": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
     "c5_hash": "SELECT COUNT(*) FROM t WHERE k1 = 1 AND k1 = 2 GROUP BY k2",
+    # C4: the calibration runs on the scan path (--no-star-tree in its child); the factor is the counter's (the gfx950
+    # half count of wide streaming reads), so it applies to the star-tree kernels' FETCH_SIZE alike
+    "c4": "SELECT COUNT(*) FROM t WHERE d1 = 1 AND d1 = 2 GROUP BY d2",
 }
 SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel", "part_aggregate_kernel",
-                "part_hash_aggregate_kernel")
-# the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch)
-LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false>")
+                "part_hash_aggregate_kernel", "startree_traverse_kernel", "startree_scan_kernel")
+# the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch; a
+# star-tree launch is the traversal, then the pre-aggregated document scan)
+LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false>", "startree_traverse_kernel")
+# the launcher's and torch.distributed.run's variables: a profiled child run is one rank of its own
+DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+            "TORCHELASTIC_MAX_RESTARTS", "PGPU_BENCH_PMC")
 
 
 def _fetch_per_launch(csv_path):
@@ -169,14 +181,20 @@ def pmc_traffic(args):
         return None
     base = [sys.executable, "-u", os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
             "--no-pmc", "--workload", args.workload, "--segments-per-gpu", str(args.local_segments),
-            "--docs-per-segment", str(args.docs_per_segment), "--inflight", "1", "--roofline-steps", "2"]
+            "--docs-per-segment", str(args.docs_per_segment), "--inflight", "1", "--roofline-steps", "2",
+            "--warmup-ms", "0", "--parity-segments", "0"]
+    if args.num_groups_limit:
+        base += ["--num-groups-limit", str(args.num_groups_limit)]
+    env = {k: v for k, v in os.environ.items() if k not in DIST_ENV}
     res = {}
     with tempfile.TemporaryDirectory() as d:
         for name, sql in (("main", args.sql), ("calib", CALIB_SQL[args.workload])):
-            cmd = [rocprof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", d, "-o", name, "--"] + base + \
-                (["--sql", sql] if sql else [])
+            extra = (["--sql", sql] if sql else []) + \
+                (["--no-star-tree"] if args.no_star_tree or name == "calib" else [])
+            cmd = [rocprof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", d, "-o", name, "--"] + base + extra
             try:
-                p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+                p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300,
+                                   env=env)
             except subprocess.TimeoutExpired:
                 print("pmc pass %s timed out" % name, file=sys.stderr)
                 return None
@@ -256,12 +274,29 @@ def host_segments(table, handles, workload, docs):
     return segs
 
 
+def attach_star_arrays(segs, workload):
+    """Each host segment's star-tree (the same builder that made the pinned trees, so the same trees) as the oracle's
+    input: seg.star_arrays, read by run_groupby(..., use_star_tree=True)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from pinot_amd.startree import StarTree
+    spec = workload.star_tree
+
+    def tree(seg):
+        st = StarTree.build(workload.schema, seg, spec["split_order"], spec["pairs"], spec["max_leaf_records"])
+        a = st.arrays()
+        st.close()
+        return a
+    with ThreadPoolExecutor(8) as ex:
+        for seg, a in zip(segs, ex.map(tree, segs)):
+            seg.star_arrays = a
+
+
 def full_parity(table, handles, query, workload, docs, args):
     """The GPU answer of the benchmarked query over the first --parity-segments segments (default: all of this
     rank's) against the oracle's over the same bytes (pulled back from HBM): bit-exact for integer / count / dictId
     work, 1e-9 relative for FLOAT / DOUBLE sums (BASELINE north_star).  Star-tree plans are checked against the
-    oracle's scan (BaseStarTreeV2Test's star-tree == scan rule); inverted-index plans compare numDocsScanned only
-    (the oracle restates the scan operator, whose numEntriesScannedInFilter differs by design)."""
+    oracle's star-tree operator over the same trees, statistics included; inverted-index plans compare
+    numDocsScanned only (the oracle restates the scan operator, whose numEntriesScannedInFilter differs by design)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
     n = len(handles) if args.parity_segments is None else max(0, min(args.parity_segments, len(handles)))
@@ -270,15 +305,64 @@ def full_parity(table, handles, query, workload, docs, args):
     t0 = time.perf_counter()
     hs = np.ascontiguousarray(handles[:n], dtype=np.int64)
     segs = host_segments(table, hs, workload, docs)
-    orc = _oracle.run_groupby_arrays(workload.schema, segs, query, nthreads=host_cores())
+    star = bool(workload.star_tree) and query.use_star_tree
+    if star:  # the oracle's star-tree operator over the same trees (statistics = star-tree documents read)
+        attach_star_arrays(segs, workload)
+    orc = _oracle.run_groupby_arrays(workload.schema, segs, query, nthreads=host_cores(), use_star_tree=star)
     del segs
     r = table.execute_groupby(hs, query)
-    star = workload.star_tree and query.use_star_tree
     cmp = _oracle.compare_result_arrays(table, r, orc, query, workload.schema,
-                                        check_stats=False if star else "docs" if workload.inverted_columns else True)
+                                        check_stats="docs" if workload.inverted_columns else True)
     cmp.update({"segments": n, "rows": n * docs, "seconds": round(time.perf_counter() - t0, 1),
                 "against": "oracle/oracle.c over the same segment bytes"})
     return cmp
+
+
+def multi_rank_parity(table, handles, query, workload, docs, res, world, rank, sharded):
+    """Parity of an N-rank query (the check full_parity makes at N = 1): every rank runs the oracle over its own
+    segments' bytes (pulled back from its HBM, the rank's cores split between the ranks of the box), rank 0 merges
+    those per-server partial results as the broker merges server responses (_oracle.merge_partial_arrays, numpy --
+    not the device combine it checks) and compares them with the GPU's merged answer: rank 0's table for an all-reduce,
+    every rank's disjoint share gathered for reduce-scatter / hash / row combines.  Statistics are per rank on both
+    sides (the combine merges groups, not statistics) and compared as sums.  Collective: every rank calls it; rank 0
+    gets the verdict dict, the others None."""
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    t0 = time.perf_counter()
+    hs = np.ascontiguousarray(handles, dtype=np.int64)
+    segs = host_segments(table, hs, workload, docs)
+    threads = max(1, host_cores() // world)
+    star = bool(workload.star_tree) and query.use_star_tree
+    err = None
+    try:
+        if star:
+            attach_star_arrays(segs, workload)
+        orc = _oracle.run_groupby_arrays(workload.schema, segs, query, nthreads=threads, use_star_tree=star)
+    except Exception as e:  # every rank reaches the gather below, whatever failed here
+        orc, err = None, "rank %d oracle: %s" % (rank, e)
+    del segs
+    gpu = _oracle.gpu_result_arrays(table, res, query) if (sharded or rank == 0) else None
+    mine = {"rank": rank, "orc": orc, "gpu": gpu, "stats": tuple(res.stats.as_tuple()), "err": err,
+            "segments": len(hs)}
+    gathered = [None] * world if rank == 0 else None
+    dist.gather_object(mine, gathered, dst=0)
+    if rank != 0:
+        return None
+    errs = [g["err"] for g in gathered if g["err"]]
+    if errs:
+        return {"ok": False, "mismatch": "; ".join(errs), "ranks": world}
+    merged = _oracle.merge_partial_arrays([g["orc"] for g in gathered], query.aggregations)
+    gpu = _oracle.concat_arrays([g["gpu"] for g in gathered]) if sharded else gathered[0]["gpu"]
+    gstats = tuple(int(sum(g["stats"][i] for g in gathered)) for i in range(4))
+    out = _oracle.compare_arrays(gpu, gstats, merged, query, workload.schema,
+                                 check_stats="docs" if workload.inverted_columns else True)
+    nseg = sum(g["segments"] for g in gathered)
+    out.update({"segments": nseg, "rows": nseg * docs, "ranks": world, "seconds": round(time.perf_counter() - t0, 1),
+                "against": "oracle/oracle.c per rank over the same segment bytes, partial results merged as the "
+                           "broker merges server responses (numpy)",
+                "merged_from": "rank 0 (all-reduced table)" if not sharded else "every rank's disjoint share"})
+    return out
 
 
 def cpu_baseline(table, handles, query, workload, docs, args):
@@ -292,18 +376,7 @@ def cpu_baseline(table, handles, query, workload, docs, args):
     threads = host_cores()
     star = bool(workload.star_tree) and query.use_star_tree
     if star:  # the path Pinot's plan picks (StarTreeUtils.isFitForStarTree): the oracle's star-tree operator
-        from concurrent.futures import ThreadPoolExecutor
-        from pinot_amd.startree import StarTree
-        spec = workload.star_tree
-
-        def tree(seg):
-            st = StarTree.build(workload.schema, seg, spec["split_order"], spec["pairs"], spec["max_leaf_records"])
-            a = st.arrays()
-            st.close()
-            return a
-        with ThreadPoolExecutor(8) as ex:
-            for seg, a in zip(segs, ex.map(tree, segs)):
-                seg.star_arrays = a
+        attach_star_arrays(segs, workload)
     _oracle.run_groupby(workload.schema, segs[:2], query, nthreads=threads, decode=False,
                         use_star_tree=star)  # warm-up
     reps, elapsed = 0, 0.0
@@ -343,13 +416,90 @@ def cpu_model():
     return None
 
 
+def launch_mode(gpus, environ, visible_gpus):
+    """How this invocation runs, decided before anything touches the GPU:
+    ("rank", N) -- one rank of N started by a launcher (torch.distributed.run or this script's own spawn): WORLD_SIZE
+                   is set and must equal --gpus;
+    ("single", 1) -- --gpus 1 without a launcher;
+    ("spawn", N) -- --gpus N > 1 without a launcher: this process starts the N ranks itself (spawn_ranks).
+    Raises SystemExit with the reason when the request cannot run: WORLD_SIZE != --gpus, or RCCL ranks (one GPU
+    each) past the visible GPUs -- PGPU_BENCH_BACKEND=host rehearses N ranks sharing the visible GPUs."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1 (got %d)" % gpus)
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit("bench.py: WORLD_SIZE=%s from the launcher but --gpus %d: the rank count and --gpus must "
+                             "match" % (ws, gpus))
+        return "rank", gpus
+    if gpus == 1:
+        return "single", 1
+    if environ.get("PGPU_BENCH_BACKEND", "rccl") != "host" and visible_gpus < gpus:
+        raise SystemExit("bench.py --gpus %d: %d GPU(s) visible, and RCCL takes one GPU per rank "
+                         "(PGPU_BENCH_BACKEND=host rehearses %d ranks sharing the visible GPUs)"
+                         % (gpus, visible_gpus, gpus))
+    return "spawn", gpus
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_env(environ, rank, world, port):
+    """A spawned rank's environment: what torch.distributed.run --nnodes=1 --master-addr 127.0.0.1 sets."""
+    env = {k: v for k, v in environ.items() if k not in DIST_ENV}
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def spawn_ranks(world, argv, extra_env=None, poll_s=0.2, grace_s=20.0, script=None):
+    """Starts `world` ranks of this script (child processes, never an exec) and waits for all of them.  The first rank
+    that fails ends the others (terminate, then kill after `grace_s`: a rank left waiting in a collective for a dead
+    peer never returns by itself).  Returns the exit code: 0, or the failed rank's (128 + signal for a signal)."""
+    import signal
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = rank_env(os.environ, r, world, port)
+        if r == 0 and extra_env:
+            env.update(extra_env)
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc, failed = 0, None
+    live = set(range(world))
+    t_fail = None
+    while live:
+        for r in sorted(live):
+            x = procs[r].poll()
+            if x is None:
+                continue
+            live.discard(r)
+            if x != 0 and failed is None:
+                failed, rc = r, (x if x > 0 else 128 - x)
+                t_fail = time.monotonic()
+                log("rank %d exited with %d: ending the other ranks" % (r, x))
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+        if live and t_fail is not None and time.monotonic() - t_fail > grace_s:
+            for q in live:
+                procs[q].kill()
+            t_fail = float("inf")  # killed once
+        time.sleep(poll_s)
+    return rc
+
+
 def main():
     args = parse_args()
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    how, _ = launch_mode(args.gpus, os.environ, torch.cuda.device_count())  # device_count() does not initialise HIP
+    world = args.gpus if how != "single" else 1
+    rank = int(os.environ.get("RANK", "0")) if how == "rank" else 0
     docs = args.docs_per_segment
     if args.segments_per_gpu:  # weak scaling
         seg_first, nseg = rank * args.segments_per_gpu, args.segments_per_gpu
@@ -361,11 +511,37 @@ def main():
         nseg = (rank + 1) * total_segments // world - seg_first
     args.local_segments = nseg
     pmc = None
-    if world == 1 and not args.no_pmc and not args.no_bytes:
-        # before this process initialises the GPU: the profiled runs are children, not exec'd
+    pmc_file = os.environ.get("PGPU_BENCH_PMC")
+    if pmc_file is not None:  # rank 0 spawned by this script: the launcher measured it before starting the ranks
+        if pmc_file:
+            try:
+                pmc = json.load(open(pmc_file))
+            except (OSError, ValueError):
+                pmc = None
+    elif rank == 0 and not args.no_pmc and not args.no_bytes:
+        # before this process initialises the GPU: the profiled runs are children, not exec'd (rank 0's share of the
+        # segments, profiled as a one-rank run)
         from pinot_amd.build import build as _build
         _build()
         pmc = pmc_traffic(args)
+    if how == "spawn":
+        import tempfile
+        extra = {}
+        if pmc:
+            fd, path = tempfile.mkstemp(prefix="pgpu_bench_pmc_", suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(pmc, f)
+            extra["PGPU_BENCH_PMC"] = path
+        else:
+            extra["PGPU_BENCH_PMC"] = ""
+        from pinot_amd.build import build as _build
+        _build()  # once, before the ranks (each rank's build() then finds the library current)
+        log("starting %d ranks (%s)" % (world, os.environ.get("PGPU_BENCH_BACKEND", "rccl")))
+        rc = spawn_ranks(world, sys.argv[1:], extra)
+        if extra.get("PGPU_BENCH_PMC"):
+            os.unlink(extra["PGPU_BENCH_PMC"])
+        sys.exit(rc)
+    import torch.distributed as dist
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # The combine across ranks is the C ABI's (pgpu_comm + pgpu_plan_combine): RCCL over xGMI, one GPU per rank.
     # PGPU_BENCH_BACKEND=host rehearses the same combine code on a box with fewer GPUs than ranks (ranks share
@@ -591,7 +767,17 @@ def main():
     value = total_rows * args.steps / elapsed
     # The scan kernel's duration for the roofline: a serialized pass (one query in flight, so no other query's
     # kernels share the GPU with the one being timed), after the timed region.
-    kernel_us = run(max(1, args.roofline_steps), 1)[1]
+    # The same pass gives the per-query latency: one query at a time, plan to result in host memory (merge included).
+    nser = max(1, args.roofline_steps)
+    torch.cuda.synchronize()
+    t_ser = time.perf_counter()
+    kernel_us = run(nser, 1)[1]
+    torch.cuda.synchronize()
+    latency_ms = (time.perf_counter() - t_ser) / nser * 1e3
+    if world > 1:
+        e = torch.tensor([latency_ms], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        latency_ms = float(e.item())
     launches = kernel_us[0][1] if kernel_us else 1
     kernel_avg_us = float(np.mean([k for k, _ in kernel_us])) / launches if kernel_us else 0.0  # per launch
 
@@ -625,15 +811,22 @@ def main():
                     "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
                     "matched_docs_per_gpu": int(matched), "launches_per_query": launches,
                     "kernel_us_per_query": round(kernel_avg_us * launches, 2)}
-        if pmc:
-            roofline["traffic"] = round(pmc["traffic"], 0)
-            roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
+    if roofline is not None and pmc:
+        roofline["traffic"] = round(pmc["traffic"], 0)
+        roofline["traffic_pmc"] = {k: v for k, v in pmc.items() if k != "traffic"}
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("bytes_alg pass done; full-size parity")
         parity = full_parity(table, handles, q, w, docs, args)
         log("parity %s; CPU baseline" % (parity and parity["ok"]))
         cpu = cpu_baseline(table, handles, q, w, docs, args)
+    elif world > 1 and args.parity_segments != 0:
+        # the merged answer (this rank's share of it for sharded combines) of one more query, against the oracle
+        res = run(1, 1, keep=1)[0][0]
+        log("rank %d: multi-rank parity" % rank)
+        parity = multi_rank_parity(table, handles, q, w, docs, res, world, rank, sharded)
+        if rank == 0:
+            log("parity %s" % parity["ok"])
 
     if rank == 0:
         line = {
@@ -644,6 +837,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup, "warmup_run": warmup_run,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            # ms_per_step is a pipelined throughput (--inflight queries overlap); one query alone takes this long
+            "latency_ms_per_query": round(latency_ms, 4),
             "higher_is_better": True,
             "scaling": "weak" if args.segments_per_gpu else "strong",
             "vs_baseline": None,

@@ -304,6 +304,15 @@ int pgpu_comm_rank(pgpu_comm comm, int32_t* rank, int32_t* nranks);
 /* Host memory, blocking: recv[nranks * bytes] = every rank's `bytes` bytes in rank order (dictionary unions, the
  * mode agreement, timing barriers -- the small control exchanges of a multi-GPU query). */
 int pgpu_comm_allgather(pgpu_comm comm, const void* send, int64_t bytes, void* recv);
+/* Waits on peers -- the host exchanges above and in the combine, and a combined plan's finalize waiting for its
+ * stream-ordered collectives -- end with PGPU_ERR_TIMEOUT after timeout_ms (<= 0: no limit of the communicator's
+ * own; default 600 000), or earlier at the query's end_time_ms / pgpu_plan_cancel.  An expired wait aborts the
+ * communicator (RCCL: ncclCommAbort, so collectives a peer never joined stop waiting on the device); every later call
+ * on it fails with PGPU_ERR_DEVICE and the caller creates a new one (BaseCombineOperator's timeout,
+ * BaseCombineOperator.java:193-203: the combine always ends by the query deadline). */
+int pgpu_comm_set_timeout(pgpu_comm comm, int64_t timeout_ms);
+/* Gives the communicator up from any thread (a server shutting a query down); see pgpu_comm_set_timeout. */
+int pgpu_comm_abort(pgpu_comm comm);
 
 /* How the ranks' partial results of one query merge. */
 #define PGPU_COMBINE_LOCAL 0          /* one rank: nothing to merge */

@@ -208,6 +208,8 @@ _PROTOS = {
     "pgpu_comm_destroy": (c_int, [c_voidp]),
     "pgpu_comm_rank": (c_int, [c_voidp, c_i32p, c_i32p]),
     "pgpu_comm_allgather": (c_int, [c_voidp, c_voidp, c_i64, c_voidp]),
+    "pgpu_comm_set_timeout": (c_int, [c_voidp, c_i64]),
+    "pgpu_comm_abort": (c_int, [c_voidp]),
     "pgpu_plan_combine_mode": (c_int, [c_voidp, c_voidp, c_i64, c_i32p, c_i32p]),
     "pgpu_plan_combine": (c_int, [c_voidp, c_voidp, c_voidp, c_voidp, c_i32, c_i32p, c_voidp, c_i64p, c_i64p]),
     "pgpu_result_combine_rows": (c_int, [c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),

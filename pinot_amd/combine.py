@@ -300,6 +300,13 @@ class Communicator:
         except Exception:
             pass
 
+    def set_timeout(self, ms):
+        """pgpu_comm_set_timeout: waits on peers end with PGPU_ERR_TIMEOUT after `ms` (and abort the communicator)."""
+        L.check(self.lib.pgpu_comm_set_timeout(self.handle, int(ms)))
+
+    def abort(self):
+        L.check(self.lib.pgpu_comm_abort(self.handle))
+
     def allgather(self, data):
         """Every rank's `data` (bytes of one length on every rank), in rank order."""
         data = bytes(data)

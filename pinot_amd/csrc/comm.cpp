@@ -52,6 +52,7 @@ struct RcclApi {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -83,6 +84,7 @@ RcclApi load_rccl() {
   sym(a.GetUniqueId, "ncclGetUniqueId");
   sym(a.CommInitRank, "ncclCommInitRank");
   sym(a.CommDestroy, "ncclCommDestroy");
+  sym(a.CommAbort, "ncclCommAbort");
   sym(a.AllReduce, "ncclAllReduce");
   sym(a.ReduceScatter, "ncclReduceScatter");
   sym(a.AllGather, "ncclAllGather");
@@ -110,8 +112,25 @@ const RcclApi& rccl() {
 ncclDataType_t nccl_type(CommDtype t) { return t == CDT_F64 ? ncclFloat64 : ncclInt64; }
 ncclRedOp_t nccl_op(CommOp op) { return op == COP_MIN ? ncclMin : op == COP_MAX ? ncclMax : ncclSum; }
 
+// Polls a stream until its work is done, within the calling thread's wait limits (Comm::wait_expired): a collective
+// whose peer never joins it must not block the caller forever.  Spins ~2 ms, then sleeps 20 us between polls.
+int poll_stream(const Comm& comm, hipStream_t s) {
+  const double t0 = comm_now_us();
+  for (int spin = 0;; ++spin) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) return host_fail(PGPU_ERR_DEVICE, "collective wait failed: %s", hipGetErrorString(e));
+    CTRY(comm.wait_expired(t0));
+    if ((spin & 63) == 63 && comm_now_us() - t0 > 2000.0) {
+      struct timespec ts = {0, 20000};
+      nanosleep(&ts, nullptr);
+    }
+  }
+}
+
 struct RcclComm : Comm {
   ncclComm_t c = nullptr;
+  std::atomic<bool> c_aborted{false};
   std::mutex mu;
   hipStream_t hs = nullptr;  // host-buffer collectives
   void* stage = nullptr;
@@ -122,14 +141,27 @@ struct RcclComm : Comm {
   hipEvent_t last = nullptr;
   bool issued = false;
   ~RcclComm() override {
-    if (c) rccl().CommDestroy(c);
+    if (c && !c_aborted.load()) rccl().CommDestroy(c);
     if (stage) hipFree(stage);
     if (last) hipEventDestroy(last);
     if (hs) hipStreamDestroy(hs);
   }
+  // Not under `mu`: the thread that gives up may be another query's (wait_plan), while this one is parked in a wait.
+  // ncclCommAbort makes the kernels of collectives still waiting on a peer exit; the communicator is unusable after.
+  void abort() override {
+    if (aborted.exchange(true)) return;
+    if (c && rccl().CommAbort && !c_aborted.exchange(true)) rccl().CommAbort(c);
+  }
   int before(hipStream_t s) {
+    CTRY(usable());
     if (issued) CHIP(hipStreamWaitEvent(s, last, 0));
     return 0;
+  }
+  // The host-buffer collectives' stream, waited for within the caller's limits; an expired wait aborts.
+  int sync_hs() {
+    const int rc = poll_stream(*this, hs);
+    if (rc == PGPU_ERR_TIMEOUT || rc == PGPU_ERR_CANCELLED) abort();
+    return rc;
   }
   int after(hipStream_t s) {
     CHIP(hipEventRecord(last, s));
@@ -159,6 +191,7 @@ struct RcclComm : Comm {
   }
   int alltoallv_host(const void* send, const int64_t* scount, void* recv, const int64_t* rcount, size_t rec) override {
     std::lock_guard<std::mutex> g(mu);
+    CTRY(usable());
     size_t st = 0, rt = 0;
     for (int p = 0; p < nranks; ++p) {
       st += (size_t)scount[p] * rec;
@@ -174,8 +207,9 @@ struct RcclComm : Comm {
     if (!rc) rc = after(hs);
     if (!rc && rt && hipMemcpyAsync(recv, (uint8_t*)d + st, rt, hipMemcpyDeviceToHost, hs) != hipSuccess)
       rc = host_fail(PGPU_ERR_DEVICE, "all-to-all staging download failed");
-    if (hipStreamSynchronize(hs) != hipSuccess && !rc) rc = host_fail(PGPU_ERR_DEVICE, "all-to-all staging failed");
-    hipFree(d);
+    if (!rc) rc = sync_hs();
+    else if (!aborted.load()) hipStreamSynchronize(hs);  // staging freed below: nothing may still read it
+    if (!aborted.load()) hipFree(d);  // (after an abort, queued work may still hold it: leaked, not freed under it)
     return rc;
   }
   int alltoallv_impl(const void* dsend, const int64_t* scount, void* drecv, const int64_t* rcount, size_t rec,
@@ -211,6 +245,7 @@ struct RcclComm : Comm {
   }
   int allgather_host(const void* send, size_t bytes, void* recv) override {
     std::lock_guard<std::mutex> g(mu);
+    CTRY(usable());
     if (bytes == 0) return 0;
     const size_t need = bytes * (size_t)nranks;
     if (need > stage_cap) {
@@ -226,18 +261,17 @@ struct RcclComm : Comm {
     NTRY(rccl().AllGather(mine, stage, bytes, ncclInt8, c, hs));  // in place
     CTRY(after(hs));
     CHIP(hipMemcpyAsync(recv, stage, need, hipMemcpyDeviceToHost, hs));
-    CHIP(hipStreamSynchronize(hs));
-    return 0;
+    return sync_hs();
   }
 };
 
 // ------------------------------------------------------------------------------------------ host transport
 constexpr int kHostMaxRanks = 64;
-constexpr double kHostTimeoutS = 600.0;
 struct HostCtl {
   struct alignas(64) Slot {
     std::atomic<uint64_t> gen;
   } slot[kHostMaxRanks];
+  alignas(64) std::atomic<int32_t> live;  // ranks that joined and have not left: the last one out removes the file
 };
 
 struct HostComm : Comm {
@@ -245,26 +279,29 @@ struct HostComm : Comm {
   HostCtl* ctl = nullptr;
   uint64_t gen = 0, seq = 0;
   std::mutex mu;
+  // No barrier on the way out: a peer that already exited (or crashed) must not hold this rank's teardown.  Each rank
+  // removes its own files; the last rank out removes the control file.
   ~HostComm() override {
     if (ctl) {
-      barrier();
-      if (rank == 0) unlink(("/dev/shm/" + name + ".ctl").c_str());
+      if (ctl->live.fetch_sub(1) == 1) unlink(("/dev/shm/" + name + ".ctl").c_str());
       munmap(ctl, sizeof(HostCtl));
     }
   }
   int barrier() {
+    CTRY(usable());
     ++gen;
     ctl->slot[rank].gen.store(gen, std::memory_order_release);
-    const auto t0 = std::chrono::steady_clock::now();
+    const double t0 = comm_now_us();
     for (int r = 0; r < nranks; ++r) {
       int spins = 0;
       while (ctl->slot[r].gen.load(std::memory_order_acquire) < gen) {
         if (++spins > 256) {
           struct timespec ts = {0, 20000};
           nanosleep(&ts, nullptr);
-          if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kHostTimeoutS)
-            return host_fail(PGPU_ERR_TIMEOUT, "host communicator: rank %d never reached barrier %llu", r,
-                             (unsigned long long)gen);
+          if (const int rc = wait_expired(t0)) {
+            abort();  // this rank's generation is ahead of its peers': later barriers would not pair up
+            return rc;
+          }
         } else {
           sched_yield();
         }
@@ -408,6 +445,42 @@ struct HostComm : Comm {
 
 }  // namespace
 
+CommWait& comm_wait() {
+  static thread_local CommWait w;
+  return w;
+}
+
+double comm_now_us() {
+  return (double)std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int Comm::usable() const {
+  if (aborted.load(std::memory_order_acquire))
+    return host_fail(PGPU_ERR_DEVICE, "communicator aborted: a collective's wait on its peers expired earlier "
+                     "(create a new communicator)");
+  return 0;
+}
+
+int Comm::wait_expired(double t0_us) const {
+  const CommWait& w = comm_wait();
+  if (w.cancel && __atomic_load_n(w.cancel, __ATOMIC_ACQUIRE))
+    return host_fail(PGPU_ERR_CANCELLED, "QueryException 503 (QUERY_CANCELLATION_ERROR): Query was cancelled while "
+                     "waiting on the other GPUs' combine");
+  if (w.end_time_ms > 0) {
+    const double now_ms = (double)std::chrono::duration_cast<std::chrono::microseconds>(
+                              std::chrono::system_clock::now().time_since_epoch()).count() / 1000.0;
+    if (now_ms >= (double)w.end_time_ms)
+      return host_fail(PGPU_ERR_TIMEOUT, "QueryException 200 (QUERY_EXECUTION_ERROR): Timed out while combining "
+                       "group-by results across GPUs");
+  }
+  const int64_t lim = timeout_ms.load(std::memory_order_relaxed);
+  if (lim > 0 && comm_now_us() - t0_us > (double)lim * 1000.0)
+    return host_fail(PGPU_ERR_TIMEOUT, "communicator: rank peers did not join a collective within %lld ms "
+                     "(rank %d of %d)", (long long)lim, rank, nranks);
+  return 0;
+}
+
 int comm_unique_id(int32_t kind, void* id) {
   memset(id, 0, PGPU_COMM_ID_BYTES);
   if (kind == PGPU_COMM_RCCL) {
@@ -470,6 +543,7 @@ int comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int3
     close(fd);
     if (m == MAP_FAILED) return host_fail(PGPU_ERR_DEVICE, "host communicator: cannot map %s", p.c_str());
     c->ctl = static_cast<HostCtl*>(m);
+    c->ctl->live.fetch_add(1);
     CTRY(c->barrier());  // every rank joined
     *out = c.release();
     return 0;

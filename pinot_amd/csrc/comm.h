@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 
@@ -21,9 +22,38 @@ namespace pgpu {
 enum CommDtype { CDT_I64 = 0, CDT_F64 = 1 };
 enum CommOp { COP_SUM = 0, COP_MIN = 1, COP_MAX = 2 };
 
+// Blocking waits on peers give up after this unless the communicator or the calling query sets another limit
+// (pgpu_comm_set_timeout; a query's end_time_ms).
+constexpr int64_t kDefaultCommTimeoutMs = 600 * 1000;
+
+// The wait limits of the calling thread's collectives: the query's deadline and cancel flag, set by the combine entry
+// points for the duration of the call (CommWaitScope).  A collective that waits on a peer past them fails instead of
+// blocking forever (a peer that failed before the collective never enters it); RCCL's communicator is aborted then.
+struct CommWait {
+  int64_t end_time_ms = 0;     // epoch ms; 0 = none
+  const int* cancel = nullptr;  // the plan's cancel flag (__atomic_* reads)
+};
+CommWait& comm_wait();
+struct CommWaitScope {
+  CommWait saved;
+  CommWaitScope(int64_t end_time_ms, const int* cancel) : saved(comm_wait()) {
+    comm_wait().end_time_ms = end_time_ms;
+    comm_wait().cancel = cancel;
+  }
+  ~CommWaitScope() { comm_wait() = saved; }
+};
+
 struct Comm {
   virtual ~Comm() {}
   int nranks = 1, rank = 0, device = 0;
+  std::atomic<int64_t> timeout_ms{kDefaultCommTimeoutMs};  // <= 0: no limit of the communicator's own
+  std::atomic<bool> aborted{false};  // a wait expired: collectives of the peers may never complete; unusable
+  // Gives the communicator up (RCCL: ncclCommAbort, so kernels of collectives a peer never joined exit).
+  virtual void abort() { aborted.store(true); }
+  // While waiting on peers since t0 (steady-clock us): 0, or fails with PGPU_ERR_CANCELLED / PGPU_ERR_TIMEOUT.
+  int wait_expired(double t0_us) const;
+  // PGPU_ERR_DEVICE once aborted.
+  int usable() const;
   // In place on the device, ordered on `s`.
   virtual int allreduce(void* d, size_t count, CommDtype t, CommOp op, hipStream_t s) = 0;
   // send: nranks x count elements; rank r receives the reduction of block r into recv (count elements).
@@ -38,6 +68,7 @@ struct Comm {
   virtual int allgather_host(const void* send, size_t bytes, void* recv) = 0;
 };
 
+double comm_now_us();  // steady clock
 int comm_unique_id(int32_t kind, void* id);
 int comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, Comm** out);
 

@@ -255,8 +255,9 @@ struct KPartParams {
   // 1 (hashed, two-level, one u32 value stream): K8c writes each record as one u64 (hk | value << 32) at mid_val
   // instead of a u32 key and a u32 value in two arrays; K8e reads it so
   int32_t mid_pair;
-  uint64_t* out_rec;                  // [rec_cap][1 + num_slots]
-  unsigned long long* out_count;
+  uint64_t* out_rec;                  // [out_cap][1 + num_slots]
+  unsigned long long* out_count;      // groups appended (counts past out_cap too: the host reports the overflow)
+  int64_t out_cap;                    // records out_rec holds (part_hash_out_cap)
 };
 // K8h: value streams a record carries in registers (plans with more use the global hash table).
 constexpr int kHashPartStreams = 4;

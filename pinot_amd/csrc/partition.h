@@ -643,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
       const uint64_t bal = __ballot(occ);
       if (occ) {
         const uint64_t r = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
-        if (r < (uint64_t)cap) {
+        if (r < (uint64_t)pp.out_cap) {  // past it: counted, not written; finalize reports the overflow
           uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
           o[0] = (uint64_t)(keys[i] * kHashInv);  // the composite key back from its hash
           if (cs) {

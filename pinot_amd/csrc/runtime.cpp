@@ -1177,6 +1177,12 @@ struct pgpu_plan_s {
   // of shard_count words at `shard`; pgpu_plan_finalize reads it
   const void* shard = nullptr;
   int64_t shard_begin = 0, shard_count = 0;
+  // pgpu_plan_combine: the slot kinds the plan was planned with, when the combine's agreement changed them (an int64
+  // SUM merged as float64), and the communicator whose stream-ordered collectives this execution's finalize waits on
+  // (an expired wait aborts it: a peer that never joined leaves them pending).  exec_prologue resets all three, so a
+  // plan executed again after a combine runs and finalizes as planned.
+  std::vector<int32_t> slot_kind_planned;
+  pgpu::Comm* comm_used = nullptr;
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -1905,6 +1911,13 @@ void hash_part_resize(pgpu_plan_s* P, int64_t groups) {
 // Records K8h may append (the groups): as finalize's compaction of a hash table sizes its output.
 int64_t part_hash_out_cap(const pgpu_plan_s* P) {
   return std::max<int64_t>(1, std::min<int64_t>(P->num_keys, std::max<int64_t>(P->total_docs, 1)));
+}
+
+// K8h found more groups than its record buffer holds (the bound above is exact for the plan's key space and docs, so
+// this is a planning bug, reported instead of a truncated result)
+int part_hash_overflow(const pgpu_plan_s* P, uint64_t groups) {
+  return fail(PGPU_ERR_DEVICE, "hashed partitions found %llu groups, past their record buffer of %lld",
+              (unsigned long long)groups, (long long)part_hash_out_cap(P));
 }
 
 // A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
@@ -2943,17 +2956,29 @@ int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
   // HIP runtime's own synchronise does) for the first ~2 ms keeps the wake-up latency of short queries at the
   // poll interval; longer waits back off to 20 us sleeps.
   const auto t0 = std::chrono::steady_clock::now();
+  // a combined plan's stream holds collectives that complete only when every peer joins them: the wait also ends at
+  // the communicator's timeout, and an expired wait aborts the communicator (the collectives' kernels exit)
+  const int64_t comm_lim = P->comm_used ? P->comm_used->timeout_ms.load(std::memory_order_relaxed) : 0;
   for (int spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(sc->busy);
     if (e == hipSuccess) return 0;
     if (e != hipErrorNotReady) return fail(PGPU_ERR_DEVICE, "query wait failed: %s", hipGetErrorString(e));
     if (cancelled(P)) {
       sc->abandoned = true;
+      if (P->comm_used) P->comm_used->abort();
       return cancel_fail();
     }
     if (P->end_time_ms > 0 && epoch_us() >= (double)P->end_time_ms * 1000.0) {
       sc->abandoned = true;
+      if (P->comm_used) P->comm_used->abort();
       return timeout_fail(P);
+    }
+    if (comm_lim > 0 && (spin & 63) == 63 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(comm_lim)) {
+      sc->abandoned = true;
+      P->comm_used->abort();
+      return fail(PGPU_ERR_TIMEOUT, "the combine's collectives did not complete within the communicator's timeout "
+                  "(%lld ms): a peer rank never joined them; communicator aborted", (long long)comm_lim);
     }
     if ((spin & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
       std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -3023,6 +3048,15 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     if (P->exec_start_ms >= P->end_time_ms) return timeout_fail(P);
     TRY(deadline_ticks(P->table, P->end_time_ms, &deadline));
   }
+  // the state a previous execution's combine left (pgpu_plan_combine): planned slot kinds, no shard, no merged table
+  if (!P->slot_kind_planned.empty()) {
+    P->slot_kind = P->slot_kind_planned;
+    P->slot_kind_planned.clear();
+  }
+  P->shard = nullptr;
+  P->shard_begin = P->shard_count = 0;
+  P->comm_used = nullptr;
+  P->merged_records = -1;
   Scratch* sc = P->scratch;
   X.nslots = (int)P->slot_kind.size();
   const int nslots = X.nslots;
@@ -3323,6 +3357,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       HIP_TRY(hipMemsetAsync(sc->counter.p, 0, 8, stream));
       pp.out_rec = sc->ckeys.as<uint64_t>();
       pp.out_count = sc->counter.as<unsigned long long>();
+      pp.out_cap = ocap;
       P->part_hash_live = true;
     } else {
       TRY(sc->rec_key.ensure((size_t)cap * 2));
@@ -3650,7 +3685,8 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     // hash table: unordered compaction, then key order on the host
     const int64_t rec = 1 + nslots;  // entry-major compact record: key, then the slot words
     int64_t cap;
-    if (P->part_hash_live) {  // K8h wrote the compacted records and their count at execute
+    const bool k8h = P->part_hash_live;
+    if (k8h) {  // K8h wrote the compacted records and their count at execute
       cap = part_hash_out_cap(P);
     } else {
       cap = std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0 ? P->merged_records
@@ -3681,6 +3717,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     if (st[5])  // stats[4]: a probe found no free slot (hash_slot) -- the table was sized below the plan's groups
       return fail(PGPU_ERR_DEVICE, "group hash table of %lld slots overflowed (plan bound %lld groups)",
                   (long long)G, (long long)P->group_bound);
+    if (k8h && st[0] > (uint64_t)cap) return part_hash_overflow(P, st[0]);
     n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)cap);
     matched = st[1];
     star_scanned = st[2] + st[3];
@@ -5329,7 +5366,8 @@ int part_hash_materialize(pgpu_plan_s* P, hipStream_t s) {
   uint64_t* st = reinterpret_cast<uint64_t*>(sc->xstage.p);
   HIP_TRY(hipMemcpyAsync(st, sc->counter.p, 8, hipMemcpyDeviceToHost, s));
   TRY(wait_plan(P, s));
-  const int64_t n = (int64_t)std::min<uint64_t>(st[0], (uint64_t)part_hash_out_cap(P));
+  if (st[0] > (uint64_t)part_hash_out_cap(P)) return part_hash_overflow(P, st[0]);
+  const int64_t n = (int64_t)st[0];
   TRY(build_hash_table(P, s, sc->ckeys.as<uint64_t>(), n));
   P->part_hash_live = false;
   return 0;
@@ -5405,7 +5443,10 @@ int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, co
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   Scratch* sc = P->scratch;
   const int nslots = (int)P->slot_kind.size();
-  if (kinds) P->slot_kind.assign(kinds, kinds + nslots);
+  if (kinds && !std::equal(P->slot_kind.begin(), P->slot_kind.end(), kinds)) {
+    if (P->slot_kind_planned.empty()) P->slot_kind_planned = P->slot_kind;  // restored by the next execution
+    P->slot_kind.assign(kinds, kinds + nslots);
+  }
   // the statistics words leave the table buffer (it is resized below)
   TRY(sc->stats.ensure(64));
   if (P->d_stats != sc->stats.as<unsigned long long>()) {
@@ -5583,6 +5624,20 @@ int pgpu_comm_rank(pgpu_comm c, int32_t* rank, int32_t* nranks) try {
   return 0;
 } PGPU_ABI_CATCH
 
+int pgpu_comm_set_timeout(pgpu_comm c, int64_t timeout_ms) try {
+  PGPU_ABI_GUARD;
+  if (!c) return fail(PGPU_ERR_INVALID_ARGUMENT, "null communicator");
+  c->impl->timeout_ms.store(timeout_ms, std::memory_order_relaxed);
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_comm_abort(pgpu_comm c) try {
+  PGPU_ABI_GUARD;
+  if (!c) return fail(PGPU_ERR_INVALID_ARGUMENT, "null communicator");
+  c->impl->abort();
+  return 0;
+} PGPU_ABI_CATCH
+
 int pgpu_comm_allgather(pgpu_comm c, const void* send, int64_t bytes, void* recv) try {
   PGPU_ABI_GUARD;
   if (!c || bytes < 0 || (bytes > 0 && (!send || !recv))) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -5661,9 +5716,37 @@ int agree_kinds(const std::vector<int64_t>& all, int nranks, int ns, int32_t* ki
 }
 }  // namespace
 
+namespace {
+// Every rank's status before a collective phase, exchanged with `bytes` of payload whose first int64 word is the
+// status (all = nranks x bytes): a rank whose own part failed still takes part in this exchange, so the ranks fail
+// together instead of some waiting in a collective the failed one never enters.  Returns this rank's own failure
+// (its message kept), or one naming the first peer that failed.
+int agree_status_with(pgpu::Comm* C, int rc, const void* payload, size_t bytes, void* all) {
+  const std::string keep = rc ? g_err : std::string();
+  TRY(C->allgather_host(payload, bytes, all));
+  if (rc) {
+    g_err = keep;
+    return rc;
+  }
+  for (int p = 0; p < C->nranks; ++p) {
+    int64_t st;
+    memcpy(&st, static_cast<const uint8_t*>(all) + (size_t)p * bytes, 8);
+    if (st) return fail((int)st, "rank %d of %d failed its part of the cross-GPU combine (error %lld)", p, C->nranks,
+                        (long long)st);
+  }
+  return 0;
+}
+int agree_status(pgpu::Comm* C, int rc) {
+  std::vector<int64_t> all(C->nranks);
+  const int64_t mine = rc;
+  return agree_status_with(C, rc, &mine, 8, all.data());
+}
+}  // namespace
+
 int pgpu_plan_combine_mode(pgpu_plan P, pgpu_comm c, int64_t shard_bytes, int32_t* mode, int32_t* kinds) try {
   PGPU_ABI_GUARD;
   if (!P || !c || !mode) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  pgpu::CommWaitScope wait_limits(P->end_time_ms, &P->cancel);
   const int N = c->impl->nranks;
   int local;
   const pgpu_plan_s* K = P;  // the plan whose key space and slots describe the query on this rank
@@ -5732,41 +5815,57 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     return fail(PGPU_ERR_INVALID_ARGUMENT, "PGPU_COMBINE_ROWS: finalize the plan, then pgpu_result_combine_rows");
   if (mode != PGPU_COMBINE_ALL_REDUCE && mode != PGPU_COMBINE_REDUCE_SCATTER && mode != PGPU_COMBINE_HASH)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "combine mode %d", mode);
-  if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: combine its finalized rows (ROWS)");
-  if (!P->executed || !P->scratch) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
-  if (P->shard) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan already combined");
   pgpu::Comm* C = c->impl;
   const int N = C->nranks, me = C->rank;
-  if (C->device != P->table->device)
-    return fail(PGPU_ERR_INVALID_ARGUMENT, "communicator on device %d, table on %d", C->device, P->table->device);
+  // the query's deadline and cancel flag bound every wait on the peers below (and finalize's, via comm_used)
+  pgpu::CommWaitScope wait_limits(P->end_time_ms, &P->cancel);
+  TRY(C->usable());
+  // This rank's own checks.  In HASH mode their outcome travels with the per-owner counts (the first host exchange),
+  // so a rank that fails here still meets its peers there and every rank fails together.  The dense modes have no
+  // host exchange (one would cost every query a round trip): a failed rank issues no collective, its peers' ones stay
+  // pending on their streams, and their finalize waits end at the query deadline or the communicator's timeout,
+  // which aborts the communicator.
+  uint32_t conv = 0;
+  int pre = 0;
+  if (P->composite) pre = fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: combine its finalized rows (ROWS)");
+  else if (!P->executed || !P->scratch) pre = fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
+  else if (P->shard) pre = fail(PGPU_ERR_INVALID_ARGUMENT, "plan already combined");
+  else if (C->device != P->table->device)
+    pre = fail(PGPU_ERR_INVALID_ARGUMENT, "communicator on device %d, table on %d", C->device, P->table->device);
+  else if (mode == PGPU_COMBINE_HASH && !P->hash)
+    pre = fail(PGPU_ERR_UNSUPPORTED, "dense group tables merge element-wise (ALL_REDUCE / REDUCE_SCATTER)");
+  else if (mode != PGPU_COMBINE_HASH && P->hash)
+    pre = fail(PGPU_ERR_UNSUPPORTED, "hash-mode tables merge with PGPU_COMBINE_HASH");
+  if (!pre) pre = check_kinds(P->slot_kind, kinds, &conv);
+  if (mode != PGPU_COMBINE_HASH && pre) return pre;
   DeviceGuard g(P->table->device);
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : P->table->stream;
   Scratch* sc = P->scratch;
   const int ns = (int)P->slot_kind.size();
-  uint32_t conv = 0;
-  TRY(check_kinds(P->slot_kind, kinds, &conv));
   if (mode == PGPU_COMBINE_HASH) {
-    if (!P->hash) return fail(PGPU_ERR_UNSUPPORTED, "dense group tables merge element-wise (ALL_REDUCE / REDUCE_SCATTER)");
-    std::vector<int64_t> counts(N), all((size_t)N * N), rcount(N);
-    TRY(pgpu_plan_exchange_counts(P, s, N, counts.data()));
-    TRY(C->allgather_host(counts.data(), (size_t)N * 8, all.data()));
+    // per rank: [status, count for owner 0, ..., count for owner N-1]
+    std::vector<int64_t> counts(N + 1, 0), all((size_t)N * (N + 1)), rcount(N);
+    if (!pre) pre = pgpu_plan_exchange_counts(P, s, N, counts.data() + 1);
+    counts[0] = pre;
+    TRY(agree_status_with(C, pre, counts.data(), (size_t)(N + 1) * 8, all.data()));
     int64_t total = 0, nrecv = 0;
     for (int p = 0; p < N; ++p) {
-      total += counts[p];
-      rcount[p] = all[(size_t)p * N + me];
+      total += counts[1 + p];
+      rcount[p] = all[(size_t)p * (N + 1) + 1 + me];
       nrecv += rcount[p];
     }
     const size_t rec = (size_t)(1 + ns) * 8;
-    TRY(sc->xsend.ensure((size_t)std::max<int64_t>(total, 1) * rec));
-    TRY(pgpu_plan_exchange_export(P, s, N, kinds, sc->xsend.p, total));
-    TRY(sc->xrecv.ensure((size_t)std::max<int64_t>(nrecv, 1) * rec));
-    TRY(C->alltoallv(sc->xsend.p, counts.data(), sc->xrecv.p, rcount.data(), rec, s));
+    int rc = sc->xsend.ensure((size_t)std::max<int64_t>(total, 1) * rec);
+    if (!rc) rc = pgpu_plan_exchange_export(P, s, N, kinds, sc->xsend.p, total);
+    if (!rc) rc = sc->xrecv.ensure((size_t)std::max<int64_t>(nrecv, 1) * rec);
+    TRY(agree_status(C, rc));  // before the all-to-all: every rank has its records and room for its peers'
+    P->comm_used = C;
+    TRY(C->alltoallv(sc->xsend.p, counts.data() + 1, sc->xrecv.p, rcount.data(), rec, s));
     TRY(pgpu_plan_exchange_merge(P, s, kinds, nrecv ? sc->xrecv.p : nullptr, nrecv));
     if (key_begin) *key_begin = 0;
     if (key_count) *key_count = P->num_keys;
     return 0;
   }
-  if (P->hash) return fail(PGPU_ERR_UNSUPPORTED, "hash-mode tables merge with PGPU_COMBINE_HASH");
   uint64_t* table = reinterpret_cast<uint64_t*>(d_table ? d_table : const_cast<void*>(P->d_table_used));
   if (!table) return fail(PGPU_ERR_INVALID_ARGUMENT, "no group table");
   const int64_t G = P->num_keys;
@@ -5774,7 +5873,11 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     if ((conv >> k) & 1u)
       if (launch_i64_to_f64(table + (size_t)k * G, G, s))
         return fail(PGPU_ERR_DEVICE, "slot conversion launch failed: %s", hipGetErrorString(hipGetLastError()));
-  if (kinds) P->slot_kind.assign(kinds, kinds + ns);
+  if (kinds && !std::equal(P->slot_kind.begin(), P->slot_kind.end(), kinds)) {
+    if (P->slot_kind_planned.empty()) P->slot_kind_planned = P->slot_kind;  // restored when executed again
+    P->slot_kind.assign(kinds, kinds + ns);
+  }
+  P->comm_used = C;
   auto dtype = [&](int k) { return P->slot_kind[k] == SLOT_SUM_F64 ? pgpu::CDT_F64 : pgpu::CDT_I64; };
   auto op = [&](int k) {
     return P->slot_kind[k] == SLOT_MIN_KEY ? pgpu::COP_MIN : P->slot_kind[k] == SLOT_MAX_KEY ? pgpu::COP_MAX : pgpu::COP_SUM;
@@ -5830,10 +5933,14 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
 int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!r || !c || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  if ((int)r->slot_kind.size() != r->num_slots) return fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
   pgpu::Comm* C = c->impl;
   const int N = C->nranks, me = C->rank;
-  if (r->compact.load(std::memory_order_acquire)) TRY(pgpu::result_expand(r));
+  TRY(C->usable());
+  // a rank whose own steps fail still meets its peers in the next exchange (its status word first), so every rank
+  // fails together
+  int pre = 0;
+  if ((int)r->slot_kind.size() != r->num_slots) pre = fail(PGPU_ERR_UNSUPPORTED, "result without slot kinds");
+  else if (r->compact.load(std::memory_order_acquire)) pre = pgpu::result_expand(r);
   // agree on the slot kinds; the group ids index the ranks' dictionary snapshots, which must be the same
   std::vector<int64_t> mine(CI_WORDS, 0), all((size_t)N * CI_WORDS, 0);
   uint64_t h = 0x84222325cbf29ce4ull;
@@ -5843,9 +5950,11 @@ int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) try {
   mine[CI_KEYS] = r->num_keys;
   mine[CI_SLOTS] = r->num_slots;
   mine[CI_DIGEST] = (int64_t)h;
-  for (int s = 0; s < r->num_slots && s < kMaxSlots; ++s) mine[CI_KINDS + s] = r->slot_kind[s];
+  for (int s = 0; s < r->num_slots && s < kMaxSlots && s < (int)r->slot_kind.size(); ++s)
+    mine[CI_KINDS + s] = r->slot_kind[s];
+  mine[CI_MODE] = pre;  // the status word
   DeviceGuard g(C->device);
-  TRY(C->allgather_host(mine.data(), mine.size() * 8, all.data()));
+  TRY(agree_status_with(C, pre, mine.data(), mine.size() * 8, all.data()));
   for (int p = 0; p < N; ++p) {
     const int64_t* w = all.data() + (size_t)p * CI_WORDS;
     if (w[CI_KEYS] != mine[CI_KEYS] || w[CI_SLOTS] != mine[CI_SLOTS])
@@ -5857,13 +5966,16 @@ int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) try {
   std::vector<int32_t> kinds(std::max(r->num_slots, 1));
   TRY(agree_kinds(all, N, r->num_slots, kinds.data()));
   const int w = r->num_keys + r->num_slots;
-  std::vector<int64_t> rows((size_t)std::max<int64_t>(r->n, 1) * w), counts(N), cm((size_t)N * N), rcount(N);
-  TRY(pgpu_result_exchange_rows(r, N, kinds.data(), rows.data(), counts.data()));
-  TRY(C->allgather_host(counts.data(), (size_t)N * 8, cm.data()));
+  // per rank: [status, rows for owner 0, ..., rows for owner N-1]
+  std::vector<int64_t> rows((size_t)std::max<int64_t>(r->n, 1) * w), counts(N + 1, 0), cm((size_t)N * (N + 1)),
+      rcount(N);
+  const int rc = pgpu_result_exchange_rows(r, N, kinds.data(), rows.data(), counts.data() + 1);
+  counts[0] = rc;
+  TRY(agree_status_with(C, rc, counts.data(), (size_t)(N + 1) * 8, cm.data()));
   int64_t nrecv = 0;
-  for (int p = 0; p < N; ++p) nrecv += rcount[p] = cm[(size_t)p * N + me];
+  for (int p = 0; p < N; ++p) nrecv += rcount[p] = cm[(size_t)p * (N + 1) + 1 + me];
   std::vector<int64_t> recv((size_t)std::max<int64_t>(nrecv, 1) * w);
-  TRY(C->alltoallv_host(rows.data(), counts.data(), recv.data(), rcount.data(), (size_t)w * 8));
+  TRY(C->alltoallv_host(rows.data(), counts.data() + 1, recv.data(), rcount.data(), (size_t)w * 8));
   return pgpu_result_merge_rows(r, nrecv ? recv.data() : nullptr, nrecv, kinds.data(), out);
 } PGPU_ABI_CATCH
 

@@ -424,8 +424,14 @@ def compare_result_arrays(table, r, orc, q, schema, rel=1e-9, check_stats=True):
     = every statistic, "docs" = numDocsScanned only (index-backed leaves scan no entries), False = none (star-tree
     plans scan pre-aggregated documents).  Returns a dict (ok, groups, max_rel_err of the FP sums, first mismatch)
     instead of raising: bench.py reports it in its line."""
+    return compare_arrays(gpu_result_arrays(table, r, q), r.stats.as_tuple(), orc, q, schema, rel, check_stats)
+
+
+def compare_arrays(gpu, gpu_stats, orc, q, schema, rel=1e-9, check_stats=True):
+    """compare_result_arrays on a GPU answer already in array form: gpu = (keys, values, AVG counts) as
+    gpu_result_arrays returns them (sorted by key), gpu_stats the 4 statistics; orc as run_groupby_arrays returns it."""
     types = {n: t for n, t in schema}
-    gk, gv, gc = gpu_result_arrays(table, r, q)
+    gk, gv, gc = gpu
     ok_, ov, oc, ostats = orc
     ok_, ov, oc = sort_by_key(ok_.astype(gk.dtype) if len(ok_) else ok_.reshape(0, gk.shape[1]), ov, oc)
     out = {"ok": True, "groups": int(len(gk)), "max_rel_err_fp_sum": 0.0, "mismatch": None}
@@ -451,11 +457,49 @@ def compare_result_arrays(table, r, orc, q, schema, rel=1e-9, check_stats=True):
             bad("%s(%s) group %d: gpu %r, oracle %r" % (fn, col, i, gv[a][i], ov[a][i]))
         if fn == "AVG" and not np.array_equal(gc[a], oc[a]):
             bad("AVG(%s) counts" % col)
-    if check_stats is True and r.stats.as_tuple() != tuple(ostats):
-        bad("statistics: gpu %s, oracle %s" % (r.stats.as_tuple(), tuple(ostats)))
-    elif check_stats == "docs" and r.stats.as_tuple()[0] != ostats[0]:
-        bad("numDocsScanned: gpu %d, oracle %d" % (r.stats.as_tuple()[0], ostats[0]))
+    if check_stats is True and tuple(gpu_stats) != tuple(ostats):
+        bad("statistics: gpu %s, oracle %s" % (tuple(gpu_stats), tuple(ostats)))
+    elif check_stats == "docs" and gpu_stats[0] != ostats[0]:
+        bad("numDocsScanned: gpu %d, oracle %d" % (gpu_stats[0], ostats[0]))
     return out
+
+
+def concat_arrays(parts):
+    """Disjoint per-rank answers (gpu_result_arrays triples: reduce-scattered key ranges, hash owners' shares) as one
+    answer sorted by key."""
+    parts = list(parts)
+    keys = np.concatenate([p[0] for p in parts], axis=0)
+    vals = np.concatenate([p[1] for p in parts], axis=1)
+    cnts = np.concatenate([p[2] for p in parts], axis=1)
+    return sort_by_key(keys, vals, cnts)
+
+
+def merge_partial_arrays(parts, aggregations):
+    """The merge of per-server partial results (run_groupby_arrays outputs, one per rank's segments), as the broker
+    merges server responses (GroupByDataTableReducer / GroupByOrderByCombineOperator.java:170-181): per group COUNT,
+    SUM and AVG's (sum, count) add, MIN / MAX take the min / max; the statistics add.  numpy, independent of the
+    device combine it checks (no group-count limit may bind: the bench's workloads never reach theirs)."""
+    parts = list(parts)
+    keys = np.concatenate([p[0] for p in parts], axis=0)
+    vals = np.concatenate([p[1] for p in parts], axis=1)
+    cnts = np.concatenate([p[2] for p in parts], axis=1)
+    stats = tuple(int(sum(p[3][i] for p in parts)) for i in range(4))
+    if len(keys) == 0:
+        return keys, vals, cnts, stats
+    keys, vals, cnts = sort_by_key(keys, vals, cnts)
+    new = np.ones(len(keys), dtype=bool)
+    if keys.shape[1]:
+        new[1:] = np.any(keys[1:] != keys[:-1], axis=1)
+    else:
+        new[1:] = False
+    starts = np.nonzero(new)[0]
+    mv = np.empty((vals.shape[0], len(starts)), dtype=vals.dtype)
+    mc = np.empty((cnts.shape[0], len(starts)), dtype=cnts.dtype)
+    for a, (fn, _) in enumerate(aggregations):
+        red = np.minimum if fn == "MIN" else np.maximum if fn == "MAX" else np.add
+        mv[a] = red.reduceat(vals[a], starts)
+        mc[a] = np.add.reduceat(cnts[a], starts)
+    return keys[starts], mv, mc, stats
 
 
 def segments_from_table(table, handles, schema, docs):

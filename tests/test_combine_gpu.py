@@ -101,3 +101,30 @@ def test_combine_mode_after_combine_is_rejected(rccl_table):
     plan.finalize(s)
     plan.close()
     stream.synchronize()
+
+
+@pytest.mark.parametrize("name", ["all_reduce", "reduce_scatter", "hash"])
+def test_plan_executed_again_after_combine_runs_as_planned(oracle, rccl_table, name):
+    """pgpu_plan_combine changed the plan for good (an int64 SUM slot agreed as float64, the
+    reduce-scattered shard, the merged hash table), so executing the plan again ran the scan with a float64 slot over
+    an integer column and finalize returned the stale shard.  Now exec_prologue restores the planned state: execute,
+    combine (with the int64 SUM forced to float64 -- what another rank's float64 sum would agree), execute again,
+    finalize -- the answer is the plain one, integers exact."""
+    from pinot_amd.combine import combine_mode, combine_plan
+    table, handles, segs, comm = rccl_table
+    sql, limit, shard_bytes = {c[0]: (c[1], c[2], c[3]) for c in CASES}[name]
+    q = parse_query(sql, num_groups_limit=limit)
+    stream = torch.cuda.Stream()
+    s = stream.cuda_stream
+    plan = table.plan(handles, q)
+    mode, kinds = combine_mode(plan, comm, shard_bytes)
+    forced = [L.SLOT_SUM_F64 if k == L.SLOT_SUM_I64 else k for k in kinds]
+    assert forced != kinds  # the query has an integer SUM
+    plan.execute(s)
+    combine_plan(plan, comm, s, mode, forced)
+    first = plan.finalize(s)
+    _check(oracle, first, segs, q, limit)
+    plan.execute(s)  # again, without a combine
+    res = plan.finalize(s)
+    plan.close()
+    _check(oracle, res, segs, q, limit)  # integer SUMs compared exactly: a float64 slot read as int64 would differ

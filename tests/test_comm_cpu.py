@@ -111,3 +111,59 @@ def test_communicator_from_process_group():
         vals, bad = out[r]
         assert vals == [1, 2, 3, 7, 11]
         assert "communicator" in bad
+
+
+def _absent_peer_rank(uid, rank, q):
+    """Rank 1 joins and leaves at once (as a peer that failed before the collective); rank 0's all-gather must end at
+    its communicator timeout, not block, and the communicator is unusable afterwards."""
+    import time
+    try:
+        from pinot_amd.combine import Communicator
+        c = Communicator(L.COMM_HOST, uid, 2, rank, 0)
+        if rank == 1:
+            t0 = time.monotonic()
+            c.close()  # no barrier on the way out: a peer's teardown never waits for the others
+            q.put((rank, "closed", time.monotonic() - t0))
+            return
+        c.set_timeout(1500)
+        t0 = time.monotonic()
+        try:
+            c.allgather(b"12345678")
+            first = ("no error", 0)
+        except L.PinotGpuError as e:
+            first = (e.code, e.message)
+        waited = time.monotonic() - t0
+        try:
+            c.allgather(b"12345678")
+            second = ("no error", 0)
+        except L.PinotGpuError as e:
+            second = (e.code, e.message)
+        t1 = time.monotonic()
+        c.close()
+        q.put((rank, first, second, waited, time.monotonic() - t1))
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, "error: %r" % e))
+
+
+def test_host_comm_absent_peer_times_out_and_aborts():
+    """a rank that fails before a collective must not leave its peers blocked forever (the host
+    transport gave up only after 600 s, and its destructor ran a barrier)."""
+    import os
+    from pinot_amd.combine import Communicator
+    uid = Communicator.unique_id(L.COMM_HOST)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_absent_peer_rank, args=(uid, r, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict((item[0], item[1:]) for item in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=30)
+    assert out[1][0] == "closed" and out[1][1] < 5, out[1]
+    first, second, waited, close_s = out[0]
+    assert first[0] == L.PGPU_ERR_TIMEOUT and "did not join" in first[1], first
+    assert 1.0 <= waited < 30, waited
+    assert second[0] == L.PGPU_ERR_DEVICE and "aborted" in second[1], second
+    assert close_s < 5
+    # the last rank out removed the control file
+    assert not os.path.exists("/dev/shm/%s.ctl" % uid.rstrip(b"\0").decode())

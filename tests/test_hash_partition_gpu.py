@@ -108,3 +108,18 @@ def test_group_paths(oracle, sparse):
         with t.plan(hs, q) as p:
             assert p.group_path() == path, sql
         assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+
+
+def test_in_filter_narrows_the_key_space_to_a_dense_table(oracle, sparse):
+    """The IN-filtered shape r04 dropped from QUERIES after its path assertion failed: the conjunct `c IN (1, 3, 5, 7)`
+    bounds the group-by column c to the global ids of [1, 7], so the key space the planner sizes is 3000 x 3000 x 7 =
+    6.3e7 < 2^26 -- a dense table, not hashed partitions (the filter-restricted key space, runtime.cpp "Key space
+    restricted by the filter").  The path is asserted as the planner should pick it, and the values against the
+    oracle."""
+    t, hs, segs = sparse
+    q = parse_query("SELECT SUM(m), MAX(m) FROM t WHERE m > 0 AND c IN (1, 3, 5, 7) GROUP BY c, a, b",
+                    num_groups_limit=10 ** 9)
+    with t.plan(hs, q) as p:
+        assert p.group_path() in ("global", "partitioned"), p.group_path()
+        assert p.layout()[1] == len(t.dictionary("a")) * len(t.dictionary("b")) * 7 < 2 ** 26
+    assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)

@@ -117,6 +117,18 @@ def test_workload_c4_star_tree(oracle, gpu_lib):
         o = oracle.run_groupby_arrays(w.schema, segs, q)
         r = t.execute_groupby(hs, q)
         assert_same_arrays(t, r, o, q, w.schema)
+        # ... and the C star-tree operator's answer over the same trees, statistics included (numDocsScanned = star-tree
+        # documents read, entries scanned in / post filter): StarTreeFilterOperator.java:185-226 +
+        # StarTreeGroupByExecutor restated in oracle.c (run_star_segment)
+        from pinot_amd.startree import StarTree
+        spec = w.star_tree
+        for seg in segs:
+            st = StarTree.build(w.schema, seg, spec["split_order"], spec["pairs"], spec["max_leaf_records"])
+            seg.star_arrays = st.arrays()
+            st.close()
+        o_star = oracle.run_groupby_arrays(w.schema, segs, q, use_star_tree=True)
+        res = oracle.compare_result_arrays(t, r, o_star, q, w.schema, rel=REL, check_stats=True)
+        assert res["ok"], res
         q.use_star_tree = False
         rs = t.execute_groupby(hs, q)
         assert_same_arrays(t, rs, o, q, w.schema)

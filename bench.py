@@ -152,7 +152,7 @@ SCAN_KERNELS = ("filter_groupby_kernel", "part_pass_kernel", "part_split_kernel"
                 "part_hash_aggregate_kernel", "startree_traverse_kernel", "startree_scan_kernel")
 # the kernel that opens one scan launch (the partitioned group-by is a pipeline of four kernels per launch; a
 # star-tree launch is the traversal, then the pre-aggregated document scan)
-LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false>", "startree_traverse_kernel")
+LAUNCH_KERNELS = ("filter_groupby_kernel", "part_pass_kernel<false", "startree_traverse_kernel")
 # the launcher's and torch.distributed.run's variables: a profiled child run is one rank of its own
 DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
             "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",

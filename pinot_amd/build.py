@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, "libpinotgpu.so")
 # build in parallel.
 SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime"), ("startree.cpp", [], "startree"),
            ("filter_stats.cpp", [], "filter_stats"), ("comm.cpp", [], "comm"), ("server_response.cpp", [], "server_response"),
-           ("k_partition.hip", [], "k_partition"), ("k_hashsort.hip", [], "k_hashsort")] + \
+           ("k_partition.hip", [], "k_partition"), ("k_hashfinal.hip", [], "k_hashfinal")] + \
     [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
     [("k_startree.hip", ["-DPGPU_MODE=%d" % m], "k_startree_%d" % m) for m in range(3)]
 HEADERS = ["internal.h", "device.h", "scan_direct.h", "host_common.h", "startree_kernels.h",

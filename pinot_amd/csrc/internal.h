@@ -255,9 +255,16 @@ struct KPartParams {
   // 1 (hashed, two-level, one u32 value stream): K8c writes each record as one u64 (hk | value << 32) at mid_val
   // instead of a u32 key and a u32 value in two arrays; K8e reads it so
   int32_t mid_pair;
+  // K8c staging (part_pass_kernel STAGE 1 / 2): 0 = off; else the records' form (1: pack_bits u32, 2: mid_pair u64),
+  // and the u32 word of K8c's LDS where the waves' staging regions start (set by launch_partitioned)
+  int32_t staged;
+  int32_t stage_off;
   uint64_t* out_rec;                  // [out_cap][1 + num_slots]
   unsigned long long* out_count;      // groups appended (counts past out_cap too: the host reports the overflow)
   int64_t out_cap;                    // records out_rec holds (part_hash_out_cap)
+  // [num_parts][2][num_slots]: each partition's range of every slot's words (order-preserving u64, min then max) --
+  // the compact result form's widths without a pass over the records (launch_hash_minmax_parts folds them)
+  unsigned long long* out_mm;
 };
 // K8h: value streams a record carries in registers (plans with more use the global hash table).
 constexpr int kHashPartStreams = 4;
@@ -355,17 +362,14 @@ int launch_exchange_scatter(const uint64_t* table, const unsigned long long* has
                             void* stream);
 int launch_i64_to_f64(uint64_t* p, int64_t n, void* stream);
 // k_hashsort.hip: hash-mode finalize on the device (radix sort of the compacted records by key, decode to columns).
-int hash_sort_temp_bytes(int64_t n, int key_bits, size_t* bytes);
 int launch_hash_minmax(const uint64_t* rec, const unsigned long long* count, int64_t cap, int32_t num_slots,
                        unsigned long long* mm, void* stream);
-int launch_hash_sort_compact(const uint64_t* rec, int64_t n, int32_t num_slots, int key_bits, int32_t key_width,
-                             const int32_t* width, const int64_t* slot_off, void* tmp, size_t temp_bytes,
-                             uint64_t* keys_a, uint64_t* keys_b, uint32_t* idx_a, uint32_t* idx_b, uint8_t* out,
-                             void* stream);
-int launch_hash_sort_decode(const uint64_t* rec, int64_t n, int32_t num_slots, int32_t num_keys, const int64_t* stride,
-                            const int64_t* card, const int64_t* off, int key_bits, void* tmp, size_t temp_bytes,
-                            uint64_t* keys_a, uint64_t* keys_b, uint32_t* idx_a, uint32_t* idx_b, uint8_t* out,
-                            size_t slot_off, void* stream);
+int launch_hash_minmax_parts(const unsigned long long* part_mm, int32_t num_parts, int32_t num_slots,
+                             unsigned long long* mm, void* stream);
+int launch_hash_compact(const uint64_t* rec, int64_t n, int32_t num_slots, int32_t key_width, const int32_t* width,
+                        const int64_t* slot_off, uint8_t* out, void* stream);
+int launch_hash_decode(const uint64_t* rec, int64_t n, int32_t num_slots, int32_t num_keys, const int64_t* stride,
+                       const int64_t* card, const int64_t* off, uint8_t* out, size_t slot_off, void* stream);
 int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, const int32_t* slot_kind, uint64_t* table,
                          unsigned long long* hash_keys, int64_t num_keys, void* stream);
 // Compact form of a large dense table: counts per chunk + exclusive scan (total into *total) + each slot's range over
@@ -385,7 +389,7 @@ int launch_compact_ordered_scatter(const uint64_t* table, int32_t num_slots, int
                                    int32_t num_key_cols, const uint32_t* chunk_scratch, void* out, int64_t cap,
                                    void* stream);
 // Partitioned group-by (k_partition.hip): K8a count, scan, K8c scatter, K8d aggregate into p.base.table.
-int occupancy_part_pass(size_t lds_bytes);
+int occupancy_part_pass(size_t pass_lds, int num_parts, int num_coarse, int staged);
 int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* stream);
 // In-place exclusive prefix sum of n u32 (one workgroup; n up to a few 10^4).
 int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);

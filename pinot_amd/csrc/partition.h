@@ -33,6 +33,8 @@
 // aggregateGroupBySV + GroupByCombineOperator merge); results are identical (integer
 // accumulators exact; double sums within the path's 1e-9 relative bound — their order is not fixed).
 #pragma once
+#include <type_traits>
+
 #include "device.h"
 
 namespace pgpu {
@@ -189,6 +191,98 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   }
 }
 
+// Wave-scope ordering of LDS accesses (the LDS unit serves one wave's instructions in order; this keeps the compiler
+// from moving them across the point).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// u32 words of a wave's K8c staging region (part_scatter_half_staged): run counters / starts [64], store offsets
+// [64], run of each staged record [1024 u8], staged records [1024 u32 or u64].
+constexpr int kStageWaveWords32 = 64 + 64 + 256 + 1024;
+constexpr int kStageWaveWords64 = 64 + 64 + 256 + 2048;
+
+// K8c, staged (one u32 or u64 word per record, <= 64 coarse runs): the records of a wave's half-group (<= 1024: 64
+// lanes x 16 docs) are counting-sorted by coarse run in the wave's own LDS region -- rank within the run by a wave-local
+// counter, one workgroup-cursor reservation per run and wave (lane r reserves run r), an exclusive scan of the runs'
+// counts -- and then stored in run order: consecutive lanes store consecutive positions of one run, so a store
+// instruction touches a few lines instead of one line per lane.
+//   W64 = false: pack_bits records, (key within its coarse run) | (value - pack_min) << cbits, to mid_key;
+//   W64 = true : mid_pair records, hk | value << 32, to mid_val.
+template <int H, bool W64>
+__device__ __forceinline__ void part_scatter_half_staged(const KPartParams& pp, const SegView& S, int64_t group,
+                                                         uint32_t m, uint32_t* cursor, uint32_t* ws) {
+  const KParams& p = pp.base;
+  const int lane = threadIdx.x & 63;
+  uint32_t* wcnt = ws;                                          // per run: count, then local start
+  int32_t* wdelta = reinterpret_cast<int32_t*>(ws + 64);        // per run: global position - local start
+  uint8_t* bkt = reinterpret_cast<uint8_t*>(ws + 128);          // per staged record: its run
+  int32_t key[16];
+  part_keys<H>(p, S, group, key);
+  const KCol& c = S.cols[pp.stream_col[0]];
+  uint32_t ids[16];
+  decode_group<H>(c.fwd, c.bits, group, ids);
+  int64_t v[16];
+  if (c.dkey) {
+    gmem<int64_t>* __restrict__ dk = gp(c.dkey);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dk[ids[i]] : pp.pack_min;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = c.key_base + (int64_t)ids[i];
+  }
+  using Word = typename std::conditional<W64, uint64_t, uint32_t>::type;
+  Word word[16];
+  uint32_t run[16];
+  if (!W64) {
+    const int cbits = pp.pshift + pp.cshift;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      run[i] = (uint32_t)key[i] >> cbits;
+      word[i] = (Word)((uint32_t)(key[i] & ((1 << cbits) - 1)) | ((uint32_t)(v[i] - pp.pack_min) << cbits));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t hk = part_hash((uint32_t)key[i]);
+      run[i] = hpart(pp, hk) >> pp.cshift;
+      word[i] = (Word)((uint64_t)hk | ((uint64_t)(uint32_t)v[i] << 32));
+    }
+  }
+  wcnt[lane] = 0u;
+  wave_sync();
+  uint32_t rank[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) rank[i] = ((m >> i) & 1u) ? atomicAdd(&wcnt[run[i]], 1u) : 0u;
+  wave_sync();
+  const uint32_t cnt = wcnt[lane];
+  const uint32_t g = cnt ? atomicAdd(&cursor[lane], cnt) : 0u;  // run `lane`'s positions in the workgroup's run
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  const uint32_t excl = incl - cnt;
+  const uint32_t total = __shfl(incl, 63);
+  wdelta[lane] = (int32_t)(g - excl);
+  wcnt[lane] = excl;
+  wave_sync();
+  Word* words = reinterpret_cast<Word*>(ws + 128 + 256);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((m >> i) & 1u) {
+      const uint32_t slot = wcnt[run[i]] + rank[i];
+      bkt[slot] = (uint8_t)run[i];
+      words[slot] = word[i];
+    }
+  wave_sync();
+  Word* __restrict__ out = W64 ? reinterpret_cast<Word*>(pp.mid_val) : reinterpret_cast<Word*>(pp.mid_key);
+  for (uint32_t s = lane; s < total; s += 64) out[(uint32_t)((int32_t)s + wdelta[bkt[s]])] = words[s];
+  wave_sync();  // the region is free for the next half-group
+}
+
 template <int H>
 __device__ __forceinline__ void part_count_half(const KPartParams& pp, const SegView& S, int64_t group, uint32_t m,
                                                 uint32_t* hist) {
@@ -199,14 +293,19 @@ __device__ __forceinline__ void part_count_half(const KPartParams& pp, const Seg
     if ((m >> i) & 1u) atomicAdd(&hist[pp.hashed ? hpart(pp, part_hash((uint32_t)key[i])) : (uint32_t)key[i] >> pp.pshift], 1u);
 }
 
-// K8a (SCATTER = false) / K8c (SCATTER = true).  LDS: [num_parts u32 histogram / cursors] [filter stack].
-template <bool SCATTER>
+// K8a (SCATTER = false) / K8c (SCATTER = true; STAGE 0: each record stored from its lane, 1 / 2: the u32 / u64
+// one-word records staged per wave, part_scatter_half_staged).  LDS: [u32 histogram of num_parts (K8a) / cursors of
+// num_coarse (K8c)] [filter stack] and, staged, from u32 word pp.stage_off one region of kStageWaveWords32 / 64 words
+// per wave (part_pass_lds).
+template <bool SCATTER, int STAGE = 0>
 __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const KParams& p = pp.base;
   const int tid = threadIdx.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
-  uint32_t* stack = hist + ((pp.num_parts + 3) & ~3);
+  uint32_t* stack = hist + (((SCATTER ? pp.num_coarse : pp.num_parts) + 3) & ~3);
+  uint32_t* ws = reinterpret_cast<uint32_t*>(lds) + pp.stage_off +
+                 (tid >> 6) * (STAGE == 2 ? kStageWaveWords64 : kStageWaveWords32);
   // Deadline: the flag expand_tiles_kernel set when the query's end time had passed before this launch.  Every
   // pass reads it at its start and it cannot change while they run, so K8c scatters exactly the docs K8a counted
   // (its cursors run inside K8a's reservations) or nothing, like K8e / K8d.
@@ -241,7 +340,10 @@ __global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp)
     mask = eval_filter(p, S, gclamp, mask, stack);
     matched += __popc(mask);
     if (!__any(mask != 0u)) continue;
-    if (SCATTER) {
+    if (SCATTER && STAGE) {
+      if (__any((mask & 0xFFFFu) != 0u)) part_scatter_half_staged<0, STAGE == 2>(pp, S, gclamp, mask & 0xFFFFu, hist, ws);
+      if (__any((mask >> 16) != 0u)) part_scatter_half_staged<16, STAGE == 2>(pp, S, gclamp, mask >> 16, hist, ws);
+    } else if (SCATTER) {
       if (__any((mask & 0xFFFFu) != 0u)) part_scatter_half<0>(pp, S, gclamp, mask & 0xFFFFu, hist);
       if (__any((mask >> 16) != 0u)) part_scatter_half<16>(pp, S, gclamp, mask >> 16, hist);
     } else {
@@ -539,6 +641,10 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
   __shared__ uint32_t pending;
   __shared__ uint32_t wave_tot[kBlock / 64];
   __shared__ unsigned long long blk_base;
+  // this partition's range of every slot's words over all rounds (order-preserving u64: min at [s], max at [ns + s])
+  __shared__ unsigned long long blk_mm[2 * kMaxSlots];
+  if (pp.out_mm)
+    for (int i = tid; i < 2 * ns; i += kBlock) blk_mm[i] = i < ns ? ~0ull : 0ull;
   const uint32_t r0 = pp.part_start[blockIdx.x];
   uint32_t n = pp.part_start[blockIdx.x + 1] - r0;
   const int64_t cap = pp.rec_cap;
@@ -637,30 +743,101 @@ __global__ __launch_bounds__(kBlock) void part_hash_aggregate_kernel(const KPart
     __syncthreads();
     uint64_t at = blk_base;
     for (int w = 0; w < (tid >> 6); ++w) at += wave_tot[w];
+    // the slot ranges of the groups written, tracked in registers while writing them when there are few slots (the
+    // compact result's widths; order-preserving u64), else by a pass over the table below
+    constexpr int kMmRegs = 4;
+    const bool mm_regs = pp.out_mm && ns <= kMmRegs;
+    unsigned long long rlo[kMmRegs], rhi[kMmRegs];
+#pragma unroll
+    for (int s = 0; s < kMmRegs; ++s) {
+      rlo[s] = ~0ull;
+      rhi[s] = 0ull;
+    }
     for (int i0 = 0; i0 < S; i0 += kBlock) {
       const int i = i0 + tid;
       const bool occ = i < S && keys[i] != ~0u;
       const uint64_t bal = __ballot(occ);
       if (occ) {
         const uint64_t r = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
-        if (r < (uint64_t)pp.out_cap) {  // past it: counted, not written; finalize reports the overflow
-          uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
-          o[0] = (uint64_t)(keys[i] * kHashInv);  // the composite key back from its hash
-          if (cs) {
-            const uint64_t w = lds[i], c = w >> 40;
+        uint64_t* o = pp.out_rec + r * (uint64_t)(1 + ns);
+        const bool in_cap = r < (uint64_t)pp.out_cap;  // past it: counted, not written; finalize reports the overflow
+        if (in_cap) o[0] = (uint64_t)(keys[i] * kHashInv);  // the composite key back from its hash
+        if (cs) {
+          const uint64_t w = lds[i], c = w >> 40;
+          const uint64_t sum = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)c * pp.pack_min);
+          if (in_cap) {
             o[1] = c;
-            o[2] = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)c * pp.pack_min);
-          } else {
-            for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
+            o[2] = sum;
           }
+          rlo[0] = min(rlo[0], (unsigned long long)(c ^ (1ull << 63)));
+          rhi[0] = max(rhi[0], (unsigned long long)(c ^ (1ull << 63)));
+          rlo[1] = min(rlo[1], (unsigned long long)(sum ^ (1ull << 63)));
+          rhi[1] = max(rhi[1], (unsigned long long)(sum ^ (1ull << 63)));
+        } else if (mm_regs) {
+#pragma unroll
+          for (int s = 0; s < kMmRegs; ++s)
+            if (s < ns) {
+              const uint64_t w = lds[(int64_t)s * S + i];
+              if (in_cap) o[1 + s] = w;
+              rlo[s] = min(rlo[s], (unsigned long long)(w ^ (1ull << 63)));
+              rhi[s] = max(rhi[s], (unsigned long long)(w ^ (1ull << 63)));
+            }
+        } else if (in_cap) {
+          for (int s = 0; s < ns; ++s) o[1 + s] = lds[(int64_t)s * S + i];
         }
       }
       at += (uint64_t)__popcll(bal);
+    }
+    if (mm_regs) {
+#pragma unroll
+      for (int s = 0; s < kMmRegs; ++s) {
+        if (s >= ns) continue;
+        unsigned long long lo = rlo[s], hi = rhi[s];
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long a = (unsigned long long)__shfl_xor((long long)lo, o);
+          const unsigned long long b = (unsigned long long)__shfl_xor((long long)hi, o);
+          lo = a < lo ? a : lo;
+          hi = b > hi ? b : hi;
+        }
+        if (lane == 0) {
+          atomicMin(&blk_mm[s], lo);
+          atomicMax(&blk_mm[ns + s], hi);
+        }
+      }
+    } else if (pp.out_mm) {  // many slots: per slot a pass over the round's entries, per wave one LDS atomic each
+      for (int s = 0; s < ns; ++s) {
+        unsigned long long lo = ~0ull, hi = 0ull;
+        for (int i = tid; i < S; i += kBlock) {
+          if (keys[i] == ~0u) continue;
+          uint64_t w;
+          if (cs) {
+            const uint64_t x = lds[i], c = x >> 40;
+            w = s == 0 ? c : (uint64_t)((int64_t)(x & ((1ull << 40) - 1)) + (int64_t)c * pp.pack_min);
+          } else {
+            w = lds[(int64_t)s * S + i];
+          }
+          const unsigned long long o = w ^ (1ull << 63);
+          lo = o < lo ? o : lo;
+          hi = o > hi ? o : hi;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long a = (unsigned long long)__shfl_xor((long long)lo, o);
+          const unsigned long long b = (unsigned long long)__shfl_xor((long long)hi, o);
+          lo = a < lo ? a : lo;
+          hi = b > hi ? b : hi;
+        }
+        if (lane == 0) {
+          atomicMin(&blk_mm[s], lo);
+          atomicMax(&blk_mm[ns + s], hi);
+        }
+      }
     }
     __syncthreads();
     n = pending;
     __syncthreads();
   }
+  if (pp.out_mm)
+    for (int i = tid; i < 2 * ns; i += kBlock) pp.out_mm[(int64_t)blockIdx.x * 2 * ns + i] = blk_mm[i];
 }
 
 }  // namespace pgpu

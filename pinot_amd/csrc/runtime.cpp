@@ -544,7 +544,8 @@ struct Scratch {
   DevBuf leap_maps, mask_jobs, leaf_masks;  // numEntriesScannedInFilter: LEAP2 maps, GENERIC leaf bitmaps
   DevBuf xcursor;                       // cross-GPU exchange: per-owner record cursors
   DevBuf xsend, xrecv, xshard;          // pgpu_plan_combine: exported / received records, the reduce-scattered shard
-  DevBuf hsort;                         // hash-mode finalize: sort keys / indexes, decoded columns, sort temp
+  DevBuf hsort;                         // hash-mode finalize: the decoded columns / compact form
+  DevBuf part_mm;                       // hashed partitions: each partition's slot ranges (KPartParams.out_mm)
   HostPinned xstage;                    // their initial values (pinned: the upload is asynchronous)
   // Pinned staging: `stage` is the source of the execution's asynchronous uploads (records, bitsets); `readback`
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
@@ -572,7 +573,7 @@ struct Scratch {
     part_start.release(); block_off.release(); rec_key.release(); rec_val.release(); stage_keys.release();
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
-    xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release(); hsort.release();
+    xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release(); hsort.release(); part_mm.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -1130,6 +1131,7 @@ struct pgpu_plan_s {
   int64_t set_words_bound = 0;            // streamed plans: upper bound of the SET bitset words
   int64_t tile_bound = 0;                 // streamed plans: upper bound of the tiles
   int part_shift = 0, num_parts = 0, part_grid = 0;
+  int part_grid_staged[2] = {0, 0};  // the grid when K8c runs staged (u32 / u64 records): set at the first execution
   size_t part_lds = 0;
   std::vector<int32_t> stream_col, stream_f64, slot_stream;
   bool part_val32 = false;  // KPartParams.val32
@@ -1890,6 +1892,17 @@ void hash_part_bits(int64_t groups, int nslots, int* pbits, int* sbits) {
   *sbits = sb;
 }
 
+// Coarse runs of the two-level scatter: 2^cshift consecutive partitions each, at most 64 (KPartParams.cshift).
+int part_coarse_shift(int num_parts) {
+  int cshift = 0;
+  while ((num_parts + (1 << cshift) - 1) >> cshift > 64) ++cshift;
+  return cshift;
+}
+int part_coarse_runs(int num_parts) {
+  const int cshift = part_coarse_shift(num_parts);
+  return (num_parts + (1 << cshift) - 1) >> cshift;
+}
+
 // A cached hashed-partition plan re-shaped for the groups its last execution found (plan_cache_get): the partition
 // count, the pass kernels' LDS and grid follow.
 void hash_part_resize(pgpu_plan_s* P, int64_t groups) {
@@ -1903,7 +1916,8 @@ void hash_part_resize(pgpu_plan_s* P, int64_t groups) {
   P->part_sbits = sbits;
   P->num_parts = (int)parts;
   P->part_lds = pass_lds;
-  int per_cu = occupancy_part_pass(pass_lds);
+  P->part_grid_staged[0] = P->part_grid_staged[1] = 0;
+  int per_cu = occupancy_part_pass(pass_lds, (int)parts, part_coarse_runs((int)parts), 0);
   per_cu = std::max(1, std::min(per_cu, 4));
   P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(P->num_tiles, (int64_t)P->table->num_cus * per_cu));
 }
@@ -2727,7 +2741,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           }
         }
         P->part_lds = pass_lds;
-        int per_cu = occupancy_part_pass(pass_lds);
+        int per_cu = occupancy_part_pass(pass_lds, (int)parts, part_coarse_runs((int)parts), 0);
         per_cu = std::max(1, std::min(per_cu, 4));
         P->part_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tile_base, (int64_t)t->num_cus * per_cu));
       }
@@ -3320,10 +3334,9 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     for (int sl = 0; sl < nslots; ++sl) pp.slot_stream[sl] = P->slot_stream[sl];
     const int64_t cap = std::max<int64_t>(P->total_docs, 1);
     TRY(sc->part_start.ensure((size_t)(P->num_parts + 1) * 4));
-    int cshift = 0;
-    while ((P->num_parts + (1 << cshift) - 1) >> cshift > 64) ++cshift;
+    const int cshift = part_coarse_shift(P->num_parts);
     pp.cshift = cshift;
-    pp.num_coarse = (P->num_parts + (1 << cshift) - 1) >> cshift;
+    pp.num_coarse = part_coarse_runs(P->num_parts);
     pp.chunks_per_coarse = std::max(1, 1024 / pp.num_coarse);
     {  // K8e batch: as many records as fit 96 KB of LDS beside the per-partition counters, a multiple of kBlock
       const int kb = P->part_hash ? 4 : 2;  // staged key bytes
@@ -3331,7 +3344,6 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       const int64_t b = (96 * 1024 - fixed) / (8 * pp.num_streams + 4 + kb) / kBlock * kBlock;
       pp.split_batch = (int)std::max<int64_t>(kBlock, std::min<int64_t>(kSplitBatch, b));
     }
-    TRY(sc->block_off.ensure((size_t)P->part_grid * pp.num_coarse * 4));
     TRY(sc->coarse_fill.ensure((size_t)pp.num_coarse * 4));
     TRY(sc->fine_fill.ensure((size_t)P->num_parts * 4));
     if (cshift > 0) {
@@ -3358,13 +3370,14 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       pp.out_rec = sc->ckeys.as<uint64_t>();
       pp.out_count = sc->counter.as<unsigned long long>();
       pp.out_cap = ocap;
+      TRY(sc->part_mm.ensure((size_t)P->num_parts * 2 * nslots * 8));
+      pp.out_mm = sc->part_mm.as<unsigned long long>();
       P->part_hash_live = true;
     } else {
       TRY(sc->rec_key.ensure((size_t)cap * 2));
     }
     TRY(sc->rec_val.ensure(std::max<size_t>((size_t)cap * 8 * pp.num_streams, 8)));
     pp.part_start = sc->part_start.as<uint32_t>();
-    pp.block_off = sc->block_off.as<uint32_t>();
     pp.rec_key = sc->rec_key.as<uint16_t>();
     pp.rec_val = sc->rec_val.as<uint64_t>();
     pp.rec_cap = cap;
@@ -3397,7 +3410,24 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
         pp.pack_range = P->part_pack_range;
       }
     }
-    if (launch_partitioned(pp, P->part_grid, P->part_lds, stream))
+    int grid = P->part_grid;
+#ifndef PGPU_PART_NO_STAGE  // (defined only by an A/B build of the library: every record stored from its lane)
+    // one-word records with <= 64 coarse runs: K8c stages each wave's records by run in LDS and stores them in runs;
+    // the grid (K8a's too) follows that instance's occupancy
+    pp.staged = pp.cshift > 0 && pp.num_coarse <= 64 ? (pp.pack_bits > 0 ? 1 : pp.mid_pair ? 2 : 0) : 0;
+    if (pp.staged) {
+      if (P->part_grid_staged[pp.staged - 1] <= 0) {
+        const int per_cu =
+            std::max(1, std::min(occupancy_part_pass(P->part_lds, P->num_parts, pp.num_coarse, pp.staged), 4));
+        P->part_grid_staged[pp.staged - 1] =
+            (int)std::max<int64_t>(1, std::min<int64_t>(P->num_tiles, (int64_t)P->table->num_cus * per_cu));
+      }
+      grid = P->part_grid_staged[pp.staged - 1];
+    }
+#endif
+    TRY(sc->block_off.ensure((size_t)grid * pp.num_coarse * 4));
+    pp.block_off = sc->block_off.as<uint32_t>();
+    if (launch_partitioned(pp, grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
     const int rc = launch_filter_groupby(kp, P->mode,
@@ -3703,8 +3733,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     const bool want_compact = P->stage_end.empty() && !no_compact_h;
     TRY(sc->counter.ensure(64 + (size_t)kMaxSlots * 16));  // (no regrowth: the first allocation is 4 KB)
     unsigned long long* d_mm = reinterpret_cast<unsigned long long*>(sc->counter.as<uint8_t>() + 64);
-    if (want_compact && launch_hash_minmax(sc->ckeys.as<uint64_t>(), sc->counter.as<unsigned long long>(), cap, nslots,
-                                           d_mm, stream))
+    if (want_compact &&
+        (k8h ? launch_hash_minmax_parts(sc->part_mm.as<unsigned long long>(), P->num_parts, nslots, d_mm, stream)
+             : launch_hash_minmax(sc->ckeys.as<uint64_t>(), sc->counter.as<unsigned long long>(), cap, nslots, d_mm,
+                                  stream)))
       return fail(PGPU_ERR_DEVICE, "slot range launch failed: %s", hipGetErrorString(hipGetLastError()));
     TRY(sc->readback.ensure(64 + (size_t)nslots * 16));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
@@ -3725,18 +3757,17 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     if (P->groups_seen && P->merged_records < 0) P->groups_seen->store(n, std::memory_order_relaxed);
     static const bool host_sort = getenv_flag("PGPU_HASH_HOST_SORT");  // A/B: sort and decode on the host
     if (n >= 4096 && P->stage_end.empty() && !host_sort) {
-      // sorted by key on the device (k_hashsort.hip), held in compact form when that moves fewer bytes
+      // Decoded on the device in one streaming pass over the records, in their (hash / partition) order -- the
+      // LONG_MAP holder's iteration order is fastutil's hash order (DictionaryBasedGroupKeyGenerator.java:693, :719)
+      // and no consumer depends on group order -- held in compact form when that moves fewer bytes (C5-sized
+      // results: 10M groups): composite keys at 4 or 8 bytes instead of the decoded dictIds, and each slot at the
+      // narrowest width of its range (as the dense compact form); the host decodes it on first access
+      // (result_expand).
       int key_bits = 1;
       {
         const long double space = (long double)P->key_stride[nk - 1] * (long double)P->key_card[nk - 1];
         while (key_bits < 64 && (long double)(INT64_C(1) << key_bits) < space) ++key_bits;
       }
-      size_t tmp_bytes = 0;
-      if (hash_sort_temp_bytes(n, key_bits, &tmp_bytes))
-        return fail(PGPU_ERR_DEVICE, "hash sort sizing failed: %s", hipGetErrorString(hipGetLastError()));
-      // Compact form when it moves fewer bytes (C5-sized results: 10M groups): sorted composite keys at 4 or 8
-      // bytes instead of the decoded dictIds, and each slot at the narrowest width of its range (as the dense
-      // compact form); the host decodes it on first access (result_expand).
       const int32_t key_width = key_bits <= 32 ? 4 : 8;
       std::vector<int32_t> width(nslots, 8);
       std::vector<int64_t> woff(nslots, 0);
@@ -3748,16 +3779,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
         cbytes += ((size_t)n * width[s2] + 7) & ~size_t(7);
       }
       if (want_compact && cbytes < (size_t)n * (4 * nk + 8 * nslots)) {
-        const size_t a = ((size_t)n * 8 + 255) & ~size_t(255), b = ((size_t)n * 4 + 255) & ~size_t(255);
-        const size_t ob = (cbytes + 255) & ~size_t(255);
-        TRY(sc->hsort.ensure(2 * a + 2 * b + ob + tmp_bytes + 256));
-        uint8_t* base = sc->hsort.as<uint8_t>();
-        uint8_t* out = base + 2 * a + 2 * b;
-        if (launch_hash_sort_compact(sc->ckeys.as<uint64_t>(), n, nslots, key_bits, key_width, width.data(),
-                                     woff.data(), out + ob, tmp_bytes, reinterpret_cast<uint64_t*>(base),
-                                     reinterpret_cast<uint64_t*>(base + a), reinterpret_cast<uint32_t*>(base + 2 * a),
-                                     reinterpret_cast<uint32_t*>(base + 2 * a + b), out, stream))
-          return fail(PGPU_ERR_DEVICE, "hash sort / compact launch failed: %s", hipGetErrorString(hipGetLastError()));
+        TRY(sc->hsort.ensure(cbytes + 256));
+        uint8_t* out = sc->hsort.as<uint8_t>();
+        if (launch_hash_compact(sc->ckeys.as<uint64_t>(), n, nslots, key_width, width.data(), woff.data(), out, stream))
+          return fail(PGPU_ERR_DEVICE, "hash compact launch failed: %s", hipGetErrorString(hipGetLastError()));
         R->num_keys = nk;
         R->num_slots = nslots;
         R->n = n;
@@ -3776,30 +3801,14 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       }
     }
     if (n >= 4096 && P->stage_end.empty() && !host_sort) {
-      // sorted by key and decoded into the columnar result on the device: one copy back
-      int key_bits = 1;
-      {
-        const long double space = (long double)P->key_stride[nk - 1] * (long double)P->key_card[nk - 1];
-        while (key_bits < 64 && (long double)(INT64_C(1) << key_bits) < space) ++key_bits;
-      }
-      size_t tmp_bytes = 0;
-      if (hash_sort_temp_bytes(n, key_bits, &tmp_bytes))
-        return fail(PGPU_ERR_DEVICE, "hash sort sizing failed: %s", hipGetErrorString(hipGetLastError()));
+      // decoded into the columnar result on the device: one copy back
       const size_t slot_off = pgpu_result_s::slot_offset(nk, n);
       const size_t out_bytes = slot_off + (size_t)nslots * n * 8;
-      const size_t a = ((size_t)n * 8 + 255) & ~size_t(255), b = ((size_t)n * 4 + 255) & ~size_t(255);
-      const size_t ob = (out_bytes + 255) & ~size_t(255);
-      TRY(sc->hsort.ensure(2 * a + 2 * b + ob + tmp_bytes + 256));
-      uint8_t* base = sc->hsort.as<uint8_t>();
-      uint64_t* keys_a = reinterpret_cast<uint64_t*>(base);
-      uint64_t* keys_b = reinterpret_cast<uint64_t*>(base + a);
-      uint32_t* idx_a = reinterpret_cast<uint32_t*>(base + 2 * a);
-      uint32_t* idx_b = reinterpret_cast<uint32_t*>(base + 2 * a + b);
-      uint8_t* out = base + 2 * a + 2 * b;
-      if (launch_hash_sort_decode(sc->ckeys.as<uint64_t>(), n, nslots, nk, P->key_stride.data(), P->key_card.data(),
-                                  P->key_off.data(), key_bits, out + ob, tmp_bytes, keys_a, keys_b, idx_a, idx_b, out,
-                                  slot_off, stream))
-        return fail(PGPU_ERR_DEVICE, "hash sort / decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+      TRY(sc->hsort.ensure(out_bytes + 256));
+      uint8_t* out = sc->hsort.as<uint8_t>();
+      if (launch_hash_decode(sc->ckeys.as<uint64_t>(), n, nslots, nk, P->key_stride.data(), P->key_card.data(),
+                             P->key_off.data(), out, slot_off, stream))
+        return fail(PGPU_ERR_DEVICE, "hash decode launch failed: %s", hipGetErrorString(hipGetLastError()));
       TRY(R->alloc(nk, nslots, n));
       HIP_TRY(hipMemcpyAsync(R->buf.p, out, out_bytes, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
@@ -3906,7 +3915,7 @@ int pgpu::result_expand(pgpu_result_s* R) {
   const int nk = R->num_keys, ns = R->num_slots;
   const int64_t n = R->n;
   TRY(R->alloc(nk, ns, n));
-  if (R->ckey_width) {  // sorted composite keys (hash-mode results): decode each row's key
+  if (R->ckey_width) {  // composite keys (hash-mode results): decode each row's key
     const uint8_t* kb = reinterpret_cast<const uint8_t*>(R->cbuf.p);
     constexpr int64_t kRowsPerTask = 1 << 20;
     const int64_t ktasks = (n + kRowsPerTask - 1) / kRowsPerTask;

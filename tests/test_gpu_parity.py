@@ -446,6 +446,8 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
                     "SELECT MIN(n), MAX(n), SUM(n) FROM t GROUP BY k1, k2, k3",
                     "SELECT SUM(n), MIN(n), MAX(m), COUNT(*) FROM t GROUP BY k1, k2, k3",
                     "SELECT SUM(l), MAX(l), MIN(n), COUNT(*) FROM t GROUP BY k1, k2, k3",
+                    # packed records of filtered docs: K8c's staged write-out with partial lane masks
+                    "SELECT SUM(m), COUNT(*) FROM t WHERE q < 0 OR m > 900 GROUP BY k1, k2, k3",
                     "SELECT COUNT(*) FROM t GROUP BY k1, k2, k3"):  # no value stream at all
             qi = parse_query(sql, num_groups_limit=10 ** 7)
             assert_same(t.execute_groupby(hs, qi),

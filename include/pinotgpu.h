@@ -93,6 +93,35 @@ int pgpu_table_create(int device, int num_columns, const char* const* column_nam
                       pgpu_table* out);
 int pgpu_table_destroy(pgpu_table table);
 
+/* Executor settings of a table: what a Pinot server's configuration sets.  The JNI shim maps its
+ * pinot.server.query.executor.gpu.* keys (PinotConfiguration, as InstancePlanMakerImplV2 reads its
+ * max.execution.threads / num.groups.limit / min.segment.group.trim.size keys, InstancePlanMakerImplV2.java:75-110)
+ * onto these fields; INTEGRATION.md lists the mapping.  pgpu_config_default fills every field with the library's
+ * default, which a new table starts with.  Settings apply to plans made after pgpu_table_set_config (the table's
+ * compiled-plan cache is cleared); a plan already made keeps the settings it was planned with. */
+typedef struct {
+  int32_t struct_size;            /* sizeof(pgpu_config) as the caller compiled it: later fields keep their defaults */
+  int32_t plan_cache;             /* 1 (default): a repeated query (same bytes, same segments) reuses its compiled
+                                     plan; 0: every query is planned afresh (pgpu_query.options can opt out per query) */
+  int32_t partitioned_group_by;   /* 1 (default): dense key spaces whose table is >= 32 MB are radix-partitioned and
+                                     aggregated per partition in LDS (K8a-K8d); 0: global atomics into the table */
+  int32_t hash_partitions;        /* 1 (default): key spaces past every dense table and below 2^31 are aggregated by
+                                     hashed partitions (K8h, LDS hash tables); 0: the global hash table */
+  int32_t hash_partition_bits;    /* most partition bits of hashed partitions, 0..14 (default 14) */
+  int32_t hash_partition_lds_kb;  /* LDS of one hashed partition's table, KB, 1..128 (default 0: 20 KB-class tables) */
+  int32_t lds_table_kb;           /* largest group table privatised in LDS per workgroup, KB (default 112) */
+  int32_t plan_chunk_segments;    /* segments per host planning task (default 4096) */
+  int32_t stream_chunks;          /* scan launches of pgpu_plan_create_execute's streamed plan (default 1) */
+  int32_t compact_results;        /* 1 (default): large results cross PCIe in the compact form (presence bitmap /
+                                     keys + narrowed slot words) and are decoded on first access; 0: columnar */
+  int32_t star_tree_workgroups;   /* workgroups of the star-tree document scan (default 0: the library's choice) */
+  double dense_selectivity;       /* estimated selectivity from which plans take the dense scan instance
+                                     (default 0.25; > 1 = never) */
+} pgpu_config;
+int pgpu_config_default(pgpu_config* out);
+int pgpu_table_set_config(pgpu_table table, const pgpu_config* config);
+int pgpu_table_get_config(pgpu_table table, pgpu_config* out);
+
 /* One column of an ImmutableSegment as Pinot holds it in memory (PinotDataBuffer views; the JNI shim takes the
  * addresses from PinotDataBuffer.toDirectByteBuffer, segspi/memory/PinotDataBuffer.java:382). */
 typedef struct {

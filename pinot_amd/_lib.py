@@ -109,6 +109,19 @@ class StarTreeDescC(ctypes.Structure):
                 ("metric_f64", ctypes.POINTER(c_f64p)), ("metric_i64", ctypes.POINTER(c_i64p))]
 
 
+class ConfigC(ctypes.Structure):
+    """pgpu_config (include/pinotgpu.h): a table's executor settings."""
+    _fields_ = [("struct_size", ctypes.c_int32), ("plan_cache", ctypes.c_int32),
+                ("partitioned_group_by", ctypes.c_int32), ("hash_partitions", ctypes.c_int32),
+                ("hash_partition_bits", ctypes.c_int32), ("hash_partition_lds_kb", ctypes.c_int32),
+                ("lds_table_kb", ctypes.c_int32), ("plan_chunk_segments", ctypes.c_int32),
+                ("stream_chunks", ctypes.c_int32), ("compact_results", ctypes.c_int32),
+                ("star_tree_workgroups", ctypes.c_int32), ("dense_selectivity", ctypes.c_double)]
+
+
+CONFIG_FIELDS = [f for f, _ in ConfigC._fields_ if f != "struct_size"]
+
+
 class PinotGpuError(RuntimeError):
     def __init__(self, code, message):
         super().__init__("pgpu error %d: %s" % (code, message))
@@ -142,6 +155,9 @@ _PROTOS = {
     "pgpu_last_error": (c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pgpu_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "pgpu_table_create": (c_int, [c_int, c_int, c_char_pp, c_i32p, ctypes.POINTER(c_voidp)]),
+    "pgpu_config_default": (c_int, [ctypes.POINTER(ConfigC)]),
+    "pgpu_table_set_config": (c_int, [c_voidp, ctypes.POINTER(ConfigC)]),
+    "pgpu_table_get_config": (c_int, [c_voidp, ctypes.POINTER(ConfigC)]),
     "pgpu_table_destroy": (c_int, [c_voidp]),
     "pgpu_pin_segment": (c_int, [c_voidp, ctypes.POINTER(SegmentDesc), c_i64p]),
     "pgpu_unpin_segment": (c_int, [c_voidp, c_i64]),

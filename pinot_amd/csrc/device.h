@@ -857,8 +857,14 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? load_off(dv, ids[i] << 3) : 0.0;
 #else
       gmem<double>* __restrict__ dv = gp(c.dval);
+#ifdef PGPU_DIAG_NO_DVAL_GATHER  // diagnostic build only (wrong sums): the dictionary gathers' share of the traffic
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? (double)ids[i] : 0.0;
+      (void)dv;
+#else
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;
+#endif
 #endif
       for (int r = s; r < e; ++r) {
         if (p.slot_kind[r] != SLOT_SUM_F64) continue;

@@ -50,7 +50,7 @@ using namespace pgpu;
 // ================================================================================================ errors
 namespace {
 
-// PGPU_CRASH_TRACE=1 (diagnostics): on SIGSEGV / SIGBUS / SIGABRT print the faulting address and the native frames
+// PGPU_TRACE=crash (diagnostics): on SIGSEGV / SIGBUS / SIGABRT print the faulting address and the native frames
 // (backtrace_symbols_fd: object, symbol or offset -- resolve offsets with addr2line -f -C -e <object>), then hand the
 // signal to the previously installed handler (Python's faulthandler prints the Python stacks).
 struct sigaction g_prev_segv, g_prev_bus, g_prev_abrt;
@@ -80,10 +80,22 @@ void crash_trace_handler(int sig, siginfo_t* si, void* uc) {
   signal(sig, SIG_DFL);
   raise(sig);
 }
+// Diagnostics: PGPU_TRACE, the one environment variable the library reads -- comma-separated words, none of which
+// changes a result: "1" (per-phase host times of every plan, execution and finalize on stderr), "crash" (on
+// SIGSEGV / SIGBUS / SIGABRT print the native frames), "check" (a scan launch's records and tile map are read back
+// and checked before the launch), "serialize" (entry points run one at a time: isolates host races from device ones).
+// Executor settings are pgpu_config's (pgpu_table_set_config), never the environment.
+bool diag(const char* word) {
+  static const std::string v = [] {
+    const char* e = getenv("PGPU_TRACE");
+    return "," + std::string(e ? e : "") + ",";
+  }();
+  return v.find("," + std::string(word) + ",") != std::string::npos;
+}
+
 struct CrashTraceInstaller {
   void install() {
-    const char* v = getenv("PGPU_CRASH_TRACE");
-    if (!v || v[0] != '1') return;
+    if (!diag("crash")) return;
     void* warm[2];
     backtrace(warm, 2);  // loads the unwinder now, not inside the handler
     struct sigaction sa;
@@ -107,12 +119,8 @@ void install_crash_trace() {
 thread_local std::string g_err;
 
 // PGPU_TRACE=1: per-phase host timings on stderr (diagnostics only).
-bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] == '1';
-}
 bool trace_on() {
-  static const bool on = getenv("PGPU_TRACE") && getenv("PGPU_TRACE")[0] == '1';
+  static const bool on = diag("1");
   return on;
 }
 double now_us() {
@@ -293,22 +301,19 @@ HostPool& host_pool() {
 }
 // Segments per planning task.  Measured on MI355X hosts: translating the 1000 segments of C3 takes ~90 us on one
 // thread, and waking pool workers costs more than it saves below a few thousand segments, so lists shorter than
-// this are planned on the calling thread.  PGPU_PLAN_CHUNK_SEGS overrides it (tests).
+// this are planned on the calling thread.  pgpu_config.plan_chunk_segments sets it (tests).
 // Launches of a streamed plan: equal chunks, so every launch of the scan kernel covers the same work (the
 // roofline's per-launch bytes and rocprof's average launch agree).  Measured on MI355X (C3, 1000 segments): four
 // streamed launches took 1.115 ms per query against 0.950 ms for one -- each launch boundary costs the scan's
 // ramp and tail (~33 us) plus the in-stream record upload, more than the ~130 us of planning it hides -- so plans
-// run as one launch unless PGPU_STREAM_CHUNKS asks for more (tests exercise the streamed path with it).
-int stream_chunk_count(size_t nseg) {
-  const char* v = getenv("PGPU_STREAM_CHUNKS");
-  if (v && atoi(v) > 0) return std::min<int>(atoi(v), (int)std::max<size_t>(nseg, 1));
+// run as one launch unless pgpu_config.stream_chunks asks for more (tests exercise the streamed path with it).
+int stream_chunk_count(const pgpu_config& cfg, size_t nseg) {
+  if (cfg.stream_chunks > 1) return std::min<int>(cfg.stream_chunks, (int)std::max<size_t>(nseg, 1));
   return 1;
 }
 
-size_t plan_chunk_segs() {
-  const char* v = getenv("PGPU_PLAN_CHUNK_SEGS");
-  const long n = v ? atol(v) : 0;
-  return n > 0 ? (size_t)n : 4096;
+size_t plan_chunk_segs(const pgpu_config& cfg) {
+  return cfg.plan_chunk_segments > 0 ? (size_t)cfg.plan_chunk_segments : 4096;
 }
 
 // ================================================================================================ values
@@ -584,8 +589,30 @@ struct GenScratch {
 
 }  // namespace
 
+// pgpu_config_default: the library's settings (include/pinotgpu.h documents each field).
+pgpu_config default_config() {
+  pgpu_config c;
+  memset(&c, 0, sizeof c);
+  c.struct_size = (int32_t)sizeof(pgpu_config);
+  c.plan_cache = 1;
+  c.partitioned_group_by = 1;
+  c.hash_partitions = 1;
+  c.hash_partition_bits = 14;
+  c.hash_partition_lds_kb = 0;
+  c.lds_table_kb = 112;
+  c.plan_chunk_segments = 4096;
+  c.stream_chunks = 1;
+  c.compact_results = 1;
+  c.star_tree_workgroups = 0;
+  c.dense_selectivity = 0.25;
+  return c;
+}
+
 struct pgpu_table_s {
   int device = 0;
+  // executor settings (pgpu_table_set_config); plans copy them when they are made
+  mutable std::mutex cfg_mu;
+  pgpu_config cfg = default_config();
   std::vector<std::string> names;
   std::vector<int32_t> types;
   std::mutex mu;
@@ -1061,7 +1088,13 @@ struct StreamExec {
 
 }  // namespace
 
+pgpu_config table_config(const pgpu_table_s* t) {
+  std::lock_guard<std::mutex> g(t->cfg_mu);
+  return t->cfg;
+}
+
 struct pgpu_plan_s {
+  pgpu_config cfg = default_config();  // the table's settings when the plan was made
   pgpu_table_s* table = nullptr;
   std::vector<Segment*> segs;
   std::shared_ptr<PlanRefs> refs;         // keeps segs and the LUTs the records point at alive
@@ -1816,11 +1849,9 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 // The slot whose table word also carries the COUNT (KParams.pack_slot), or -1: the first integer SUM over a column
 // whose values are >= 0 in every segment, when `max_count` (the most docs one word can see) bounds both halves of the
 // word -- count < 2^(64 - shift), sum < 2^shift.  Not with star-tree segments (K6 keeps its own table layout).
-// PGPU_NO_PACK_COUNT=1: never (A/B).
 int32_t pack_slot_for(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_query* q, int64_t max_count,
                       int shift) {
-  static const bool off = getenv_flag("PGPU_NO_PACK_COUNT");
-  if (off || P->slot_kind.empty() || P->slot_kind[0] != SLOT_COUNT || shift <= 0 || shift >= 64) return -1;
+  if (P->slot_kind.empty() || P->slot_kind[0] != SLOT_COUNT || shift <= 0 || shift >= 64) return -1;
   if (max_count >= (INT64_C(1) << (64 - shift))) return -1;
   for (const Segment* s : P->segs)
     if (s->star && !(q->options & PGPU_OPT_NO_STAR_TREE)) return -1;
@@ -1863,10 +1894,9 @@ int32_t hash_pack_slot(const pgpu_table_s* t, const pgpu_plan_s* P, const pgpu_q
 }
 
 // Hashed partitions (KPartParams.hashed) for a MODE_HASH plan: single-stage keys whose composite key fits int32
-// (part_keys' arithmetic and the records' u32 keys).  PGPU_NO_PART_HASH=1: the global hash table (A/B).
+// (part_keys' arithmetic and the records' u32 keys), unless pgpu_config.hash_partitions is 0 (the global hash table).
 bool part_hash_eligible(const pgpu_plan_s* P, int64_t G) {
-  static const bool off = getenv_flag("PGPU_NO_PART_HASH");
-  return !off && P->mode == MODE_HASH && P->stage_end.empty() && G > 0 && G < (INT64_C(1) << 31) && P->key_bias == 0;
+  return P->cfg.hash_partitions && P->mode == MODE_HASH && P->stage_end.empty() && G > 0 && G < (INT64_C(1) << 31) && P->key_bias == 0;
 }
 
 // Hashed partitions' shape for `groups` expected groups: 2^pbits partitions (K8a / K8c's LDS histogram: at most
@@ -1874,14 +1904,14 @@ bool part_hash_eligible(const pgpu_plan_s* P, int64_t G) {
 // workgroups on a CU, so the tables are 2^10 entries at a load of at most ~0.6 and partitions are added first; past
 // kMaxParts partitions the tables grow, up to kHashPartLdsMax (more groups than that take further K8h rounds).
 // Measured on c5_hash (10^7 groups, r04, ms per query): 2^14 x 2^10 (20 KB) 3.69-3.72, 2^13 x 2^11 (40 KB)
-// 4.06-4.17, 2^13 x 2^12 (80 KB) 7.67, 2^14 x 2^12 11.7-12.7; the global hash table 14.8.  PGPU_PART_HASH_LDS_KB /
-// PGPU_PART_HASH_PBITS (read per plan: A/B, and tests that force K8h's extra rounds) cap the table bytes and the
+// 4.06-4.17, 2^13 x 2^12 (80 KB) 7.67, 2^14 x 2^12 11.7-12.7; the global hash table 14.8.  pgpu_config's
+// hash_partition_lds_kb / hash_partition_bits (tests force K8h's extra rounds with them) cap the table bytes and the
 // partition bits.
-void hash_part_bits(int64_t groups, int nslots, int* pbits, int* sbits) {
-  const char* lk = getenv("PGPU_PART_HASH_LDS_KB");
-  const int64_t lds_cap = lk && atoi(lk) > 0 ? std::min<int64_t>((int64_t)atoi(lk) * 1024, 128 * 1024) : kHashPartLdsMax;
-  const char* pb = getenv("PGPU_PART_HASH_PBITS");
-  const int max_pbits = pb && *pb ? std::max(0, std::min(14, atoi(pb))) : 14;
+void hash_part_bits(const pgpu_config& cfg, int64_t groups, int nslots, int* pbits, int* sbits) {
+  const int64_t lds_cap = cfg.hash_partition_lds_kb > 0
+                              ? std::min<int64_t>((int64_t)cfg.hash_partition_lds_kb * 1024, 128 * 1024)
+                              : kHashPartLdsMax;
+  const int max_pbits = std::max(0, std::min(14, cfg.hash_partition_bits));
   auto fits = [&](int p, int sb) { return (long double)groups <= 0.6L * (long double)(int64_t(1) << (p + sb)); };
   int sb = 10;
   while (sb > 8 && (int64_t)part_hash_lds(sb, nslots) > lds_cap) --sb;
@@ -1908,7 +1938,7 @@ int part_coarse_runs(int num_parts) {
 void hash_part_resize(pgpu_plan_s* P, int64_t groups) {
   const int nslots = (int)P->slot_kind.size();
   int pbits = 0, sbits = 0;
-  hash_part_bits(groups, nslots, &pbits, &sbits);
+  hash_part_bits(P->cfg, groups, nslots, &pbits, &sbits);
   const int64_t parts = int64_t(1) << pbits;
   const size_t pass_lds = (size_t)((parts + 3) & ~int64_t(3)) * 4 + (P->pure_and ? 0 : (size_t)kMaxStack * kBlock * 4);
   if (pass_lds > 96 * 1024) return;
@@ -1934,16 +1964,11 @@ int part_hash_overflow(const pgpu_plan_s* P, uint64_t groups) {
               (unsigned long long)groups, (long long)part_hash_out_cap(P));
 }
 
-// A/B knob: PGPU_DICT_GATHERS=1 keeps the LUT / dictionary lookups of consecutive-value dictionaries (KCol).
-bool dict_gathers_forced() {
-  static const bool on = getenv("PGPU_DICT_GATHERS") && getenv("PGPU_DICT_GATHERS")[0] == '1';
-  return on;
-}
-
 int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, const pgpu_query* q, pgpu_plan_s* P,
                      const StreamExec* se = nullptr) {
   if (!q) return fail(PGPU_ERR_INVALID_ARGUMENT, "null query");
   const double t_start = trace_on() ? now_us() : 0;
+  P->cfg = table_config(t);
   const int ncols = (int)t->names.size();
   // num_group_by == 0: aggregation-only (AggregationOperator, core/operator/query/AggregationOperator.java:58-95):
   // one accumulator row (key space G = 1), reduced per wave before any atomic.
@@ -2121,7 +2146,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         const Column& col = s->cols[c];
         P->refs->luts.push_back(col.lut);
         KeyLut& kl = P->key_lut[i * nk + j];
-        kl.lut = col.lut_off >= 0 && !dict_gathers_forced() ? nullptr : reinterpret_cast<const int32_t*>(col.lut->p);
+        kl.lut = col.lut_off >= 0 ? nullptr : reinterpret_cast<const int32_t*>(col.lut->p);
         kl.off = col.lut_off;
       }
       for (size_t k = 1; k < P->slot_kind.size(); ++k)
@@ -2138,7 +2163,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // digit becomes (global id - key_off[j]); the kernels subtract key_bias = sum key_off[j] * stride[j] once.  Same
   // groups, a table (and slab fold, and compaction) sized by what the filter admits.
   std::vector<int64_t> klo(P->key_cols.size(), 0), kspan(gcard);
-  if (P->pure_and && !getenv_flag("PGPU_NO_KEY_RESTRICT")) {
+  if (P->pure_and) {
     for (size_t j = 0; j < P->key_cols.size(); ++j) {
       const int c = P->key_cols[j];
       const Dict& gd = *P->key_dicts[j];
@@ -2237,9 +2262,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   const int nslots = (int)P->slot_kind.size();
   constexpr int64_t kDenseGlobalMax = int64_t(1) << 26;
   // LDS-privatised tables up to 112 KB (one workgroup per CU at the top end): measured on MI355X, an 80 KB table
-  // (C4: 5000 groups x 2 slots) runs 2.1x faster in LDS than with global atomics.  PGPU_LDS_BUDGET: A/B knob.
-  const char* lb = getenv("PGPU_LDS_BUDGET");
-  const int64_t kLdsBudget = lb && atol(lb) > 0 ? atol(lb) : 112 * 1024;
+  // (C4: 5000 groups x 2 slots) runs 2.1x faster in LDS than with global atomics.  pgpu_config.lds_table_kb.
+  const int64_t kLdsBudget = (int64_t)std::max(1, P->cfg.lds_table_kb) * 1024;
   // direct kernel LDS: [table (MODE_LDS)] [filter stack (general programs)] [per-wave match queues]
   const size_t stack_bytes = (pure_and ? 0 : (size_t)kMaxStack * kBlock * 4) + (size_t)(kBlock / 64) * 2 * kWaveQ * 4;
   for (Segment* s : P->segs) P->total_docs += s->num_docs;
@@ -2477,7 +2501,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           kc[j].lut_off = kl.off;
         }
         if (qcol_val[j]) {  // accumulator operand: value arrays, built once (ensure_values) and never replaced
-          kc[j].dkey = c.key_affine && !dict_gathers_forced() ? nullptr : c.d_key;
+          kc[j].dkey = c.key_affine ? nullptr : c.d_key;
           kc[j].key_base = c.key_base;
           kc[j].dval = c.d_val;
         }
@@ -2525,7 +2549,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           kl[k].negate = 0;
         }
         bool bitdir = false;
-        if (lh.kind == LEAF_BITMAP && lh.inv_ids.size() == 1 && !getenv_flag("PGPU_NO_BITDIR")) {
+        if (lh.kind == LEAF_BITMAP && lh.inv_ids.size() == 1) {
           // one dictId (no OR to compute): the scan reads its containers in place through a block directory --
           // BITMAP containers word by word, ARRAY containers (< 4096 docs of a block, e.g. a segment's partial last
           // block) by a binary search of their sorted offsets (array_group_mask); entry = payload address, | 1 and
@@ -2617,27 +2641,24 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
       // CUs; each flushes its table slab once
       const int64_t per_cu = P->mode == MODE_LDS ? std::max<int64_t>(1, std::min<int64_t>(2, (160 * 1024) /
                                                       std::max<size_t>(P->star_lds_bytes, 1))) : 8;
-      static const int64_t want_env = getenv("PGPU_STAR_WGS") ? atol(getenv("PGPU_STAR_WGS")) : 0;  // A/B knob
-      P->star_chunks = (int)(want_env > 0 ? want_env : (int64_t)t->num_cus * per_cu);
+      const int64_t want = P->cfg.star_tree_workgroups;  // pgpu_config
+      P->star_chunks = (int)(want > 0 ? want : (int64_t)t->num_cus * per_cu);
     }
     // Dense instance when tiles are expected to hold >= 8 matches per 32-doc group on average: below that the sparse
     // instance's per-match batches win (measured on MI355X, r04 session x: the C4 scan path at 15 % selectivity
-    // 195 -> 170 us with the sparse instance; C2 at 50 % 577 us dense vs 1468 sparse).  PGPU_DENSE_SEL: A/B.
+    // 195 -> 170 us with the sparse instance; C2 at 50 % 577 us dense vs 1468 sparse).  pgpu_config.dense_selectivity.
     {
-      static const double dense_sel = getenv("PGPU_DENSE_SEL") ? atof(getenv("PGPU_DENSE_SEL")) : 0.25;
-      P->dense = P->mode != MODE_HASH && P->sel_estimate >= dense_sel && !getenv_flag("PGPU_NO_DENSE");
+      P->dense = P->mode != MODE_HASH && P->sel_estimate >= P->cfg.dense_selectivity;
     }
     {
       bool f64 = false;
       for (int k : P->slot_kind) f64 |= k == SLOT_SUM_F64;
-      static const bool no_simple = getenv_flag("PGPU_NO_SIMPLE");  // A/B
       // (a streamed plan configures before its later chunks are planned: never simple)
-      P->dense_simple = P->dense && !P->gathers && !f64 && P->tile_bound == 0 && !no_simple;
+      P->dense_simple = P->dense && !P->gathers && !f64 && P->tile_bound == 0;
     }
     // the sparse instance with the index + scan pair: two-leaf AND plans with an in-place index leaf
     P->pair_variant = !P->dense && P->pure_and && P->num_leaves == 2 && P->leaf_kinds[LEAF_BITDIR] > 0;
-    static const bool no_fast = getenv_flag("PGPU_NO_FAST_INSTANCE");  // A/B
-    P->fast_variant = !P->dense && !P->pair_variant && P->pure_and && P->num_leaves <= kFastLeaves && !no_fast;
+    P->fast_variant = !P->dense && !P->pair_variant && P->pure_and && P->num_leaves <= kFastLeaves;
     const int variant = P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0;
     int per_cu;  // resident workgroups per CU
     {
@@ -2675,13 +2696,13 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     const bool dense_part = P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes;
     const bool hash_part = part_hash_eligible(P, G);
     if ((dense_part || hash_part) && P->star.empty() && tile_base > 0 && P->total_docs < (int64_t)UINT32_MAX &&
-        !getenv_flag("PGPU_NO_PARTITION")) {
+        P->cfg.partitioned_group_by) {
       int shift = 16;
       while (shift > 8 && ((int64_t)nslots << shift) * 8 > kPartLds) --shift;
       int64_t parts = (G + (int64_t(1) << shift) - 1) >> shift;
       int pbits = 0, sbits = 0;
       if (hash_part) {
-        hash_part_bits(P->group_bound, nslots, &pbits, &sbits);
+        hash_part_bits(P->cfg, P->group_bound, nslots, &pbits, &sbits);
         shift = 0;
         parts = int64_t(1) << pbits;
       }
@@ -2710,7 +2731,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->slot_stream = sstream;
         // u32 record values when every stream is an integer column whose values fit int32 in every segment
         // (sorted dictionaries: the first and last entries bound them)
-        bool v32 = !getenv_flag("PGPU_PART_VAL64");
+        bool v32 = true;
         for (size_t j = 0; j < scol.size() && v32; ++j) {
           const int c = P->query_cols[scol[j]];
           if (sf64[j]) v32 = false;
@@ -2728,7 +2749,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         P->part_val32 = v32;
         // one integer stream: its value range, for packing values into the coarse records (KPartParams.pack_bits)
         P->part_pack_range = -1;
-        if (v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn && !getenv_flag("PGPU_NO_PACK")) {
+        if (v32 && scol.size() == 1 && P->query_cols[scol[0]] != kDocIdColumn) {
           int64_t lo = INT64_MAX, hi = INT64_MIN;
           for (const Segment* s : P->segs) {
             const Column& col = s->cols[P->query_cols[scol[0]]];
@@ -2795,11 +2816,11 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // operator on its own worker thread, BaseCombineOperator.java:85-115).
   const bool part_eligible = ((P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes) ||
                               part_hash_eligible(P, G)) &&
-                             !getenv_flag("PGPU_NO_PARTITION");
+                             P->cfg.partitioned_group_by;
   // CHAIN / LEAP2 statistics need the direct kernel's register fast path (a pure AND of <= kFastLeaves leaves)
   P->in_kernel_stats = P->pure_and && P->num_leaves <= kFastLeaves && !part_eligible;
   P->leaf_perm = perm;
-  const int stream_chunks = se ? stream_chunk_count(nseg) : 1;
+  const int stream_chunks = se ? stream_chunk_count(P->cfg, nseg) : 1;
   if (se && !any_star && !any_inv && !any_raw_leaf && !part_eligible && stream_chunks > 1) {
     for (Segment* s : P->segs) {
       P->tile_bound += (s->num_docs + kTileDocs - 1) / kTileDocs;
@@ -2844,7 +2865,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
               now_us() - t_start, P->segs.size());
     return 0;
   }
-  const int nchunks = any_star ? 1 : (int)std::min<size_t>(host_pool().size() + 1, (nseg + plan_chunk_segs() - 1) / plan_chunk_segs());
+  const int nchunks = any_star ? 1 : (int)std::min<size_t>(host_pool().size() + 1, (nseg + plan_chunk_segs(P->cfg) - 1) / plan_chunk_segs(P->cfg));
   std::vector<Chunk> chunks(std::max(nchunks, 1));
   auto run_chunk = [&](int c) {
     Chunk& C = chunks[c];
@@ -2866,7 +2887,7 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   // tiles per CU run.  The scan kernel's direct path only: not with leap-frog statistics (their per-(tile, wave)
   // bytes are whole 32-doc groups) nor the partitioned group-by (its own passes).
   if (tile_base > 0 && tile_base < 2 * (int64_t)t->num_cus && !P->any_leap2 && P->star.empty() &&
-      !(P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes) && !getenv_flag("PGPU_NO_TILE_SPLIT")) {
+      !(P->mode == MODE_GLOBAL && (int64_t)nslots * G * 8 >= kPartMinBytes)) {
     int sh = 1;
     while (sh < 2 && (tile_base << sh) < 2 * (int64_t)t->num_cus) ++sh;
     P->tile_shift = sh;
@@ -3034,8 +3055,7 @@ int launch_raw_leaves(const pgpu_plan_s* P, Scratch* sc, hipStream_t stream) {
 void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow) {
   *pack_slot = P->mode == MODE_LDS || P->mode == MODE_HASH ? P->pack_slot : -1;  // planned with the table layout
   *narrow = 0;
-  static const bool off = getenv_flag("PGPU_NO_DENSE_NARROW");
-  if (off || !P->dense || P->mode != MODE_LDS || P->num_keys <= 1 || !P->star.empty() || P->grid <= 0) return;
+  if (!P->dense || P->mode != MODE_LDS || P->num_keys <= 1 || !P->star.empty() || P->grid <= 0) return;
   for (size_t s = 0; s < P->slot_kind.size() && s < 32; ++s) {
     const int kind = P->slot_kind[s], c = P->slot_tcol[s];
     if ((kind != SLOT_MIN_KEY && kind != SLOT_MAX_KEY) || c < 0 || c == kDocIdColumn) continue;
@@ -3184,17 +3204,13 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.tile_shift = P->tile_shift;
   // Tile order: interleaved (the tiles in flight on an XCD come from ~one segment: its dictionaries stay in that
   // XCD's L2 for the dense path's per-doc gathers) or chunked (a workgroup's tiles follow each other in one segment:
-  // its records and leaf registers are loaded once per run).  PGPU_TILE_ORDER=0/1 forces one (A/B).
+  // its records and leaf registers are loaded once per run).
   {
-    static const char* fo = getenv("PGPU_TILE_ORDER");
-    kp.tile_chunks = fo ? (atoi(fo) == 1 ? 1 : 0) : (P->dense ? 0 : 1);
+    kp.tile_chunks = P->dense ? 0 : 1;
   }
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
-  {
-    static const bool no_pair = getenv_flag("PGPU_NO_PAIR_LEAVES");  // A/B
-    kp.pair_leaves = no_pair ? 0 : 1;
-  }
+  kp.pair_leaves = 1;
   dense_lds_forms(P, &kp.pack_slot, &kp.narrow);
   kp.pack_shift = P->pack_shift;
   kp.stats = stats;
@@ -3266,11 +3282,11 @@ int exec_upload_chunk(pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, cons
 
 // Launches the scan of chunk c (records already uploaded): tile map of its records, then the scan kernel (or the
 // partitioned group-by) over its tiles into slab region c.
-// PGPU_CHECK_LAUNCH=1 (diagnostics): before a scan launch, the records and tile map the kernel will read are copied
+// PGPU_TRACE=check (diagnostics): before a scan launch, the records and tile map the kernel will read are copied
 // back and compared with the plan's host records (pointer fields patched at upload skipped); a mismatch fails the
 // query (PGPU_ERR_DEVICE) instead of launching on them.
 bool check_launch_on() {
-  static const bool on = getenv("PGPU_CHECK_LAUNCH") && getenv("PGPU_CHECK_LAUNCH")[0] == '1';
+  static const bool on = diag("check");
   return on;
 }
 int check_launch_inputs(const pgpu_plan_s* P, hipStream_t stream, const ExecCtx& X, const LaunchChunk& C) {
@@ -3356,8 +3372,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     pp.fine_fill = sc->fine_fill.as<uint32_t>();
     if (P->part_hash) {
       pp.hashed = 1;
-      static const bool no_pair = getenv_flag("PGPU_NO_MID_PAIR");  // A/B: key and value arrays
-      pp.mid_pair = !no_pair && cshift > 0 && pp.num_streams == 1 && P->part_val32 && !P->stream_f64[0] ? 1 : 0;
+      pp.mid_pair = cshift > 0 && pp.num_streams == 1 && P->part_val32 && !P->stream_f64[0] ? 1 : 0;
       pp.pbits = P->part_pbits;
       pp.sbits = P->part_sbits;
       TRY(sc->rec_key32.ensure((size_t)cap * 4));
@@ -3386,13 +3401,11 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       // hashed partitions: K8e's records packed as hk below the partition bits | (value - pack_min) above them
       int vb = 0;
       while (vb < 32 && (P->part_pack_range >> vb) != 0) ++vb;
-      static const bool no_fine = getenv_flag("PGPU_NO_FINE_PACK");
-      if (!no_fine && vb <= P->part_pbits) {
+      if (vb <= P->part_pbits) {
         pp.fine_pack = 1;
         pp.pack_min = P->part_pack_min;
         pp.pack_range = P->part_pack_range;
-        static const bool no_cs = getenv_flag("PGPU_NO_CS_PACK");  // A/B: two LDS atomics per record
-        pp.cs_pack = !no_cs && nslots == 2 && P->slot_kind[0] == SLOT_COUNT && P->slot_kind[1] == SLOT_SUM_I64 &&
+        pp.cs_pack = nslots == 2 && P->slot_kind[0] == SLOT_COUNT && P->slot_kind[1] == SLOT_SUM_I64 &&
                      P->slot_stream[1] == 0 ? 1 : 0;
       }
     } else if (!P->part_hash && cshift > 0 && P->part_pack_range >= 0) {
@@ -3402,10 +3415,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
       if ((P->part_pack_range >> vb) == 0) {
         pp.pack_bits = std::max(vb, 1);
         pp.pack_min = P->part_pack_min;
-        static const bool no_fine = getenv_flag("PGPU_NO_FINE_PACK");  // A/B: 6-byte final records
-        pp.fine_pack = !no_fine && pp.pshift + pp.pack_bits <= 32 && pp.num_streams == 1 ? 1 : 0;
-        static const bool no_cs = getenv_flag("PGPU_NO_CS_PACK");  // A/B: two LDS atomics per record
-        pp.cs_pack = pp.fine_pack && !no_cs && nslots == 2 && P->slot_kind[0] == SLOT_COUNT &&
+        pp.fine_pack = pp.pshift + pp.pack_bits <= 32 && pp.num_streams == 1 ? 1 : 0;
+        pp.cs_pack = pp.fine_pack && nslots == 2 && P->slot_kind[0] == SLOT_COUNT &&
                      P->slot_kind[1] == SLOT_SUM_I64 && P->slot_stream[1] == 0 ? 1 : 0;
         pp.pack_range = P->part_pack_range;
       }
@@ -3661,8 +3672,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       narrow_bytes += n * width[s];
     }
     const int64_t bitmap_words = (G + 63) / 64;
-    static const bool no_compact = getenv_flag("PGPU_NO_COMPACT_RESULT");
-    const bool compact = !no_compact && n > 0 && bitmap_words * 8 + narrow_bytes < n * (4 * nk + 8 * nslots);
+    const bool compact = P->cfg.compact_results && n > 0 && bitmap_words * 8 + narrow_bytes < n * (4 * nk + 8 * nslots);
     if (compact) {
       const int64_t cap = n;
       TRY(sc->ckeys.ensure((size_t)bitmap_words * 8 + (size_t)nslots * cap * 8));
@@ -3729,8 +3739,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
         return fail(PGPU_ERR_DEVICE, "compact launch failed");
     }
     // each slot's range over the records, read back with their count (the compact form's widths, below)
-    static const bool no_compact_h = getenv_flag("PGPU_NO_COMPACT_RESULT");
-    const bool want_compact = P->stage_end.empty() && !no_compact_h;
+    const bool want_compact = P->stage_end.empty() && P->cfg.compact_results;
     TRY(sc->counter.ensure(64 + (size_t)kMaxSlots * 16));  // (no regrowth: the first allocation is 4 KB)
     unsigned long long* d_mm = reinterpret_cast<unsigned long long*>(sc->counter.as<uint8_t>() + 64);
     if (want_compact &&
@@ -3755,8 +3764,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     star_scanned = st[2] + st[3];
     P->star_docs_read = (int64_t)st[4];
     if (P->groups_seen && P->merged_records < 0) P->groups_seen->store(n, std::memory_order_relaxed);
-    static const bool host_sort = getenv_flag("PGPU_HASH_HOST_SORT");  // A/B: sort and decode on the host
-    if (n >= 4096 && P->stage_end.empty() && !host_sort) {
+    if (n >= 4096 && P->stage_end.empty()) {
       // Decoded on the device in one streaming pass over the records, in their (hash / partition) order -- the
       // LONG_MAP holder's iteration order is fastutil's hash order (DictionaryBasedGroupKeyGenerator.java:693, :719)
       // and no consumer depends on group order -- held in compact form when that moves fewer bytes (C5-sized
@@ -3800,7 +3808,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
         n = -1;  // held compact
       }
     }
-    if (n >= 4096 && P->stage_end.empty() && !host_sort) {
+    if (n >= 4096 && P->stage_end.empty()) {
       // decoded into the columnar result on the device: one copy back
       const size_t slot_off = pgpu_result_s::slot_offset(nk, n);
       const size_t out_bytes = slot_off + (size_t)nslots * n * 8;
@@ -4206,9 +4214,8 @@ int composite_finalize(pgpu_plan_s* P, hipStream_t stream, pgpu_result_s* R) {
 // ------------------------------------------------------------------------------------------ plan cache
 constexpr size_t kPlanCacheEntries = 16;
 
-bool plan_cache_enabled(const pgpu_query* q) {
-  static const bool off = getenv("PGPU_PLAN_CACHE") && getenv("PGPU_PLAN_CACHE")[0] == '0';
-  return !off && q && !(q->options & PGPU_OPT_NO_PLAN_CACHE);
+bool plan_cache_enabled(const pgpu_table_s* t, const pgpu_query* q) {
+  return table_config(t).plan_cache && q && !(q->options & PGPU_OPT_NO_PLAN_CACHE);
 }
 
 // The bytes that determine a compiled plan: table version, segment handles, and every field of the query
@@ -4320,12 +4327,12 @@ void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
 
 }  // namespace
 
-// PGPU_SERIALIZE_ABI=1 (diagnostics): every entry point of this file runs under one process-wide lock, so
+// PGPU_TRACE=serialize (diagnostics): every entry point of this file runs under one process-wide lock, so
 // concurrent callers are serialised (isolates host-side races from device-side ones).
 namespace {
 std::recursive_mutex g_abi_mu;
 bool abi_serialize() {
-  static const bool on = getenv("PGPU_SERIALIZE_ABI") && getenv("PGPU_SERIALIZE_ABI")[0] == '1';
+  static const bool on = diag("serialize");
   return on;
 }
 struct AbiGuard {
@@ -4424,6 +4431,41 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
     t->num_cus = cus;
   *out = t.release();
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_config_default(pgpu_config* out) try {
+  PGPU_ABI_GUARD;
+  if (!out) return fail(PGPU_ERR_INVALID_ARGUMENT, "null config");
+  *out = default_config();
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_table_set_config(pgpu_table t, const pgpu_config* c) try {
+  PGPU_ABI_GUARD;
+  if (!t || !c || c->struct_size <= (int32_t)offsetof(pgpu_config, plan_cache))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "bad config arguments");
+  // fields past the caller's struct keep their defaults
+  pgpu_config v = default_config();
+  memcpy(&v, c, std::min<size_t>((size_t)c->struct_size, sizeof v));
+  v.struct_size = (int32_t)sizeof v;
+  if (v.hash_partition_bits < 0 || v.hash_partition_bits > 14 || v.hash_partition_lds_kb < 0 ||
+      v.hash_partition_lds_kb > 128 || v.lds_table_kb < 1 || v.lds_table_kb > 160 || v.plan_chunk_segments < 1 ||
+      v.stream_chunks < 1 || v.star_tree_workgroups < 0 || !(v.dense_selectivity >= 0.0))
+    return fail(PGPU_ERR_INVALID_ARGUMENT, "config value out of range");
+  {
+    std::lock_guard<std::mutex> g(t->cfg_mu);
+    t->cfg = v;
+  }
+  t->version.fetch_add(1);  // compiled plans were made with the previous settings
+  plan_cache_clear(t);
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_table_get_config(pgpu_table t, pgpu_config* out) try {
+  PGPU_ABI_GUARD;
+  if (!t || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *out = table_config(t);
   return 0;
 } PGPU_ABI_CATCH
 
@@ -5135,7 +5177,7 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
   auto P = std::make_unique<pgpu_plan_s>();
   // A cached plan is never a numGroupsLimit split (composite plans are not cached) and the split decision is a
   // function of the cache key (query, segments, pinned-state version): a hit skips it.
-  const bool cache = plan_cache_enabled(q);
+  const bool cache = plan_cache_enabled(t, q);
   const std::string key = cache ? plan_cache_key(t, handles, nsegs, q) : std::string();
   if (!cache || !plan_cache_get(t, key, P.get())) {
     bool composite = false;
@@ -5209,7 +5251,7 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   DeviceGuard g(t->device);
   auto P = std::make_unique<pgpu_plan_s>();
   // a cache hit skips the numGroupsLimit split decision (pgpu_plan_create)
-  const bool cache = plan_cache_enabled(q);
+  const bool cache = plan_cache_enabled(t, q);
   const std::string key = cache ? plan_cache_key(t, handles, nsegs, q) : std::string();  // before planning
   const bool hit = cache && plan_cache_get(t, key, P.get());
   const double tt1 = trace_on() ? now_us() : 0;

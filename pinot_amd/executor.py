@@ -210,8 +210,9 @@ def _key_str(x):
 
 
 class GpuTable:
-    def __init__(self, schema, device=0):
-        """schema: list of (column name, type name 'INT'|'LONG'|'FLOAT'|'DOUBLE'|'STRING')."""
+    def __init__(self, schema, device=0, config=None):
+        """schema: list of (column name, type name 'INT'|'LONG'|'FLOAT'|'DOUBLE'|'STRING'); config: executor settings
+        (pgpu_config field -> value, see set_config)."""
         self.lib = L.load()
         self.names = [n for n, _ in schema]
         self.types = [L.TYPE_NAMES[t] if isinstance(t, str) else int(t) for _, t in schema]
@@ -224,6 +225,34 @@ class GpuTable:
         self.handle = h
         self._dict_cache = {}
         self._snapshots = {}  # dictionary snapshot id -> values (results index the snapshot their plan saw)
+        if config:
+            self.set_config(**config)
+
+    # ------------------------------------------------------------------ executor settings
+    def config(self):
+        """The table's pgpu_config as a dict (pgpu_table_get_config)."""
+        c = L.ConfigC()
+        L.check(self.lib.pgpu_table_get_config(self.handle, ctypes.byref(c)))
+        return {f: getattr(c, f) for f in L.CONFIG_FIELDS}
+
+    def set_config(self, **fields):
+        """pgpu_table_set_config: the named fields changed, the others kept (plan_cache, partitioned_group_by,
+        hash_partitions, hash_partition_bits, hash_partition_lds_kb, lds_table_kb, plan_chunk_segments, stream_chunks,
+        compact_results, star_tree_workgroups, dense_selectivity -- include/pinotgpu.h).  Plans made afterwards use
+        them (the compiled-plan cache is cleared)."""
+        cur = self.config()
+        bad = set(fields) - set(cur)
+        if bad:
+            raise ValueError("unknown config fields: %s" % sorted(bad))
+        cur.update(fields)
+        c = L.ConfigC(ctypes.sizeof(L.ConfigC), **cur)
+        L.check(self.lib.pgpu_table_set_config(self.handle, ctypes.byref(c)))
+
+    def reset_config(self):
+        """The library's defaults (pgpu_config_default)."""
+        c = L.ConfigC()
+        L.check(self.lib.pgpu_config_default(ctypes.byref(c)))
+        L.check(self.lib.pgpu_table_set_config(self.handle, ctypes.byref(c)))
 
     def close(self):
         if self.handle:

@@ -38,8 +38,8 @@ def assert_same(gpu, orc, q, schema):
                 assert x == y, (k, fn, x, y)
 
 
-def gpu_table(schema, segments):
-    t = GpuTable(schema)
+def gpu_table(schema, segments, config=None):
+    t = GpuTable(schema, config=config)
     handles = [t.pin_segment(s) for s in segments]
     return t, handles
 
@@ -209,13 +209,13 @@ def _random_filter(rng, seg, depth=0):
 
 
 @pytest.mark.parametrize("seed", list(range(12)))
-def test_random_queries_vs_oracle(oracle, gpu_lib, seed, monkeypatch):
-    if seed % 2:  # streamed plans: every segment its own launch, planned while the previous ones run
-        monkeypatch.setenv("PGPU_STREAM_CHUNKS", "4")
+def test_random_queries_vs_oracle(oracle, gpu_lib, seed):
+    # odd seeds: streamed plans -- every segment its own launch, planned while the previous ones run
+    cfg = {"stream_chunks": 4} if seed % 2 else None
     rng = np.random.default_rng(1000 + seed)
     nseg = int(rng.integers(1, 5))
     segs = [_random_segment(oracle, rng, SCHEMA_R, int(rng.integers(1, 40000))) for _ in range(nseg)]
-    t, hs = gpu_table(SCHEMA_R, segs)
+    t, hs = gpu_table(SCHEMA_R, segs, cfg)
     try:
         for qi in range(4):
             gb = list(rng.choice(["a", "b", "e", "c"], size=int(rng.integers(1, 3)), replace=False))
@@ -403,13 +403,11 @@ def test_num_groups_limit_not_reached_is_exact(oracle, sv):
 
 @pytest.mark.parametrize("partitioned", [True, False], ids=["partitioned", "atomics"])
 @pytest.mark.parametrize("docs", [1, 4097, 150_000])
-def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned, monkeypatch):
+def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned):
     """C5 shape (3-column composite key over a ~10^6 key space, INT_MAP holder in Pinot): the dense global table
     -- built by the partitioned group-by (partition.h) or by global atomics -- and its ordered device compaction
     (count / scan / scatter) give the oracle's groups in ascending key order, across chunk boundaries and with
     fewer docs than keys."""
-    if not partitioned:
-        monkeypatch.setenv("PGPU_NO_PARTITION", "1")
     rng = np.random.default_rng(docs)
     schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("n", "INT"), ("l", "LONG"),
               ("q", "INT")]
@@ -423,7 +421,7 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned,
                                                  "n": rng.integers(-2 ** 31, 2 ** 31, size=docs),
                                                  "l": rng.integers(-2 ** 40, 2 ** 40, size=docs),
                                                  "q": rng.integers(-500, 500, size=docs)}))
-    t, hs = gpu_table(schema, segs)
+    t, hs = gpu_table(schema, segs, None if partitioned else {"partitioned_group_by": 0})
     try:
         q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
                         num_groups_limit=10 ** 7)
@@ -492,13 +490,13 @@ def test_finalize_key_range_shards(oracle, gpu_lib):
 
 @pytest.mark.parametrize("chunk", [0, 64], ids=["one_thread", "chunks_of_64"])
 @pytest.mark.parametrize("launches", [1, 4, 7])
-def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, launches, monkeypatch):
+def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, launches):
     """Plans over hundreds of segments translate their predicates in parallel chunks (host worker pool); the
     concatenated records (tile offsets, IN-set bitsets) must give the oracle's combined result, including
     segments the filter prunes (EmptyFilterOperator) in the middle of a chunk."""
+    cfg = {"stream_chunks": launches}
     if chunk:
-        monkeypatch.setenv("PGPU_PLAN_CHUNK_SEGS", str(chunk))
-    monkeypatch.setenv("PGPU_STREAM_CHUNKS", str(launches))
+        cfg["plan_chunk_segments"] = chunk
     rng = np.random.default_rng(11)
     schema = [("g", "INT"), ("f", "INT"), ("v", "LONG")]
     segs = []
@@ -507,7 +505,7 @@ def test_many_segments_chunked_planning(oracle, gpu_lib, chunk, launches, monkey
         lo = 0 if i % 7 else 5000  # every 7th segment has no f value below 5000: pruned by the range leaf
         segs.append(oracle.make_segment(schema, {"g": rng.integers(0, 40, n), "f": rng.integers(lo, lo + 200, n),
                                                  "v": rng.integers(-10 ** 9, 10 ** 9, n)}))
-    t, hs = gpu_table(schema, segs)
+    t, hs = gpu_table(schema, segs, cfg)
     try:
         q = parse_query("SELECT COUNT(*), SUM(v), MIN(v) FROM t WHERE f < 150 AND g IN (1, 3, 5, 17, 39) GROUP BY g")
         r = t.execute_groupby(hs, q)
@@ -909,5 +907,29 @@ def test_plan_cache_reuse_and_invalidation(oracle):
         r3 = t.execute_groupby(hs, q)
         assert_same(r3, o, q, schema)
         assert r3.stats.as_tuple() == o.stats
+    finally:
+        t.close()
+
+
+def test_table_config_roundtrip(gpu_lib):
+    """pgpu_table_set_config / _get_config: fields set are kept, others keep their values, out-of-range values are
+    refused, a caller's shorter struct leaves the later fields at their defaults."""
+    import ctypes
+    t = GpuTable([("a", "INT")], config={"stream_chunks": 3, "dense_selectivity": 0.5})
+    try:
+        c = t.config()
+        assert c["stream_chunks"] == 3 and c["dense_selectivity"] == 0.5 and c["plan_cache"] == 1
+        t.set_config(plan_cache=0)
+        assert t.config()["plan_cache"] == 0 and t.config()["stream_chunks"] == 3
+        for bad in ({"hash_partition_bits": 15}, {"lds_table_kb": 0}, {"stream_chunks": 0},
+                    {"dense_selectivity": float("nan")}):
+            with pytest.raises(L.PinotGpuError):
+                t.set_config(**bad)
+        short = L.ConfigC(8, 0)  # struct_size covers plan_cache only
+        L.check(t.lib.pgpu_table_set_config(t.handle, ctypes.byref(short)))
+        c = t.config()
+        assert c["plan_cache"] == 0 and c["stream_chunks"] == 1 and c["dense_selectivity"] == 0.25
+        t.reset_config()
+        assert t.config()["plan_cache"] == 1
     finally:
         t.close()

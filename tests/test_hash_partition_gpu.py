@@ -50,28 +50,32 @@ def test_hash_partitions_match_oracle(oracle, sparse, sql):
     assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
 
 
-def test_hash_partition_rounds(oracle, sparse, monkeypatch):
+def test_hash_partition_rounds(oracle, sparse):
     """One partition of 2^sbits LDS slots for ~2e5 groups: K8h loops over rounds, each placing the keys that find a
     slot and compacting the rest in place."""
     t, hs, segs = sparse
-    monkeypatch.setenv("PGPU_PART_HASH_PBITS", "0")
-    for sql in QUERIES[:2]:
-        q = parse_query(sql, num_groups_limit=10 ** 9)
-        q.no_plan_cache = True  # planned afresh under the knob
-        with t.plan(hs, q) as p:
-            assert p.group_path() == "hash_partitioned"
-        assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+    t.set_config(hash_partition_bits=0)
+    try:
+        for sql in QUERIES[:2]:
+            q = parse_query(sql, num_groups_limit=10 ** 9)
+            with t.plan(hs, q) as p:
+                assert p.group_path() == "hash_partitioned"
+            assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+    finally:
+        t.reset_config()
 
 
-def test_hash_partition_rounds_packed(oracle, sparse, monkeypatch):
+def test_hash_partition_rounds_packed(oracle, sparse):
     """Packed records (hashed key bits | value) left pending: 128 partitions of 256-entry LDS tables for ~1 800 groups
     each, so K8h writes packed words back and re-reads them over several rounds."""
     t, hs, segs = sparse
-    monkeypatch.setenv("PGPU_PART_HASH_LDS_KB", "4")  # 256 entries
-    monkeypatch.setenv("PGPU_PART_HASH_PBITS", "7")   # 128 partitions: 7 bits, just room for the 7-bit values
-    q = parse_query(QUERIES[3], num_groups_limit=10 ** 9)
-    q.no_plan_cache = True
-    assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+    # 256-entry tables (4 KB), 128 partitions: 7 bits, just room for the 7-bit values
+    t.set_config(hash_partition_lds_kb=4, hash_partition_bits=7)
+    try:
+        q = parse_query(QUERIES[3], num_groups_limit=10 ** 9)
+        assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+    finally:
+        t.reset_config()
 
 
 def test_hash_partitions_exchange_materialises_table(oracle, sparse):

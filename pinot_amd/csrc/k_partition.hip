@@ -39,8 +39,16 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
     hipLaunchKernelGGL((part_pass_kernel<true, 0>), dim3(grid), dim3(kBlock), scatter_lds, s, pc);
   if (pp.cshift > 0) {
     if (hipMemsetAsync(pp.fine_fill, 0, (size_t)pp.num_parts * 4, s) != hipSuccess) return -1;
-    hipLaunchKernelGGL(part_split_kernel, dim3(pp.num_coarse * pp.chunks_per_coarse), dim3(kBlock),
-                       part_split_lds(pp.cshift, pp.num_streams, pp.split_batch, pp.hashed ? 4 : 2), s, pp);
+    const dim3 sgrid(pp.num_coarse * pp.chunks_per_coarse);
+#ifndef PGPU_PART_NO_SPLIT_WORDS  // (defined only by an A/B build of the library)
+    if (pp.fine_pack && pp.hashed)
+      hipLaunchKernelGGL(part_split_words_kernel<true>, sgrid, dim3(kBlock), part_split_words_lds(pp.cshift), s, pp);
+    else if (pp.fine_pack)
+      hipLaunchKernelGGL(part_split_words_kernel<false>, sgrid, dim3(kBlock), part_split_words_lds(pp.cshift), s, pp);
+    else
+#endif
+      hipLaunchKernelGGL(part_split_kernel, sgrid, dim3(kBlock),
+                         part_split_lds(pp.cshift, pp.num_streams, pp.split_batch, pp.hashed ? 4 : 2), s, pp);
   }
   if (pp.hashed) {
     if (pp.num_streams > kHashPartStreams || pp.sbits < 8 || pp.sbits > 14) return -1;
@@ -48,7 +56,12 @@ int launch_partitioned(const KPartParams& pp, int grid, size_t pass_lds, void* s
                        part_hash_lds(pp.sbits, pp.base.num_slots), s, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
+  // cs_pack: COUNT + SUM in one word per key (part_aggregate_kernel)
+#ifndef PGPU_PART_CS_FULL_LDS  // (defined only by an A/B build: the LDS of every slot's row, two workgroups per CU)
+  const size_t agg_lds = (pp.cs_pack ? (size_t)1 : (size_t)pp.base.num_slots) * ((size_t)1 << pp.pshift) * 8;
+#else
   const size_t agg_lds = (size_t)pp.base.num_slots * ((size_t)1 << pp.pshift) * 8;
+#endif
   hipLaunchKernelGGL(part_aggregate_kernel, dim3(pp.num_parts), dim3(kBlock), agg_lds, s, pp);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

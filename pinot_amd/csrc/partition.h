@@ -507,6 +507,112 @@ __global__ __launch_bounds__(kBlock) void part_split_kernel(const KPartParams pp
   }
 }
 
+// K8e, one final u32 word per record (KPartParams.fine_pack: C5's packed records, c5_hash's hashed ones): the same
+// batch sort with the record's final word computed in registers at load time, so the staging holds 8 bytes per record
+// (word, position) instead of 14-16, batches are twice as large (half the reservation round trips per record), and
+// the next batch's records are loaded while the current one is placed and written out.  HASHED: hk below the
+// partition bits | (value - pack_min) << (32 - pbits), from mid_pair words or mid_key + u32 mid_val; else the key
+// within the partition | (value - pack_min) << pshift, from pack_bits mid_key words.  LDS: counters / histogram /
+// bucket starts [2^cshift each], then kSplitWordsBatch words and positions.
+constexpr int kSplitWordsBatch = 4096;
+constexpr size_t part_split_words_lds(int cshift) {
+  return (size_t)3 * ((size_t)1 << cshift) * 4 + (size_t)kSplitWordsBatch * 8;
+}
+template <bool HASHED>
+__global__ __launch_bounds__(kBlock) void part_split_words_kernel(const KPartParams pp) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const int tid = threadIdx.x;
+  if (pp.base.deadline && pp.base.stats[5]) return;
+  const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
+  const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
+  const int NP = 1 << pp.cshift;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+  uint32_t* hist = cnt + NP;
+  uint32_t* bstart = hist + NP;
+  uint32_t* sword = bstart + NP;
+  uint32_t* spos = sword + kSplitWordsBatch;
+  __shared__ uint32_t wtot[kBlock / 64];
+  const uint32_t cs = pp.part_start[p0], ce = pp.part_start[p1];
+  const uint32_t r0 = cs + (uint32_t)((uint64_t)(ce - cs) * j / pp.chunks_per_coarse);
+  const uint32_t r1 = cs + (uint32_t)((uint64_t)(ce - cs) * (j + 1) / pp.chunks_per_coarse);
+  const int cbits = pp.pshift + pp.cshift;
+  const uint32_t kmask = (1u << cbits) - 1u, low = (1u << pp.pshift) - 1u;
+  const int lb = 32 - pp.pbits;
+  const uint32_t hlow = HASHED ? (1u << lb) - 1u : 0u;
+  constexpr int NB = kSplitWordsBatch / kBlock;
+  const int per = (NP + kBlock - 1) / kBlock;
+  uint32_t part[NB], word[NB];
+  // batch b0's records -> (partition within the run, final word); part = ~0u past the batch's end
+  auto load = [&](uint32_t b0) {
+    const uint32_t n = b0 < r1 ? min((uint32_t)kSplitWordsBatch, r1 - b0) : 0u;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t i = tid + b * kBlock;
+      const uint32_t r = b0 + (i < n ? i : 0u);
+      if (HASHED) {
+        uint32_t hk, v;
+        if (pp.mid_pair) {
+          const uint64_t w = n ? pp.mid_val[r] : 0ull;
+          hk = (uint32_t)w;
+          v = (uint32_t)(w >> 32);
+        } else {
+          hk = n ? pp.mid_key[r] : 0u;
+          v = n ? reinterpret_cast<const uint32_t*>(pp.mid_val)[r] : 0u;
+        }
+        part[b] = i < n ? hpart(pp, hk) & (uint32_t)(NP - 1) : ~0u;
+        word[b] = (hk & hlow) | ((uint32_t)((int64_t)v - pp.pack_min) << lb);
+      } else {
+        const uint32_t w = n ? pp.mid_key[r] : 0u;
+        const uint32_t kk = w & kmask;
+        part[b] = i < n ? kk >> pp.pshift : ~0u;
+        word[b] = (kk & low) | ((w >> cbits) << pp.pshift);
+      }
+    }
+  };
+  load(r0);
+  uint32_t* __restrict__ r32 = reinterpret_cast<uint32_t*>(pp.rec_val);
+  for (uint32_t b0 = r0; b0 < r1; b0 += kSplitWordsBatch) {
+    const uint32_t n = min((uint32_t)kSplitWordsBatch, r1 - b0);
+    for (int i = tid; i < NP; i += kBlock) hist[i] = 0u;
+    __syncthreads();  // (also: the previous batch's write-out has read the staged words)
+    uint32_t rank[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) rank[b] = part[b] != ~0u ? atomicAdd(&hist[part[b]], 1u) : 0u;
+    __syncthreads();
+    {  // exclusive prefix of the batch histogram; the batch's run in each partition reserved with one atomic
+      const int lane = tid & 63, w = tid >> 6;
+      uint32_t acc = 0;
+      for (int i = tid * per; i < min(NP, (tid + 1) * per); ++i) acc += hist[i];
+      uint32_t incl = acc;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) wtot[w] = incl;
+      __syncthreads();
+      uint32_t run = incl - acc;
+      for (int v = 0; v < w; ++v) run += wtot[v];
+      for (int i = tid * per; i < min(NP, (tid + 1) * per); ++i) {
+        bstart[i] = run;
+        const uint32_t h = hist[i];
+        run += h;
+        cnt[i] = h && i < np ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (part[b] == ~0u) continue;
+      const uint32_t l = bstart[part[b]] + rank[b];
+      sword[l] = word[b];
+      spos[l] = cnt[part[b]] + rank[b];
+    }
+    load(b0 + kSplitWordsBatch);  // the next batch in flight while this one is written out
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kBlock) r32[spos[i]] = sword[i];
+  }
+}
+
 // K8d: partition blockIdx.x -> its key range of every table row.  LDS: [num_slots][1 << pshift] u64.
 __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParams pp) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -515,36 +621,59 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
   if (p.deadline && p.stats[5]) return;
   const int PR = 1 << pp.pshift;
   const int ns = p.num_slots;
-  for (int i = tid; i < ns * PR; i += kBlock) lds[i] = slot_init(p.slot_kind[i / PR]);
+  // cs_pack: one word per key (LDS of PR words, part_aggregate_lds), COUNT + SUM from 0; else every slot's row
+  for (int i = tid; i < (pp.cs_pack ? PR : ns * PR); i += kBlock) lds[i] = pp.cs_pack ? 0ull : slot_init(p.slot_kind[i / PR]);
   __syncthreads();
   const uint32_t r0 = pp.part_start[blockIdx.x], r1 = pp.part_start[blockIdx.x + 1];
-  // COUNT + SUM in one LDS word per key when this partition's records bound both halves (uniform per workgroup)
-  if (pp.cs_pack && (r1 - r0) < (1u << 24) && (uint64_t)(r1 - r0) * (uint64_t)pp.pack_range < (1ull << 40)) {
+  // COUNT + SUM in one LDS word per key (the table is PR words, 32 KB for C5: four workgroups per CU instead of
+  // two), over chunks of records small enough that every key's count stays below 2^24 and its sum of offsets below
+  // 2^40; the first chunk stores the partition's slice of both rows, later ones (a partition of more than ~10^9
+  // offsets' worth of records) add to it -- the partition is this workgroup's alone.
+  if (pp.cs_pack) {
     constexpr int NB = 16;
     const uint32_t* __restrict__ r32 = reinterpret_cast<const uint32_t*>(pp.rec_val);
     const uint32_t low = (1u << pp.pshift) - 1u;
     unsigned long long* w64 = reinterpret_cast<unsigned long long*>(lds);  // slot 0's words
-    for (uint32_t base = r0 + tid; base < r1; base += NB * kBlock) {
-      uint32_t wr[NB];
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const uint32_t r = base + b * kBlock;
-        wr[b] = r32[r < r1 ? r : r0];
-      }
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        if (base + b * kBlock < r1) atomicAdd(w64 + (wr[b] & low), (1ull << 40) | (unsigned long long)(wr[b] >> pp.pshift));
-    }
-    __syncthreads();
+    const uint64_t by_sum = (1ull << 40) / (uint64_t)(pp.pack_range > 0 ? pp.pack_range : 1);
+    const uint32_t lim = (uint32_t)(by_sum < (1ull << 24) - 1 ? (by_sum > 0 ? by_sum : 1) : (1ull << 24) - 1);
     const int64_t G = p.num_keys_total;
     const int64_t k0 = (int64_t)blockIdx.x * PR;
     const int n = (int)(G - k0 < PR ? G - k0 : PR);
-    for (int i = tid; i < n; i += kBlock) {
-      const uint64_t w = lds[i];
-      const uint64_t cnt = w >> 40;
-      p.table[k0 + i] = cnt;                                                              // COUNT (slot 0)
-      p.table[G + k0 + i] = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)cnt * pp.pack_min);  // SUM
-    }
+    uint32_t c0 = r0;
+    do {
+      const uint32_t c1 = r1 - c0 > lim ? c0 + lim : r1;
+      if (c0 != r0) {
+        for (int i = tid; i < PR; i += kBlock) lds[i] = 0ull;
+        __syncthreads();
+      }
+      for (uint32_t base = c0 + tid; base < c1; base += NB * kBlock) {
+        uint32_t wr[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const uint32_t r = base + b * kBlock;
+          wr[b] = r32[r < c1 ? r : c0];
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          if (base + b * kBlock < c1)
+            atomicAdd(w64 + (wr[b] & low), (1ull << 40) | (unsigned long long)(wr[b] >> pp.pshift));
+      }
+      __syncthreads();
+      for (int i = tid; i < n; i += kBlock) {
+        const uint64_t w = lds[i];
+        const uint64_t cnt = w >> 40;
+        const uint64_t sum = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)cnt * pp.pack_min);
+        if (c0 == r0) {
+          p.table[k0 + i] = cnt;      // COUNT (slot 0)
+          p.table[G + k0 + i] = sum;  // SUM
+        } else {
+          p.table[k0 + i] += cnt;
+          p.table[G + k0 + i] += sum;
+        }
+      }
+      __syncthreads();  // the words are read before the next chunk clears them
+      c0 = c1;
+    } while (c0 < r1);
     return;
   }
   // Two workgroups per CU (the LDS table), so latency is hidden by loads in flight per lane: NB records per lane

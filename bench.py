@@ -75,7 +75,18 @@ def parse_args():
     p.add_argument("--no-star-tree", action="store_true", help="query option useStarTree=false (scan path)")
     p.add_argument("--num-groups-limit", type=int, default=None, help="query option numGroupsLimit (default: the "
                    "workload's)")
+    p.add_argument("--config", default=None, help="table executor settings, field=value[,field=value] "
+                   "(pgpu_config fields, e.g. dense_selectivity=0.5)")
     return p.parse_args()
+
+
+def parse_config(text):
+    """--config: "field=value,field=value" -> {field: int or float} (pgpu_config, include/pinotgpu.h)."""
+    out = {}
+    for item in filter(None, (text or "").split(",")):
+        k, _, v = item.partition("=")
+        out[k.strip()] = float(v) if "." in v else int(v)
+    return out
 
 
 def compulsory_bytes(table, handles, query, docs_per_segment, inverted_columns=()):
@@ -187,6 +198,8 @@ def pmc_traffic(args):
             "--warmup-ms", "0", "--parity-segments", "0"]
     if args.num_groups_limit:
         base += ["--num-groups-limit", str(args.num_groups_limit)]
+    if args.config:
+        base += ["--config", args.config]
     env = {k: v for k, v in os.environ.items() if k not in DIST_ENV}
     res = {}
     with tempfile.TemporaryDirectory() as d:
@@ -578,7 +591,7 @@ def main():
     q = parse_query(w.sql, num_groups_limit=args.num_groups_limit or w.num_groups_limit)
     if args.no_star_tree:
         q.use_star_tree = False
-    table = GpuTable(w.schema, device=device)
+    table = GpuTable(w.schema, device=device, config=parse_config(args.config) or None)
     t_gen = time.perf_counter()
     handles = []
     for i in range(nseg):
@@ -849,7 +862,8 @@ def main():
             "config": {"workload": w.name, "query": w.sql, "segments_per_gpu": nseg, "docs_per_segment": docs,
                        "rows_per_gpu": nseg * docs, "global_rows": int(total_rows), "parallelism": "dp%d" % world,
                        "groups": ngroups, "setup_s": round(t_gen, 1), "queries_in_flight": inflight,
-                       "combine": L.COMBINE_NAMES[mode] + (" (pgpu_plan_combine, %s)" % backend if world > 1 else "")},
+                       "combine": L.COMBINE_NAMES[mode] + (" (pgpu_plan_combine, %s)" % backend if world > 1 else ""),
+                       **({"executor_config": parse_config(args.config)} if args.config else {})},
             "roofline": roofline,
             "host_profile_us": {k: round(v / args.steps * 1e6, 1) for k, v in phases.items()} if args.host_profile else None,
             "cpu_baseline": cpu,

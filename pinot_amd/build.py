@@ -1,5 +1,6 @@
 """In-tree build of libpinotgpu.so (gfx950) with hipcc.  No cmake / ninja / torch extension machinery: the
 library is a plain shared object with a C ABI (include/pinotgpu.h)."""
+import hashlib
 import os
 import shutil
 import subprocess
@@ -54,21 +55,38 @@ def build(force=False, verbose=False, defines=(), out=None):
     os.makedirs(objdir, exist_ok=True)
     procs = []
     objs = []
+    # an object is rebuilt when its command, its source or any header changed (key file beside the object)
+    common = hashlib.sha1()
+    for h in HEADERS + ["../../include/pinotgpu.h"]:
+        with open(os.path.join(CSRC, h), "rb") as f:
+            common.update(f.read())
     for src, extra, name in SOURCES:
         obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
         # host sources carry line tables (-g does not change -O3 host code): crash traces resolve with addr2line
         dbg = ["-g"] if src.endswith(".cpp") else []
         cmd = [hipcc] + flags + dbg + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        key = common.copy()
+        key.update(" ".join(cmd).encode())
+        with open(os.path.join(CSRC, src), "rb") as f:
+            key.update(f.read())
+        key = key.hexdigest()
+        if not force and os.path.exists(obj) and os.path.exists(obj + ".key"):
+            with open(obj + ".key") as f:
+                if f.read() == key:
+                    continue
         if verbose:
             print(" ".join(cmd))
-        procs.append((src, subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                            text=True)))
+        procs.append((src, obj, key, subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                                      text=True)))
     errors = []
-    for src, pr in procs:
+    for src, obj, key, pr in procs:
         out, _ = pr.communicate()
         if pr.returncode != 0:
             errors.append("%s:\n%s" % (src, out[-8000:]))
+        else:
+            with open(obj + ".key", "w") as f:
+                f.write(key)
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
     cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs + ["-ldl"]

@@ -229,29 +229,28 @@ __device__ __forceinline__ uint32_t bitdir_mask(uint64_t e, int negate, int64_t 
 }
 
 // A LEAF_BITDIR leaf (an inverted index read in place) beside a LEAF_RANGE scan of B-bit dictIds, evaluated
-// together: the scan column's words are requested before the directory -> container chain, so a tile waits two
-// memory round trips instead of three (the scan's after the chain).  Both masks come back; the caller applies
-// them in Pinot's order (index leaf, then the scan on its survivors).
+// together: the scan column's words and the container word are requested together (the block's directory entry `e`
+// comes from the caller, which keeps it across the 8 tiles of a 65536-doc block), so a tile waits one memory round
+// trip instead of three.  Both masks come back; the caller applies them in Pinot's order (index leaf, then the scan
+// on its survivors).
 template <int B>
 __device__ __forceinline__ void bitdir_range_b(const uint32_t* __restrict__ words, uint32_t lo, uint32_t span,
-                                               const uint64_t* dir, int neg0, int64_t group, uint32_t& m0,
-                                               uint32_t& m1) {
+                                               uint64_t e, int neg0, int64_t group, uint32_t& m0, uint32_t& m1) {
   uint32_t w[B + 1];
   load_group<B, true>(words, w);
-  m0 = bitdir_mask(gp(dir)[group >> 11], neg0, group);
+  m0 = bitdir_mask(e, neg0, group);
   m1 = span == 1 ? eq_all<B>(w, lo, std::make_integer_sequence<int, 32>{})
                  : range_all<B>(w, lo, lo + span, std::make_integer_sequence<int, 32>{});
 }
 __device__ __forceinline__ void bitdir_range(const uint32_t* fwd, int bits, uint32_t lo, uint32_t span, int neg1,
-                                             const uint64_t* dir, int neg0, int64_t group, uint32_t& m0,
-                                             uint32_t& m1) {
+                                             uint64_t e, int neg0, int64_t group, uint32_t& m0, uint32_t& m1) {
   const uint32_t* words = fwd + group * (int64_t)bits;
   m0 = 0;
   m1 = 0;
   switch (bits) {
 #define PGPU_CASE(B)                                                 \
   case B:                                                            \
-    bitdir_range_b<B>(words, lo, span, dir, neg0, group, m0, m1); \
+    bitdir_range_b<B>(words, lo, span, e, neg0, group, m0, m1); \
     break;
     PGPU_CASE(1) PGPU_CASE(2) PGPU_CASE(3) PGPU_CASE(4) PGPU_CASE(5) PGPU_CASE(6) PGPU_CASE(7) PGPU_CASE(8)
     PGPU_CASE(9) PGPU_CASE(10) PGPU_CASE(11) PGPU_CASE(12) PGPU_CASE(13) PGPU_CASE(14) PGPU_CASE(15)
@@ -322,6 +321,24 @@ struct SegView {
   const KCol* cols;
   const KLeaf* leaves;
 };
+
+// Index of local dictId `id` in a column's value arrays (KCol.dkey / dval): the id itself, or -- table-global value
+// arrays -- id + the global ids missing from the segment's dictionary below it.  Threshold k is t_k + k (t_k the local
+// id above the k-th missing value, runtime.cpp ensure_value_map), so the running index is compared, no memory access.
+__device__ __forceinline__ uint32_t vidx(const KCol& c, uint32_t id) {
+  for (int k = 0; k < c.ngaps; ++k) id += id >= c.gaps[k] ? 1u : 0u;
+  return id;
+}
+// The same for N ids of one segment (c wave-uniform: the thresholds are scalar operands).
+template <int N>
+__device__ __forceinline__ void vidx_n(const KCol& c, uint32_t (&ids)[N]) {
+  const int ng = c.ngaps;
+  for (int k = 0; k < ng; ++k) {
+    const uint32_t g = c.gaps[k];
+#pragma unroll
+    for (int i = 0; i < N; ++i) ids[i] += ids[i] >= g ? 1u : 0u;
+  }
+}
 
 __device__ __forceinline__ SegView seg_view(const KParams& p, int seg) {
   const uint8_t* base = p.segs + (int64_t)seg * p.seg_stride;
@@ -577,7 +594,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       live[b] = idx[b] >= 0;
     }
   }
-  uint32_t id[NB];
+  uint32_t id[NB], vi[NB];  // dictIds, and their indexes in the value arrays (vidx)
   int prev_col = -1;
   for (int s = 0; s < p.num_slots; ++s) {
     const int kind = p.slot_kind[s];
@@ -593,16 +610,20 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
           const KCol& c = S[b].cols[col];
           id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
         }
+        if (!SIMPLE) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) vi[b] = vidx(S[b].cols[col], id[b]);
+        }
         prev_col = col;
       }
       if (!SIMPLE && kind == SLOT_SUM_F64) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) dval[b] = gp(S[b].cols[col].dval)[id[b]];
+        for (int b = 0; b < NB; ++b) dval[b] = gp(S[b].cols[col].dval)[vi[b]];
       } else {
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const KCol& c = S[b].cols[col];
-          ikey[b] = !SIMPLE && c.dkey ? gp(c.dkey)[id[b]] : c.key_base + (int64_t)id[b];
+          ikey[b] = !SIMPLE && c.dkey ? gp(c.dkey)[vi[b]] : c.key_base + (int64_t)id[b];
         }
       }
     }
@@ -816,6 +837,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
     }
     const KCol& c = S.cols[col];
     decode_group<H>(c.fwd, c.bits, group, ids);
+    if (!SIMPLE) vidx_n(c, ids);  // table-global value arrays (one segment): dictIds -> their indexes
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run
       int64_t v[16];
       if (!SIMPLE && c.dkey) {
@@ -861,6 +883,12 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? (double)ids[i] : 0.0;
       (void)dv;
+#elif defined(PGPU_DIAG_SHARED_DVAL)  // diagnostic build only (wrong sums): every segment gathers from segment 0's
+      // dictionary (in bounds: ids below 2^16), i.e. the access pattern of one table-global dictionary array
+      gmem<double>* __restrict__ dv0 = gp(seg_view(p, 0).cols[col].dval);
+      (void)dv;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv0[ids[i] & 0xFFFFu] : 0.0;
 #else
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? dv[ids[i]] : 0.0;

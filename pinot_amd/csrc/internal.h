@@ -29,8 +29,8 @@ constexpr int kMaxStack = 8;                // filter evaluation stack depth
 constexpr int kFwdPadWords = 4;
 constexpr int kWaveQ = 256;                 // direct kernel: per-wave queue of sparse matched docs (LDS, u32)
 constexpr int kFlushAt = 128;               // ... aggregated in 2-per-lane batches once it holds this many
-constexpr int kDenseGroupMin = 256;
-constexpr int kFastLeaves = 4;              // pure-AND programs up to this many leaves keep them in registers         // matches per wave-tile (of 2048 docs) above which whole groups are decoded
+constexpr int kDenseGroupMin = 256;        // matches per wave-tile (of 2048 docs) above which whole groups are decoded
+constexpr int kFastLeaves = 4;              // pure-AND programs up to this many leaves keep them in registers
 
 // LEAF_DOCRANGE: a predicate on a sorted column (SortedIndexBasedFilterOperator, core/operator/filter/
 // SortedIndexBasedFilterOperator.java:51-125): docIds [lo, lo + span), evaluated without reading any column.
@@ -65,6 +65,10 @@ struct KLeaf {
 // dictionary is a contiguous run of the table-global one (global dictId = dictId + lut_off); `dkey` null = an
 // INT / LONG dictionary of consecutive values (value = key_base + dictId).  Typical of bounded integer columns
 // (C1, C2, C5's metrics and keys), it saves a dependent gather per matched doc.
+// Missing global values a segment's accumulator dictionary may have and still be read through the table-global
+// value arrays (KCol.gaps).
+constexpr int kMaxValueGaps = 16;
+
 struct KCol {
   const uint32_t* fwd;
   const int32_t* lut;
@@ -73,6 +77,12 @@ struct KCol {
   int64_t key_base;
   int32_t bits;
   int32_t lut_off;
+  // Accumulator operands with table-global value arrays (runtime.cpp ensure_value_map): dkey / dval are the table's
+  // arrays from the global dictId of the segment's first value on, and local dictId i is at i + the number of global
+  // ids missing from the segment's dictionary below it -- ngaps thresholds in mapped space, applied in order as
+  // i += (i >= gaps[k]) (vidx); 0 for the segment's own arrays or a contiguous run of the global dictionary.
+  int32_t ngaps;
+  uint32_t gaps[kMaxValueGaps];
 };
 
 // Per-plan, per-segment record (uploaded once per plan): a KSegHdr followed by num_cols KCol and num_leaves
@@ -142,6 +152,8 @@ struct KParams {
   // scans stop taking tiles and set stats[5] (BaseCombineOperator.java:79-132 / GroupByCombineOperator.java:193-203
   // give up at the same point; the host then reports the timeout instead of a partial result)
   uint64_t deadline;
+  // diagnostics build only (PGPU_DIAG_WG_TIMES, PGPU_TRACE=wgtimes): per workgroup {start, tile loop end, end, tiles}
+  unsigned long long* diag_times;
 };
 
 // leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to

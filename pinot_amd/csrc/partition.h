@@ -56,6 +56,9 @@ __device__ __forceinline__ uint32_t hpart(const KPartParams& pp, uint32_t hk) {
   return pp.pbits ? hk >> (32 - pp.pbits) : 0u;
 }
 
+// A value stream's dictIds -> their indexes in its value arrays (KCol.gaps; a no-op for the segment's own arrays).
+__device__ __forceinline__ void map_value_ids(const KCol& c, uint32_t (&ids)[16]) { vidx_n(c, ids); }
+
 // Composite keys of docs [32*group + H, +16) of segment S.
 template <int H>
 __device__ __forceinline__ void part_keys(const KParams& p, const SegView& S, int64_t group, int32_t (&key)[16]) {
@@ -92,6 +95,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     const KCol& c = S.cols[pp.stream_col[0]];
     uint32_t ids[16];
     decode_group<H>(c.fwd, c.bits, group, ids);
+    map_value_ids(c, ids);
     int64_t v[16];
     if (c.dkey) {
       gmem<int64_t>* __restrict__ dk = gp(c.dkey);
@@ -113,6 +117,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     const KCol& c = S.cols[pp.stream_col[0]];
     uint32_t ids[16];
     decode_group<H>(c.fwd, c.bits, group, ids);
+    map_value_ids(c, ids);
     uint32_t v[16];
     if (c.dkey) {
       gmem<int64_t>* __restrict__ dk = gp(c.dkey);
@@ -158,6 +163,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   for (int s = 0; s < pp.num_streams; ++s) {
     const KCol& c = S.cols[pp.stream_col[s]];
     decode_group<H>(c.fwd, c.bits, group, ids);
+    map_value_ids(c, ids);
     uint64_t* __restrict__ out = (two ? pp.mid_val : pp.rec_val) + (int64_t)s * pp.rec_cap;
     if (pp.stream_f64[s]) {
       gmem<double>* __restrict__ dv = gp(c.dval);
@@ -223,6 +229,7 @@ __device__ __forceinline__ void part_scatter_half_staged(const KPartParams& pp, 
   const KCol& c = S.cols[pp.stream_col[0]];
   uint32_t ids[16];
   decode_group<H>(c.fwd, c.bits, group, ids);
+  map_value_ids(c, ids);
   int64_t v[16];
   if (c.dkey) {
     gmem<int64_t>* __restrict__ dk = gp(c.dkey);
@@ -524,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void part_split_words_kernel(const KPartPar
   const int tid = threadIdx.x;
   if (pp.base.deadline && pp.base.stats[5]) return;
   const int c = blockIdx.x / pp.chunks_per_coarse, j = blockIdx.x % pp.chunks_per_coarse;
-  const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift), np = p1 - p0;
+  const int p0 = c << pp.cshift, p1 = min(pp.num_parts, (c + 1) << pp.cshift);
   const int NP = 1 << pp.cshift;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
   uint32_t* hist = cnt + NP;
@@ -596,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void part_split_words_kernel(const KPartPar
         bstart[i] = run;
         const uint32_t h = hist[i];
         run += h;
-        cnt[i] = h && i < np ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
+        cnt[i] = h && p0 + i < p1 ? pp.part_start[p0 + i] + atomicAdd(&pp.fine_fill[p0 + i], h) : 0u;
       }
     }
     __syncthreads();

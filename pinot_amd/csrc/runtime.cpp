@@ -451,6 +451,11 @@ struct Column {
   std::shared_ptr<DevMem> lut;      // int32 local -> global dictId; replaced, never rewritten, on dictionary growth
   uint64_t lut_version = ~0ull;
   int32_t lut_off = -1;             // >= 0: the LUT is lut[i] = lut_off + i (KCol.lut_off)
+  // accumulator operand read through the table-global value arrays (ensure_value_map): the global dictId of local
+  // id 0 (-1: the segment's own arrays) and the KCol.gaps thresholds
+  uint64_t vmap_version = ~0ull;
+  int32_t vgap_first = -1;
+  std::vector<uint32_t> vgaps;
   int64_t* d_key = nullptr;
   double* d_val = nullptr;
   bool key_affine = false;          // INT / LONG dictionary of consecutive values: d_key[i] = key_base + i
@@ -511,7 +516,15 @@ struct Segment {
 // versions its records point at.
 struct PlanRefs {
   std::vector<std::shared_ptr<Segment>> segs;
-  std::vector<std::shared_ptr<DevMem>> luts;
+  std::vector<std::shared_ptr<DevMem>> luts;  // LUTs, value maps and table-global value arrays the records point at
+};
+// An accumulator column's value arrays in one plan segment, as planned (ensure_value_map): the segment's own (keys /
+// vals null), or the table's from the segment's first value on, with the gap thresholds (KCol.gaps).
+struct ValMap {
+  const int64_t* keys = nullptr;
+  const double* vals = nullptr;
+  int32_t ngaps = 0;
+  std::array<uint32_t, kMaxValueGaps> gaps{};
 };
 // A group-by key column's LUT in one plan segment, as planned: lut null = consecutive run (global = id + off).
 struct KeyLut {
@@ -621,6 +634,14 @@ struct pgpu_table_s {
   int64_t next_handle = 1;
   std::vector<std::shared_ptr<const Dict>> global;  // current snapshot per column (replaced under mu)
   std::vector<uint64_t> global_version;
+  // Table-global value arrays of accumulator columns (ensure_global_values): the global dictionary's values as
+  // order-preserving int64 keys and as doubles, indexed by global dictId -- one array every segment's gathers share,
+  // instead of each segment's own (C2's md: 100 dictionaries of 800 KB competing for the XCD L2s)
+  struct GlobalValues {
+    uint64_t version = ~0ull;
+    std::shared_ptr<DevMem> keys, vals;
+  };
+  std::vector<GlobalValues> gvalues;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Scratch>> scratch_pool;
   GenScratch gen;
@@ -837,6 +858,74 @@ int ensure_values(pgpu_table_s* t, Segment& s, int col, hipStream_t stream) {
     c.key_affine = span == (__int128)(c.card - 1);
     c.key_base = c.dict.iv[0];
   }
+  return 0;
+}
+
+// Dictionaries of at least this many entries are read through the table-global value arrays when their segment's
+// dictionary lacks at most kMaxValueGaps of the global values (smaller ones stay L2-resident on their own).
+#ifndef PGPU_NO_GLOBAL_VALUES  // (defined only by an A/B build of the library: every segment's own arrays)
+constexpr int32_t kGlobalValuesMinCard = 8192;
+#else
+constexpr int32_t kGlobalValuesMinCard = INT32_MAX;
+#endif
+
+// The table-global value arrays of `col` for its current global dictionary (under the table mutex).
+int ensure_global_values(pgpu_table_s* t, int col, hipStream_t stream) {
+  auto& gv = t->gvalues[col];
+  if (gv.version == t->global_version[col] && gv.keys) return 0;
+  const Dict& g = *t->global[col];
+  const size_t n = std::max<size_t>(g.size(), 1);
+  std::vector<int64_t> key(n, 0);
+  std::vector<double> val(n, 0.0);
+  for (size_t i = 0; i < g.size(); ++i) {
+    if (is_int_type(g.type)) {
+      key[i] = g.iv[i];
+      val[i] = (double)g.iv[i];
+    } else {
+      key[i] = double_key(g.dv[i]);
+      val[i] = g.dv[i];
+    }
+  }
+  auto k = std::make_shared<DevMem>(), v = std::make_shared<DevMem>();
+  HIP_TRY(hipMalloc(&k->p, sizeof(int64_t) * n));
+  HIP_TRY(hipMalloc(&v->p, sizeof(double) * n));
+  HIP_TRY(hipMemcpyAsync(k->p, key.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(v->p, val.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  if (!gv.keys) t->device_bytes += 16 * (int64_t)n;
+  gv.keys = std::move(k);  // the previous arrays live on in the plans that reference them
+  gv.vals = std::move(v);
+  gv.version = t->global_version[col];
+  return 0;
+}
+
+// How (seg, col)'s local dictIds index the table-global value arrays (under the table mutex): from the global id of
+// local id 0 on, skipping the global values the segment's dictionary lacks -- at most kMaxValueGaps of them, as
+// thresholds (KCol.gaps, vidx) -- or not at all (dictionaries below kGlobalValuesMinCard, or more missing values: the
+// segment's own arrays).
+int ensure_value_map(pgpu_table_s* t, Segment& s, int col) {
+  Column& c = s.cols[col];
+  if (c.vmap_version == t->global_version[col]) return 0;
+  c.vgap_first = -1;
+  c.vgaps.clear();
+  c.vmap_version = t->global_version[col];
+  if (c.raw || c.card < kGlobalValuesMinCard) return 0;
+  const Dict& g = *t->global[col];
+  int64_t prev = -1, first = -1;
+  std::vector<uint32_t> gaps;
+  for (int32_t i = 0; i < c.card; ++i) {
+    const int64_t gi = global_index_of(g, c.dict, i);
+    if (gi < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "value missing from the global dictionary (column %d)", col);
+    if (i == 0) first = gi;
+    // each global id skipped before local id i: a threshold at i, in mapped space (+ the thresholds before it)
+    for (int64_t d = i == 0 ? 0 : gi - prev - 1; d > 0; --d) {
+      if ((int)gaps.size() == kMaxValueGaps) return 0;
+      gaps.push_back((uint32_t)(i + (int64_t)gaps.size()));
+    }
+    prev = gi;
+  }
+  c.vgap_first = (int32_t)first;
+  c.vgaps = std::move(gaps);
   return 0;
 }
 
@@ -1099,6 +1188,8 @@ struct pgpu_plan_s {
   std::vector<Segment*> segs;
   std::shared_ptr<PlanRefs> refs;         // keeps segs and the LUTs the records point at alive
   std::vector<KeyLut> key_lut;            // [segment][group-by column] LUT as planned (taken under the table mutex)
+  std::vector<int32_t> val_cols;          // accumulator table columns with table-global value arrays somewhere
+  std::vector<ValMap> val_map;            // [segment][val_cols index] as planned
   const uint32_t* docid_fwd = nullptr;    // the $docId column as planned (identity forward index + values)
   const int64_t* docid_key = nullptr;
   int docid_bits = 0;
@@ -2153,6 +2244,42 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         if (P->slot_tcol[k] != kDocIdColumn) TRY(ensure_values(t, *s, P->slot_tcol[k], stream));
       if (P->first_doc_slot) TRY(ensure_docid(t, s->num_docs, stream));
     }
+    // accumulator columns whose values are gathered (FLOAT / DOUBLE, or integers not consecutive): the table-global
+    // arrays where a segment's dictionary maps onto the global one
+    P->val_cols.clear();
+    for (size_t k = 1; k < P->slot_kind.size(); ++k) {
+      const int c = P->slot_tcol[k];
+      if (c == kDocIdColumn || std::find(P->val_cols.begin(), P->val_cols.end(), c) != P->val_cols.end()) continue;
+      bool any = false;
+      for (Segment* s : P->segs) {
+        const Column& col = s->cols[c];
+        if (col.raw || col.card < kGlobalValuesMinCard || (is_int_type(t->types[c]) && col.key_affine)) continue;
+        TRY(ensure_value_map(t, *s, c));
+        any |= col.vgap_first >= 0;
+      }
+      if (any) {
+        TRY(ensure_global_values(t, c, stream));
+        P->val_cols.push_back(c);
+      }
+    }
+    P->val_map.assign(P->segs.size() * P->val_cols.size(), ValMap{});
+    for (size_t v = 0; v < P->val_cols.size(); ++v) {
+      const int c = P->val_cols[v];
+      const auto& gv = t->gvalues[c];
+      P->refs->luts.push_back(gv.keys);
+      P->refs->luts.push_back(gv.vals);
+      for (size_t i = 0; i < P->segs.size(); ++i) {
+        const Column& col = P->segs[i]->cols[c];
+        ValMap& vm = P->val_map[i * P->val_cols.size() + v];
+        if (col.raw || col.card < kGlobalValuesMinCard || (is_int_type(t->types[c]) && col.key_affine) ||
+            col.vmap_version != t->global_version[c] || col.vgap_first < 0)
+          continue;
+        vm.keys = reinterpret_cast<const int64_t*>(gv.keys->p) + col.vgap_first;
+        vm.vals = reinterpret_cast<const double*>(gv.vals->p) + col.vgap_first;
+        vm.ngaps = (int32_t)col.vgaps.size();
+        std::copy(col.vgaps.begin(), col.vgaps.end(), vm.gaps.begin());
+      }
+    }
     P->docid_fwd = t->d_docid_fwd;
     P->docid_key = t->d_docid_key;
     P->docid_bits = t->docid_bits;
@@ -2504,6 +2631,18 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
           kc[j].dkey = c.key_affine ? nullptr : c.d_key;
           kc[j].key_base = c.key_base;
           kc[j].dval = c.d_val;
+          // or the table-global ones, as planned under the table mutex (ensure_value_map)
+          const int tc = P->query_cols[j];
+          for (size_t v = 0; v < P->val_cols.size(); ++v) {
+            if (P->val_cols[v] != tc) continue;
+            const ValMap& vm = P->val_map[i * P->val_cols.size() + v];
+            if (vm.keys) {
+              kc[j].dkey = vm.keys;
+              kc[j].dval = vm.vals;
+              kc[j].ngaps = vm.ngaps;
+              std::copy(vm.gaps.begin(), vm.gaps.end(), kc[j].gaps);
+            }
+          }
         }
       }
       for (int j = 0; j < nqc; ++j)
@@ -3110,16 +3249,17 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
   // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag): right after the group table when
   // the table is internal, so finalize reads both with one copy
+  constexpr size_t kStatsBytes = 64;
   unsigned long long* stats;
   if (!d_table) {
-    TRY(sc->table.ensure((size_t)X.words * 8 + 64));
+    TRY(sc->table.ensure((size_t)X.words * 8 + kStatsBytes));
     stats = reinterpret_cast<unsigned long long*>(sc->table.as<uint8_t>() + (size_t)X.words * 8);
   } else {
-    TRY(sc->stats.ensure(64));
+    TRY(sc->stats.ensure(kStatsBytes));
     stats = sc->stats.as<unsigned long long>();
   }
   P->d_stats = stats;
-  HIP_TRY(hipMemsetAsync(stats, 0, 64, stream));
+  HIP_TRY(hipMemsetAsync(stats, 0, kStatsBytes, stream));
   X.segrec = sc->segrec.as<uint8_t>();
   X.sets = sc->sets.as<uint32_t>();
   TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
@@ -3318,6 +3458,52 @@ int check_launch_inputs(const pgpu_plan_s* P, hipStream_t stream, const ExecCtx&
   return 0;
 }
 
+// PGPU_TRACE=wgtimes with a PGPU_DIAG_WG_TIMES build: every scan launch is synchronised and its workgroups' start /
+// tile-loop end / end times (wall clock, relative to the earliest start) summarised on stderr -- how much of a launch
+// is its ramp, its tail and the imbalance of the static tile split.
+unsigned long long* g_diag_times = nullptr;
+int diag_wg_times_begin(KParams& kp, int grid, hipStream_t stream) {
+  constexpr int kMaxWgs = 1 << 16;
+  if (grid > kMaxWgs) return 0;
+  if (!g_diag_times) HIP_TRY(hipMalloc(&g_diag_times, (size_t)kMaxWgs * 32));
+  HIP_TRY(hipMemsetAsync(g_diag_times, 0, (size_t)grid * 32, stream));
+  kp.diag_times = g_diag_times;
+  return 0;
+}
+
+int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream_t stream) {
+  if (!kp.diag_times) return 0;
+  std::vector<unsigned long long> h((size_t)grid * 4);
+  HIP_TRY(hipMemcpyAsync(h.data(), kp.diag_times, h.size() * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  int khz = 100000;
+  hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device);
+  const double us = 1000.0 / khz;
+  unsigned long long t0 = ~0ull;
+  for (int b = 0; b < grid; ++b) if (h[4 * b + 2]) t0 = std::min(t0, h[4 * b]);
+  if (t0 == ~0ull) return 0;
+  std::vector<double> st, le, en, tiles;
+  double xcd_end[8] = {0};
+  for (int b = 0; b < grid; ++b) {
+    if (!h[4 * b + 2]) continue;
+    st.push_back((h[4 * b] - t0) * us);
+    le.push_back((h[4 * b + 1] - t0) * us);
+    en.push_back((h[4 * b + 2] - t0) * us);
+    tiles.push_back((double)h[4 * b + 3]);
+    xcd_end[b & 7] = std::max(xcd_end[b & 7], en.back());
+  }
+  auto pct = [](std::vector<double> v, double q) {
+    std::sort(v.begin(), v.end());
+    return v[std::min(v.size() - 1, (size_t)(q * (v.size() - 1) + 0.5))];
+  };
+  fprintf(stderr, "[pgpu] wgtimes grid %d tiles %d: start p50 %.1f max %.1f | loop end p0 %.1f p10 %.1f p50 %.1f p90 %.1f "
+          "max %.1f | end max %.1f us | tiles/wg %.0f..%.0f | xcd end %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f\n",
+          grid, kp.num_tiles, pct(st, 0.5), pct(st, 1.0), pct(le, 0.0), pct(le, 0.1), pct(le, 0.5), pct(le, 0.9),
+          pct(le, 1.0), pct(en, 1.0), pct(tiles, 0.0), pct(tiles, 1.0), xcd_end[0], xcd_end[1], xcd_end[2], xcd_end[3],
+          xcd_end[4], xcd_end[5], xcd_end[6], xcd_end[7]);
+  return 0;
+}
+
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c) {
   Scratch* sc = P->scratch;
   KParams kp = X.kp;
@@ -3441,10 +3627,13 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (launch_partitioned(pp, grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
+    static const bool wg_times = diag("wgtimes");
+    if (wg_times) TRY(diag_wg_times_begin(kp, grid, stream));
     const int rc = launch_filter_groupby(kp, P->mode,
                                          P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0,
                                          grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (wg_times) TRY(diag_wg_times_report(P->table, kp, grid, stream));
   }
   HIP_TRY(hipEventRecord(sc->cev[2 * c + 1], stream));
   if (C.num_tiles > 0 && P->any_leap2 && P->leap_reserved && !P->partitioned) {
@@ -4424,6 +4613,7 @@ int pgpu_table_create(int device, int num_columns, const char* const* names, con
     d->id = g_dict_ids.fetch_add(1);
     t->global.push_back(std::move(d));
     t->global_version.push_back(0);
+    t->gvalues.emplace_back();
   }
   DeviceGuard g(device);
   HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));

@@ -79,6 +79,10 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   // tile loop changes the sparse instance's register allocation (108 -> 134 VGPRs, one wave less per SIMD; an
   // in-loop check cost 18% on C3, measured).  A scan already running is abandoned by the host (wait_plan).
   if (p.deadline && p.stats[5]) return;
+#ifdef PGPU_DIAG_WG_TIMES
+  const unsigned long long diag_t0 = wall_clock64();
+  unsigned long long diag_t1 = 0;
+#endif
 
   if (MODE == MODE_LDS) {
     for (int64_t i = tid; i < table_words; i += kBlock) {
@@ -125,6 +129,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
     int64_t tile_base = 0;
     int nd = 0;
     int stats = 0;  // the segment's KSegHdr.stats
+    // PAIR: the index leaf's directory entry of the current 65536-doc block (8 tiles), wave-uniform
+    int32_t pair_blk = -1;
+    uint64_t pair_e = 0;
     // named registers, not an array: a runtime-guarded array of structs lands in scratch
     LeafReg R0{}, R1{}, R2{}, R3{};
     const int nl = p.num_leaves;
@@ -145,6 +152,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         tile_base = S.hdr->tile_base;
         nd = S.hdr->num_docs;
         stats = S.hdr->stats;
+        pair_blk = -1;
         if (fast) PGPU_LOAD_LEAVES();
       }
       const int64_t lt = t - tile_base;
@@ -168,8 +176,13 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         if (PAIR && !DENSE && !leap && nl == 2 && R0.kind == LEAF_BITDIR && R1.kind == LEAF_RANGE && p.pair_leaves) {
           // index leaf + scan leaf (the indexed C3 shape): both requested together (bitdir_range), applied in order
           uint32_t m0, m1;
-          bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, reinterpret_cast<const uint64_t*>(R0.set),
-                       R0.negate, gclamp, m0, m1);
+          // a tile lies inside one block (256 of its 2048 groups): the block and its entry are wave-uniform
+          const int32_t blk = __builtin_amdgcn_readfirstlane((int32_t)(gclamp >> 11));
+          if (blk != pair_blk) {
+            pair_blk = blk;
+            pair_e = reinterpret_cast<const uint64_t*>(R0.set)[blk];
+          }
+          bitdir_range(R1.fwd, R1.bits, R1.lo, R1.span, R1.negate, pair_e, R0.negate, gclamp, m0, m1);
           if (__any(mask != 0u)) {
             if ((stats >> 4) & 1) in_filter += __popc(mask);
             mask &= m0;
@@ -243,6 +256,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
       for (int k = lane; k < kk; k += 64)
         p.leap_maps[(t_begin + (int64_t)k * t_step) * (kBlock / 64) + wave] = lmaps[k * (kBlock / 64) + wave];
   }
+#ifdef PGPU_DIAG_WG_TIMES
+  diag_t1 = wall_clock64();
+#endif
   // numDocsScanned / numEntriesScannedInFilter: one atomic per workgroup (block_stats_add)
 #if PGPU_STATS_PER_WAVE
   for (int off = 32; off > 0; off >>= 1) matched += __shfl_xor(matched, off);
@@ -280,6 +296,15 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
       for (int64_t i = tid; i < table_words; i += kBlock) out[i] = lds[i];
     }
   }
+#ifdef PGPU_DIAG_WG_TIMES
+  if (tid == 0 && p.diag_times) {
+    unsigned long long* d = p.diag_times + 4 * (int64_t)blockIdx.x;
+    d[0] = diag_t0;
+    d[1] = diag_t1;
+    d[2] = wall_clock64();
+    d[3] = (unsigned long long)kk;
+  }
+#endif
 }
 
 }  // namespace pgpu

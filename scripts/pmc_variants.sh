@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes (scripts/pmc_kernel.sh) of one workload under several env variants: VARIANTS="A=0 B=1|A=1" (| between
+# PMC passes (scripts/pmc_kernel.sh) of one workload under several environment variants (library builds:
+# PGPU_LIB=pinot_amd/libpinotgpu_ab_x.so): VARIANTS="A=0 B=1|A=1" (| between
 # variants, spaces inside one), TAGP=prefix, plus pmc_kernel.sh's KREGEX / ARGS / SQL / PASSES.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 IFS='|' read -ra VS <<< "${VARIANTS:-PGPU_X=0}"

@@ -933,3 +933,65 @@ def test_table_config_roundtrip(gpu_lib):
         assert t.config()["plan_cache"] == 1
     finally:
         t.close()
+
+
+def test_table_global_value_arrays(oracle, gpu_lib):
+    """Accumulator columns with large dictionaries are gathered from the table-global value arrays (runtime.cpp
+    ensure_value_map, KCol.gaps, device.h vidx): a segment whose dictionary lacks a few global values maps its dictIds
+    past them with thresholds, a contiguous run by an offset alone; more than kMaxValueGaps (16) missing values keep the
+    segment's own arrays.  Dense, sparse, partitioned and aggregation-only scans against the oracle, before and after a
+    pin grows the global dictionary (new arrays, new maps)."""
+    rng = np.random.default_rng(77)
+    table_d = np.round(rng.uniform(-1e5, 1e5, 20000), 4)
+    table_d = np.unique(table_d)
+    table_i = np.unique(rng.integers(-10 ** 12, 10 ** 12, 20000))
+    schema = [("g", "INT"), ("f", "INT"), ("x", "DOUBLE"), ("y", "LONG"), ("k", "INT")]
+
+    def seg(n, xs, ys, seed):
+        r = np.random.default_rng(seed)
+        return oracle.make_segment(schema, {"g": r.integers(0, 50, n), "f": r.integers(0, 100, n),
+                                            "x": r.choice(xs, n), "y": r.choice(ys, n),
+                                            "k": r.integers(0, 40000, n)})
+
+    # every value present (forced), except a few single values: single gaps
+    def near_full(vals, drop, n, seed):
+        keep = np.delete(vals, drop)
+        r = np.random.default_rng(seed)
+        return np.concatenate([keep, r.choice(keep, n - len(keep))])
+
+    n = 60000
+    segs = []
+    # single missing values, none (a contiguous run), adjacent ones at both ends, 20 (the segment's own arrays)
+    for i, drop in enumerate(([5, 900, 12345], [], [0, 1, 100, 101, 102, -1], list(range(7, 2000, 99)))):
+        xs = near_full(table_d, drop, n, 10 + i)
+        ys = near_full(table_i, drop, n, 20 + i)
+        s = oracle.make_segment(schema, {"g": np.random.default_rng(i).integers(0, 50, n),
+                                         "f": np.random.default_rng(i + 5).integers(0, 100, n),
+                                         "x": np.random.default_rng(i + 9).permutation(xs),
+                                         "y": np.random.default_rng(i + 7).permutation(ys),
+                                         "k": np.random.default_rng(i + 3).integers(0, 40000, n)})
+        segs.append(s)
+    t, hs = gpu_table(schema, segs)
+    try:
+        queries = ["SELECT SUM(x), MIN(x), MAX(y), SUM(y), AVG(x), COUNT(*) FROM t WHERE f < 60 GROUP BY g",  # dense
+                   "SELECT SUM(x), MAX(x), MIN(y) FROM t WHERE f = 7 GROUP BY g",                          # sparse
+                   "SELECT SUM(y), COUNT(*) FROM t GROUP BY g, k",   # 2M keys: partitioned (one 8-B stream)
+                   "SELECT SUM(x), MIN(y), COUNT(*) FROM t WHERE f < 50"]                                 # agg-only
+        for sql in queries:
+            q = parse_query(sql, num_groups_limit=10 ** 9)
+            if q.group_by:
+                assert_same(t.execute_groupby(hs, q), oracle.run_groupby(schema, segs, q), q, schema)
+            else:
+                r = t.execute_aggregation(hs, q)
+                (exp,) = oracle.run_groupby(schema, segs, q).groups.values()
+                assert r.values[0] == pytest.approx(exp[0], rel=REL)
+                assert r.values[1:] == list(exp[1:])
+        # a pin that adds values grows the global dictionaries: new arrays and maps for the next plans
+        extra = seg(n, np.concatenate([table_d, [1e9, -1e9]]), np.concatenate([table_i, [7, 11]]), 99)
+        hs2 = hs + [t.pin_segment(extra)]
+        segs2 = segs + [extra]
+        for sql in queries[:3]:
+            q = parse_query(sql, num_groups_limit=10 ** 9)
+            assert_same(t.execute_groupby(hs2, q), oracle.run_groupby(schema, segs2, q), q, schema)
+    finally:
+        t.close()

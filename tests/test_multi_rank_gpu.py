@@ -347,3 +347,65 @@ def test_two_rank_query_flow_matches_oracle(oracle, gpu_lib, tmp_path, transport
         og, oe = np.lexsort(keys.T[::-1]), np.lexsort(ek.T[::-1])
         np.testing.assert_array_equal(keys[og], ek[oe], err_msg=wname)
         np.testing.assert_array_equal(vals[:, og], ev[:, oe], err_msg=wname)
+
+
+def _failing_rank_worker(rank, uid, out_dir):
+    """HASH-mode combine where rank 1 passes a plan it never executed (its own check fails): both ranks must return
+    an error, quickly -- rank 0 from the status word of the counts exchange -- and neither may hang in a collective
+    (a rank that failed alone left its peers blocked)."""
+    import time
+    from pinot_amd import _lib as L
+    from pinot_amd.combine import Communicator, combine_mode, combine_plan, union_dictionaries_comm
+    from pinot_amd.executor import GpuTable
+    import _oracle
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    comm = Communicator(L.COMM_HOST, uid, WORLD, rank, 0)
+    comm.set_timeout(60_000)
+    table = GpuTable(SCHEMA, device=0)
+    try:
+        handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(rank * SEGS_PER_RANK + i)))
+                   for i in range(SEGS_PER_RANK)]
+        union_dictionaries_comm(table, ["d", "e", "f", "mi"], comm)
+        q = parse_query(CASES["hash"][0], num_groups_limit=CASES["hash"][1])
+        probe = table.plan(handles, q)
+        mode, kinds = combine_mode(probe, comm, 0)
+        probe.close()
+        assert mode == L.COMBINE_HASH, mode
+        plan = table.plan(handles, q) if rank == 1 else table.plan_execute(handles, q, stream.cuda_stream)
+        t0 = time.monotonic()
+        try:
+            combine_plan(plan, comm, stream.cuda_stream, mode, kinds)
+            outcome = "ok"
+        except L.PinotGpuError as e:
+            outcome = "%d %s" % (e.code, e.message)
+        waited = time.monotonic() - t0
+        stream.synchronize()
+        plan.close()
+        with open(os.path.join(out_dir, "fail_%d.txt" % rank), "w") as f:
+            f.write("%.3f\n%s" % (waited, outcome))
+    finally:
+        table.close()
+        comm.close()
+
+
+@pytest.mark.timeout(200)
+def test_combine_rank_failure_fails_every_rank(gpu_lib, tmp_path):
+    from pinot_amd import _lib as L
+    from pinot_amd.combine import Communicator
+    uid = Communicator.unique_id(L.COMM_HOST)
+    ctx = mp.spawn(_failing_rank_worker, args=(uid, str(tmp_path)), nprocs=WORLD, join=False)
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > 150:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail("ranks did not finish")
+    res = {}
+    for r in range(WORLD):
+        waited, outcome = open(tmp_path / ("fail_%d.txt" % r)).read().split("\n", 1)
+        res[r] = (float(waited), outcome)
+    assert res[1][1].startswith(str(L.PGPU_ERR_INVALID_ARGUMENT)) and "not executed" in res[1][1], res
+    assert res[0][1].startswith(str(L.PGPU_ERR_INVALID_ARGUMENT)) and "rank 1 of 2 failed" in res[0][1], res
+    assert res[0][0] < 30 and res[1][0] < 30, res

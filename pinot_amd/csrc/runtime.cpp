@@ -197,6 +197,7 @@ struct DevBuf {
   size_t cap = 0;
   int ensure(size_t n) {
     if (n <= cap) return 0;
+    if (p && trace_on()) fprintf(stderr, "[pgpu] device buffer grows %zu -> %zu bytes\n", cap, n + n / 4);
     if (p) HIP_TRY(hipFree(p));
     p = nullptr;
     size_t c = std::max<size_t>(n + n / 4, 4096);
@@ -569,6 +570,7 @@ struct Scratch {
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
   // free it while its uploads may still be queued behind other queries' work on a shared stream.
   HostPinned stage, readback, starstage, bitstage, maskstage;
+  std::vector<uint8_t> starrec_sent;  // the star-tree records last uploaded to `starrec` (a repeat skips the copy)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
   // A query that timed out returns while its device work may still run (wait_plan): the scratch goes back to the
@@ -576,6 +578,16 @@ struct Scratch {
   hipEvent_t busy = nullptr;
   bool abandoned = false;
   std::shared_ptr<DeviceImage> image;  // the plan image the last execution read (kept while it may still run)
+  // device bytes held (acquire_scratch prefers the scratch that has grown the most)
+  size_t footprint() const {
+    size_t n = 0;
+    for (const DevBuf* b : {&docbits, &bittasks, &bitblocks, &rawtasks, &segrec, &sets, &slab, &table, &hash_keys,
+                            &stats, &ckeys, &cslots, &counter, &bitmap, &tile_seg, &starrec, &starwork, &part_start,
+                            &block_off, &rec_key, &rec_val, &rec_key32, &stage_keys, &coarse_fill, &fine_fill,
+                            &mid_key, &mid_val, &leap_maps, &mask_jobs, &leaf_masks, &hsort, &part_mm})
+      n += b->cap;
+    return n;
+  }
   void release() {
     if (busy) { hipEventDestroy(busy); busy = nullptr; }
     abandoned = false;
@@ -585,6 +597,7 @@ struct Scratch {
     segrec.release(); tile_seg.release(); sets.release(); slab.release(); table.release(); hash_keys.release(); stats.release();
     ckeys.release(); cslots.release(); counter.release(); bitmap.release(); stage.release(); readback.release();
     starrec.release();
+    starrec_sent.clear();
     starstage.release();
     bitstage.release();
     starwork.release();
@@ -1347,16 +1360,26 @@ int64_t hash_capacity(int64_t groups) {
   return cap;
 }
 
+// The free scratch that has grown the most: a query then finds its buffers at size, where handing out the first free
+// one had a steady stream of repeated queries take a scratch that a smaller query had sized and grow it -- hipFree
+// waits for the whole device (C4's star path at 3 queries in flight: one launch of 7 ms in a 20-query run).
 Scratch* acquire_scratch(pgpu_table_s* t) {
   std::lock_guard<std::mutex> g(t->mu);
+  std::unique_ptr<Scratch>* best = nullptr;
+  size_t best_bytes = 0;
   for (auto& s : t->scratch_pool)
     if (s && (!s->abandoned || hipEventQuery(s->busy) != hipErrorNotReady)) {
-      Scratch* r = s.release();
-      s.reset();
-      r->abandoned = false;
-      return r;
+      const size_t b = s->footprint();
+      if (!best || b > best_bytes) {
+        best = &s;
+        best_bytes = b;
+      }
     }
-  return new Scratch();
+  if (!best) return new Scratch();
+  Scratch* r = best->release();
+  best->reset();
+  r->abandoned = false;
+  return r;
 }
 void release_scratch(pgpu_table_s* t, Scratch* s) {
   if (!s) return;
@@ -1864,6 +1887,9 @@ int plan_star_segment(pgpu_plan_s* P, size_t seg_index, Segment* s, const pgpu_q
 
 struct ExecCtx {
   KParams kp;
+  // PGPU_TRACE=1: host time marks of the execution, printed when it took over a millisecond
+  std::vector<std::pair<const char*, double>> marks;
+  void mark(const char* what) { if (trace_on()) marks.emplace_back(what, now_us()); }
   // where this execution's records, bitsets and tile map live: the scratch, or the cached plan's DeviceImage
   uint8_t* segrec = nullptr;
   uint32_t* sets = nullptr;
@@ -3241,7 +3267,9 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     sc->cev.resize(2 * max_chunks, nullptr);
     for (size_t i = old; i < sc->cev.size(); ++i) HIP_TRY(hipEventCreate(&sc->cev[i]));
   }
+  X.mark("events");
   HIP_TRY(hipEventRecord(sc->ev[0], stream));
+  X.mark("event 0 recorded");
   TRY(sc->sets.ensure(std::max<size_t>(std::max<size_t>(P->set_words.size(), (size_t)P->set_words_bound) * 4, 16)));
   const size_t rec_cap = std::max<size_t>((size_t)P->segs.size() * P->seg_stride, P->segrec.size());
   TRY(sc->segrec.ensure(std::max<size_t>(rec_cap, 16)));
@@ -3259,7 +3287,9 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     stats = sc->stats.as<unsigned long long>();
   }
   P->d_stats = stats;
+  X.mark("buffers");
   HIP_TRY(hipMemsetAsync(stats, 0, kStatsBytes, stream));
+  X.mark("statistics memset queued");
   X.segrec = sc->segrec.as<uint8_t>();
   X.sets = sc->sets.as<uint32_t>();
   TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
@@ -3658,9 +3688,14 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   if (nl == 0) HIP_TRY(hipEventRecord(sc->ev[1], stream));
   if (!P->star.empty()) {
     // star-tree segments: K5 traversal then K6 residual scan + aggregation into the same group table
+    X.mark("before star buffers");
     TRY(sc->starwork.ensure((size_t)P->star_work_bytes + P->star.size() * 8 + 16));
     int64_t* seg_total = reinterpret_cast<int64_t*>(sc->starwork.as<uint8_t>() + P->star_work_bytes);
-    TRY(sc->starrec.ensure(P->star.size() * sizeof(KStarSeg)));
+    {
+      const void* before = sc->starrec.p;
+      TRY(sc->starrec.ensure(P->star.size() * sizeof(KStarSeg)));
+      if (sc->starrec.p != before) sc->starrec_sent.clear();  // a new buffer holds nothing yet
+    }
     std::vector<KStarSeg> recs = P->star;
     for (size_t i = 0; i < recs.size(); ++i) {
       uint8_t* base = sc->starwork.as<uint8_t>() + P->star_work_off[i];
@@ -3672,13 +3707,23 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     }
     for (auto& f : P->star_match_fix)
       recs[std::get<0>(f)].match[std::get<1>(f)] = X.sets + std::get<2>(f);
-    TRY(sc->starstage.ensure(recs.size() * sizeof(KStarSeg)));
-    memcpy(sc->starstage.p, recs.data(), recs.size() * sizeof(KStarSeg));
-    HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, recs.size() * sizeof(KStarSeg), hipMemcpyHostToDevice,
-                           stream));
+    // The records (this scratch's work buffers, the plan's match sets) are the same for every execution of a cached
+    // plan on this scratch: uploaded when they differ from the last upload.  A small host-to-device copy could block
+    // the host for milliseconds behind other streams' work (C4 at 3 queries in flight: 5.4 ms in one execution).
+    const size_t rbytes = recs.size() * sizeof(KStarSeg);
+    X.mark("star buffers + records built");
+    if (sc->starrec_sent.size() != rbytes || memcmp(sc->starrec_sent.data(), recs.data(), rbytes) != 0) {
+      TRY(sc->starstage.ensure(rbytes));
+      memcpy(sc->starstage.p, recs.data(), rbytes);
+      HIP_TRY(hipMemcpyAsync(sc->starrec.p, sc->starstage.p, rbytes, hipMemcpyHostToDevice, stream));
+      sc->starrec_sent.assign(reinterpret_cast<const uint8_t*>(recs.data()),
+                              reinterpret_cast<const uint8_t*>(recs.data()) + rbytes);
+    }
+    X.mark("star records copy queued");
     if (launch_startree_traverse(sc->starrec.as<KStarSeg>(), (int)recs.size(), seg_total, kp.deadline, kp.stats,
                                  stream))
       return fail(PGPU_ERR_DEVICE, "star-tree traversal launch failed: %s", hipGetErrorString(hipGetLastError()));
+    X.mark("K5 launched");
     KStarParams sp;
     memset(&sp, 0, sizeof sp);
     sp.num_wgs = P->star_chunks;
@@ -3706,6 +3751,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
       if (P->mode == MODE_LDS) sp.slab = kp.slab + (X.slabs_used + (int64_t)b * P->star_chunks) * words;
       if (launch_startree_scan(sp, P->mode, P->star_lds_bytes, stream))
         return fail(PGPU_ERR_DEVICE, "star-tree scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+      X.mark("K6 launched");
     }
   }
   if (!P->generic.empty()) {
@@ -3729,6 +3775,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
                            stream));
   }
   HIP_TRY(hipEventRecord(sc->ev[2], stream));
+  X.mark("event 2 recorded");
   if (P->mode == MODE_LDS) {
     // fold every slab written: the scan launches' (back to back) and the star-tree chunks' after them
     const int64_t all = X.slabs_used + (int64_t)P->star_batches * P->star_chunks;
@@ -3750,7 +3797,18 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   HIP_TRY(hipEventRecord(sc->ev[3], stream));
   P->last_stream = stream;
   P->executed = true;
-  if (trace_on()) fprintf(stderr, "[pgpu] execute: %.1f us host\n", now_us() - X.t_start);
+  if (trace_on()) {
+    const double end = now_us();
+    fprintf(stderr, "[pgpu] execute: %.1f us host\n", end - X.t_start);
+    if (end - X.t_start > 1000.0) {
+      double prev = X.t_start;
+      for (const auto& m : X.marks) {
+        fprintf(stderr, "[pgpu]   %s +%.1f us\n", m.first, m.second - prev);
+        prev = m.second;
+      }
+      fprintf(stderr, "[pgpu]   (end) +%.1f us\n", end - prev);
+    }
+  }
   return 0;
 }
 

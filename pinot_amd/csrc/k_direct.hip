@@ -10,10 +10,14 @@
 namespace pgpu {
 
 // variant: 0 the sparse instance, 1 the dense one, 2 the dense one for "simple" plans (aggregate_batch's SIMPLE),
-// 3 the sparse one with the index + scan pair (bitdir_range), 4 the sparse one for pure-AND plans (FAST).
+// 3 the sparse one with the index + scan pair (bitdir_range), 4 the sparse one for pure-AND plans (FAST), 5 that one
+// with 4-doc lane batches (plans of estimated selectivity >= 1/16).
 int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, int variant, int grid, size_t lds_bytes, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (variant == 4)
+  if (variant == 5)
+    hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, false, false, false, true, 4>), dim3(grid), dim3(kBlock),
+                       lds_bytes, s, p);
+  else if (variant == 4)
     hipLaunchKernelGGL((filter_groupby_kernel<PGPU_MODE, false, false, false, true>), dim3(grid), dim3(kBlock),
                        lds_bytes, s, p);
   else if (variant == 3)
@@ -33,7 +37,9 @@ int PGPU_CAT(launch_direct_mode, PGPU_MODE)(const KParams& p, int variant, int g
 int PGPU_CAT(occupancy_direct_mode, PGPU_MODE)(int variant, size_t lds_bytes) {
   int n = 0;
   const hipError_t e =
-      variant == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      variant == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         &n, filter_groupby_kernel<PGPU_MODE, false, false, false, true, 4>, kBlock, lds_bytes)
+      : variant == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                          &n, filter_groupby_kernel<PGPU_MODE, false, false, false, true>, kBlock, lds_bytes)
       : variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, filter_groupby_kernel<PGPU_MODE, false, false, true>,
                                                                    kBlock, lds_bytes)

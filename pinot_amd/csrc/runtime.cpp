@@ -943,6 +943,7 @@ int ensure_value_map(pgpu_table_s* t, Segment& s, int col) {
 }
 
 int64_t padded_fwd_words(int64_t num_docs, int bits);
+int scan_variant(const pgpu_plan_s* P);
 
 // Identity forward index of the virtual $docId column over docs [0, n): Pinot's MSB-first fixed-bit layout of the
 // values 0..n-1 (a sorted "dictionary" of docIds), and the values as int64 (the MIN slot's keys).
@@ -1262,6 +1263,7 @@ struct pgpu_plan_s {
   bool gathers = false;                   // some segment's key LUT or operand dictionary is read (not simple)
   bool pair_variant = false;              // sparse instance with the index + scan pair (variant 3)
   bool fast_variant = false;              // sparse instance for pure-AND plans of <= kFastLeaves leaves (variant 4)
+  bool fast_wide = false;                 // ... with 4-doc lane batches: estimated selectivity >= 1/16 (variant 5)
   bool partitioned = false;               // large dense table: partitioned group-by (partition.h) instead of atomics
   std::vector<LaunchChunk> chunks;        // scan launches (one unless the plan was streamed)
   int launches_done = 0;
@@ -2824,7 +2826,8 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
     // the sparse instance with the index + scan pair: two-leaf AND plans with an in-place index leaf
     P->pair_variant = !P->dense && P->pure_and && P->num_leaves == 2 && P->leaf_kinds[LEAF_BITDIR] > 0;
     P->fast_variant = !P->dense && !P->pair_variant && P->pure_and && P->num_leaves <= kFastLeaves;
-    const int variant = P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0;
+    P->fast_wide = P->fast_variant && P->sel_estimate >= 1.0 / 16;
+    const int variant = scan_variant(P);
     int per_cu;  // resident workgroups per CU
     {
       static std::mutex occ_mu;
@@ -3488,6 +3491,12 @@ int check_launch_inputs(const pgpu_plan_s* P, hipStream_t stream, const ExecCtx&
   return 0;
 }
 
+// The scan instance a plan launches (k_direct.hip): 2 dense "simple", 1 dense, 3 index + scan pair, 5 / 4 pure-AND
+// sparse with 4 / 2-doc lane batches, 0 the general sparse one.
+int scan_variant(const pgpu_plan_s* P) {
+  return P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_wide ? 5 : P->fast_variant ? 4 : 0;
+}
+
 // PGPU_TRACE=wgtimes with a PGPU_DIAG_WG_TIMES build: every scan launch is synchronised and its workgroups' start /
 // tile-loop end / end times (wall clock, relative to the earliest start) summarised on stderr -- how much of a launch
 // is its ramp, its tail and the imbalance of the static tile split.
@@ -3660,7 +3669,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     static const bool wg_times = diag("wgtimes");
     if (wg_times) TRY(diag_wg_times_begin(kp, grid, stream));
     const int rc = launch_filter_groupby(kp, P->mode,
-                                         P->dense_simple ? 2 : P->dense ? 1 : P->pair_variant ? 3 : P->fast_variant ? 4 : 0,
+                                         scan_variant(P),
                                          grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (wg_times) TRY(diag_wg_times_report(P->table, kp, grid, stream));

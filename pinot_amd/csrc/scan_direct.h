@@ -49,7 +49,10 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 // DENSE: the plan expects dense tiles (estimated selectivity >= 1/4, runtime.cpp): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
-template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAST = false>
+// LANE_BATCH: matched docs per aggregate_batch where a lane's 32-doc group has more than 2 -- 4 in the pure-AND sparse
+// instance for plans of estimated selectivity >= 1/16 (C4's scan path at 15 %: 174 -> 150 us), 2 elsewhere (4 cost
+// C3, where that path is rare, 1.5 % -- 710 -> 722 us -- and the dense instance's C2 2 %).
+template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAST = false, int LANE_BATCH = 2>
 #ifndef PGPU_MIN_WAVES
 #define PGPU_MIN_WAVES 1
 #endif
@@ -217,10 +220,8 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         // dense tile: whole-group decode of the group-by / aggregated columns
         aggregate_group<MODE, SIMPLE>(p, S, gclamp, mask, tbl, G);
       } else if (__any(cnt > 2u)) {
-        // dense: the lane's own 32-doc group, LB matched docs per batch (the lines are already cached): 4 in the
-        // sparse instances (C4's scan path at 15 % selectivity: 174 -> 151 us), 2 in the dense ones (the whole-group
-        // decode takes the dense wave-tiles; 4 cost C2 2 %)
-        constexpr int LB = DENSE ? 2 : 4;
+        // dense: the lane's own 32-doc group, LANE_BATCH matched docs per batch (the lines are already cached)
+        constexpr int LB = LANE_BATCH;
         while (__any(mask != 0u)) {
           int64_t doc[LB];
           bool ok[LB];

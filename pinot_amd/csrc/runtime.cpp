@@ -3376,11 +3376,11 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   kp.key_bias = P->key_bias;
   kp.tile_shift = P->tile_shift;
   // Tile order: interleaved (the tiles in flight on an XCD come from ~one segment: its dictionaries stay in that
-  // XCD's L2 for the dense path's per-doc gathers) or chunked (a workgroup's tiles follow each other in one segment:
-  // its records and leaf registers are loaded once per run).
-  {
-    kp.tile_chunks = P->dense ? 0 : 1;
-  }
+  // XCD's L2 for the per-doc gathers) or chunked (a workgroup's tiles follow each other in one segment: its records
+  // and leaf registers are loaded once per run).  Plans with many matches (dense, and the sparse ones of estimated
+  // selectivity >= 1/16) gather enough to want the former: C4's scan path 151 -> 141 us interleaved, where C3
+  // (0.18 %) loses 7 % and the indexed C3 15 % (profiles/r05_ab_summary.txt, session za).
+  kp.tile_chunks = P->dense || P->fast_wide ? 0 : 1;
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.pair_leaves = 1;

@@ -349,6 +349,21 @@ __device__ __forceinline__ SegView seg_view(const KParams& p, int seg) {
   return v;
 }
 
+// Word j of a compact slot column at `width` bytes (two's complement, little-endian).
+__device__ __forceinline__ void put_compact(uint8_t* o, int64_t j, int width, uint64_t v) {
+  switch (width) {
+    case 1: o[j] = (uint8_t)v; break;
+    case 2: reinterpret_cast<uint16_t*>(o)[j] = (uint16_t)v; break;
+    case 3:
+      o[3 * j] = (uint8_t)v;
+      o[3 * j + 1] = (uint8_t)(v >> 8);
+      o[3 * j + 2] = (uint8_t)(v >> 16);
+      break;
+    case 4: reinterpret_cast<uint32_t*>(o)[j] = (uint32_t)v; break;
+    default: reinterpret_cast<uint64_t*>(o)[j] = v; break;
+  }
+}
+
 __device__ __forceinline__ uint64_t slot_init(int kind) {
   if (kind == SLOT_MIN_KEY) return (uint64_t)INT64_MAX;
   if (kind == SLOT_MAX_KEY) return (uint64_t)INT64_MIN;

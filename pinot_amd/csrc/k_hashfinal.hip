@@ -84,13 +84,7 @@ __global__ __launch_bounds__(256) void hash_compact_kernel(const uint64_t* __res
     else reinterpret_cast<uint64_t*>(out)[r] = e[0];
     for (int s = 0; s < num_slots; ++s) {
       const uint64_t v = e[1 + s];
-      uint8_t* o = out + sw.off[s];
-      switch (sw.w[s]) {
-        case 1: o[r] = (uint8_t)v; break;
-        case 2: reinterpret_cast<uint16_t*>(o)[r] = (uint16_t)v; break;
-        case 4: reinterpret_cast<uint32_t*>(o)[r] = (uint32_t)v; break;
-        default: reinterpret_cast<uint64_t*>(o)[r] = v; break;
-      }
+      put_compact(out + sw.off[s], r, sw.w[s], v);
     }
   }
 }

@@ -304,8 +304,13 @@ __device__ __forceinline__ void part_count_half(const KPartParams& pp, const Seg
 // one-word records staged per wave, part_scatter_half_staged).  LDS: [u32 histogram of num_parts (K8a) / cursors of
 // num_coarse (K8c)] [filter stack] and, staged, from u32 word pp.stage_off one region of kStageWaveWords32 / 64 words
 // per wave (part_pass_lds).
+// K8a / K8c held to 4 waves per SIMD (128 VGPRs): the staged K8c compiled to 130 and ran 3 (C5: K8c 403 -> 355 us,
+// K8a 147 -> 126 us with the larger grid they share; r05 session zc)
+#ifndef PGPU_PART_PASS_MIN_WAVES
+#define PGPU_PART_PASS_MIN_WAVES 4
+#endif
 template <bool SCATTER, int STAGE = 0>
-__global__ __launch_bounds__(kBlock) void part_pass_kernel(const KPartParams pp) {
+__global__ __launch_bounds__(kBlock, PGPU_PART_PASS_MIN_WAVES) void part_pass_kernel(const KPartParams pp) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const KParams& p = pp.base;
   const int tid = threadIdx.x;

@@ -4235,6 +4235,12 @@ int pgpu::result_expand(pgpu_result_s* R) {
       switch (R->cwidth[s]) {
         case 1: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int8_t*>(src)[r]; break;
         case 2: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int16_t*>(src)[r]; break;
+        case 3:  // 24-bit little-endian, sign-extended
+          for (int64_t r = r0; r < r1; ++r) {
+            const uint32_t u = (uint32_t)src[3 * r] | (uint32_t)src[3 * r + 1] << 8 | (uint32_t)src[3 * r + 2] << 16;
+            dst[r] = (uint64_t)(int64_t)((int32_t)(u << 8) >> 8);
+          }
+          break;
         case 4: for (int64_t r = r0; r < r1; ++r) dst[r] = (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(src)[r]; break;
         default: memcpy(dst + r0, reinterpret_cast<const uint64_t*>(src) + r0, (size_t)(r1 - r0) * 8); break;
       }

@@ -410,7 +410,7 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned)
     fewer docs than keys."""
     rng = np.random.default_rng(docs)
     schema = [("k1", "INT"), ("k2", "INT"), ("k3", "INT"), ("m", "INT"), ("x", "DOUBLE"), ("n", "INT"), ("l", "LONG"),
-              ("q", "INT")]
+              ("q", "INT"), ("r", "INT")]
     segs = []
     for _ in range(2):
         segs.append(oracle.make_segment(schema, {"k1": rng.integers(0, 400, size=docs),
@@ -420,7 +420,8 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned)
                                                  "x": rng.uniform(-1e6, 1e6, size=docs),
                                                  "n": rng.integers(-2 ** 31, 2 ** 31, size=docs),
                                                  "l": rng.integers(-2 ** 40, 2 ** 40, size=docs),
-                                                 "q": rng.integers(-500, 500, size=docs)}))
+                                                 "q": rng.integers(-500, 500, size=docs),
+                                                 "r": rng.integers(-200000, 200000, size=docs)}))
     t, hs = gpu_table(schema, segs, None if partitioned else {"partitioned_group_by": 0})
     try:
         q = parse_query("SELECT SUM(m), COUNT(*), MIN(x), MAX(m), AVG(x) FROM t GROUP BY k1, k2, k3",
@@ -446,7 +447,9 @@ def test_high_cardinality_ordered_compaction(oracle, gpu_lib, docs, partitioned)
                     "SELECT SUM(l), MAX(l), MIN(n), COUNT(*) FROM t GROUP BY k1, k2, k3",
                     # packed records of filtered docs: K8c's staged write-out with partial lane masks
                     "SELECT SUM(m), COUNT(*) FROM t WHERE q < 0 OR m > 900 GROUP BY k1, k2, k3",
-                    "SELECT COUNT(*) FROM t GROUP BY k1, k2, k3"):  # no value stream at all
+                    "SELECT COUNT(*) FROM t GROUP BY k1, k2, k3",  # no value stream at all
+                    # sums past 16 bits and within 24, negative included: 3-byte words in the compact result form
+                    "SELECT SUM(r), MIN(r), COUNT(*) FROM t GROUP BY k1, k2, k3"):
             qi = parse_query(sql, num_groups_limit=10 ** 7)
             assert_same(t.execute_groupby(hs, qi),
                         oracle.run_groupby(schema, segs, qi, combine=False, max_initial_capacity=10000), qi, schema)

@@ -165,3 +165,13 @@ def test_merge_partial_arrays_is_the_broker_merge():
         e = expect[int(k)]
         assert list(vals[:, i]) == [e[0], e[1], e[2], e[3], e[4]] and cnts[4, i] == e[5]
     assert stats == (2000, 2000, 4000, 2000)
+
+
+def test_parse_config_fields():
+    """bench.py --config: pgpu_config fields as integers / floats; the names must be the ABI's (GpuTable rejects
+    unknown ones)."""
+    from pinot_amd import _lib as L
+    cfg = bench.parse_config("dense_selectivity=0.5,plan_cache=0, stream_chunks=3")
+    assert cfg == {"dense_selectivity": 0.5, "plan_cache": 0, "stream_chunks": 3}
+    assert set(cfg) <= set(L.CONFIG_FIELDS)
+    assert bench.parse_config(None) == {} and bench.parse_config("") == {}

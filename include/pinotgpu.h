@@ -328,6 +328,7 @@ typedef struct pgpu_comm_s* pgpu_comm;
 #define PGPU_COMM_ID_BYTES 128
 int pgpu_comm_unique_id(int32_t kind, void* id /* PGPU_COMM_ID_BYTES */);
 int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int32_t device, pgpu_comm* out);
+/* Drops the handle; the communicator goes with the last plan combined on it (pgpu_plan_finalize / _destroy). */
 int pgpu_comm_destroy(pgpu_comm comm);
 int pgpu_comm_rank(pgpu_comm comm, int32_t* rank, int32_t* nranks);
 /* Host memory, blocking: recv[nranks * bytes] = every rank's `bytes` bytes in rank order (dictionary unions, the
@@ -342,6 +343,17 @@ int pgpu_comm_allgather(pgpu_comm comm, const void* send, int64_t bytes, void* r
 int pgpu_comm_set_timeout(pgpu_comm comm, int64_t timeout_ms);
 /* Gives the communicator up from any thread (a server shutting a query down); see pgpu_comm_set_timeout. */
 int pgpu_comm_abort(pgpu_comm comm);
+/* *aborted = 1 once the communicator was given up (a wait on peers expired, or pgpu_comm_abort): every collective on
+ * it fails with PGPU_ERR_DEVICE until pgpu_comm_recreate. */
+int pgpu_comm_status(pgpu_comm comm, int32_t* aborted);
+/* Collective over the handle's ranks: a fresh communicator of the same transport, ranks and device from a new id
+ * (made by one rank with pgpu_comm_unique_id and handed to the others out of band, as for pgpu_comm_create -- the
+ * aborted one cannot carry it), replacing the handle's; the timeout carries over.  The recovery after one rank's
+ * failure aborted the communicator (BaseCombineOperator.java:101-107, 193-203: a failed or timed-out combine fails
+ * that query only, the server keeps serving): every rank calls it, then the next query combines as before.  Plans
+ * combined on the old communicator keep it alive until they are finalized or destroyed.  No other call may use the
+ * handle while it runs. */
+int pgpu_comm_recreate(pgpu_comm comm, const void* id);
 
 /* How the ranks' partial results of one query merge. */
 #define PGPU_COMBINE_LOCAL 0          /* one rank: nothing to merge */
@@ -397,9 +409,11 @@ int pgpu_plan_scanned_segments(pgpu_plan plan, uint8_t* out);
  * leaf_masks[i] its matching docs (bit d % 32 of word d / 32; may be NULL for EMPTY / ALL leaves).  Pinot's
  * iterators (AndDocIdSet / OrDocIdSet merging, SVScanDocIdIterator.applyAnd, AndDocIdIterator leap-frog,
  * OrDocIdIterator) are replayed over the sets.  The plans compute the same statistic on the device; this entry is
- * the host form (a caller holding the doc sets, tests). */
+ * the host form (a caller holding the doc sets, tests).  PGPU_LEAF_RANGE_INDEX (RangeIndexBasedFilterOperator) is an
+ * index-based leaf ranked after the bitmap leaves; the entries of its own partial-match scan are not included (the
+ * caller adds them: pgpu_range_index_partial_entries). */
 enum pgpu_leaf_type { PGPU_LEAF_EMPTY = 0, PGPU_LEAF_MATCH_ALL = 1, PGPU_LEAF_SCAN = 2, PGPU_LEAF_SORTED = 3,
-                      PGPU_LEAF_BITMAP = 4 };
+                      PGPU_LEAF_BITMAP = 4, PGPU_LEAF_RANGE_INDEX = 5 };
 int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t num_filter_ops, const int32_t* leaf_types,
                                 const uint32_t* const* leaf_masks, int32_t num_leaves, int32_t num_docs,
                                 int64_t* out);
@@ -463,7 +477,10 @@ int pgpu_result_key_dictionary(pgpu_result r, int key, uint64_t* snapshot_id, in
 int pgpu_result_key_dictionary_i64(pgpu_result r, int key, int64_t* out);
 int pgpu_result_key_dictionary_f64(pgpu_result r, int key, double* out);
 int pgpu_result_key_dictionary_str(pgpu_result r, int key, uint8_t* blob, int64_t blob_cap, int64_t* offsets);
-/* [n][num_group_by] global dictionary ids, groups ordered by ascending composite key. */
+/* [n][num_group_by] global dictionary ids, in the result's group order: ascending composite key for dense tables
+ * (Pinot's ARRAY / INT_MAP holders) and hash-mode results below 4096 groups; larger hash-mode results (the LONG_MAP
+ * holder, whose iterator runs in fastutil hash order) come in partition order, which may differ between runs.  The
+ * trims (pgpu_result_trim_sql / _trim_pql) compare composite keys themselves, so their output never depends on it. */
 int pgpu_result_group_ids(pgpu_result r, int32_t* out);
 /* Column `key` of the above ([n] dictIds of group-by column `key`): a plain copy, the layout the result holds. */
 int pgpu_result_group_ids_column(pgpu_result r, int key, int32_t* out);
@@ -557,6 +574,32 @@ int pgpu_attach_inverted_index(pgpu_table table, int64_t segment_handle, int32_t
  * cardinalities (num_docs for a single-value column's complete index). */
 int pgpu_inverted_index_check(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
                               int64_t* total_docs);
+
+/* A range index (`<column>.bitmap.range`, DefaultIndexReaderProvider.newRangeIndexReader,
+ * seglocal/segment/index/readers/DefaultIndexReaderProvider.java:128-139) of a dictionary-encoded column of a pinned
+ * segment.  A RANGE predicate on the column (unless it is sorted) then runs as RangeIndexBasedFilterOperator
+ * (FilterOperatorUtils.java:57-62): an index-based leaf, ordered after the bitmap leaves in an AND (:143-178), whose
+ * docs are exactly the predicate's matches (read here from the forward index) and whose numEntriesScannedInFilter is
+ * its partial-match scan (RangeIndexBasedFilterOperator.java:110-126):
+ *   version 1 (RangeIndexCreator / RangeIndexReaderImpl): header (version, value type "INT", range count, the ranges'
+ *             first dictIds + the last range's end, bitmap offsets) and one Roaring bitmap per range, all read and
+ *             validated; the partial matches are the first and last ranges the predicate touches
+ *             (RangeIndexReaderImpl.java:198-264);
+ *   version 2 (BitSlicedRangeIndexCreator / BitSlicedRangeIndexReader): exact, no partial matches (0 entries); only
+ *             the header is read.
+ * Another version is skipped as Pinot skips it (no range index, PGPU_OK); a malformed version-1 file fails with
+ * PGPU_ERR_INVALID_ARGUMENT; raw (no-dictionary) columns: PGPU_ERR_UNSUPPORTED.  Re-attaching replaces the index;
+ * num_bytes = 0 detaches it.  Plans created before keep what they planned with. */
+int pgpu_attach_range_index(pgpu_table table, int64_t segment_handle, int32_t column, const void* bytes,
+                            int64_t num_bytes);
+/* Host check of a range index file without a table: *version (0 = not a range index Pinot loads), *num_ranges and
+ * the documents of its ranges (total_docs, the column's docs for a complete index). */
+int pgpu_range_index_check(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
+                           int32_t* version, int32_t* num_ranges, int64_t* total_docs);
+/* numEntriesScannedInFilter of RangeIndexBasedFilterOperator for the dictId range [lo, hi] (inclusive) over a range
+ * index file: the documents of its partial-match bitmap (0 for version 2). */
+int pgpu_range_index_partial_entries(const void* bytes, int64_t num_bytes, int32_t cardinality, int32_t num_docs,
+                                     int32_t lo, int32_t hi, int64_t* entries);
 
 /* Host-side reader of a raw forward index (PGPU_FWD_RAW_FIXED bytes; FixedByteChunkSVForwardIndexReader.readValuesSV
  * over every chunk, LZ4 chunks decompressed as LZ4Decompressor / LZ4WithLengthDecompressor do): num_docs values of a

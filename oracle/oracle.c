@@ -727,10 +727,12 @@ static inline int pred_apply(const pred_eval* e, int id) {
 /* Operator tree after FilterPlanNode.constructPhysicalOperator (core/plan/FilterPlanNode.java:146-247) and
  * FilterOperatorUtils (:42-135): EMPTY, MATCH_ALL, leaf operators (scan / sorted-index / bitmap-index), AND, OR,
  * NOT.  Leaf choice = FilterOperatorUtils.getLeafFilterOperator (:42-82): RANGE on a sorted column ->
- * SortedIndexBasedFilterOperator, else scan (no range indexes here); EQ / NOT_EQ / IN / NOT_IN on a sorted column
+ * SortedIndexBasedFilterOperator, on a column with a range index -> RangeIndexBasedFilterOperator, else scan;
+ * EQ / NOT_EQ / IN / NOT_IN on a sorted column
  * -> sorted, else on a column with an inverted index -> BitmapBasedFilterOperator, else scan.  NOT is not part of
  * the 0.10 FilterContext; it is modelled as a scan-based iterator over its child (match = child does not match). */
-enum { FN_EMPTY = 0, FN_ALL = 1, FN_SCAN = 2, FN_AND = 3, FN_OR = 4, FN_NOT = 5, FN_SORTED = 6, FN_BITMAP = 7 };
+enum { FN_EMPTY = 0, FN_ALL = 1, FN_SCAN = 2, FN_AND = 3, FN_OR = 4, FN_NOT = 5, FN_SORTED = 6, FN_BITMAP = 7,
+       FN_RANGEIDX = 8 };
 typedef struct fnode {
   int type;
   int pred;              /* leaves: predicate index */
@@ -745,11 +747,74 @@ static void fn_free(fnode* n) {
   free(n->child); free(n);
 }
 
+/* ---- range index (RangeIndexReaderImpl / BitSlicedRangeIndexReader, seglocal/segment/index/readers/): the reader a
+ * column's `.bitmap.range` bytes give (DefaultIndexReaderProvider.newRangeIndexReader :128-139: version 1 or 2, any
+ * other version is skipped -- no range index). */
+static int32_t be_i32(const uint8_t* b) {
+  return (int32_t)(((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]);
+}
+static int64_t be_i64(const uint8_t* b) { return (int64_t)(((uint64_t)(uint32_t)be_i32(b) << 32) | (uint32_t)be_i32(b + 4)); }
+static int range_index_version(const or_column* c) {
+  if (!c->range_index || c->range_index_len < 4 || c->raw) return 0;
+  int v = be_i32(c->range_index);
+  return v == 1 || v == 2 ? v : 0;
+}
+/* ImmutableRoaringBitmap.getCardinality of a portable serialisation: the sum of the containers' cardinalities, read
+ * from the descriptive header (cookie 12346: u32 size; 12347 | (size - 1) << 16: run-container bitmap) -- each
+ * container's (u16 key, u16 cardinality - 1). */
+static int64_t roaring_card(const uint8_t* b, int64_t n) {
+  if (n < 4) return -1;
+  uint32_t cookie = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+  int64_t size, pos;
+  if ((cookie & 0xFFFF) == 12347) { size = (cookie >> 16) + 1; pos = 4 + (size + 7) / 8; }
+  else if (cookie == 12346) {
+    if (n < 8) return -1;
+    size = (int64_t)((uint32_t)b[4] | ((uint32_t)b[5] << 8) | ((uint32_t)b[6] << 16) | ((uint32_t)b[7] << 24));
+    pos = 8;
+  } else return -1;
+  if (pos + size * 4 > n) return -1;
+  int64_t card = 0;
+  for (int64_t i = 0; i < size; i++) card += (int64_t)((uint32_t)b[pos + 4 * i + 2] | ((uint32_t)b[pos + 4 * i + 3] << 8)) + 1;
+  return card;
+}
+/* RangeIndexBasedFilterOperator.getNextBlock (:57-129) entries for the dictIds [start, end): the size of
+ * getPartiallyMatchingDocIds(startDictId, endDictId - 1), which its ScanBasedFilterOperator's applyAnd scans; 0 for a
+ * bit-sliced (exact) index.  Version 1 layout (RangeIndexCreator.seal, big-endian): version, value type name, range
+ * count R, R range starts + the last range's end (INT: dictIds), R + 1 bitmap offsets, the bitmaps. */
+static int64_t range_partial_entries(const or_column* c, int start, int end) {
+  if (range_index_version(c) != 1) return 0;
+  const uint8_t* b = c->range_index;
+  int64_t off = 4;
+  int32_t tlen = be_i32(b + off);
+  off += 4 + tlen;
+  int32_t R = be_i32(b + off);
+  off += 4;
+  const uint8_t* starts = b + off;          /* _rangeStartArray, then _lastRangeEnd */
+  const uint8_t* offs = b + off + 4 * ((int64_t)R + 1); /* _bitmapIndexOffset */
+  int first = -2, last = -2;
+  int vals[2] = {start, end - 1};
+  for (int k = 0; k < 2; k++) { /* findRangeId (RangeIndexReaderImpl.java:198-205) */
+    int id = -2;
+    for (int i = 0; i < R; i++)
+      if (vals[k] < be_i32(starts + 4 * i)) { id = i - 1; break; }
+    if (id == -2) id = vals[k] <= be_i32(starts + 4 * R) ? R - 1 : R;
+    if (k == 0) first = id; else last = id;
+  }
+  int out_first = first < 0 || first >= R, out_last = last < 0 || last >= R;
+#define RANGE_DOCS(i) roaring_card(b + be_i64(offs + 8 * (int64_t)(i)), be_i64(offs + 8 * ((int64_t)(i) + 1)) - be_i64(offs + 8 * (int64_t)(i)))
+  /* getPartialMatchesInRange (:252-260): the first and last ranges (disjoint docs; OR of a range with itself is it) */
+  if (out_first) return out_last ? 0 : RANGE_DOCS(last);
+  if (out_last) return RANGE_DOCS(first);
+  return first == last ? RANGE_DOCS(first) : RANGE_DOCS(first) + RANGE_DOCS(last);
+#undef RANGE_DOCS
+}
+
 /* reorderAndFilterChildOperators priorities (FilterOperatorUtils.java:143-178). */
 static int and_priority(const fnode* n) {
   switch (n->type) {
     case FN_SORTED: return 0;
     case FN_BITMAP: return 1;
+    case FN_RANGEIDX: return 2; /* RangeIndexBasedFilterOperator */
     case FN_AND: return 3;
     case FN_OR: return 4;
     default: return 5; /* scan (single-value columns), NOT */
@@ -773,6 +838,7 @@ static fnode* build_filter_tree(const or_segment* seg, const or_query* q, const 
       else {
         int type = FN_SCAN;
         if (c->is_sorted) type = FN_SORTED;                                    /* :57-58, :73-74 */
+        else if (pr->type == OR_PRED_RANGE && range_index_version(c)) type = FN_RANGEIDX; /* :60-62 */
         else if (pr->type != OR_PRED_RANGE && c->has_inverted) type = FN_BITMAP; /* :76-77 */
         n = fn_new(type);
         n->pred = op->arg;
@@ -841,7 +907,7 @@ static int node_match(const fnode* n, const or_segment* seg, const pred_eval* ev
   switch (n->type) {
     case FN_EMPTY: return 0;
     case FN_ALL: return 1;
-    case FN_SCAN: case FN_SORTED: case FN_BITMAP: {
+    case FN_SCAN: case FN_SORTED: case FN_BITMAP: case FN_RANGEIDX: {
       const or_column* c = &seg->columns[q->predicates[n->pred].column];
       if (evals[n->pred].kind == 5) return raw_apply(&evals[n->pred], doc);
       return pred_apply(&evals[n->pred], fixedbit_read(c->fwd, doc, c->bits));
@@ -865,6 +931,7 @@ typedef struct iter {
   int type;
   int next_doc;            /* scan / idx / and / all */
   int64_t scanned;         /* scan: _numEntriesScanned */
+  int64_t partial;         /* idx of a RangeIndexBasedFilterOperator: its partial-match scan's entries */
   const fnode* node;       /* scan: the leaf (or NOT) node */
   uint64_t* bits;          /* idx: docId set */
   int sorted;              /* idx: a SortedDocIdIterator */
@@ -1028,10 +1095,14 @@ static iter* it_build(const fnode* n, const or_segment* seg, const pred_eval* ev
       it->node = n;
       return it;
     }
-    case FN_SORTED: case FN_BITMAP: {
+    case FN_SORTED: case FN_BITMAP: case FN_RANGEIDX: {
       uint64_t* bits = calloc((size_t)(nw ? nw : 1), 8);
       for (int d = 0; d < nd; d++) if (node_match(n, seg, evals, q, d)) bits[d >> 6] |= 1ull << (d & 63);
-      return it_new_idx(bits, n->type == FN_SORTED, seg, evals, q, pool);
+      iter* it = it_new_idx(bits, n->type == FN_SORTED, seg, evals, q, pool);
+      if (n->type == FN_RANGEIDX) /* matches | scan(partial matches): the predicate's docs, BitmapDocIdSet */
+        it->partial = range_partial_entries(&seg->columns[q->predicates[n->pred].column], evals[n->pred].start,
+                                            evals[n->pred].end);
+      return it;
     }
     default: break;
   }
@@ -1091,7 +1162,7 @@ static iter* it_build(const fnode* n, const or_segment* seg, const pred_eval* ev
 }
 static int64_t pool_scanned(iter_pool* p) {
   int64_t s = 0;
-  for (int i = 0; i < p->n; i++) if (p->all[i]->type == IT_SCAN) s += p->all[i]->scanned;
+  for (int i = 0; i < p->n; i++) s += (p->all[i]->type == IT_SCAN ? p->all[i]->scanned : 0) + p->all[i]->partial;
   return s;
 }
 static void pool_free(iter_pool* p) {

@@ -55,6 +55,10 @@ typedef struct {
                            FixedByteChunkSVForwardIndexWriter bytes (PASS_THROUGH chunks) */
   int32_t raw;          /* 1: no-dictionary column (cardinality 0), values read by FixedByteChunkSVForwardIndexReader */
   int64_t fwd_len;      /* bytes of fwd (raw columns: the chunk file, whose last chunk runs to its end) */
+  const uint8_t* range_index; /* `<column>.bitmap.range` bytes (NULL: none): a RANGE predicate on the unsorted column
+                                 runs as RangeIndexBasedFilterOperator (FilterOperatorUtils.java:57-62) -- version 1
+                                 (RangeIndexReaderImpl) or 2 (BitSlicedRangeIndexReader); other versions are skipped */
+  int64_t range_index_len;
 } or_column;
 
 /* FixedByteChunkSVForwardIndexReader.getInt / getLong / getFloat / getDouble on an uncompressed (PASS_THROUGH)

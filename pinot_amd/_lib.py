@@ -66,7 +66,7 @@ class PredicateC(ctypes.Structure):
 OPT_NO_STAR_TREE = 1
 OPT_SQL_GROUP_BY = 2
 OPT_NO_PLAN_CACHE = 4
-LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP = 0, 1, 2, 3, 4
+LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP, LEAF_RANGE_INDEX = 0, 1, 2, 3, 4, 5
 
 
 ORDER_GROUP_BY, ORDER_AGGREGATION = 0, 1
@@ -226,6 +226,11 @@ _PROTOS = {
     "pgpu_comm_allgather": (c_int, [c_voidp, c_voidp, c_i64, c_voidp]),
     "pgpu_comm_set_timeout": (c_int, [c_voidp, c_i64]),
     "pgpu_comm_abort": (c_int, [c_voidp]),
+    "pgpu_comm_status": (c_int, [c_voidp, c_i32p]),
+    "pgpu_attach_range_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),
+    "pgpu_range_index_check": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32p, c_i32p, c_i64p]),
+    "pgpu_range_index_partial_entries": (c_int, [c_voidp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i64p]),
+    "pgpu_comm_recreate": (c_int, [c_voidp, c_voidp]),
     "pgpu_plan_combine_mode": (c_int, [c_voidp, c_voidp, c_i64, c_i32p, c_i32p]),
     "pgpu_plan_combine": (c_int, [c_voidp, c_voidp, c_voidp, c_voidp, c_i32, c_i32p, c_voidp, c_i64p, c_i64p]),
     "pgpu_result_combine_rows": (c_int, [c_voidp, c_voidp, ctypes.POINTER(c_voidp)]),
@@ -266,8 +271,15 @@ def load(path=None):
     except ImportError:
         pass
     lib = ctypes.CDLL(p)
+    # an A/B build of an earlier tree (PGPU_LIB, scripts/ab_lib.sh) may lack entry points added since; the
+    # in-tree library must export every one
+    ab = os.path.abspath(p) != os.path.abspath(LIB_PATH)
     for name, (res, args) in _PROTOS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and ab:
+            continue
+        if fn is None:
+            raise ImportError("libpinotgpu.so does not export %s (rebuild it)" % name)
         fn.restype = res
         fn.argtypes = args
     if lib.pgpu_abi_version() != 3:

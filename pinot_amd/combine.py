@@ -307,6 +307,19 @@ class Communicator:
     def abort(self):
         L.check(self.lib.pgpu_comm_abort(self.handle))
 
+    @property
+    def aborted(self):
+        """pgpu_comm_status: the communicator was given up (an expired wait on a peer, or abort())."""
+        v = ctypes.c_int32()
+        L.check(self.lib.pgpu_comm_status(self.handle, ctypes.byref(v)))
+        return bool(v.value)
+
+    def recreate(self, uid):
+        """pgpu_comm_recreate (collective): a fresh communicator of the same ranks from a new id, replacing an aborted
+        one -- the server keeps serving after one rank's failed combine."""
+        buf = ctypes.create_string_buffer(bytes(uid), L.COMM_ID_BYTES)
+        L.check(self.lib.pgpu_comm_recreate(self.handle, buf))
+
     def allgather(self, data):
         """Every rank's `data` (bytes of one length on every rank), in rank order."""
         data = bytes(data)

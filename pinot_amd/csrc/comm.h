@@ -14,6 +14,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 
 #include "../../include/pinotgpu.h"
 
@@ -74,6 +75,10 @@ int comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank, int3
 
 }  // namespace pgpu
 
+// Shared ownership: a plan combined on the communicator keeps it alive (pgpu_plan_s::comm_used: finalize reads its
+// timeout and may abort it) after pgpu_comm_destroy has dropped the caller's handle -- e.g. a server that replaces an
+// aborted communicator while other plans combined on it are still unfinalized.
 struct pgpu_comm_s {
-  pgpu::Comm* impl = nullptr;
+  std::shared_ptr<pgpu::Comm> impl;
+  int32_t kind = PGPU_COMM_RCCL;  // the transport pgpu_comm_recreate builds the replacement on
 };

@@ -21,6 +21,17 @@ template <typename T>
 using gmem = const __attribute__((address_space(1))) T;
 template <typename T>
 __device__ __forceinline__ gmem<T>* gp(const T* p) { return (gmem<T>*)p; }
+// Reads of the plan's segment records and tile map, which no kernel writes: through the constant address space, so
+// their wave-uniform loads stay scalar loads (SMEM) whatever the kernel stores elsewhere.  Through generic or global
+// pointers the compiler proves a load unclobbered only when no store or atomic can run before it, so a global atomic
+// ahead of the tile loop (the run-time tile claims) had turned them into vector loads: the sparse scan instances went
+// 112 -> 145 VGPRs (3 waves per SIMD instead of 4).
+template <typename T>
+using cmem = const __attribute__((address_space(4))) T;
+using KColC = cmem<KCol>;
+using KLeafC = cmem<KLeaf>;
+template <typename T>
+__device__ __forceinline__ cmem<T>* cp(const T* p) { return (cmem<T>*)p; }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -311,27 +322,27 @@ __device__ __forceinline__ uint32_t raw_group_mask(int kind, int64_t lo, int64_t
   return m;
 }
 
-__device__ __forceinline__ uint32_t leaf_mask(const KLeaf& L, const KCol& C, int64_t group) {
+__device__ __forceinline__ uint32_t leaf_mask(KLeafC& L, KColC& C, int64_t group) {
   return leaf_eval(L.kind, L.negate, L.lo, L.span, L.set, C.fwd, C.bits, group);
 }
 
 // ---------------------------------------------------------------------------------------------- helpers
 struct SegView {
-  const KSegHdr* hdr;
-  const KCol* cols;
-  const KLeaf* leaves;
+  cmem<KSegHdr>* hdr;
+  KColC* cols;
+  KLeafC* leaves;
 };
 
 // Index of local dictId `id` in a column's value arrays (KCol.dkey / dval): the id itself, or -- table-global value
 // arrays -- id + the global ids missing from the segment's dictionary below it.  Threshold k is t_k + k (t_k the local
 // id above the k-th missing value, runtime.cpp ensure_value_map), so the running index is compared, no memory access.
-__device__ __forceinline__ uint32_t vidx(const KCol& c, uint32_t id) {
+__device__ __forceinline__ uint32_t vidx(KColC& c, uint32_t id) {
   for (int k = 0; k < c.ngaps; ++k) id += id >= c.gaps[k] ? 1u : 0u;
   return id;
 }
 // The same for N ids of one segment (c wave-uniform: the thresholds are scalar operands).
 template <int N>
-__device__ __forceinline__ void vidx_n(const KCol& c, uint32_t (&ids)[N]) {
+__device__ __forceinline__ void vidx_n(KColC& c, uint32_t (&ids)[N]) {
   const int ng = c.ngaps;
   for (int k = 0; k < ng; ++k) {
     const uint32_t g = c.gaps[k];
@@ -343,9 +354,9 @@ __device__ __forceinline__ void vidx_n(const KCol& c, uint32_t (&ids)[N]) {
 __device__ __forceinline__ SegView seg_view(const KParams& p, int seg) {
   const uint8_t* base = p.segs + (int64_t)seg * p.seg_stride;
   SegView v;
-  v.hdr = reinterpret_cast<const KSegHdr*>(base);
-  v.cols = reinterpret_cast<const KCol*>(base + sizeof(KSegHdr));
-  v.leaves = reinterpret_cast<const KLeaf*>(base + sizeof(KSegHdr) + sizeof(KCol) * p.num_cols);
+  v.hdr = cp(reinterpret_cast<const KSegHdr*>(base));
+  v.cols = cp(reinterpret_cast<const KCol*>(base + sizeof(KSegHdr)));
+  v.leaves = cp(reinterpret_cast<const KLeaf*>(base + sizeof(KSegHdr) + sizeof(KCol) * p.num_cols));
   return v;
 }
 
@@ -389,8 +400,8 @@ __device__ __forceinline__ uint32_t leaf_mask_reg(const LeafReg& R, int64_t grou
 
 __device__ __forceinline__ LeafReg load_leaf_reg(const KParams& p, const SegView& S, int l) {
   LeafReg r;
-  const KLeaf& L = S.leaves[l];
-  const KCol& C = S.cols[p.leaf_col[l]];
+  KLeafC& L = S.leaves[l];
+  KColC& C = S.cols[p.leaf_col[l]];
   r.fwd = C.fwd;
   r.bits = C.bits;
   r.kind = L.kind;
@@ -577,13 +588,13 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
     uint32_t id[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const KCol& c = S[b].cols[kc];
+      KColC& c = S[b].cols[kc];
       id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
     }
     int32_t g[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {  // the lanes' docs may come from different segments: per-lane select
-      const KCol& c = S[b].cols[kc];
+      KColC& c = S[b].cols[kc];
       g[b] = !SIMPLE && c.lut ? gp(c.lut)[id[b]] : (int32_t)id[b] + c.lut_off;
     }
 #pragma unroll
@@ -622,7 +633,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       if (col != prev_col) {  // SUM/MIN/MAX of one column share the dictId gather
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-          const KCol& c = S[b].cols[col];
+          KColC& c = S[b].cols[col];
           id[b] = gather_id(c.fwd, c.bits, ok[b] ? doc[b] : 0);
         }
         if (!SIMPLE) {
@@ -637,7 +648,7 @@ __device__ __forceinline__ void aggregate_batch(const KParams& p, const SegView 
       } else {
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-          const KCol& c = S[b].cols[col];
+          KColC& c = S[b].cols[col];
           ikey[b] = !SIMPLE && c.dkey ? gp(c.dkey)[vi[b]] : c.key_base + (int64_t)id[b];
         }
       }
@@ -811,7 +822,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
 #pragma unroll
   for (int i = 0; i < 16; ++i) key[i] = -(int32_t)p.key_bias;  // dense key spaces: < 2^31 after the bias
   for (int j = 0; j < p.num_keys; ++j) {
-    const KCol& c = S.cols[p.key_col[j]];
+    KColC& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
     const int32_t stride = (int32_t)p.key_stride[j];
     if (!SIMPLE && c.lut) {  // segment-uniform: the whole wave reads one segment here
@@ -850,7 +861,7 @@ __device__ __forceinline__ void aggregate_half(const KParams& p, const SegView& 
       need_f |= p.slot_kind[e] == SLOT_SUM_F64;
       ++e;
     }
-    const KCol& c = S.cols[col];
+    KColC& c = S.cols[col];
     decode_group<H>(c.fwd, c.bits, group, ids);
     if (!SIMPLE) vidx_n(c, ids);  // table-global value arrays (one segment): dictIds -> their indexes
     if (need_i) {  // the 16 lookups in flight together, then every integer-keyed slot of the run

@@ -14,14 +14,17 @@ namespace pgpu {
 namespace {
 
 bool is_primitive(int type) {
-  return type == SN_SCAN || type == SN_SORTED || type == SN_BITMAP || type == SN_NOT;
+  return type == SN_SCAN || type == SN_SORTED || type == SN_BITMAP || type == SN_RANGEIDX || type == SN_NOT;
 }
+// Index-based leaves: their docIdSet is a sorted range or a bitmap, no iterator scans for them.
+bool is_index(int type) { return type == SN_SORTED || type == SN_BITMAP || type == SN_RANGEIDX; }
 
 // reorderAndFilterChildOperators priorities (FilterOperatorUtils.java:143-178); NOT ranks with the scans.
 int and_priority(int type) {
   switch (type) {
     case SN_SORTED: return 0;
     case SN_BITMAP: return 1;
+    case SN_RANGEIDX: return 2;
     case SN_AND: return 3;
     case SN_OR: return 4;
     default: return 5;
@@ -47,7 +50,7 @@ StatTree build_stat_tree(const std::vector<int32_t>& ops, const std::vector<int3
   for (int32_t e : ops) {
     const int op = e >> 16, arg = e & 0xFFFF;
     if (op == OP_LEAF) {
-      static const int kType[] = {SN_EMPTY, SN_ALL, SN_SCAN, SN_SORTED, SN_BITMAP};
+      static const int kType[] = {SN_EMPTY, SN_ALL, SN_SCAN, SN_SORTED, SN_BITMAP, SN_RANGEIDX};
       st.push_back(add(kType[leaf[arg]], arg));
     } else if (op == OP_NOT) {
       const int32_t c = st.back();
@@ -94,7 +97,7 @@ StatsPlan classify_stat_tree(const StatTree& t, int64_t num_docs) {
   StatsPlan p;
   const StatNode& r = t.nodes[t.root];
   switch (r.type) {
-    case SN_EMPTY: case SN_ALL: case SN_SORTED: case SN_BITMAP: return p;  // no scan-based iterator
+    case SN_EMPTY: case SN_ALL: case SN_SORTED: case SN_BITMAP: case SN_RANGEIDX: return p;  // no scan-based iterator
     case SN_SCAN: case SN_NOT: p.constant = num_docs; return p;          // iterated over every doc
     default: break;
   }
@@ -109,7 +112,7 @@ StatsPlan classify_stat_tree(const StatTree& t, int64_t num_docs) {
   int nidx = 0, nscan = 0, nnot = 0;
   for (int32_t c : r.kids) {
     const int ty = t.nodes[c].type;
-    if (ty == SN_SORTED || ty == SN_BITMAP) { ++nidx; p.index_leaves.push_back(t.nodes[c].leaf); }
+    if (is_index(ty)) { ++nidx; p.index_leaves.push_back(t.nodes[c].leaf); }
     else if (ty == SN_SCAN) { ++nscan; p.scan_leaves.push_back(t.nodes[c].leaf); }
     else ++nnot;
   }
@@ -120,6 +123,21 @@ StatsPlan classify_stat_tree(const StatTree& t, int64_t num_docs) {
   }
   p.kind = nscan == 2 ? STATS_LEAP2 : STATS_GENERIC;  // AndDocIdIterator over the children
   return p;
+}
+
+std::vector<int32_t> range_index_leaves(const StatTree& t) {
+  std::vector<int32_t> out;
+  if (t.root < 0) return out;
+  std::vector<int32_t> st{t.root};
+  while (!st.empty()) {
+    const StatNode& n = t.nodes[st.back()];
+    st.pop_back();
+    if (n.type == SN_RANGEIDX) out.push_back(n.leaf);
+    if (n.type == SN_AND || n.type == SN_OR)
+      for (int32_t k : n.kids) st.push_back(k);
+  }
+  std::sort(out.begin(), out.end());
+  return out;
 }
 
 // ------------------------------------------------------------------------------------------------ replay
@@ -271,7 +289,7 @@ struct Replay {
     switch (s.type) {
       case SN_EMPTY: b.w.assign(nw, 0u); break;
       case SN_ALL: b.w.assign(nw, ~0u); break;
-      case SN_SCAN: case SN_SORTED: case SN_BITMAP: b = leaf_bits(s.leaf); break;
+      case SN_SCAN: case SN_SORTED: case SN_BITMAP: case SN_RANGEIDX: b = leaf_bits(s.leaf); break;
       case SN_NOT: b = match(s.kids[0]); for (auto& x : b.w) x = ~x; break;
       case SN_AND:
         b.w.assign(nw, ~0u);
@@ -308,7 +326,7 @@ struct Replay {
       case SN_EMPTY: return make(IT_EMPTY);
       case SN_ALL: return make(IT_ALL);
       case SN_SCAN: case SN_NOT: { It* it = make(IT_SCAN); it->bits = match(node); return it; }
-      case SN_SORTED: case SN_BITMAP: {
+      case SN_SORTED: case SN_BITMAP: case SN_RANGEIDX: {
         It* it = make(IT_IDX);
         it->bits = match(node);
         it->sorted = s.type == SN_SORTED;
@@ -395,7 +413,7 @@ extern "C" int pgpu_filter_entries_scanned(const pgpu_filter_op* filter, int32_t
   if (num_filter_ops && depth != 1) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "malformed filter program");
   std::vector<const uint32_t*> masks(num_leaves, nullptr);
   for (int i = 0; i < num_leaves; ++i) {
-    if (types[i] < SL_EMPTY || types[i] > SL_BITMAP) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad leaf type");
+    if (types[i] < SL_EMPTY || types[i] > SL_RANGEIDX) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "bad leaf type");
     if (types[i] >= SL_SCAN) {
       if (!leaf_masks || !leaf_masks[i]) return host_fail(PGPU_ERR_INVALID_ARGUMENT, "leaf %d has no doc set", i);
       masks[i] = leaf_masks[i];

@@ -17,14 +17,18 @@
 
 namespace pgpu {
 
-// Pinot leaf operator of a predicate in one segment (FilterOperatorUtils.getLeafFilterOperator).
-enum StatLeaf : int32_t { SL_EMPTY = 0, SL_ALL = 1, SL_SCAN = 2, SL_SORTED = 3, SL_BITMAP = 4 };
+// Pinot leaf operator of a predicate in one segment (FilterOperatorUtils.getLeafFilterOperator).  SL_RANGEIDX:
+// RangeIndexBasedFilterOperator (a RANGE predicate on an unsorted column with a range index, :57-62) -- its docIdSet
+// is a BitmapDocIdSet like an inverted leaf's; the entries of its own partial-match scan
+// (RangeIndexBasedFilterOperator.java:110-126) do not depend on the rest of the tree and are added by the caller.
+enum StatLeaf : int32_t { SL_EMPTY = 0, SL_ALL = 1, SL_SCAN = 2, SL_SORTED = 3, SL_BITMAP = 4, SL_RANGEIDX = 5 };
+constexpr int kStatLeafKinds = 6;
 
 // Physical filter tree of one segment after folding (EmptyFilterOperator / MatchAllFilterOperator removed as
 // FilterPlanNode and getAnd/OrFilterOperator do), AND children in reorderAndFilterChildOperators order.  NOT is not
 // part of the reference's 0.10 FilterContext; it is a scan-based iterator over its child (the oracle's model).
 enum StatNodeType : int32_t { SN_EMPTY = 0, SN_ALL = 1, SN_SCAN = 2, SN_SORTED = 3, SN_BITMAP = 4, SN_NOT = 5,
-                              SN_AND = 6, SN_OR = 7 };
+                              SN_AND = 6, SN_OR = 7, SN_RANGEIDX = 8 };
 struct StatNode {
   int32_t type = SN_ALL;
   int32_t leaf = -1;           // leaves: predicate index
@@ -47,6 +51,9 @@ struct StatsPlan {
   std::vector<int32_t> scan_leaves;  //   scan leaves in Pinot's order; STATS_LEAP2: the two scans (A, B)
 };
 StatsPlan classify_stat_tree(const StatTree& t, int64_t num_docs);
+// Predicate indexes of the range-index leaves whose operator runs (SN_RANGEIDX nodes not under a NOT, which
+// evaluates its child per document): each adds its partial-match scan's entries.
+std::vector<int32_t> range_index_leaves(const StatTree& t);
 
 // Replays Pinot's iterators over the leaves' match bitmaps (leaf_masks[leaf]: word g bit i = doc 32g + i, the
 // predicate's own match, negation included) and returns numEntriesScannedInFilter of the segment.

@@ -78,7 +78,8 @@ struct pgpu_result_s {
   int num_keys = 0;
   int num_aggs = 0;
   int num_slots = 0;
-  // Groups in ascending composite-key order, columnar in one pinned buffer: int32 group-by dictIds
+  // Groups columnar in one pinned buffer (ascending composite key, except hash-mode results of >= 4096 groups: their
+  // partition order -- order-dependent consumers compare keys, server_response.cpp KeyOrder): int32 group-by dictIds
   // [num_keys][n], then (8-aligned) u64 accumulator words [num_slots][n]; slot 0 = COUNT.
   pgpu::HostPinned buf;
   std::shared_ptr<pgpu::ResultPool> pool;

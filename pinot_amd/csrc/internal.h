@@ -154,6 +154,12 @@ struct KParams {
   uint64_t deadline;
   // diagnostics build only (PGPU_DIAG_WG_TIMES, PGPU_TRACE=wgtimes): per workgroup {start, tile loop end, end, tiles}
   unsigned long long* diag_times;
+  // Run-time balance of chunked plans (tile_chunks = 1): the static runs cover tiles [0, claim_base); the rest is
+  // claimed claim_tiles at a time through *claim (zeroed with the statistics per execution) by whichever workgroup
+  // finishes its work first.  claim = null: the static runs cover every tile.
+  unsigned int* claim;
+  int32_t claim_base;
+  int32_t claim_tiles;
 };
 
 // leaf_masks_kernel work item: groups [group0, group0 + 256) of plan record `rec`; its leaves' masks go to

@@ -57,7 +57,7 @@ __device__ __forceinline__ uint32_t hpart(const KPartParams& pp, uint32_t hk) {
 }
 
 // A value stream's dictIds -> their indexes in its value arrays (KCol.gaps; a no-op for the segment's own arrays).
-__device__ __forceinline__ void map_value_ids(const KCol& c, uint32_t (&ids)[16]) { vidx_n(c, ids); }
+__device__ __forceinline__ void map_value_ids(KColC& c, uint32_t (&ids)[16]) { vidx_n(c, ids); }
 
 // Composite keys of docs [32*group + H, +16) of segment S.
 template <int H>
@@ -66,7 +66,7 @@ __device__ __forceinline__ void part_keys(const KParams& p, const SegView& S, in
 #pragma unroll
   for (int i = 0; i < 16; ++i) key[i] = -(int32_t)p.key_bias;
   for (int j = 0; j < p.num_keys; ++j) {
-    const KCol& c = S.cols[p.key_col[j]];
+    KColC& c = S.cols[p.key_col[j]];
     decode_group<H>(c.fwd, c.bits, group, ids);
     const int32_t stride = (int32_t)p.key_stride[j];
     if (c.lut) {
@@ -92,7 +92,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   const int cbits = pp.pshift + pp.cshift;  // key bits within a coarse partition
   const bool two = pp.cshift > 0;
   if (pp.pack_bits) {  // one integer stream, packed above the key bits: one u32 per record
-    const KCol& c = S.cols[pp.stream_col[0]];
+    KColC& c = S.cols[pp.stream_col[0]];
     uint32_t ids[16];
     decode_group<H>(c.fwd, c.bits, group, ids);
     map_value_ids(c, ids);
@@ -114,7 +114,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
     return;
   }
   if (pp.mid_pair) {  // hashed, one u32 value: (hk | value << 32) in one 8-byte word, one scattered store per record
-    const KCol& c = S.cols[pp.stream_col[0]];
+    KColC& c = S.cols[pp.stream_col[0]];
     uint32_t ids[16];
     decode_group<H>(c.fwd, c.bits, group, ids);
     map_value_ids(c, ids);
@@ -161,7 +161,7 @@ __device__ __forceinline__ void part_scatter_half(const KPartParams& pp, const S
   }
   uint32_t ids[16];
   for (int s = 0; s < pp.num_streams; ++s) {
-    const KCol& c = S.cols[pp.stream_col[s]];
+    KColC& c = S.cols[pp.stream_col[s]];
     decode_group<H>(c.fwd, c.bits, group, ids);
     map_value_ids(c, ids);
     uint64_t* __restrict__ out = (two ? pp.mid_val : pp.rec_val) + (int64_t)s * pp.rec_cap;
@@ -226,7 +226,7 @@ __device__ __forceinline__ void part_scatter_half_staged(const KPartParams& pp, 
   uint8_t* bkt = reinterpret_cast<uint8_t*>(ws + 128);          // per staged record: its run
   int32_t key[16];
   part_keys<H>(p, S, group, key);
-  const KCol& c = S.cols[pp.stream_col[0]];
+  KColC& c = S.cols[pp.stream_col[0]];
   uint32_t ids[16];
   decode_group<H>(c.fwd, c.bits, group, ids);
   map_value_ids(c, ids);

@@ -44,6 +44,7 @@
 #include "host_common.h"
 #include "host_result.h"
 #include "internal.h"
+#include "range_index.h"
 
 using namespace pgpu;
 
@@ -462,6 +463,7 @@ struct Column {
   bool key_affine = false;          // INT / LONG dictionary of consecutive values: d_key[i] = key_base + i
   int64_t key_base = 0;
   std::shared_ptr<InvIndex> inv;    // bitmap inverted index, if attached
+  std::shared_ptr<const RangeIdx> rng;  // range index, if attached (RANGE leaves: RangeIndexBasedFilterOperator)
   // raw (no-dictionary) column: d_key / d_val hold the values per doc (read through the table's identity $docId
   // forward index), raw_min / raw_max bound integer sums
   bool raw = false;
@@ -1323,7 +1325,7 @@ struct pgpu_plan_s {
   // (an expired wait aborts it: a peer that never joined leaves them pending).  exec_prologue resets all three, so a
   // plan executed again after a combine runs and finalizes as planned.
   std::vector<int32_t> slot_kind_planned;
-  pgpu::Comm* comm_used = nullptr;
+  std::shared_ptr<pgpu::Comm> comm_used;  // the communicator of the last combine (shared: outlives pgpu_comm_destroy)
   // First-seen emulation (composite plans, see split_for_groups_limit): parts executed and finalized one after
   // another at finalize, their rows truncated / capped and merged on the host.
   bool first_doc_slot = false;            // this plan carries the hidden MIN($docId) slot (last slot)
@@ -1914,15 +1916,17 @@ struct SegStats {
   int kind = STATS_CONST;
   int64_t const_per_doc = 0;
   int32_t rec_stats = KSTATS_NONE;
+  std::vector<int32_t> range_leaves;  // range-index leaves whose partial-match scan counts (range_index_leaves)
 };
 SegStats classify_segment_stats(const pgpu_plan_s* P, uint64_t sig) {
   std::vector<int32_t> lt(P->num_leaves);
-  for (int l = P->num_leaves - 1; l >= 0; --l) { lt[l] = (int32_t)(sig % 5); sig /= 5; }
+  for (int l = P->num_leaves - 1; l >= 0; --l) { lt[l] = (int32_t)(sig % kStatLeafKinds); sig /= kStatLeafKinds; }
   SegStats ss;
   ss.tree = build_stat_tree(P->ops, lt);
   const StatsPlan sp = classify_stat_tree(ss.tree, 1);
   ss.kind = sp.kind;
   ss.const_per_doc = sp.constant;
+  ss.range_leaves = range_index_leaves(ss.tree);
   std::vector<int> pos(P->num_leaves);  // predicate index -> evaluation position in the kernel
   for (int k = 0; k < P->num_leaves; ++k) pos[P->leaf_perm[k]] = k;
   if (sp.kind == STATS_CHAIN && P->in_kernel_stats) {
@@ -2533,20 +2537,23 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
   for (int l = 0; l < P->num_leaves; ++l) perm[l] = l;
   if (P->pure_and && P->num_leaves > 1) {
     // FilterOperatorUtils.reorderAndFilterChildOperators (:143-178): sorted-index leaves, then bitmap
-    // (inverted-index) leaves, then scans.
-    std::vector<int> first, second, rest;
+    // (inverted-index) leaves, then range-index leaves, then scans.
+    std::vector<int> first, second, third, rest;
     for (int l = 0; l < P->num_leaves; ++l) {
       const pgpu_predicate& pr = q->predicates[l];
       const bool eq_in = pr.type == PGPU_PRED_EQ || pr.type == PGPU_PRED_NOT_EQ || pr.type == PGPU_PRED_IN ||
                          pr.type == PGPU_PRED_NOT_IN;
       bool all_sorted = !P->segs.empty(), all_inv = !P->segs.empty() && eq_in && !P->no_inverted;
+      bool all_rng = !P->segs.empty() && pr.type == PGPU_PRED_RANGE;
       for (Segment* s : P->segs) {
         all_sorted &= s->cols[pr.column].sorted;
         all_inv &= s->cols[pr.column].inv != nullptr && !s->star;
+        all_rng &= s->cols[pr.column].rng != nullptr;
       }
-      (all_sorted ? first : all_inv ? second : rest).push_back(l);
+      (all_sorted ? first : all_inv ? second : all_rng ? third : rest).push_back(l);
     }
     first.insert(first.end(), second.begin(), second.end());
+    first.insert(first.end(), third.begin(), third.end());
     first.insert(first.end(), rest.begin(), rest.end());
     perm = first;
     std::vector<int32_t> slots(P->num_leaves);
@@ -2591,9 +2598,13 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         for (int l = 0; l < P->num_leaves; ++l) {
           const pgpu_predicate& pr = q->predicates[l];
           const Column& col = s->cols[pr.column];
+          // FilterOperatorUtils.getLeafFilterOperator (:42-82): sorted column -> SortedIndexBasedFilterOperator;
+          // RANGE with a range index -> RangeIndexBasedFilterOperator; other predicates with an inverted index ->
+          // BitmapBasedFilterOperator; else a scan
           const int k = tri[l] == T_NONE ? SL_EMPTY : tri[l] == T_ALL ? SL_ALL : col.sorted ? SL_SORTED :
-                        (pr.type != PGPU_PRED_RANGE && col.inv) ? SL_BITMAP : SL_SCAN;
-          sig = sig * 5 + (uint64_t)k;
+                        (pr.type != PGPU_PRED_RANGE && col.inv) ? SL_BITMAP :
+                        (pr.type == PGPU_PRED_RANGE && col.rng && leaves[l].kind == LEAF_RANGE) ? SL_RANGEIDX : SL_SCAN;
+          sig = sig * kStatLeafKinds + (uint64_t)k;
         }
         auto it = stat_cache.find(sig);
         if (it == stat_cache.end()) it = stat_cache.emplace(sig, classify_segment_stats(P, sig)).first;
@@ -2601,6 +2612,10 @@ int plan_create_impl(pgpu_table_s* t, const int64_t* handles, int32_t nsegs, con
         rec_stats = ss.rec_stats;
         C.any_leap2 |= (rec_stats & 3) == KSTATS_LEAP2;
         if (ss.kind == STATS_CONST) C.entries += ss.const_per_doc * s->num_docs;
+        for (int l : ss.range_leaves) {  // RangeIndexBasedFilterOperator's own partial-match scan
+          const LeafHost& lh = leaves[l];
+          C.entries += s->cols[q->predicates[l].column].rng->partial_entries(lh.lo, (int64_t)lh.lo + lh.span - 1);
+        }
         if (ss.kind == STATS_GENERIC)
           C.generic.push_back({(int64_t)(C.rec.size() / P->seg_stride), s->num_docs, ss.tree, 0});
       }
@@ -3543,6 +3558,27 @@ int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream
   return 0;
 }
 
+// Run-time claims of a chunked scan launch (KParams.claim): workgroups with equal static runs finish up to a third
+// apart (C3: p0 79 / max 122 us at 125 segments, 643 / 884 at 1000 -- r05 session j), so the static runs cover only
+// the first kClaimStaticPm / 1000 of the tiles and the rest is claimed in runs of 1/kClaimDiv of a workgroup's share.
+// The counters are u32 words 12..15 of the statistics block (zeroed per execution): launches 0-3 of a plan.
+#ifndef PGPU_CLAIM_STATIC_PM
+#define PGPU_CLAIM_STATIC_PM 750
+#endif
+#ifndef PGPU_CLAIM_DIV
+#define PGPU_CLAIM_DIV 16
+#endif
+void set_tile_claims(KParams& kp, unsigned long long* d_stats, int grid, int launch) {
+  kp.claim = nullptr;
+#ifndef PGPU_NO_CLAIM
+  const int64_t share = (int64_t)kp.num_tiles / std::max(grid, 1);
+  if (!kp.tile_chunks || grid < 64 || (grid & 7) || launch >= 4 || share < 8) return;
+  kp.claim = reinterpret_cast<unsigned int*>(d_stats + 6) + launch;
+  kp.claim_base = (int32_t)((int64_t)kp.num_tiles * PGPU_CLAIM_STATIC_PM / 1000);
+  kp.claim_tiles = (int32_t)std::max<int64_t>(1, share / PGPU_CLAIM_DIV);
+#endif
+}
+
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c) {
   Scratch* sc = P->scratch;
   KParams kp = X.kp;
@@ -3668,6 +3704,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
   } else if (C.num_tiles > 0) {
     static const bool wg_times = diag("wgtimes");
     if (wg_times) TRY(diag_wg_times_begin(kp, grid, stream));
+    set_tile_claims(kp, P->d_stats, grid, c);
     const int rc = launch_filter_groupby(kp, P->mode,
                                          scan_variant(P),
                                          grid, P->lds_bytes, stream);
@@ -5023,6 +5060,14 @@ int parse_inverted_index(const uint8_t* b, int64_t num_bytes, int64_t card, int3
 }
 }  // namespace
 
+}  // extern "C"
+bool pgpu::roaring_cardinality(const uint8_t* b, int64_t n, int32_t num_docs, int64_t* docs) {
+  std::vector<uint32_t> words;
+  std::vector<InvIndex::Cont> conts;
+  return parse_roaring(b, n, num_docs, words, conts, docs);
+}
+extern "C" {
+
 namespace {
 void put_le16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); }
 void put_le32(std::vector<uint8_t>& o, uint32_t v) { put_le16(o, v & 0xFFFF); put_le16(o, v >> 16); }
@@ -5162,6 +5207,29 @@ int pgpu_attach_inverted_index(pgpu_table t, int64_t h, int32_t column, const vo
   if (col.inv) t->device_bytes -= col.inv->bytes;  // freed when the last plan using it is destroyed
   t->device_bytes += inv->bytes;
   col.inv = inv;
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_attach_range_index(pgpu_table t, int64_t h, int32_t column, const void* bytes, int64_t num_bytes) try {
+  PGPU_ABI_GUARD;
+  if (!t || (!bytes && num_bytes) || num_bytes < 0) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  t->version++;
+  plan_cache_clear(t);
+  std::lock_guard<std::mutex> lk(t->mu);
+  auto it = t->segments.find(h);
+  if (it == t->segments.end()) return fail(PGPU_ERR_NOT_FOUND, "unknown segment handle %lld", (long long)h);
+  Segment& seg = *it->second;
+  if (column < 0 || column >= (int)seg.cols.size()) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad column %d", column);
+  Column& col = seg.cols[column];
+  if (num_bytes == 0) {
+    col.rng.reset();
+    return 0;
+  }
+  if (col.raw) return fail(PGPU_ERR_UNSUPPORTED, "range index on raw (no-dictionary) column %d", column);
+  auto r = std::make_shared<RangeIdx>();
+  TRY(parse_range_index(reinterpret_cast<const uint8_t*>(bytes), num_bytes, col.card, seg.num_docs, r.get()));
+  if (r->version == 0) col.rng.reset();  // a version Pinot does not load: no range index
+  else col.rng = r;
   return 0;
 } PGPU_ABI_CATCH
 
@@ -5917,7 +5985,8 @@ int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank,
   pgpu::Comm* c = nullptr;
   TRY(pgpu::comm_create(kind, id, nranks, rank, device, &c));
   auto h = new pgpu_comm_s();
-  h->impl = c;
+  h->impl.reset(c);
+  h->kind = kind;
   *out = h;
   return 0;
 } PGPU_ABI_CATCH
@@ -5925,8 +5994,26 @@ int pgpu_comm_create(int32_t kind, const void* id, int32_t nranks, int32_t rank,
 int pgpu_comm_destroy(pgpu_comm c) try {
   PGPU_ABI_GUARD;
   if (!c) return 0;
-  delete c->impl;
-  delete c;
+  delete c;  // the communicator itself goes with its last reference (plans combined on it hold one)
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_comm_recreate(pgpu_comm c, const void* id) try {
+  PGPU_ABI_GUARD;
+  if (!c || !id) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  pgpu::Comm* fresh = nullptr;
+  const pgpu::Comm& old = *c->impl;
+  TRY(pgpu::comm_create(c->kind, id, old.nranks, old.rank, old.device, &fresh));
+  fresh->timeout_ms.store(old.timeout_ms.load(std::memory_order_relaxed), std::memory_order_relaxed);
+  // plans combined on the old communicator keep it (pgpu_plan_s::comm_used) until they are finalized or destroyed
+  c->impl.reset(fresh);
+  return 0;
+} PGPU_ABI_CATCH
+
+int pgpu_comm_status(pgpu_comm c, int32_t* aborted) try {
+  PGPU_ABI_GUARD;
+  if (!c || !aborted) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *aborted = c->impl->aborted.load() ? 1 : 0;
   return 0;
 } PGPU_ABI_CATCH
 
@@ -6129,7 +6216,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     return fail(PGPU_ERR_INVALID_ARGUMENT, "PGPU_COMBINE_ROWS: finalize the plan, then pgpu_result_combine_rows");
   if (mode != PGPU_COMBINE_ALL_REDUCE && mode != PGPU_COMBINE_REDUCE_SCATTER && mode != PGPU_COMBINE_HASH)
     return fail(PGPU_ERR_INVALID_ARGUMENT, "combine mode %d", mode);
-  pgpu::Comm* C = c->impl;
+  pgpu::Comm* C = c->impl.get();
   const int N = C->nranks, me = C->rank;
   // the query's deadline and cancel flag bound every wait on the peers below (and finalize's, via comm_used)
   pgpu::CommWaitScope wait_limits(P->end_time_ms, &P->cancel);
@@ -6173,7 +6260,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     if (!rc) rc = pgpu_plan_exchange_export(P, s, N, kinds, sc->xsend.p, total);
     if (!rc) rc = sc->xrecv.ensure((size_t)std::max<int64_t>(nrecv, 1) * rec);
     TRY(agree_status(C, rc));  // before the all-to-all: every rank has its records and room for its peers'
-    P->comm_used = C;
+    P->comm_used = c->impl;
     TRY(C->alltoallv(sc->xsend.p, counts.data() + 1, sc->xrecv.p, rcount.data(), rec, s));
     TRY(pgpu_plan_exchange_merge(P, s, kinds, nrecv ? sc->xrecv.p : nullptr, nrecv));
     if (key_begin) *key_begin = 0;
@@ -6191,7 +6278,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     if (P->slot_kind_planned.empty()) P->slot_kind_planned = P->slot_kind;  // restored when executed again
     P->slot_kind.assign(kinds, kinds + ns);
   }
-  P->comm_used = C;
+  P->comm_used = c->impl;
   auto dtype = [&](int k) { return P->slot_kind[k] == SLOT_SUM_F64 ? pgpu::CDT_F64 : pgpu::CDT_I64; };
   auto op = [&](int k) {
     return P->slot_kind[k] == SLOT_MIN_KEY ? pgpu::COP_MIN : P->slot_kind[k] == SLOT_MAX_KEY ? pgpu::COP_MAX : pgpu::COP_SUM;
@@ -6247,7 +6334,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
 int pgpu_result_combine_rows(pgpu_result r, pgpu_comm c, pgpu_result* out) try {
   PGPU_ABI_GUARD;
   if (!r || !c || !out) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
-  pgpu::Comm* C = c->impl;
+  pgpu::Comm* C = c->impl.get();
   const int N = C->nranks, me = C->rank;
   TRY(C->usable());
   // a rank whose own steps fail still meets its peers in the next exchange (its status word first), so every rank

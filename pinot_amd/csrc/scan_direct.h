@@ -105,11 +105,19 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   uint32_t in_filter = 0;  // STATS_CHAIN entries of this lane (< 2^32: at most 4 leaves x 32 docs x tiles)
   const int64_t T = p.num_tiles;
   int64_t t_begin, t_end, t_step;
+  // run-time claims (chunked plans): the static runs end at claim_base, the rest goes claim_tiles at a time to the
+  // workgroups that finish first.  The next claim is issued before the run it follows, so its atomic's round trip
+  // overlaps that run's loads; one barrier per run hands it to the other waves.
+  const bool dyn = p.claim != nullptr && gridDim.x >= 64 && (gridDim.x & 7) == 0 && p.tile_chunks;
+  __shared__ uint32_t claim_at[2];
+  uint32_t next_claim = 0;
+  if (dyn && tid == 0) next_claim = atomicAdd(p.claim, (uint32_t)p.claim_tiles);
   if (gridDim.x >= 64 && (gridDim.x & 7) == 0 && p.tile_chunks) {
     // chunked: each workgroup a contiguous run of its XCD's eighth -- consecutive tiles of one segment, so the
     // segment's records are read once per run instead of once per tile (plans without per-doc gathers)
+    const int64_t TS = dyn ? p.claim_base : T;
     const int64_t x = blockIdx.x & 7, i = blockIdx.x >> 3, nx = gridDim.x >> 3;
-    const int64_t lo = x * T / 8, len = (x + 1) * T / 8 - lo;
+    const int64_t lo = x * TS / 8, len = (x + 1) * TS / 8 - lo;
     t_begin = lo + i * len / nx;
     t_end = lo + (i + 1) * len / nx;
     t_step = 1;
@@ -126,6 +134,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   // FAST: an instance for plans whose filter is a pure AND of at most kFastLeaves leaves (the general program
   // evaluator compiled out)
   const bool fast = FAST || (p.pure_and && p.num_leaves <= kFastLeaves);
+  for (int run = 0;; ++run) {
   if (t_begin < t_end) {
     int seg = -1;
     SegView S{};
@@ -145,10 +154,10 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
     if (nl > 2) R2 = load_leaf_reg(p, S, 2);    \
     if (nl > 3) R3 = load_leaf_reg(p, S, 3);    \
   } while (0)
-    int next_seg = p.tile_seg[t_begin];
+    int next_seg = cp(p.tile_seg)[t_begin];
     for (int64_t t = t_begin; t < t_end; t += t_step) {
       const int cur_seg = next_seg;
-      if (t + t_step < t_end) next_seg = p.tile_seg[t + t_step];  // one tile ahead
+      if (t + t_step < t_end) next_seg = cp(p.tile_seg)[t + t_step];  // one tile ahead
       if (cur_seg != seg) {
         seg = cur_seg;
         S = seg_view(p, seg);
@@ -257,11 +266,24 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
       }
       ++kk;
     }
-    if (qn) flush_wave_queue<MODE, SIMPLE>(p, wq, wqs, qn, lane, tbl, G);
     if (p.leap_maps)  // each wave stores its own bytes (tiles of other segments hold don't-care values)
       for (int k = lane; k < kk; k += 64)
         p.leap_maps[(t_begin + (int64_t)k * t_step) * (kBlock / 64) + wave] = lmaps[k * (kBlock / 64) + wave];
+    kk = 0;
   }
+    if (!dyn) break;
+    if (tid == 0) claim_at[run & 1] = next_claim;
+    __syncthreads();
+    // (readfirstlane: a value read from LDS is not known to be wave-uniform, and divergent loop bounds would move the
+    // loop's scalars into VGPRs -- 112 -> 149 in the sparse instances)
+    const int64_t c0 = (int64_t)p.claim_base + (uint32_t)__builtin_amdgcn_readfirstlane((int)claim_at[run & 1]);
+    if (c0 >= T) break;
+    if (tid == 0) next_claim = atomicAdd(p.claim, (uint32_t)p.claim_tiles);
+    t_begin = c0;
+    t_end = c0 + p.claim_tiles < T ? c0 + p.claim_tiles : T;
+    t_step = 1;
+  }
+  if (qn) flush_wave_queue<MODE, SIMPLE>(p, wq, wqs, qn, lane, tbl, G);
 #ifdef PGPU_DIAG_WG_TIMES
   diag_t1 = wall_clock64();
 #endif

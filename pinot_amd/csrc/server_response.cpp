@@ -70,12 +70,30 @@ int dcmp(double a, double b) {
   return x == y ? 0 : (x < y ? -1 : 1);
 }
 
+// Ascending composite-key order of two rows (group-by column 0 least significant, the mixed-radix key of
+// DictionaryBasedGroupKeyGenerator.java:276-323 over table-global dictIds).  Dense results come back in that order
+// already, but hash-mode results of 4096 groups and more come in partition / hash order (the LONG_MAP holder's
+// iteration order), so every consumer that depends on an order compares the keys, not the row indexes.
+struct KeyOrder {
+  std::vector<const int32_t*> g;
+  explicit KeyOrder(const pgpu_result_s* R) {
+    pgpu_result_s* S = const_cast<pgpu_result_s*>(R);
+    for (int j = 0; j < R->num_keys; ++j) g.push_back(S->gid(j));
+  }
+  bool less(int64_t x, int64_t y) const {
+    for (int j = (int)g.size() - 1; j >= 0; --j)
+      if (g[j][x] != g[j][y]) return g[j][x] < g[j][y];
+    return x < y;
+  }
+};
+
 // TableResizer's comparator over ORDER BY expressions (group-by column: dictId order = value order of the sorted
-// global dictionary; aggregation: its final result).  Ties fall back to the composite-key order (row order), so
-// the choice among equal records -- thread-order dependent in Pinot -- is deterministic here.
+// global dictionary; aggregation: its final result).  Ties fall back to the composite-key order, so the choice among
+// equal records -- thread-order dependent in Pinot -- is deterministic here.
 struct RowOrder {
   const pgpu_result_s* R;
   std::vector<pgpu_order_by> ob;
+  KeyOrder key{R};
   bool less(int64_t x, int64_t y) const {
     for (const pgpu_order_by& o : ob) {
       int c;
@@ -87,7 +105,7 @@ struct RowOrder {
       }
       if (c) return o.ascending ? c < 0 : c > 0;
     }
-    return x < y;
+    return key.less(x, y);
   }
 };
 
@@ -360,10 +378,9 @@ int pgpu_result_trim_sql(pgpu_result r, const pgpu_sql_trim* spec, pgpu_result* 
     rows = top_rows(n, std::min(trim, n), [&](int64_t x, int64_t y) { return ord.less(x, y); });
   } else {
     // no ORDER BY: the table stops taking new keys at `limit` groups (which ones is thread-order dependent in
-    // Pinot; here the smallest composite keys)
-    const int64_t k = std::min<int64_t>(spec->limit, n);
-    rows.resize(k);
-    std::iota(rows.begin(), rows.end(), 0);
+    // Pinot; here the smallest composite keys, whatever order the result holds its rows in)
+    const KeyOrder key(r);
+    rows = top_rows(n, std::min<int64_t>(spec->limit, n), [&](int64_t x, int64_t y) { return key.less(x, y); });
   }
   return copy_rows(r, rows, out);
 } PGPU_ABI_CATCH
@@ -385,10 +402,11 @@ int pgpu_result_trim_pql(pgpu_result r, int32_t limit, int32_t final_results, in
                                   (long long)k);
     // MIN keeps the smallest values, every other function the largest (getSorter, :162-181); ties by key
     const bool min_order = r->agg_fn[a] == PGPU_AGG_MIN;
+    const KeyOrder key(r);
     std::vector<int64_t> top = top_rows(r->n, k, [&](int64_t x, int64_t y) {
       const int c = dcmp(agg_final(r, a, x), agg_final(r, a, y));
       if (c) return min_order ? c < 0 : c > 0;
-      return x < y;
+      return key.less(x, y);
     });
     std::copy(top.begin(), top.end(), rows + (int64_t)a * cap);
   }

@@ -48,7 +48,8 @@ class AvgPair:
 
 
 class GroupByResult:
-    """Groups in ascending composite-key order, held columnar (numpy) as the C ABI returns them; the Python form
+    """Groups in the C result's order (ascending composite key; hash-mode results of >= 4096 groups in partition
+    order, as the LONG_MAP holder iterates in hash order), held columnar (numpy) as the C ABI returns them; the Python form
     ({key tuple: [aggregation results]}) is built on first use of `keys` / `values` / `as_dict()`."""
 
     def __init__(self, keys=None, values=None, stats=None, exact=None, columnar=None, holder=None, table=None,
@@ -299,6 +300,9 @@ class GpuTable:
                 inv = getattr(seg.columns[name], "inv_bytes", None)
                 if inv is not None:
                     self.attach_inverted_index(h.value, name, inv)
+                rng = getattr(seg.columns[name], "range_bytes", None)
+                if rng is not None:
+                    self.attach_range_index(h.value, name, rng)
         except Exception:
             self.lib.pgpu_unpin_segment(self.handle, h.value)  # no half-loaded segment stays pinned
             raise
@@ -310,6 +314,13 @@ class GpuTable:
         buf = ctypes.create_string_buffer(bytes(inv_bytes), max(len(inv_bytes), 1))
         L.check(self.lib.pgpu_attach_inverted_index(self.handle, handle, self.names.index(column),
                                                     ctypes.cast(buf, ctypes.c_void_p), len(inv_bytes)))
+
+    def attach_range_index(self, handle, column, range_bytes):
+        """Pins a column's range index (RangeIndexReaderImpl / BitSlicedRangeIndexReader bytes) for the pinned segment
+        `handle`: RANGE predicates on it then run as RangeIndexBasedFilterOperator leaves (b"" detaches it)."""
+        buf = ctypes.create_string_buffer(bytes(range_bytes), max(len(range_bytes), 1))
+        L.check(self.lib.pgpu_attach_range_index(self.handle, handle, self.names.index(column),
+                                                 ctypes.cast(buf, ctypes.c_void_p), len(range_bytes)))
 
     def attach_startree(self, handle, star_tree):
         """Pins a StarTree (pinot_amd.startree) for the pinned segment `handle`."""

@@ -18,7 +18,8 @@ returns (no per-group Python objects until a caller iterates):
                            getDoubleResult(groupKey) / getResult(groupKey) (AvgPair for AVG);
   AggregationGroupByResult AggregationGroupByResult.java:31-81: getGroupKeyIterator, getStringGroupKeyIterator,
                            getResultForKey, getResultForGroupId (AggregationFunction.extractGroupByResult).
-Group ids are dense [0, numKeys) in the result's order (ascending composite key), the order the ARRAY holder's
+Group ids are dense [0, numKeys) in the result's order (ascending composite key -- hash-mode results of >= 4096 groups
+in partition order, as the LONG_MAP holder's iterator runs in hash order), the order the ARRAY holder's
 iterator produces.  Errors follow the reference: a bad literal raises BadQueryRequestException; a shape outside
 the GPU path raises UnsupportedQueryError (the Java shim keeps Pinot's CPU operator for it).
 """

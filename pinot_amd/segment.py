@@ -24,6 +24,7 @@ class ColumnData:
     fwd_format: int = L.FWD_FIXED_BIT
     is_sorted: bool = False
     inv_bytes: bytes = None  # bitmap inverted index (<column>.bitmap.inv), if the column has one
+    range_bytes: bytes = None  # range index (<column>.bitmap.range, version 1 or 2), if the column has one
 
 
 @dataclass

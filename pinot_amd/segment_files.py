@@ -156,6 +156,48 @@ def build_inverted_index(dict_ids, cardinality, run_optimize=False):
     return offs.astype(">i4").tobytes() + b"".join(bitmaps)
 
 
+def build_range_index(dict_ids, cardinality, num_ranges=None):
+    """RangeIndexCreator (version 1, seglocal/segment/creator/impl/inv/RangeIndexCreator.java) of a dictionary-encoded
+    single-value column, whose values are its dictIds (DefaultIndexCreatorProvider.newRangeIndexCreator: INT): the
+    values sorted, ranges of more than ceil(numValues / numRanges) values (default 20 ranges) cut where the value
+    changes (seal()), then big-endian: version, value type name, range count, the ranges' first values + the last
+    range's last value, the bitmap offsets (from the start of the file; the last one = the file size), and each
+    range's serialised RoaringBitmap of docIds."""
+    ids = np.asarray(dict_ids, dtype=np.int64)
+    n = ids.size
+    per_range = (n + (num_ranges or 20) - 1) // (num_ranges or 20)
+    order = np.argsort(ids, kind="stable")
+    vals = ids[order]
+    ranges, start = [], 0
+    for i in range(n):  # seal(): `if (i > start + boundary) { if (value changed) cut }`
+        if i > start + per_range and vals[i] != vals[i - 1]:
+            ranges.append((start, i - 1))
+            start = i
+    ranges.append((start, n - 1))
+    out = bytearray(struct.pack(">i", 1))
+    out += struct.pack(">i", 3) + b"INT"
+    out += struct.pack(">i", len(ranges))
+    for a, _ in ranges:
+        out += struct.pack(">i", int(vals[a]))
+    out += struct.pack(">i", int(vals[ranges[-1][1]]))
+    bitmaps = [serialize_roaring(np.sort(order[a:b + 1])) for a, b in ranges]
+    off = len(out) + 8 * (len(ranges) + 1)
+    out += struct.pack(">q", off)
+    for bm in bitmaps:
+        off += len(bm)
+        out += struct.pack(">q", off)
+    return bytes(out) + b"".join(bitmaps)
+
+
+def build_range_index_bitsliced_header(min_value=0):
+    """The header of a version-2 (BitSlicedRangeIndexCreator) range index -- version, the column's minimum (dictId 0
+    for a dictionary-encoded column) -- followed by a placeholder for its RangeBitmap body, which readers of this
+    repository never parse: the index is exact, so the GPU path reads the matches from the forward index and scans
+    no partial matches (BitSlicedRangeIndexReader.getPartiallyMatchingDocIds: null).  Format parity of the body is
+    not claimed (RoaringBitmap 0.9.23's RangeBitmap is absent here)."""
+    return struct.pack(">iq", 2, int(min_value)) + b"\0" * 16
+
+
 def build_inverted_index_native(fwd_bytes, bits, num_docs, cardinality):
     """The same file from the library's host creator (pgpu_build_inverted_index; no GPU involved)."""
     import ctypes

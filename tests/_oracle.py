@@ -29,7 +29,8 @@ class OrColumn(ctypes.Structure):
     _fields_ = [("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("entry_width", ctypes.c_int32), ("padding_byte", ctypes.c_int32), ("is_sorted", ctypes.c_int32),
                 ("has_inverted", ctypes.c_int32), ("dict", ctypes.c_void_p), ("fwd", ctypes.c_void_p),
-                ("raw", ctypes.c_int32), ("fwd_len", ctypes.c_int64)]
+                ("raw", ctypes.c_int32), ("fwd_len", ctypes.c_int64), ("range_index", ctypes.c_void_p),
+                ("range_index_len", ctypes.c_int64)]
 
 
 class OrStarTree(ctypes.Structure):
@@ -184,10 +185,14 @@ class _OrSeg:
             d = ctypes.create_string_buffer(bytes(c.dict_bytes), max(len(c.dict_bytes), 1))
             f = ctypes.create_string_buffer(bytes(c.fwd_bytes) + b"\0" * 16, len(c.fwd_bytes) + 16)
             self.keep += [d, f]
+            rng = getattr(c, "range_bytes", None)
+            r = ctypes.create_string_buffer(bytes(rng), max(len(rng), 1)) if rng else None
+            self.keep.append(r)
             cols[i] = OrColumn(c.data_type, c.cardinality, c.bits_per_element, c.entry_width, c.padding_byte,
                                int(c.is_sorted), int(getattr(c, "inv_bytes", None) is not None),
                                ctypes.cast(d, ctypes.c_void_p), ctypes.cast(f, ctypes.c_void_p),
-                               int(c.fwd_format == L.FWD_RAW_FIXED), len(c.fwd_bytes))
+                               int(c.fwd_format == L.FWD_RAW_FIXED), len(c.fwd_bytes),
+                               ctypes.cast(r, ctypes.c_void_p) if r is not None else None, len(rng) if rng else 0)
         self.keep.append(cols)
         self.seg = OrSegment(seg.num_docs, len(schema), cols)
         star = getattr(seg, "star_arrays", None)  # StarTree.arrays() of the segment's star-tree, if any

@@ -127,3 +127,36 @@ def test_in_filter_narrows_the_key_space_to_a_dense_table(oracle, sparse):
         assert p.group_path() in ("global", "partitioned"), p.group_path()
         assert p.layout()[1] == len(t.dictionary("a")) * len(t.dictionary("b")) * 7 < 2 ** 26
     assert_same(t.execute_groupby(hs, q), oracle.run_groupby(SCHEMA, segs, q), q, SCHEMA)
+
+
+def _key_order(k):
+    """Ascending composite key (DictionaryBasedGroupKeyGenerator mixed radix, column 0 least significant): the
+    dictionaries are sorted, so value order is dictId order."""
+    return tuple(reversed(k))
+
+
+def test_hash_result_trims_order_by_key(oracle, sparse):
+    """Hash-mode results of >= 4096 groups come back in partition order: the SQL trim without ORDER BY
+    still keeps the smallest composite keys, and ORDER BY / PQL ties still fall back to the composite key."""
+    t, hs, segs = sparse
+    q = parse_query("SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c LIMIT 100", num_groups_limit=10 ** 9)
+    with t.plan(hs, q) as p:
+        assert p.group_path() == "hash_partitioned"
+    r = t.execute_groupby(hs, q)
+    exp = oracle.run_groupby(SCHEMA, segs, q)
+    exp_d = exp.groups
+    assert len(r) == len(exp_d) >= 4096
+    keys = sorted(exp_d, key=_key_order)
+    assert r.keys != keys  # partition order: the trims below must not rely on row order
+    trimmed = r.trim_sql(q)
+    assert trimmed.keys == keys[:100]
+    assert [v[0] for v in trimmed.values] == [exp_d[k][0] for k in keys[:100]]
+    # ORDER BY COUNT(*) DESC: the top max(limit * 5, 5000) rows, count ties broken by composite key
+    qo = parse_query("SELECT COUNT(*), SUM(m) FROM t GROUP BY a, b, c ORDER BY COUNT(*) DESC LIMIT 10",
+                     num_groups_limit=10 ** 9)
+    ordered = r.trim_sql(qo)
+    want = sorted(exp_d, key=lambda k: (-exp_d[k][0], _key_order(k)))[:5000]
+    assert ordered.keys == want
+    # PQL: per function the top groups, ties by composite key
+    top = r.trim_pql(50, final=True)
+    assert [k for k, _ in top[0]] == sorted(exp_d, key=lambda k: (-exp_d[k][0], _key_order(k)))[:50]

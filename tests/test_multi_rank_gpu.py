@@ -409,3 +409,80 @@ def test_combine_rank_failure_fails_every_rank(gpu_lib, tmp_path):
     assert res[1][1].startswith(str(L.PGPU_ERR_INVALID_ARGUMENT)) and "not executed" in res[1][1], res
     assert res[0][1].startswith(str(L.PGPU_ERR_INVALID_ARGUMENT)) and "rank 1 of 2 failed" in res[0][1], res
     assert res[0][0] < 30 and res[1][0] < 30, res
+
+
+def _recovery_worker(rank, uids, out_dir):
+    """Communicator recovery: rank 1 fails a dense all-reduce combine (a plan it never executed),
+    so rank 0's all-reduce waits on a peer that never comes, times out and aborts the communicator.  Both ranks then
+    recreate it from a fresh id (pgpu_comm_recreate) and the next query combines correctly."""
+    import time
+    from pinot_amd import _lib as L
+    from pinot_amd.combine import Communicator, combine_mode, combine_plan, union_dictionaries_comm
+    from pinot_amd.executor import GpuTable
+    import _oracle
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    stream = torch.cuda.current_stream().cuda_stream
+    comm = Communicator(L.COMM_HOST, uids[0], WORLD, rank, 0)
+    comm.set_timeout(3000)
+    table = GpuTable(SCHEMA, device=0)
+    lines = []
+    try:
+        handles = [table.pin_segment(_oracle.make_segment(SCHEMA, _segment_columns(rank * SEGS_PER_RANK + i)))
+                   for i in range(SEGS_PER_RANK)]
+        union_dictionaries_comm(table, ["d", "e", "f", "mi"], comm)
+        q = parse_query(CASES["small"][0], num_groups_limit=CASES["small"][1])
+        probe = table.plan(handles, q)
+        nslots, nkeys, _ = probe.layout()
+        mode, kinds = combine_mode(probe, comm, 1 << 62)
+        probe.close()
+        assert mode == L.COMBINE_ALL_REDUCE, mode
+        d_table = torch.empty((nslots, nkeys), dtype=torch.int64, device="cuda")
+        ptr = d_table.data_ptr()
+        plan = table.plan(handles, q) if rank == 1 else table.plan_execute(handles, q, stream, ptr)
+        t0 = time.monotonic()
+        try:
+            combine_plan(plan, comm, stream, mode, kinds, d_table=ptr)
+            plan.finalize(stream, ptr)
+            outcome = "ok"
+        except L.PinotGpuError as e:
+            outcome = "%d %s" % (e.code, e.message.replace("\n", " "))
+        lines.append("%.3f %d %s" % (time.monotonic() - t0, int(comm.aborted), outcome))
+        plan.close()
+        # recovery: every rank recreates the communicator from a new id, then the query runs again
+        comm.recreate(uids[1])
+        lines.append("recreated %d" % int(comm.aborted))
+        res = _run_dense_comm(table, handles, q, stream, False, comm)
+        _dump(os.path.join(out_dir, "recovered_%d.npz" % rank), table, res, q)
+    finally:
+        with open(os.path.join(out_dir, "recovery_%d.txt" % rank), "w") as f:
+            f.write("\n".join(lines))
+        table.close()
+        comm.close()
+
+
+@pytest.mark.timeout(200)
+def test_comm_recreate_after_rank_failure(oracle, gpu_lib, tmp_path):
+    from pinot_amd import _lib as L
+    from pinot_amd.combine import Communicator
+    uids = [Communicator.unique_id(L.COMM_HOST), Communicator.unique_id(L.COMM_HOST)]
+    ctx = mp.spawn(_recovery_worker, args=(uids, str(tmp_path)), nprocs=WORLD, join=False)
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > 150:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail("ranks did not finish")
+    logs = [open(tmp_path / ("recovery_%d.txt" % r)).read().split("\n") for r in range(WORLD)]
+    # rank 1 fails its own check at once; rank 0's all-reduce gives up at the 3 s communicator timeout and aborts it
+    assert logs[1][0].split(" ", 2)[2].startswith(str(L.PGPU_ERR_INVALID_ARGUMENT)), logs
+    w0, ab0, out0 = logs[0][0].split(" ", 2)
+    assert out0.startswith(str(L.PGPU_ERR_TIMEOUT)) and int(ab0) == 1 and float(w0) < 30, logs
+    assert logs[0][1] == "recreated 0" and logs[1][1] == "recreated 0", logs
+    q = parse_query(CASES["small"][0], num_groups_limit=CASES["small"][1])
+    parts = [_load(tmp_path / ("recovered_%d.npz" % r)) for r in range(WORLD)]
+    maps = [_as_map(*p) for p in parts]
+    assert maps[0].keys() == maps[1].keys() and all((maps[0][k] == maps[1][k]).all() for k in maps[0])
+    segs = [oracle.make_segment(SCHEMA, _segment_columns(s)) for s in range(WORLD * SEGS_PER_RANK)]
+    _compare("recovered", maps[0], _as_map(*_oracle_arrays(oracle, SCHEMA, segs, q)), q, {"md"})

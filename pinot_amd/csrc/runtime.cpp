@@ -3558,10 +3558,12 @@ int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream
   return 0;
 }
 
-// Run-time claims of a chunked scan launch (KParams.claim): workgroups with equal static runs finish up to a third
-// apart (C3: p0 79 / max 122 us at 125 segments, 643 / 884 at 1000 -- r05 session j), so the static runs cover only
-// the first kClaimStaticPm / 1000 of the tiles and the rest is claimed in runs of 1/kClaimDiv of a workgroup's share.
-// The counters are u32 words 12..15 of the statistics block (zeroed per execution): launches 0-3 of a plan.
+// Run-time claims of a chunked scan launch (KParams.claim; library builds with -DPGPU_TILE_CLAIMS only): the static
+// runs cover the first PGPU_CLAIM_STATIC_PM / 1000 of the tiles and the rest is claimed in runs of 1/PGPU_CLAIM_DIV
+// of a workgroup's share.  The counters are u32 words 12..15 of the statistics block (zeroed per execution): launches
+// 0-3 of a plan.  Measured on MI355X and not the default (r06 session b, profiles/r06_ab_summary.txt): C3's scan
+// 729 -> 711 us at 1000 segments but its pipelined step 0.687 -> 0.719 ms, and at 125 segments 119 -> 145 us (every
+// claimed tile reloads its segment's records behind a workgroup barrier).
 #ifndef PGPU_CLAIM_STATIC_PM
 #define PGPU_CLAIM_STATIC_PM 750
 #endif
@@ -3570,7 +3572,7 @@ int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream
 #endif
 void set_tile_claims(KParams& kp, unsigned long long* d_stats, int grid, int launch) {
   kp.claim = nullptr;
-#ifndef PGPU_NO_CLAIM
+#ifdef PGPU_TILE_CLAIMS
   const int64_t share = (int64_t)kp.num_tiles / std::max(grid, 1);
   if (!kp.tile_chunks || grid < 64 || (grid & 7) || launch >= 4 || share < 8) return;
   kp.claim = reinterpret_cast<unsigned int*>(d_stats + 6) + launch;

@@ -108,7 +108,11 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   // run-time claims (chunked plans): the static runs end at claim_base, the rest goes claim_tiles at a time to the
   // workgroups that finish first.  The next claim is issued before the run it follows, so its atomic's round trip
   // overlaps that run's loads; one barrier per run hands it to the other waves.
+#ifdef PGPU_TILE_CLAIMS
   const bool dyn = p.claim != nullptr && gridDim.x >= 64 && (gridDim.x & 7) == 0 && p.tile_chunks;
+#else
+  constexpr bool dyn = false;  // (set_tile_claims, runtime.cpp: an A/B build's option, not the default)
+#endif
   __shared__ uint32_t claim_at[2];
   uint32_t next_claim = 0;
   if (dyn && tid == 0) next_claim = atomicAdd(p.claim, (uint32_t)p.claim_tiles);

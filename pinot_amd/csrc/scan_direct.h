@@ -57,7 +57,7 @@ template <int MODE, bool DENSE, bool SIMPLE = false, bool PAIR = false, bool FAS
 #define PGPU_MIN_WAVES 1
 #endif
 #ifndef PGPU_DENSE_MIN_WAVES
-#define PGPU_DENSE_MIN_WAVES 3
+#define PGPU_DENSE_MIN_WAVES 4
 #endif
 #ifndef PGPU_SIMPLE_MIN_WAVES
 #define PGPU_SIMPLE_MIN_WAVES 4

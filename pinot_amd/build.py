@@ -11,13 +11,17 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_PATH = os.path.join(HERE, "libpinotgpu.so")
 # (source, extra flags, object name): the scan kernels are compiled once per accumulator mode so the objects
 # build in parallel.
-SOURCES = [("kernels.hip", [], "kernels"), ("runtime.cpp", [], "runtime"), ("startree.cpp", [], "startree"),
+# the host runtime (rt.h): rt_* (core, dictionaries, planning, execution, numGroupsLimit / plan cache) and the C ABI
+RUNTIME = ["rt_core", "rt_dict", "rt_plan", "rt_exec", "rt_groups", "abi_table", "abi_plan", "abi_combine",
+           "abi_result"]
+SOURCES = [("kernels.hip", [], "kernels")] + [(n + ".cpp", [], n) for n in RUNTIME] + [("startree.cpp", [], "startree"),
            ("filter_stats.cpp", [], "filter_stats"), ("range_index.cpp", [], "range_index"), ("comm.cpp", [], "comm"), ("server_response.cpp", [], "server_response"),
            ("k_partition.hip", [], "k_partition"), ("k_hashfinal.hip", [], "k_hashfinal")] + \
     [("k_direct.hip", ["-DPGPU_MODE=%d" % m], "k_direct_%d" % m) for m in range(3)] + \
     [("k_startree.hip", ["-DPGPU_MODE=%d" % m], "k_startree_%d" % m) for m in range(3)]
 HEADERS = ["internal.h", "device.h", "scan_direct.h", "host_common.h", "startree_kernels.h",
-           "partition.h", "filter_stats.h", "host_result.h", "comm.h", "range_index.h"]
+           "partition.h", "filter_stats.h", "host_result.h", "comm.h", "range_index.h", "rt.h",
+           "rt_decls.h"]
 ARCH = os.environ.get("PGPU_OFFLOAD_ARCH", "gfx950")
 
 

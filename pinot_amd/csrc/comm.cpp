@@ -2,7 +2,7 @@
 //
 // What this replaces: the cross-server half of GroupByCombineOperator / GroupByOrderByCombineOperator
 // (pinot-core/.../operator/combine/GroupByCombineOperator.java:113-160, GroupByOrderByCombineOperator.java:170-181)
-// runs per GPU of one node here; the per-GPU group tables meet through these collectives (runtime.cpp's
+// runs per GPU of one node here; the per-GPU group tables meet through these collectives (abi_combine.cpp's
 // pgpu_plan_combine / pgpu_result_combine_rows).
 #include "comm.h"
 

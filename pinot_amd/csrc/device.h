@@ -335,7 +335,7 @@ struct SegView {
 
 // Index of local dictId `id` in a column's value arrays (KCol.dkey / dval): the id itself, or -- table-global value
 // arrays -- id + the global ids missing from the segment's dictionary below it.  Threshold k is t_k + k (t_k the local
-// id above the k-th missing value, runtime.cpp ensure_value_map), so the running index is compared, no memory access.
+// id above the k-th missing value, rt_dict.cpp ensure_value_map), so the running index is compared, no memory access.
 __device__ __forceinline__ uint32_t vidx(KColC& c, uint32_t id) {
   for (int k = 0; k < c.ngaps; ++k) id += id >= c.gaps[k] ? 1u : 0u;
   return id;

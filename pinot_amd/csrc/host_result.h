@@ -1,5 +1,5 @@
 // host_result.h — the host-side result of a plan (pgpu_result) and the pinned buffers behind it, shared by the
-// runtime (runtime.cpp) and the server-response / broker-reduce code (server_response.cpp).  Not part of the ABI.
+// runtime (rt_*.cpp, abi_*.cpp) and the server-response / broker-reduce code (server_response.cpp).  Not part of the ABI.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -69,7 +69,7 @@ struct ResultPool {
 
 struct pgpu_result_s;
 namespace pgpu {
-// Builds the columnar form of a result held in compact form (runtime.cpp); 0 or a PGPU_ERR_* status.
+// Builds the columnar form of a result held in compact form (rt_exec.cpp); 0 or a PGPU_ERR_* status.
 int result_expand(pgpu_result_s* r);
 }  // namespace pgpu
 
@@ -90,7 +90,7 @@ struct pgpu_result_s {
   // what the rows are (DataTable / trimming): table columns and types of the group-by keys, per aggregation its
   // function and table column (-1: COUNT(*)), and numGroupsLimitReached
   std::vector<int32_t> key_cols, key_types, agg_fn, agg_col;
-  // per group-by key: the table-global dictionary snapshot its group ids index (runtime.cpp's Dict)
+  // per group-by key: the table-global dictionary snapshot its group ids index (rt.h's Dict)
   std::vector<std::shared_ptr<const void>> key_dicts;
   bool groups_limit_reached = false;
   // Compact form (large tables, e.g. C5's 10M groups): the groups are the set bits of the bitmap at the start

@@ -1,5 +1,5 @@
 // internal.h — device-side data layout shared by the gfx950 kernels (kernels.hip) and the host runtime
-// (runtime.cpp).  Not part of the ABI.
+// (rt_*.cpp, abi_*.cpp).  Not part of the ABI.
 //
 // HBM layout of a pinned segment column (one hipMalloc per segment, columns packed back to back):
 //   fwd   : Pinot's forward-index bytes verbatim (MSB-first, big-endian bit packing of
@@ -77,7 +77,7 @@ struct KCol {
   int64_t key_base;
   int32_t bits;
   int32_t lut_off;
-  // Accumulator operands with table-global value arrays (runtime.cpp ensure_value_map): dkey / dval are the table's
+  // Accumulator operands with table-global value arrays (rt_dict.cpp ensure_value_map): dkey / dval are the table's
   // arrays from the global dictId of the segment's first value on, and local dictId i is at i + the number of global
   // ids missing from the segment's dictionary below it -- ngaps thresholds in mapped space, applied in order as
   // i += (i >= gaps[k]) (vidx); 0 for the segment's own arrays or a contiguous run of the global dictionary.

@@ -29,7 +29,7 @@ struct RangeIdx {
 // PGPU_ERR_INVALID_ARGUMENT with the thread's last error set.  Pure host code.
 int parse_range_index(const uint8_t* b, int64_t n, int64_t card, int32_t num_docs, RangeIdx* out);
 
-// Cardinality of a portable Roaring bitmap whose docs are below num_docs (runtime.cpp parse_roaring); false on
+// Cardinality of a portable Roaring bitmap whose docs are below num_docs (abi_table.cpp parse_roaring); false on
 // malformed input.
 bool roaring_cardinality(const uint8_t* b, int64_t n, int32_t num_docs, int64_t* docs);
 

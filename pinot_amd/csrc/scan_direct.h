@@ -46,7 +46,7 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
 }
 
 // ---------------------------------------------------------------------------------------------- K3 fused
-// DENSE: the plan expects dense tiles (estimated selectivity >= 1/4, runtime.cpp): wave-tiles with >= kDenseGroupMin matches
+// DENSE: the plan expects dense tiles (estimated selectivity >= 1/4, rt_plan.cpp): wave-tiles with >= kDenseGroupMin matches
 // decode whole groups of the group-by / aggregated columns (aggregate_group).  A separate instance because that
 // path needs ~45 more VGPRs, which would halve the occupancy of the sparse path.
 // LANE_BATCH: matched docs per aggregate_batch where a lane's 32-doc group has more than 2 -- 4 in the pure-AND sparse
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
 #ifdef PGPU_TILE_CLAIMS
   const bool dyn = p.claim != nullptr && gridDim.x >= 64 && (gridDim.x & 7) == 0 && p.tile_chunks;
 #else
-  constexpr bool dyn = false;  // (set_tile_claims, runtime.cpp: an A/B build's option, not the default)
+  constexpr bool dyn = false;  // (set_tile_claims, rt_exec.cpp: an A/B build's option, not the default)
 #endif
   __shared__ uint32_t claim_at[2];
   uint32_t next_claim = 0;

@@ -6,7 +6,7 @@ LZ4WithLengthCompressor.java) the decompressed length as a little-endian int, th
 valid block: this is a plain greedy compressor of the published LZ4 block format (sequences of token, literal-length
 bytes, literals, 2-byte little-endian offset, match-length bytes; minimum match 4; the last 5 bytes are literals and
 no match starts within the last 12), fast enough for test segments.  The reader that matters -- the product's -- is
-in libpinotgpu.so (runtime.cpp, used at pin time), checked against the oracle's independent decoder.
+in libpinotgpu.so (rt_dict.cpp, used at pin time), checked against the oracle's independent decoder.
 """
 import struct
 

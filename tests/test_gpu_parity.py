@@ -939,7 +939,7 @@ def test_table_config_roundtrip(gpu_lib):
 
 
 def test_table_global_value_arrays(oracle, gpu_lib):
-    """Accumulator columns with large dictionaries are gathered from the table-global value arrays (runtime.cpp
+    """Accumulator columns with large dictionaries are gathered from the table-global value arrays (rt_dict.cpp
     ensure_value_map, KCol.gaps, device.h vidx): a segment whose dictionary lacks a few global values maps its dictIds
     past them with thresholds, a contiguous run by an offset alone; more than kMaxValueGaps (16) missing values keep the
     segment's own arrays.  Dense, sparse, partitioned and aggregation-only scans against the oracle, before and after a

@@ -117,7 +117,7 @@ def test_group_paths(oracle, sparse):
 def test_in_filter_narrows_the_key_space_to_a_dense_table(oracle, sparse):
     """The IN-filtered shape r04 dropped from QUERIES after its path assertion failed: the conjunct `c IN (1, 3, 5, 7)`
     bounds the group-by column c to the global ids of [1, 7], so the key space the planner sizes is 3000 x 3000 x 7 =
-    6.3e7 < 2^26 -- a dense table, not hashed partitions (the filter-restricted key space, runtime.cpp "Key space
+    6.3e7 < 2^26 -- a dense table, not hashed partitions (the filter-restricted key space, rt_plan.cpp "Key space
     restricted by the filter").  The path is asserted as the planner should pick it, and the values against the
     oracle."""
     t, hs, segs = sparse

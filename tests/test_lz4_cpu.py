@@ -1,6 +1,6 @@
 """LZ4 raw chunks and raw-value predicates, CPU side.
 
-Two independent LZ4 block decoders -- the product's (runtime.cpp, reached through pgpu_raw_forward_index_values, the
+Two independent LZ4 block decoders -- the product's (rt_dict.cpp, reached through pgpu_raw_forward_index_values, the
 decoder pgpu_pin_segment runs) and the oracle's (or_lz4_decompress / or_raw_decode) -- are checked against:
   - the reference's own vector: TestCompression.java round-trips "testing123" through LZ4 and LZ4_LENGTH_PREFIXED; a
     10-byte input is one literal-only sequence, token 0xA0 (LZ4 block format, lz4-java 1.7 -- absent from

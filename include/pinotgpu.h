@@ -236,6 +236,10 @@ typedef struct {
 /* Compile the plan afresh instead of reusing the table's cached compilation of the same query over the same
  * segments (the cache is dropped whenever pinned state changes; PGPU_PLAN_CACHE=0 disables it process-wide). */
 #define PGPU_OPT_NO_PLAN_CACHE 4
+/* Record HIP timing events around the execution's kernels for pgpu_plan_timing.  Off by default: each event is a
+ * marker packet between two dependent dispatches of the stream (about 10 us per query of gaps at 125 segments,
+ * measured), so a serving query carries none.  Not part of the plan-cache key. */
+#define PGPU_OPT_TIMING 8
 
 /* A query compiled against a list of pinned segments (InstancePlanMakerImplV2.makeInstancePlan +
  * per-segment AggregationGroupByPlanNode: predicate evaluators per segment, group-key layout, accumulators). */
@@ -389,7 +393,8 @@ int pgpu_execute_groupby(pgpu_table table, const int64_t* segment_handles, int32
 int pgpu_plan_create_execute(pgpu_table table, const int64_t* segment_handles, int32_t num_segments,
                              const pgpu_query* q, void* stream, void* d_table, pgpu_plan* out);
 
-/* Timing of the last execution of this plan (HIP events on the execution stream), microseconds:
+/* Timing of the last execution of this plan (HIP events on the execution stream; the query carried PGPU_OPT_TIMING,
+ * else PGPU_ERR_INVALID_ARGUMENT), microseconds:
  * [0] whole execute, [1] the scan kernel launches (summed), [2] number of scan launches, [3] the star-tree kernels
  * (traversal + pre-aggregated document scan; 0 without star-tree segments).  out holds 4 doubles. */
 int pgpu_plan_timing(pgpu_plan plan, double* out4);

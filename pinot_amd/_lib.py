@@ -66,6 +66,7 @@ class PredicateC(ctypes.Structure):
 OPT_NO_STAR_TREE = 1
 OPT_SQL_GROUP_BY = 2
 OPT_NO_PLAN_CACHE = 4
+OPT_TIMING = 8
 LEAF_EMPTY, LEAF_MATCH_ALL, LEAF_SCAN, LEAF_SORTED, LEAF_BITMAP, LEAF_RANGE_INDEX = 0, 1, 2, 3, 4, 5
 
 

@@ -287,6 +287,7 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
     if (cache) plan_cache_put(t, key, *P);
   }
   P->end_time_ms = q->end_time_ms;
+  P->timed = (q->options & PGPU_OPT_TIMING) != 0;
   P->scratch = acquire_scratch(t);
   *out = P.release();
   return 0;
@@ -367,6 +368,7 @@ int pgpu_plan_create_execute(pgpu_table t, const int64_t* handles, int32_t nsegs
   se.d_table = d_table;
   const double tt2 = trace_on() ? now_us() : 0;
   P->end_time_ms = q->end_time_ms;
+  P->timed = (q->options & PGPU_OPT_TIMING) != 0;
   P->scratch = acquire_scratch(t);  // before plan_create_impl takes the table lock (acquire_scratch locks it too)
   const double tt3 = trace_on() ? now_us() : 0;
   int rc = 0;

@@ -37,11 +37,8 @@ int pgpu_plan_timing(pgpu_plan P, double* out3) try {
   PGPU_ABI_GUARD;
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");
   if (P->composite) return fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: timing is per part");
+  if (!P->timed) return fail(PGPU_ERR_INVALID_ARGUMENT, "execution not timed (query option PGPU_OPT_TIMING)");
   Scratch* sc = P->scratch;
-#ifdef PGPU_NO_TIMING_EVENTS
-  for (int i = 0; i < 4; ++i) out3[i] = i == 2 ? (double)P->launches_done : 0.0;
-  return 0;
-#endif
   HIP_TRY(hipEventSynchronize(sc->ev[3]));
   float a = 0;
   HIP_TRY(hipEventElapsedTime(&a, sc->ev[0], sc->ev[3]));

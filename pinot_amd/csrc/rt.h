@@ -69,13 +69,12 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
     if (_rc) return _rc;   \
   } while (0)
 
-// The execution's timing events (pgpu_plan_timing).  PGPU_NO_TIMING_EVENTS (an A/B build of the library only): none
-// recorded -- each event is a marker packet between two dependent dispatches of the stream.
-#ifdef PGPU_NO_TIMING_EVENTS
-#define PGPU_TIMING_RECORD(ev, stream) ((void)0)
-#else
-#define PGPU_TIMING_RECORD(ev, stream) HIP_TRY(hipEventRecord(ev, stream))
-#endif
+// The execution's timing events (pgpu_plan_timing), recorded only when the query asked for them (PGPU_OPT_TIMING):
+// each event is a marker packet between two dependent dispatches of the stream.
+#define PGPU_TIMING_RECORD(P, ev, stream)                   \
+  do {                                                      \
+    if ((P)->timed) HIP_TRY(hipEventRecord(ev, stream));    \
+  } while (0)
 
 struct DeviceGuard {
   int prev = -1;
@@ -711,6 +710,7 @@ struct pgpu_plan_s {
   Scratch* scratch = nullptr;
   hipStream_t last_stream = nullptr;
   bool executed = false;
+  bool timed = false;  // PGPU_OPT_TIMING: the executions record their timing events
   const void* d_table_used = nullptr;
   bool hash = false;
   // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local

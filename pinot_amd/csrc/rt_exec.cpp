@@ -198,7 +198,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     for (size_t i = old; i < sc->cev.size(); ++i) HIP_TRY(hipEventCreate(&sc->cev[i]));
   }
   X.mark("events");
-  PGPU_TIMING_RECORD(sc->ev[0], stream);
+  PGPU_TIMING_RECORD(P, sc->ev[0], stream);
   X.mark("event 0 recorded");
   TRY(sc->sets.ensure(std::max<size_t>(std::max<size_t>(P->set_words.size(), (size_t)P->set_words_bound) * 4, 16)));
   const size_t rec_cap = std::max<size_t>((size_t)P->segs.size() * P->seg_stride, P->segrec.size());
@@ -511,8 +511,8 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   if (check_launch_on()) TRY(check_launch_inputs(P, stream, X, C));
-  if (c == 0) PGPU_TIMING_RECORD(sc->ev[1], stream);
-  PGPU_TIMING_RECORD(sc->cev[2 * c], stream);
+  if (c == 0) PGPU_TIMING_RECORD(P, sc->ev[1], stream);
+  PGPU_TIMING_RECORD(P, sc->cev[2 * c], stream);
   if (C.num_tiles > 0 && P->partitioned) {
     const int nslots = X.nslots;
     KPartParams pp;
@@ -625,7 +625,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (wg_times) TRY(diag_wg_times_report(P->table, kp, grid, stream));
   }
-  PGPU_TIMING_RECORD(sc->cev[2 * c + 1], stream);
+  PGPU_TIMING_RECORD(P, sc->cev[2 * c + 1], stream);
   if (C.num_tiles > 0 && P->any_leap2 && P->leap_reserved && !P->partitioned) {
     if (P->chunks.size() == 1 && P->mode == MODE_LDS) {  // folded into the epilogue's launch
       X.leap_segs = kp.segs;
@@ -645,7 +645,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   const int64_t words = X.words;
   KParams& kp = X.kp;
   const int nl = P->launches_done;
-  if (nl == 0) PGPU_TIMING_RECORD(sc->ev[1], stream);
+  if (nl == 0) PGPU_TIMING_RECORD(P, sc->ev[1], stream);
   if (!P->star.empty()) {
     // star-tree segments: K5 traversal then K6 residual scan + aggregation into the same group table
     X.mark("before star buffers");
@@ -734,7 +734,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     HIP_TRY(hipMemcpyAsync(sc->maskstage.p, sc->leaf_masks.p, (size_t)P->generic_words * 4, hipMemcpyDeviceToHost,
                            stream));
   }
-  PGPU_TIMING_RECORD(sc->ev[2], stream);
+  PGPU_TIMING_RECORD(P, sc->ev[2], stream);
   X.mark("event 2 recorded");
   if (P->mode == MODE_LDS) {
     // fold every slab written: the scan launches' (back to back) and the star-tree chunks' after them
@@ -754,7 +754,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   if (X.leap_nsegs > 0 &&  // deferred but no fold ran (cannot happen for a plan with scan tiles; kept exact)
       launch_leap2_compose(X.leap_segs, P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream))
     return fail(PGPU_ERR_DEVICE, "filter statistics launch failed: %s", hipGetErrorString(hipGetLastError()));
-  PGPU_TIMING_RECORD(sc->ev[3], stream);
+  PGPU_TIMING_RECORD(P, sc->ev[3], stream);
   P->last_stream = stream;
   P->executed = true;
   if (trace_on()) {

@@ -256,7 +256,8 @@ std::string plan_cache_key(pgpu_table_s* t, const int64_t* handles, int32_t nseg
   put(&q->num_aggs, 4);
   if (q->num_aggs > 0) put(q->aggs, sizeof(pgpu_agg) * (size_t)q->num_aggs);
   put(&q->num_groups_limit, 4);
-  put(&q->options, 4);
+  const int32_t opts = q->options & ~PGPU_OPT_TIMING;  // timing events are per execution, not compiled in
+  put(&opts, 4);
   return k;
 }
 

@@ -572,7 +572,8 @@ class Plan:
         return out[:self.num_segments].astype(bool)
 
     def timing_us(self):
-        """(execute, scan launches summed, number of scan launches, star-tree kernels) in microseconds."""
+        """(execute, scan launches summed, number of scan launches, star-tree kernels) in microseconds; the query
+        carried timing=True (PGPU_OPT_TIMING), else PinotGpuError."""
         out = (ctypes.c_double * 4)()
         L.check(self.lib.pgpu_plan_timing(self.handle, out))
         return out[0], out[1], out[2], out[3]

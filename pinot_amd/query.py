@@ -119,6 +119,8 @@ class QueryContext:
         self.group_trim_threshold = group_trim_threshold
         # QueryContext.getEndTimeMs: absolute deadline (ms since the epoch), 0 = none (set_timeout)
         self.end_time_ms = 0
+        # the executions record HIP timing events for GpuPlan.timing_us (PGPU_OPT_TIMING; off for serving)
+        self.timing = False
 
     def set_timeout(self, timeout_ms):
         """End time = now + timeout_ms (the broker's arrival time + queryOptions timeoutMs,
@@ -195,7 +197,8 @@ class QueryContext:
     def _options(self):
         return (0 if getattr(self, "use_star_tree", True) else L.OPT_NO_STAR_TREE) | \
             (L.OPT_SQL_GROUP_BY if getattr(self, "sql_group_by", False) else 0) | \
-            (L.OPT_NO_PLAN_CACHE if getattr(self, "no_plan_cache", False) else 0)
+            (L.OPT_NO_PLAN_CACHE if getattr(self, "no_plan_cache", False) else 0) | \
+            (L.OPT_TIMING if getattr(self, "timing", False) else 0)
 
     def _build_c(self, column_index):
         keep = []

@@ -37,7 +37,26 @@ def _agg_query():
 
 def _hash_query():
     # GROUP BY a, b: 10^10 keys -> the open-addressing hash table, one global atomic per doc (a slow scan)
-    return QueryContext(["a", "b"], [("COUNT", "*"), ("SUM", "m")], num_groups_limit=0)
+    q = QueryContext(["a", "b"], [("COUNT", "*"), ("SUM", "m")], num_groups_limit=0)
+    q.timing = True  # the tests size their deadlines from the scan's timing events (PGPU_OPT_TIMING)
+    return q
+
+
+def test_timing_events_are_opt_in(table):
+    """Timing events only for a query with PGPU_OPT_TIMING; both forms share one cached plan and agree."""
+    t, handles = table
+    q = _agg_query()
+    with t.plan_execute(handles, q) as p:
+        untimed = p.finalize()
+        with pytest.raises(L.PinotGpuError) as e:
+            p.timing_us()
+        assert e.value.code == L.PGPU_ERR_INVALID_ARGUMENT
+    q.timing = True
+    with t.plan_execute(handles, q) as p:
+        timed = p.finalize()
+        tm = p.timing_us()
+    assert tm[0] >= tm[1] > 0 and tm[2] >= 1
+    assert timed.values == untimed.values and timed.stats.as_tuple() == untimed.stats.as_tuple()
 
 
 def test_deadline_already_past(table):

@@ -152,7 +152,7 @@ struct KParams {
   // scans stop taking tiles and set stats[5] (BaseCombineOperator.java:79-132 / GroupByCombineOperator.java:193-203
   // give up at the same point; the host then reports the timeout instead of a partial result)
   uint64_t deadline;
-  // diagnostics build only (PGPU_DIAG_WG_TIMES, PGPU_TRACE=wgtimes): per workgroup {start, tile loop end, end, tiles}
+  // diagnostics build only (PGPU_DIAG_WG_TIMES, PGPU_TRACE=wgtimes): per workgroup {start, tile loop end, end, tiles | first tile << 32, HW_ID, XCC_ID, 0, 0}
   unsigned long long* diag_times;
   // Run-time balance of chunked plans (tile_chunks = 1): the static runs cover tiles [0, claim_base); the rest is
   // claimed claim_tiles at a time through *claim (zeroed with the statistics per execution) by whichever workgroup

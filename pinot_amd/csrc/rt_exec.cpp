@@ -431,33 +431,41 @@ unsigned long long* g_diag_times = nullptr;
 int diag_wg_times_begin(KParams& kp, int grid, hipStream_t stream) {
   constexpr int kMaxWgs = 1 << 16;
   if (grid > kMaxWgs) return 0;
-  if (!g_diag_times) HIP_TRY(hipMalloc(&g_diag_times, (size_t)kMaxWgs * 32));
-  HIP_TRY(hipMemsetAsync(g_diag_times, 0, (size_t)grid * 32, stream));
+  if (!g_diag_times) HIP_TRY(hipMalloc(&g_diag_times, (size_t)kMaxWgs * 64));
+  HIP_TRY(hipMemsetAsync(g_diag_times, 0, (size_t)grid * 64, stream));
   kp.diag_times = g_diag_times;
   return 0;
 }
 
 int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream_t stream) {
   if (!kp.diag_times) return 0;
-  std::vector<unsigned long long> h((size_t)grid * 4);
+  std::vector<unsigned long long> h((size_t)grid * 8);
   HIP_TRY(hipMemcpyAsync(h.data(), kp.diag_times, h.size() * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   int khz = 100000;
   hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device);
   const double us = 1000.0 / khz;
   unsigned long long t0 = ~0ull;
-  for (int b = 0; b < grid; ++b) if (h[4 * b + 2]) t0 = std::min(t0, h[4 * b]);
+  for (int b = 0; b < grid; ++b) if (h[8 * b + 2]) t0 = std::min(t0, h[8 * b]);
   if (t0 == ~0ull) return 0;
   std::vector<double> st, le, en, tiles;
   double xcd_end[8] = {0};
+  // PGPU_WGTIMES_OUT=<file>: every workgroup's raw row appended (launch separator "# grid tiles")
+  FILE* raw = getenv("PGPU_WGTIMES_OUT") ? fopen(getenv("PGPU_WGTIMES_OUT"), "a") : nullptr;
+  if (raw) fprintf(raw, "# %d %lld\n", grid, (long long)kp.num_tiles);
   for (int b = 0; b < grid; ++b) {
-    if (!h[4 * b + 2]) continue;
-    st.push_back((h[4 * b] - t0) * us);
-    le.push_back((h[4 * b + 1] - t0) * us);
-    en.push_back((h[4 * b + 2] - t0) * us);
-    tiles.push_back((double)h[4 * b + 3]);
-    xcd_end[b & 7] = std::max(xcd_end[b & 7], en.back());
+    const unsigned long long* d = &h[8 * (size_t)b];
+    if (!d[2]) continue;
+    st.push_back((d[0] - t0) * us);
+    le.push_back((d[1] - t0) * us);
+    en.push_back((d[2] - t0) * us);
+    tiles.push_back((double)(d[3] & 0xffffffffu));
+    xcd_end[d[5] & 7] = std::max(xcd_end[d[5] & 7], en.back());
+    if (raw)
+      fprintf(raw, "%d %.2f %.2f %.2f %llu %llu %llu %llu\n", b, st.back(), le.back(), en.back(), d[3] & 0xffffffffu,
+              d[3] >> 32, d[4], d[5]);
   }
+  if (raw) fclose(raw);
   auto pct = [](std::vector<double> v, double q) {
     std::sort(v.begin(), v.end());
     return v[std::min(v.size() - 1, (size_t)(q * (v.size() - 1) + 0.5))];

@@ -138,6 +138,10 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   // FAST: an instance for plans whose filter is a pure AND of at most kFastLeaves leaves (the general program
   // evaluator compiled out)
   const bool fast = FAST || (p.pure_and && p.num_leaves <= kFastLeaves);
+#ifdef PGPU_DIAG_WG_TIMES
+  const int64_t diag_first = t_begin;
+  int diag_tiles = 0;
+#endif
   for (int run = 0;; ++run) {
   if (t_begin < t_end) {
     int seg = -1;
@@ -269,6 +273,9 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
         }
       }
       ++kk;
+#ifdef PGPU_DIAG_WG_TIMES
+      ++diag_tiles;
+#endif
     }
     if (p.leap_maps)  // each wave stores its own bytes (tiles of other segments hold don't-care values)
       for (int k = lane; k < kk; k += 64)
@@ -330,11 +337,14 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   }
 #ifdef PGPU_DIAG_WG_TIMES
   if (tid == 0 && p.diag_times) {
-    unsigned long long* d = p.diag_times + 4 * (int64_t)blockIdx.x;
+    unsigned long long* d = p.diag_times + 8 * (int64_t)blockIdx.x;
     d[0] = diag_t0;
     d[1] = diag_t1;
     d[2] = wall_clock64();
-    d[3] = (unsigned long long)kk;
+    d[3] = (unsigned long long)diag_tiles | ((unsigned long long)diag_first << 32);
+    // hardware registers HW_ID (wave / SIMD / CU / SH / SE ids) and XCC_ID: which CU and XCD ran the workgroup
+    d[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    d[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 #endif
 }

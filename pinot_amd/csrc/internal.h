@@ -106,6 +106,12 @@ struct KParams {
   int32_t num_tiles;
   int32_t tile_shift;      // small plans: each 8192-doc tile is split into 1 << tile_shift tiles (16 / 8 docs per lane)
   int32_t tile_chunks;     // 1: each workgroup takes a contiguous run of tiles (else XCD-interleaved tiles)
+  // chunked runs weighted by the CU slot a workgroup is dispatched to: with slot_n resident workgroups per CU, workgroup
+  // b (b / (grid / slot_n) = its slot, dispatch order) takes a share of its XCD's tiles proportional to slot_w[slot].
+  // The SIMDs issue oldest wave first, so equal shares end slot by slot (C3: 1 : 1.08 : 1.17 : 1.27 loop-end times,
+  // the same at 125 and 1000 segments).  slot_n = 0: equal shares.
+  int32_t slot_n;
+  uint16_t slot_w[4];
   int32_t pair_leaves;     // 1: an index leaf + a range scan are evaluated together (bitdir_range; 0 = A/B off)
   int32_t num_ops;         // 0 = match all
   int32_t pure_and;        // program is LEAF... AND(n): evaluate leaves with early exit, no stack

@@ -490,6 +490,34 @@ int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream
 #ifndef PGPU_CLAIM_DIV
 #define PGPU_CLAIM_DIV 16
 #endif
+// Chunked scans: each workgroup's run of tiles weighted by the CU slot it is dispatched to (KParams.slot_w).  The
+// weights are the inverse of the measured loop-end times of equal shares per slot (r06 session f, C3 at 125 and 1000
+// segments: slot 0..3 end at 1 : 1.08 : 1.17 : 1.27 of slot 3's pace; profiles/r06_ab_summary.txt);
+// PGPU_SLOT_WEIGHTS="w0,w1,..." overrides them (A/B), "1" turns weighting off.
+void set_slot_weights(KParams& kp, int grid, int num_cus) {
+  kp.slot_n = 0;
+  const int S = num_cus > 0 && grid % num_cus == 0 ? grid / num_cus : 0;
+  if (!kp.tile_chunks || S < 2 || S > 4 || (grid & 7) || kp.claim) return;
+  static const std::vector<double> env = [] {
+    std::vector<double> w;
+    if (const char* e = getenv("PGPU_SLOT_WEIGHTS"))
+      for (const char* q = e; *q;) {
+        char* end = nullptr;
+        const double v = strtod(q, &end);
+        if (end == q) break;
+        w.push_back(v);
+        q = *end == ',' ? end + 1 : end;
+      }
+    return w;
+  }();
+  static const double kDefault[4][4] = {{1, 0, 0, 0}, {1.08, 1, 0, 0}, {1.17, 1.08, 1, 0}, {1.26, 1.17, 1.08, 1}};
+  double w[4];
+  for (int s = 0; s < S; ++s) w[s] = env.empty() ? kDefault[S - 1][s] : env[std::min<size_t>(s, env.size() - 1)];
+  if (!env.empty() && env.size() == 1) return;  // "1": equal shares
+  for (int s = 0; s < S; ++s) kp.slot_w[s] = (uint16_t)std::max(1.0, std::min(4096.0, w[s] * 256.0 + 0.5));
+  kp.slot_n = S;
+}
+
 void set_tile_claims(KParams& kp, unsigned long long* d_stats, int grid, int launch) {
   kp.claim = nullptr;
 #ifdef PGPU_TILE_CLAIMS
@@ -627,6 +655,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     static const bool wg_times = diag("wgtimes");
     if (wg_times) TRY(diag_wg_times_begin(kp, grid, stream));
     set_tile_claims(kp, P->d_stats, grid, c);
+    set_slot_weights(kp, grid, P->table->num_cus);
     const int rc = launch_filter_groupby(kp, P->mode,
                                          scan_variant(P),
                                          grid, P->lds_bytes, stream);

@@ -122,8 +122,23 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
     const int64_t TS = dyn ? p.claim_base : T;
     const int64_t x = blockIdx.x & 7, i = blockIdx.x >> 3, nx = gridDim.x >> 3;
     const int64_t lo = x * TS / 8, len = (x + 1) * TS / 8 - lo;
-    t_begin = lo + i * len / nx;
-    t_end = lo + (i + 1) * len / nx;
+    if (p.slot_n > 1) {
+      // weighted by CU slot (KParams.slot_w): the XCD's workgroups i of slot s are i in [nx s / n, nx (s+1) / n)
+      auto cum = [&](int64_t j) {  // total weight of the XCD's workgroups [0, j)
+        int64_t c = 0;
+        for (int s = 0; s < p.slot_n; ++s) {
+          const int64_t a = nx * s / p.slot_n, e = nx * (s + 1) / p.slot_n;
+          c += (j <= a ? 0 : j < e ? j - a : e - a) * (int64_t)p.slot_w[s];
+        }
+        return c;
+      };
+      const int64_t tot = cum(nx);
+      t_begin = lo + len * cum(i) / tot;
+      t_end = lo + len * cum(i + 1) / tot;
+    } else {
+      t_begin = lo + i * len / nx;
+      t_end = lo + (i + 1) * len / nx;
+    }
     t_step = 1;
   } else if (gridDim.x >= 64 && (gridDim.x & 7) == 0) {
     const int64_t x = blockIdx.x & 7;

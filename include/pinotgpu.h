@@ -117,6 +117,9 @@ typedef struct {
   int32_t star_tree_workgroups;   /* workgroups of the star-tree document scan (default 0: the library's choice) */
   double dense_selectivity;       /* estimated selectivity from which plans take the dense scan instance
                                      (default 0.25; > 1 = never) */
+  double slot_weight_step;        /* chunked scans launched with no other query's scan in flight: the workgroup
+                                     dispatched to CU slot s of S takes a share of tiles weighted 1 + step (S-1-s)
+                                     (the SIMDs issue the oldest wave first; default 0.11; 0 = equal shares) */
 } pgpu_config;
 int pgpu_config_default(pgpu_config* out);
 int pgpu_table_set_config(pgpu_table table, const pgpu_config* config);

@@ -117,7 +117,8 @@ class ConfigC(ctypes.Structure):
                 ("hash_partition_bits", ctypes.c_int32), ("hash_partition_lds_kb", ctypes.c_int32),
                 ("lds_table_kb", ctypes.c_int32), ("plan_chunk_segments", ctypes.c_int32),
                 ("stream_chunks", ctypes.c_int32), ("compact_results", ctypes.c_int32),
-                ("star_tree_workgroups", ctypes.c_int32), ("dense_selectivity", ctypes.c_double)]
+                ("star_tree_workgroups", ctypes.c_int32), ("dense_selectivity", ctypes.c_double),
+                ("slot_weight_step", ctypes.c_double)]
 
 
 CONFIG_FIELDS = [f for f, _ in ConfigC._fields_ if f != "struct_size"]

@@ -296,7 +296,11 @@ int pgpu_plan_create(pgpu_table t, const int64_t* handles, int32_t nsegs, const 
 int pgpu_plan_destroy(pgpu_plan P) try {
   PGPU_ABI_GUARD;
   if (!P) return 0;
-  for (auto& part : P->parts) release_scratch(P->table, part.plan->scratch);
+  for (auto& part : P->parts) {
+    inflight_end(part.plan.get());
+    release_scratch(P->table, part.plan->scratch);
+  }
+  inflight_end(P);
   release_scratch(P->table, P->scratch);
   delete P;
   return 0;

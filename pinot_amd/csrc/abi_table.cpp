@@ -110,7 +110,8 @@ int pgpu_table_set_config(pgpu_table t, const pgpu_config* c) try {
   v.struct_size = (int32_t)sizeof v;
   if (v.hash_partition_bits < 0 || v.hash_partition_bits > 14 || v.hash_partition_lds_kb < 0 ||
       v.hash_partition_lds_kb > 128 || v.lds_table_kb < 1 || v.lds_table_kb > 160 || v.plan_chunk_segments < 1 ||
-      v.stream_chunks < 1 || v.star_tree_workgroups < 0 || !(v.dense_selectivity >= 0.0))
+      v.stream_chunks < 1 || v.star_tree_workgroups < 0 || !(v.dense_selectivity >= 0.0) ||
+      !(v.slot_weight_step >= 0.0 && v.slot_weight_step <= 4.0))
     return fail(PGPU_ERR_INVALID_ARGUMENT, "config value out of range");
   {
     std::lock_guard<std::mutex> g(t->cfg_mu);

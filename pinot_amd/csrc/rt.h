@@ -533,6 +533,7 @@ inline pgpu_config default_config() {
   c.compact_results = 1;
   c.star_tree_workgroups = 0;
   c.dense_selectivity = 0.25;
+  c.slot_weight_step = 0.11;
   return c;
 }
 
@@ -563,6 +564,9 @@ struct pgpu_table_s {
   std::shared_ptr<ResultPool> result_pool = std::make_shared<ResultPool>();
   int64_t device_bytes = 0;
   int num_cus = 256;
+  // executions launched and not yet seen complete (wait_plan) or destroyed: a launch with none beside it has the CUs
+  // to itself (set_slot_weights)
+  std::atomic<int> scans_inflight{0};
   // The virtual $docId column (identity forward index + values, docs [0, docid_n)): the hidden MIN($docId) slot of
   // the first-seen numGroupsLimit emulation reads it like any other column.
   uint32_t* d_docid_fwd = nullptr;
@@ -711,6 +715,8 @@ struct pgpu_plan_s {
   hipStream_t last_stream = nullptr;
   bool executed = false;
   bool timed = false;  // PGPU_OPT_TIMING: the executions record their timing events
+  bool inflight_counted = false;  // counted in table->scans_inflight (inflight_begin / inflight_end)
+  bool alone = false;             // no other execution of the table was in flight when this one launched
   const void* d_table_used = nullptr;
   bool hash = false;
   // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local

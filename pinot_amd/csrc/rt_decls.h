@@ -84,7 +84,9 @@ extern unsigned long long* g_diag_times;
 int diag_wg_times_begin(KParams& kp, int grid, hipStream_t stream);
 int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream_t stream);
 void set_tile_claims(KParams& kp, unsigned long long* d_stats, int grid, int launch);
-void set_slot_weights(KParams& kp, int grid, int num_cus);
+void set_slot_weights(KParams& kp, int grid, int num_cus, double step);
+void inflight_begin(pgpu_plan_s* P);
+void inflight_end(pgpu_plan_s* P);
 int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const LaunchChunk& C, int c);
 int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X);
 int plan_execute_impl(pgpu_plan_s* P, hipStream_t stream, void* d_table);

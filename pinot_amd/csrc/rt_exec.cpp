@@ -73,9 +73,25 @@ int cancel_fail() {
 
 bool cancelled(const pgpu_plan_s* P) { return __atomic_load_n(&P->cancel, __ATOMIC_ACQUIRE) != 0; }
 
+// table->scans_inflight: counted from the execution's launch until its completion is seen or the plan is destroyed
+void inflight_begin(pgpu_plan_s* P) {
+  if (P->inflight_counted) {
+    P->alone = P->table->scans_inflight.load(std::memory_order_relaxed) == 1;
+    return;
+  }
+  P->alone = P->table->scans_inflight.fetch_add(1, std::memory_order_relaxed) == 0;
+  P->inflight_counted = true;
+}
+void inflight_end(pgpu_plan_s* P) {
+  if (!P || !P->inflight_counted || !P->table) return;
+  P->table->scans_inflight.fetch_sub(1, std::memory_order_relaxed);
+  P->inflight_counted = false;
+}
+
 int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
   if (!P->scratch) {
     HIP_TRY(hipStreamSynchronize(stream));
+    inflight_end(P);
     return 0;
   }
   Scratch* sc = P->scratch;
@@ -91,7 +107,10 @@ int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
   const int64_t comm_lim = P->comm_used ? P->comm_used->timeout_ms.load(std::memory_order_relaxed) : 0;
   for (int spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(sc->busy);
-    if (e == hipSuccess) return 0;
+    if (e == hipSuccess) {
+      inflight_end(P);
+      return 0;
+    }
     if (e != hipErrorNotReady) return fail(PGPU_ERR_DEVICE, "query wait failed: %s", hipGetErrorString(e));
     if (cancelled(P)) {
       sc->abandoned = true;
@@ -169,6 +188,7 @@ void dense_lds_forms(const pgpu_plan_s* P, int32_t* pack_slot, uint32_t* narrow)
 }
 
 int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chunks, ExecCtx& X) {
+  inflight_begin(P);
   X.t_start = trace_on() ? now_us() : 0;
   if (cancelled(P)) return cancel_fail();  // nothing is launched for a cancelled query
   uint64_t deadline = 0;
@@ -490,31 +510,21 @@ int diag_wg_times_report(pgpu_table_s* t, const KParams& kp, int grid, hipStream
 #ifndef PGPU_CLAIM_DIV
 #define PGPU_CLAIM_DIV 16
 #endif
-// Chunked scans: each workgroup's run of tiles weighted by the CU slot it is dispatched to (KParams.slot_w).  The
-// weights are the inverse of the measured loop-end times of equal shares per slot (r06 session f, C3 at 125 and 1000
-// segments: slot 0..3 end at 1 : 1.08 : 1.17 : 1.27 of slot 3's pace; profiles/r06_ab_summary.txt);
-// PGPU_SLOT_WEIGHTS="w0,w1,..." overrides them (A/B), "1" turns weighting off.
-void set_slot_weights(KParams& kp, int grid, int num_cus) {
+// Chunked scans: each workgroup's run of tiles weighted by the CU slot it is dispatched to (KParams.slot_w), for a
+// launch that has the CUs to itself (P->alone: its workgroups' slots are their dispatch order; beside another query's
+// scan the freed slots go to the newcomers in no such order) and >= kSlotWeightMinShare tiles per workgroup.  The SIMDs
+// issue the oldest wave first: equal shares end slot by slot, 1 : 1.08 : 1.17 : 1.27 (C3, 125 and 1000 segments), and
+// weighted by those ratios the per-tile times spread further (4.55 / 4.92 / 5.47 / 6.06 us at 1000 segments), so
+// pgpu_config.slot_weight_step defaults to the latter's inverse, 1 + 0.11 (S-1-s) (r06 sessions f, g:
+// profiles/r06_ab_summary.txt); 0 gives equal shares.
+constexpr int64_t kSlotWeightMinShare = 32;
+void set_slot_weights(KParams& kp, int grid, int num_cus, double step) {
   kp.slot_n = 0;
   const int S = num_cus > 0 && grid % num_cus == 0 ? grid / num_cus : 0;
-  if (!kp.tile_chunks || S < 2 || S > 4 || (grid & 7) || kp.claim) return;
-  static const std::vector<double> env = [] {
-    std::vector<double> w;
-    if (const char* e = getenv("PGPU_SLOT_WEIGHTS"))
-      for (const char* q = e; *q;) {
-        char* end = nullptr;
-        const double v = strtod(q, &end);
-        if (end == q) break;
-        w.push_back(v);
-        q = *end == ',' ? end + 1 : end;
-      }
-    return w;
-  }();
-  static const double kDefault[4][4] = {{1, 0, 0, 0}, {1.08, 1, 0, 0}, {1.17, 1.08, 1, 0}, {1.26, 1.17, 1.08, 1}};
-  double w[4];
-  for (int s = 0; s < S; ++s) w[s] = env.empty() ? kDefault[S - 1][s] : env[std::min<size_t>(s, env.size() - 1)];
-  if (!env.empty() && env.size() == 1) return;  // "1": equal shares
-  for (int s = 0; s < S; ++s) kp.slot_w[s] = (uint16_t)std::max(1.0, std::min(4096.0, w[s] * 256.0 + 0.5));
+  if (!(step > 0.0) || !kp.tile_chunks || S < 2 || S > 4 || (grid & 7) || kp.claim ||
+      kp.num_tiles < kSlotWeightMinShare * grid)
+    return;
+  for (int s = 0; s < S; ++s) kp.slot_w[s] = (uint16_t)std::min(4096.0, (1.0 + step * (S - 1 - s)) * 256.0 + 0.5);
   kp.slot_n = S;
 }
 
@@ -655,7 +665,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     static const bool wg_times = diag("wgtimes");
     if (wg_times) TRY(diag_wg_times_begin(kp, grid, stream));
     set_tile_claims(kp, P->d_stats, grid, c);
-    set_slot_weights(kp, grid, P->table->num_cus);
+    if (P->alone) set_slot_weights(kp, grid, P->table->num_cus, P->cfg.slot_weight_step);
     const int rc = launch_filter_groupby(kp, P->mode,
                                          scan_variant(P),
                                          grid, P->lds_bytes, stream);

@@ -297,6 +297,7 @@ bool plan_cache_get(pgpu_table_s* t, const std::string& key, pgpu_plan_s* P) {
     P->star_docs_read = 0;
     P->shard = nullptr;
     P->cancel = 0;
+    P->inflight_counted = false;
     // a hash table sized by the groups the last execution of this plan found (deterministic for a cached plan:
     // same query over the same pinned segments)
     if (P->hash && P->groups_seen && P->stage_end.empty() && P->merged_records < 0) {
@@ -325,6 +326,7 @@ void plan_cache_put(pgpu_table_s* t, const std::string& key, pgpu_plan_s& P) {
     P.image = std::make_shared<DeviceImage>();  // built by the first execution, shared by every later hit
   auto img = std::make_shared<pgpu_plan_s>(P);
   img->scratch = nullptr;
+  img->inflight_counted = false;
   std::lock_guard<std::mutex> g(t->cache_mu);
   // The key was taken before planning.  Every change of pinned state bumps the version before it clears the cache:
   // a plan built across such a change carries the old version in its key and may reference state of that time

@@ -61,18 +61,19 @@ def test_config_defaults():
     got = {f: getattr(c, f) for f in L.CONFIG_FIELDS}
     assert got == {"plan_cache": 1, "partitioned_group_by": 1, "hash_partitions": 1, "hash_partition_bits": 14,
                    "hash_partition_lds_kb": 0, "lds_table_kb": 112, "plan_chunk_segments": 4096, "stream_chunks": 1,
-                   "compact_results": 1, "star_tree_workgroups": 0, "dense_selectivity": 0.25}
+                   "compact_results": 1, "star_tree_workgroups": 0, "dense_selectivity": 0.25,
+                   "slot_weight_step": 0.11}
     assert lib.pgpu_config_default(None) == L.PGPU_ERR_INVALID_ARGUMENT
     assert lib.pgpu_table_set_config(None, ctypes.byref(c)) == L.PGPU_ERR_INVALID_ARGUMENT
 
 
 def test_only_diagnostics_read_from_the_environment():
-    """Executor settings come from pgpu_config, never the environment: the one variable the library reads is the
-    diagnostics switch PGPU_TRACE."""
+    """Executor settings come from pgpu_config, never the environment: the variables the library reads are the
+    diagnostics switch PGPU_TRACE and the diagnostics build's raw workgroup-times file."""
     csrc = os.path.join(ROOT, "pinot_amd", "csrc")
     names = set()
     for f in os.listdir(csrc):
         src = open(os.path.join(csrc, f)).read()
         names |= set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', src))
         assert "getenv_flag" not in src, f
-    assert names == {"PGPU_TRACE"}, names
+    assert names == {"PGPU_TRACE", "PGPU_WGTIMES_OUT"}, names

@@ -140,6 +140,7 @@ int pgpu_plan_exchange_export(pgpu_plan P, void* stream, int32_t nparts, const i
 int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, const void* d_records, int64_t n) try {
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
+  P->exported = false;
   if (n < 0 || (n > 0 && !d_records) || n > (INT64_C(1) << 40))  // the table below holds >= 2n slots
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   uint32_t conv = 0;
@@ -530,6 +531,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
                       void* d_shard, int64_t* key_begin, int64_t* key_count) try {
   PGPU_ABI_GUARD;
   if (!P || !c) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  P->exported = false;  // the table changes: finalize reads it from the device
   if (mode == PGPU_COMBINE_LOCAL) {
     if (key_begin) *key_begin = 0;
     if (key_count) *key_count = P->num_keys;

@@ -420,10 +420,12 @@ int launch_exclusive_scan_u32(uint32_t* data, int32_t n, void* stream);
 int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream);
 // Per STATS_LEAP2 record of a launch: composes its (tile, wave) maps in doc order into the segment's count
 // (stats[2] += ...).
-// reduce_slabs + leap2_compose of a one-launch plan as one launch.
+// reduce_slabs + leap2_compose of a one-launch plan as one launch; host_out (pinned, num_slots x num_keys + 6 words;
+// null = none): the table and the statistics words copied there by the last block (done: a zeroed u32 counter).
 int launch_epilogue(const uint64_t* slab, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                     int32_t num_blocks, uint64_t* out, const uint8_t* segs, int32_t seg_stride, int32_t num_segs,
-                    const uint8_t* maps, unsigned long long* stats, void* stream);
+                    const uint8_t* maps, unsigned long long* stats, uint64_t* host_out, unsigned int* done,
+                    void* stream);
 int launch_leap2_compose(const uint8_t* segs, int32_t seg_stride, int32_t num_segs, const uint8_t* maps,
                          unsigned long long* stats, void* stream);
 int launch_leaf_masks(const KParams& p, const KMaskJob* jobs, int32_t num_jobs, uint32_t* out, void* stream);

@@ -610,17 +610,38 @@ __global__ __launch_bounds__(256) void leap2_compose_kernel(const uint8_t* __res
 }
 
 // The epilogue of a one-launch LDS-table plan in one launch: the slab fold's blocks, then the leap-frog statistics'
-// blocks (independent work; one launch gap and one kernel tail less per query).
+// blocks (independent work; one launch gap and one kernel tail less per query).  host_out (small tables): the last
+// block to finish copies the table and the statistics words into pinned host memory, which finalize reads once the
+// stream has completed -- no copy launch behind the epilogue -- and re-arms the block counter `done` for the next use.
 __global__ __launch_bounds__(256) void epilogue_kernel(const uint64_t* __restrict__ slab, SlotKinds kinds,
                                                        int64_t num_keys, int32_t num_slots, int32_t num_blocks,
                                                        uint64_t* __restrict__ out, int32_t reduce_blocks,
                                                        const uint8_t* __restrict__ segs, int32_t seg_stride,
                                                        int32_t num_segs, const uint8_t* __restrict__ maps,
-                                                       unsigned long long* __restrict__ stats) {
+                                                       unsigned long long* __restrict__ stats,
+                                                       uint64_t* __restrict__ host_out, unsigned int* __restrict__ done) {
   if ((int)blockIdx.x < reduce_blocks)  // block-uniform
     reduce_slabs_block(blockIdx.x, slab, kinds, num_keys, num_slots, num_blocks, out);
   else
     leap2_compose_block((int)blockIdx.x - reduce_blocks, segs, seg_stride, num_segs, maps, stats);
+  if (!host_out) return;
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this block's table words and statistics adds before its count
+    last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int64_t words = (int64_t)num_slots * num_keys;
+  for (int64_t i = threadIdx.x; i < words + 6; i += blockDim.x) {
+    const uint64_t v = i < words ? __hip_atomic_load(out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (uint64_t)__hip_atomic_load(stats + (i - words), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host_out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The leaves' match bitmaps of STATS_GENERIC segments (the replay of filter_stats.cpp runs on the host).
@@ -1030,7 +1051,8 @@ int launch_filter_bitmap(const KParams& p, uint32_t* out_words, void* stream) {
 
 int launch_epilogue(const uint64_t* slab, const int32_t* slot_kind, int32_t num_slots, int64_t num_keys,
                     int32_t num_blocks, uint64_t* out, const uint8_t* segs, int32_t seg_stride, int32_t num_segs,
-                    const uint8_t* maps, unsigned long long* stats, void* stream) {
+                    const uint8_t* maps, unsigned long long* stats, uint64_t* host_out, unsigned int* done,
+                    void* stream) {
   SlotKinds k{};
   for (int i = 0; i < num_slots && i < kMaxSlots; ++i) k.k[i] = slot_kind[i];
   const int64_t reduce_blocks = ((int64_t)num_slots * num_keys + 7) / 8;
@@ -1038,7 +1060,7 @@ int launch_epilogue(const uint64_t* slab, const int32_t* slot_kind, int32_t num_
   if (reduce_blocks + leap_blocks < 1) return 0;
   hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)(reduce_blocks + leap_blocks)), dim3(256), 0, S(stream), slab, k,
                      num_keys, num_slots, num_blocks, out, (int32_t)reduce_blocks, segs, seg_stride, num_segs, maps,
-                     stats);
+                     stats, host_out, done);
   return PGPU_HIP_OK(hipGetLastError());
 }
 

@@ -250,6 +250,8 @@ inline double key_double(int64_t k) {
 }
 
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
+constexpr int64_t kExportBytes = 64 * 1024;  // LDS-table plans up to this size: the epilogue writes them to host memory
+constexpr int kStatsRing = 256;              // statistics entries zeroed per fill (Scratch::stats_ring)
 constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
 #ifndef PGPU_PART_LDS_KB
 #define PGPU_PART_LDS_KB 64
@@ -469,6 +471,13 @@ struct Scratch {
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
   // free it while its uploads may still be queued behind other queries' work on a shared stream.
   HostPinned stage, readback, starstage, bitstage, maskstage;
+  // Statistics words: 64-byte entries of a ring zeroed kStatsRing executions at a time (exec_prologue); an entry
+  // stays the plan's until it executes again or releases the scratch
+  DevBuf stats_ring;
+  int ring_pos = 0;
+  // small LDS-table plans: the epilogue's copy of table + statistics (pinned host) and its block counter
+  HostPinned exported;
+  DevBuf export_done;
   std::vector<uint8_t> starrec_sent;  // the star-tree records last uploaded to `starrec` (a repeat skips the copy)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> cev;  // per scan launch: (start, end)
@@ -483,7 +492,8 @@ struct Scratch {
     for (const DevBuf* b : {&docbits, &bittasks, &bitblocks, &rawtasks, &segrec, &sets, &slab, &table, &hash_keys,
                             &stats, &ckeys, &cslots, &counter, &bitmap, &tile_seg, &starrec, &starwork, &part_start,
                             &block_off, &rec_key, &rec_val, &rec_key32, &stage_keys, &coarse_fill, &fine_fill,
-                            &mid_key, &mid_val, &leap_maps, &mask_jobs, &leaf_masks, &hsort, &part_mm})
+                            &mid_key, &mid_val, &leap_maps, &mask_jobs, &leaf_masks, &hsort, &part_mm, &stats_ring,
+                            &export_done})
       n += b->cap;
     return n;
   }
@@ -504,6 +514,7 @@ struct Scratch {
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
     xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release(); hsort.release(); part_mm.release();
+    stats_ring.release(); ring_pos = 0; exported.release(); export_done.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };
@@ -717,6 +728,7 @@ struct pgpu_plan_s {
   bool timed = false;  // PGPU_OPT_TIMING: the executions record their timing events
   bool inflight_counted = false;  // counted in table->scans_inflight (inflight_begin / inflight_end)
   bool alone = false;             // no other execution of the table was in flight when this one launched
+  bool exported = false;          // the last execution's epilogue copied table + statistics to scratch->exported
   const void* d_table_used = nullptr;
   bool hash = false;
   // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local
@@ -863,6 +875,7 @@ struct ExecCtx {
   const uint8_t* leap_segs = nullptr;
   int32_t leap_nsegs = 0;
   uint64_t* table = nullptr;
+  bool external = false;  // the caller's device table (pgpu_plan_execute's d_table)
   int64_t words = 0;
   int nslots = 0;
   double t_start = 0;

@@ -225,21 +225,22 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   TRY(sc->segrec.ensure(std::max<size_t>(rec_cap, 16)));
   TRY(sc->stage.ensure(std::max<size_t>(rec_cap + (size_t)std::max<int64_t>(P->set_words_bound,
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
-  // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag): right after the group table when
-  // the table is internal, so finalize reads both with one copy
+  // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag): the next entry of the scratch's
+  // ring, whose entries are zeroed kStatsRing at a time -- one fill per kStatsRing executions instead of a fill
+  // launch (and its gap before the scan) per query
   constexpr size_t kStatsBytes = 64;
-  unsigned long long* stats;
-  if (!d_table) {
-    TRY(sc->table.ensure((size_t)X.words * 8 + kStatsBytes));
-    stats = reinterpret_cast<unsigned long long*>(sc->table.as<uint8_t>() + (size_t)X.words * 8);
-  } else {
-    TRY(sc->stats.ensure(kStatsBytes));
-    stats = sc->stats.as<unsigned long long>();
+  if (!d_table) TRY(sc->table.ensure(std::max<size_t>((size_t)X.words * 8, 8)));
+  if (sc->stats_ring.cap < kStatsBytes * kStatsRing) {
+    TRY(sc->stats_ring.ensure(kStatsBytes * kStatsRing));
+    sc->ring_pos = 0;
   }
+  if (sc->ring_pos == 0) HIP_TRY(hipMemsetAsync(sc->stats_ring.p, 0, kStatsBytes * kStatsRing, stream));
+  unsigned long long* stats = sc->stats_ring.as<unsigned long long>() + (size_t)sc->ring_pos * (kStatsBytes / 8);
+  sc->ring_pos = (sc->ring_pos + 1) % kStatsRing;
   P->d_stats = stats;
+  P->exported = false;
+  X.external = d_table != nullptr;
   X.mark("buffers");
-  HIP_TRY(hipMemsetAsync(stats, 0, kStatsBytes, stream));
-  X.mark("statistics memset queued");
   X.segrec = sc->segrec.as<uint8_t>();
   X.sets = sc->sets.as<uint32_t>();
   TRY(sc->tile_seg.ensure((size_t)std::max<int64_t>(std::max<int64_t>(P->num_tiles, P->tile_bound), 1) * 4));
@@ -789,9 +790,22 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
     if (all == 0) {
       if (launch_table_init(X.table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
-    } else if (launch_epilogue(kp.slab, P->slot_kind.data(), nslots, P->num_keys, (int32_t)all, X.table, X.leap_segs,
-                               P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats, stream)) {
-      return fail(PGPU_ERR_DEVICE, "reduce launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else {
+      // small internal tables: the epilogue's last block also writes table + statistics to pinned host memory
+      const bool exp = !X.external && X.words * 8 <= kExportBytes;
+      if (exp) {
+        TRY(sc->exported.ensure((size_t)X.words * 8 + 64));
+        if (!sc->export_done.p) {
+          TRY(sc->export_done.ensure(64));
+          HIP_TRY(hipMemsetAsync(sc->export_done.p, 0, 64, stream));
+        }
+      }
+      if (launch_epilogue(kp.slab, P->slot_kind.data(), nslots, P->num_keys, (int32_t)all, X.table, X.leap_segs,
+                          P->seg_stride, X.leap_nsegs, kp.leap_maps, kp.stats,
+                          exp ? reinterpret_cast<uint64_t*>(sc->exported.p) : nullptr, exp ? sc->export_done.as<unsigned int>() : nullptr,
+                          stream))
+        return fail(PGPU_ERR_DEVICE, "reduce launch failed: %s", hipGetErrorString(hipGetLastError()));
+      P->exported = exp;
     }
     X.leap_nsegs = 0;
   }
@@ -850,6 +864,9 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   int64_t n = 0;
   uint64_t matched = 0, star_scanned = 0;
   const int64_t words = (int64_t)nslots * G;
+  // the epilogue wrote this execution's whole table + statistics to host memory, and nothing has changed the table
+  // since (a combine clears P->exported)
+  const bool from_export = P->exported && table == P->d_table_used && key_begin == 0 && G == P->num_keys;
   double t_sync1 = 0;
   R->pool = P->table->result_pool;
   {
@@ -857,7 +874,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     // device -- it would hold the wait (and a pgpu_plan_cancel or the query's deadline) until the scan is done.  When
     // one must grow, the plan's work is waited for first (cancel- and deadline-aware), then the buffers grow.
     bool grow = sc->counter.cap < 64 + (size_t)kMaxSlots * 16 || sc->readback.cap < 64 + (size_t)nslots * 16;
-    if (!P->hash && words * 8 <= kHostCompactBytes) grow |= sc->readback.cap < (size_t)words * 8 + 64;
+    if (!P->hash && words * 8 <= kHostCompactBytes && !from_export) grow |= sc->readback.cap < (size_t)words * 8 + 64;
     else if (!P->hash) grow |= sc->cslots.cap < compact_scratch_bytes(G, nslots);
     else if (!P->part_hash_live)
       grow |= sc->ckeys.cap < (size_t)std::max<int64_t>(1, std::min<int64_t>(G, P->merged_records >= 0
@@ -870,14 +887,20 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     }
   }
   if (!P->hash && words * 8 <= kHostCompactBytes) {
-    // small dense table: one copy (table + stats) and one sync, compacted on the host in key order
-    TRY(sc->readback.ensure((size_t)words * 8 + 64));
-    uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);
-    if (reinterpret_cast<const uint8_t*>(P->d_stats) == reinterpret_cast<const uint8_t*>(table) + words * 8) {
-      HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 48, hipMemcpyDeviceToHost, stream));  // table + stats
+    // small dense table: the epilogue's copy in pinned host memory (from_export), else one or two copies (table +
+    // stats) and one sync; compacted on the host in key order
+    uint64_t* st;
+    if (from_export) {
+      st = reinterpret_cast<uint64_t*>(sc->exported.p);
     } else {
-      HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipMemcpyAsync(st + words, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+      TRY(sc->readback.ensure((size_t)words * 8 + 64));
+      st = reinterpret_cast<uint64_t*>(sc->readback.p);
+      if (reinterpret_cast<const uint8_t*>(P->d_stats) == reinterpret_cast<const uint8_t*>(table) + words * 8) {
+        HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 48, hipMemcpyDeviceToHost, stream));  // table + stats
+      } else {
+        HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipMemcpyAsync(st + words, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+      }
     }
     TRY(wait_plan(P, stream));
     t_sync1 = trace_on() ? now_us() : 0;

@@ -234,6 +234,9 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     TRY(sc->stats_ring.ensure(kStatsBytes * kStatsRing));
     sc->ring_pos = 0;
   }
+#ifdef PGPU_NO_STATS_RING  // (an A/B build of the library: one fill per execution)
+  sc->ring_pos = 0;
+#endif
   if (sc->ring_pos == 0) HIP_TRY(hipMemsetAsync(sc->stats_ring.p, 0, kStatsBytes * kStatsRing, stream));
   unsigned long long* stats = sc->stats_ring.as<unsigned long long>() + (size_t)sc->ring_pos * (kStatsBytes / 8);
   sc->ring_pos = (sc->ring_pos + 1) % kStatsRing;
@@ -792,7 +795,11 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
     } else {
       // small internal tables: the epilogue's last block also writes table + statistics to pinned host memory
+#ifdef PGPU_NO_EXPORT  // (an A/B build of the library: finalize copies the table back)
+      const bool exp = false;
+#else
       const bool exp = !X.external && X.words * 8 <= kExportBytes;
+#endif
       if (exp) {
         TRY(sc->exported.ensure((size_t)X.words * 8 + 64));
         if (!sc->export_done.p) {

@@ -794,11 +794,14 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
       if (launch_table_init(X.table, P->slot_kind.data(), nslots, P->num_keys, nullptr, stream))
         return fail(PGPU_ERR_DEVICE, "table init launch failed");
     } else {
-      // small internal tables: the epilogue's last block also writes table + statistics to pinned host memory
-#ifdef PGPU_NO_EXPORT  // (an A/B build of the library: finalize copies the table back)
-      const bool exp = false;
-#else
+      // PGPU_EPILOGUE_EXPORT (an A/B build of the library only): for small internal tables the epilogue's last block
+      // also writes table + statistics to pinned host memory and finalize launches no copy.  Measured and not the
+      // default (r06 sessions i, j): the copy launch goes, but the host sees the stream complete ~10-15 us later
+      // (C1 latency 0.057 -> 0.071 ms, C3 at 125 segments 0.163 -> 0.169).
+#ifdef PGPU_EPILOGUE_EXPORT
       const bool exp = !X.external && X.words * 8 <= kExportBytes;
+#else
+      const bool exp = false;
 #endif
       if (exp) {
         TRY(sc->exported.ensure((size_t)X.words * 8 + 64));

@@ -645,6 +645,7 @@ def main():
     trace = []  # per query: [k, launch start, launch end, finalize start, complete end] (perf_counter)
     phases = {"plan": 0.0, "merge": 0.0, "finalize": 0.0, "close": 0.0, "finalize_c": 0.0, "decode": 0.0}
     star_work = [0, 0, 0]
+    star_mbytes = [-1]
 
     def launch(k):
         """Plan + execute query k on its stream (streamed: segment chunks launch while the rest is planned), then
@@ -683,6 +684,7 @@ def main():
         if w.star_tree and not args.no_star_tree:  # star-tree plans: traversal + pre-aggregated document scan
             k_us = (tm[3], 1)
             star_work[:] = plan.star_work()
+            star_mbytes[0] = plan.star_metric_bytes()
         else:
             k_us = (tm[1], max(int(tm[2]), 1))  # scan launches of this query: summed duration, count
         fc_us, dec_us = plan.finalize_us
@@ -806,23 +808,26 @@ def main():
     log("timed region done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     roofline = None
     if not args.no_bytes and w.star_tree and not args.no_star_tree and star_work[0] > 0:
-        # star-tree bytes model: nodes x 28 B + star-tree documents read x (bits of the dimensions
-        # they are read for + 8 B per pre-aggregated metric array)
+        # star-tree bytes model (line-granular): nodes x 28 B + star-tree documents read x the bits of
+        # the dimensions they are read for + the metric arrays' 64-B sectors that hold a matched document (counted by
+        # the kernel: pgpu_plan_star_metric_bytes; without it, 8 B per document per pre-aggregated array)
         preds = []
         if q.filter is not None:
             q.filter.postfix(preds, [])
         dims = sorted(set(q.group_by) | {p.column for p in preds})
         dim_bits = sum(_col_info(table, int(handles[0]), c)[1] for c in dims)
         nslots = probe_nslots
-        per_doc = dim_bits / 8.0 + 8.0 * nslots
-        bytes_alg = star_work[1] * 28 + star_work[2] * per_doc
+        metric_bytes = star_mbytes[0] if star_mbytes[0] >= 0 else star_work[2] * 8.0 * nslots
+        per_doc = dim_bits / 8.0 + metric_bytes / max(star_work[2], 1)
+        bytes_alg = star_work[1] * 28 + star_work[2] * dim_bits / 8.0 + metric_bytes
         achieved = bytes_alg / (kernel_avg_us * 1e-6) / 1e9 if kernel_avg_us > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                     "bytes_alg_per_launch": int(bytes_alg), "kernel_us": round(kernel_avg_us, 2),
                     "kernels": "startree_traverse_kernel + startree_scan_kernel",
                     "star_segments": int(star_work[0]), "star_nodes": int(star_work[1]),
-                    "star_docs_read": int(star_work[2]), "bytes_per_star_doc": per_doc,
+                    "star_docs_read": int(star_work[2]), "bytes_per_star_doc": round(per_doc, 3),
+                    "star_metric_bytes": int(metric_bytes),
                     "launches_per_query": 1, "kernel_us_per_query": round(kernel_avg_us, 2)}
     if not args.no_bytes and (not w.star_tree or args.no_star_tree):  # scan-path bytes model
         bytes_alg, matched = compulsory_bytes(table, handles, q, docs, w.inverted_columns)

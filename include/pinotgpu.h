@@ -405,6 +405,10 @@ int pgpu_plan_timing(pgpu_plan plan, double* out4);
 /* Star-tree work of the last execution (after finalize): [0] segments answered from their star-tree, [1] their
  * tree nodes (28 bytes each, OffHeapStarTreeNode), [2] star-tree documents the residual scan read. */
 int pgpu_plan_star_work(pgpu_plan plan, int64_t* out3);
+/* Bytes of the star-tree metric arrays the last execution's document scan read (after finalize): the 64-byte
+ * sectors holding at least one matched document, summed over the arrays read; -1 where finalize did not read the
+ * counter back (tables past 512 KB).  The star path's line-granular bytes model (bench.py). */
+int pgpu_plan_star_metric_bytes(pgpu_plan plan, int64_t* bytes);
 
 /* Per plan segment (plan order): 1 if the segment is scanned, 0 if its filter folds to always-false against the
  * segment's dictionaries (EmptyFilterOperator, core/plan/FilterPlanNode.java:146-176).  out holds num_segments. */

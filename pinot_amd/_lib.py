@@ -190,6 +190,7 @@ _PROTOS = {
                                      ctypes.POINTER(c_voidp)]),
     "pgpu_plan_timing": (c_int, [c_voidp, c_f64p]),
     "pgpu_plan_star_work": (c_int, [c_voidp, c_i64p]),
+    "pgpu_plan_star_metric_bytes": (c_int, [c_voidp, c_i64p]),
     "pgpu_plan_scanned_segments": (c_int, [c_voidp, c_u8p]),
     "pgpu_attach_startree": (c_int, [c_voidp, c_i64, ctypes.POINTER(StarTreeDescC)]),
     "pgpu_attach_inverted_index": (c_int, [c_voidp, c_i64, c_i32, c_voidp, c_i64]),

@@ -91,6 +91,18 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
     for (int c : st->dim_cols) card.push_back(std::max(seg.cols[c].card, 1));
     TRY(validate_startree(d, card, st->dim_bits));
   }
+  // Metric arrays whose values are all integers of int32 range are pinned as int32 (the kernel widens them exactly):
+  // C4's SUM__m and COUNT__* -- the star-tree documents' metric bytes halve.
+  auto ints32_f = [](const double* v, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+      if (!(v[i] >= -2147483648.0 && v[i] <= 2147483647.0) || v[i] != (double)(int32_t)v[i]) return false;
+    return true;
+  };
+  auto ints32_c = [](const int64_t* v, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+      if (v[i] < INT32_MIN || v[i] > INT32_MAX) return false;
+    return true;
+  };
   for (int m = 0; m < d->num_metrics; ++m) {
     const pgpu_agg a = d->metrics[m];
     if (a.fn < PGPU_AGG_COUNT || a.fn > PGPU_AGG_AVG) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad metric function");
@@ -100,7 +112,10 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
     if (needs_f && (a.column < 0 || a.column >= (int)seg.cols.size()))
       return fail(PGPU_ERR_INVALID_ARGUMENT, "bad star-tree metric column");
     st->metrics.push_back(a);
-    bytes += (needs_f ? (int64_t)d->num_docs * 8 : 0) + (needs_c ? (int64_t)d->num_docs * 8 : 0) + 32;
+    st->mf_narrow.push_back(needs_f && ints32_f(d->metric_f64[m], d->num_docs));
+    st->mc_narrow.push_back(needs_c && ints32_c(d->metric_i64[m], d->num_docs));
+    bytes += (needs_f ? (int64_t)d->num_docs * (st->mf_narrow.back() ? 4 : 8) : 0) +
+             (needs_c ? (int64_t)d->num_docs * (st->mc_narrow.back() ? 4 : 8) : 0) + 32;
   }
   HIP_TRY(hipMalloc(&st->d_block, bytes));
   st->bytes = bytes;
@@ -120,14 +135,24 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
     const double* pf = nullptr;
     const int64_t* pc = nullptr;
     if (a.fn != PGPU_AGG_COUNT) {
-      memcpy(host.data() + off, d->metric_f64[m], (size_t)d->num_docs * 8);
+      if (st->mf_narrow[m]) {
+        int32_t* o = reinterpret_cast<int32_t*>(host.data() + off);
+        for (int64_t i = 0; i < d->num_docs; ++i) o[i] = (int32_t)d->metric_f64[m][i];
+      } else {
+        memcpy(host.data() + off, d->metric_f64[m], (size_t)d->num_docs * 8);
+      }
       pf = reinterpret_cast<const double*>((uint8_t*)st->d_block + off);
-      off += (int64_t)d->num_docs * 8 + 16;
+      off += (int64_t)d->num_docs * (st->mf_narrow[m] ? 4 : 8) + 16;
     }
     if (a.fn == PGPU_AGG_COUNT || a.fn == PGPU_AGG_AVG) {
-      memcpy(host.data() + off, d->metric_i64[m], (size_t)d->num_docs * 8);
+      if (st->mc_narrow[m]) {
+        int32_t* o = reinterpret_cast<int32_t*>(host.data() + off);
+        for (int64_t i = 0; i < d->num_docs; ++i) o[i] = (int32_t)d->metric_i64[m][i];
+      } else {
+        memcpy(host.data() + off, d->metric_i64[m], (size_t)d->num_docs * 8);
+      }
       pc = reinterpret_cast<const int64_t*>((uint8_t*)st->d_block + off);
-      off += (int64_t)d->num_docs * 8 + 16;
+      off += (int64_t)d->num_docs * (st->mc_narrow[m] ? 4 : 8) + 16;
     }
     st->d_mf.push_back(pf);
     st->d_mc.push_back(pc);

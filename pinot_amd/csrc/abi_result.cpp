@@ -33,6 +33,13 @@ int pgpu_plan_star_work(pgpu_plan P, int64_t* out3) try {
   return 0;
 } PGPU_ABI_CATCH
 
+int pgpu_plan_star_metric_bytes(pgpu_plan P, int64_t* bytes) try {
+  PGPU_ABI_GUARD;
+  if (!P || !bytes) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
+  *bytes = P->star_metric_bytes;
+  return 0;
+} PGPU_ABI_CATCH
+
 int pgpu_plan_timing(pgpu_plan P, double* out3) try {
   PGPU_ABI_GUARD;
   if (!P || !out3 || !P->executed) return fail(PGPU_ERR_INVALID_ARGUMENT, "plan not executed");

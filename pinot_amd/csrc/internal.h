@@ -187,15 +187,17 @@ struct KStarSeg {
   int32_t pred_mask;                      // dims with predicates (traversal's remaining predicate columns)
   int32_t group_mask;                     // group-by dims without predicates
   int32_t num_dims;
-  int32_t pad;
+  // bit s: src_f[s] holds int32 values (a metric whose pre-aggregated doubles are all integers of int32 range,
+  // narrowed at pin time; s < kMaxSlots = 24); bit 31: src_c[0] holds int32 counts
+  uint32_t narrow;
   const uint32_t* dim_fwd[kMaxStarDims];  // star-tree documents' dictIds (MSB-first, padded)
   int32_t dim_bits[kMaxStarDims];
   int32_t dim_card[kMaxStarDims];         // the segment's dictionary size of each group-by / predicate dim
   const uint32_t* match[kMaxStarDims];    // matching-dictId bitset of each predicate dim
   const int32_t* key_lut[kMaxKeys];       // local -> global dictId of each group-by key
   int32_t key_dim[kMaxKeys];              // dim of each group-by key
-  const double* src_f[kMaxSlots];         // per slot: pre-aggregated double per document
-  const int64_t* src_c[kMaxSlots];        // per slot: pre-aggregated count per document (slot 0; null = 1)
+  const double* src_f[kMaxSlots];         // per slot: pre-aggregated double per document (int32 if narrow)
+  const int64_t* src_c[kMaxSlots];        // per slot: pre-aggregated count per document (slot 0; null = 1; int32 if narrow)
   int32_t* ranges;                        // scratch: 2 x num_nodes (startDocId, endDocId)
   int64_t* prefix;                        // scratch: num_nodes + 1 prefix sums of range lengths
   int32_t* frontier;                      // scratch: 2 x 3 x num_nodes

@@ -381,6 +381,9 @@ struct StarTreeDev {
   std::vector<const uint32_t*> d_dim_fwd;
   std::vector<const double*> d_mf;
   std::vector<const int64_t*> d_mc;
+  // per metric: its device array holds int32 values (every pre-aggregated value an integer of int32 range; the
+  // kernel widens them exactly) -- half the bytes per star-tree document
+  std::vector<uint8_t> mf_narrow, mc_narrow;
   int dim_of(int col) const {
     for (int d = 0; d < num_dims; ++d) if (dim_cols[d] == col) return d;
     return -1;
@@ -791,6 +794,7 @@ struct pgpu_plan_s {
   size_t star_lds_bytes = 0;
   int32_t star_cache_ints = 0;  // K6 LDS cache of key LUTs + match sets (max over the star-tree segments; 0: off)
   int64_t star_segments = 0;
+  int64_t star_metric_bytes = -1;  // K6's metric-array sectors (64 B) holding a matched doc, x 64 (small tables)
   int64_t star_docs_read = 0;                                // star-tree documents K6 read (after finalize)
 };
 

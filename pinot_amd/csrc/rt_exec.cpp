@@ -877,6 +877,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
   // the epilogue wrote this execution's whole table + statistics to host memory, and nothing has changed the table
   // since (a combine clears P->exported)
   const bool from_export = P->exported && table == P->d_table_used && key_begin == 0 && G == P->num_keys;
+  P->star_metric_bytes = -1;  // read back by the small-table path only
   double t_sync1 = 0;
   R->pool = P->table->result_pool;
   {
@@ -906,10 +907,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
       TRY(sc->readback.ensure((size_t)words * 8 + 64));
       st = reinterpret_cast<uint64_t*>(sc->readback.p);
       if (reinterpret_cast<const uint8_t*>(P->d_stats) == reinterpret_cast<const uint8_t*>(table) + words * 8) {
-        HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 48, hipMemcpyDeviceToHost, stream));  // table + stats
+        HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8 + 64, hipMemcpyDeviceToHost, stream));  // table + stats
       } else {
         HIP_TRY(hipMemcpyAsync(st, table, (size_t)words * 8, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipMemcpyAsync(st + words, P->d_stats, 48, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipMemcpyAsync(st + words, P->d_stats, 64, hipMemcpyDeviceToHost, stream));
       }
     }
     TRY(wait_plan(P, stream));
@@ -918,6 +919,7 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     matched = st[words];
     star_scanned = st[words + 1] + st[words + 2];
     P->star_docs_read = (int64_t)st[words + 3];
+    P->star_metric_bytes = (int64_t)st[words + 7] * 64;
     for (int64_t k = 0; k < G; ++k) n += st[k] != 0;
     TRY(R->alloc(nk, nslots, n));
     int64_t j = 0;

@@ -416,8 +416,11 @@ int plan_star_segment(pgpu_plan_s* P, size_t seg_index, Segment* s, const pgpu_q
   }
   // slot sources
   const int cnt_pair = st->pair(PGPU_AGG_COUNT, -1);
-  if (cnt_pair >= 0) k.src_c[0] = st->d_mc[cnt_pair];
-  else if (has_avg) k.src_c[0] = st->d_mc[st->pair(PGPU_AGG_AVG, avg_col)];
+  const int cnt_m = cnt_pair >= 0 ? cnt_pair : has_avg ? st->pair(PGPU_AGG_AVG, avg_col) : -1;
+  if (cnt_m >= 0) {
+    k.src_c[0] = st->d_mc[cnt_m];
+    if (st->mc_narrow[cnt_m]) k.narrow |= 1u << 31;
+  }
   for (size_t sl = 1; sl < P->slot_kind.size(); ++sl) {
     const int col = P->slot_tcol[sl];
     int m = -1;
@@ -431,6 +434,7 @@ int plan_star_segment(pgpu_plan_s* P, size_t seg_index, Segment* s, const pgpu_q
     }
     if (m < 0 || !st->d_mf[m]) return 0;
     k.src_f[sl] = st->d_mf[m];
+    if (st->mf_narrow[m]) k.narrow |= 1u << sl;
   }
   // predicate dims: AND of the composites' matching dictIds; always-true composites are dropped
   std::vector<std::vector<uint32_t>> match(st->num_dims);

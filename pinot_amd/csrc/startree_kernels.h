@@ -166,10 +166,12 @@ __device__ __forceinline__ void star_decode(const uint32_t* __restrict__ fwd, in
 }
 
 // Aggregates the docs of `mask` (bits H..H+15 of the lane's group g) of star-tree segment S.
+// sectors: 64-byte sectors of the metric arrays holding a matched doc, for the bytes model (statistics word 7).
 template <int MODE, int H>
 __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const KStarSeg& S, int64_t g, uint32_t mask,
                                                     const int32_t* __restrict__ cache, bool cached,
-                                                    uint64_t* __restrict__ tbl, int64_t G) {
+                                                    uint64_t* __restrict__ tbl, int64_t G,
+                                                    unsigned long long& sectors) {
   uint32_t m = (mask >> H) & 0xFFFFu;
   // dense key spaces (MODE_LDS / MODE_GLOBAL) stay below 2^31: 32-bit keys
   using KeyT = typename std::conditional<MODE == MODE_HASH, int64_t, int32_t>::type;
@@ -205,24 +207,42 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
       }
   }
   const int64_t d0 = g * 32 + H;
+  // a half's 16 docs: one 64-B sector of an int32 array, two of an 8-byte one
+  const unsigned sec4 = m != 0u, sec8 = ((m & 0xFFu) != 0u) + ((m >> 8) != 0u);
   for (int s = 0; s < p.num_slots; ++s) {
     const int kind = p.slot_kind[s];
     uint64_t* __restrict__ row = tbl + (int64_t)s * G;
     if (kind == SLOT_COUNT) {  // COUNT adds the pre-aggregated count (1 per document when the tree has none)
       const bool has = S.src_c[0] != nullptr;
-      gmem<int64_t>* __restrict__ src = gp(S.src_c[0]);
+      const bool nar = (S.narrow >> 31) & 1u;
       int64_t c[16];
+      if (nar) {
+        gmem<int32_t>* __restrict__ src = gp(reinterpret_cast<const int32_t*>(S.src_c[0]));
 #pragma unroll
-      for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? src[d0 + i] : 1;
+        for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? (int64_t)src[d0 + i] : 1;
+      } else {
+        gmem<int64_t>* __restrict__ src = gp(S.src_c[0]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? src[d0 + i] : 1;
+      }
+      if (has) sectors += nar ? sec4 : sec8;
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         if ((m >> i) & 1u) atomicAdd(reinterpret_cast<unsigned long long*>(row + key[i]), (unsigned long long)c[i]);
       continue;
     }
-    gmem<double>* __restrict__ src = gp(S.src_f[s]);
     double v[16];
+    if ((S.narrow >> s) & 1u) {  // integral values of int32 range: exact as doubles
+      gmem<int32_t>* __restrict__ src = gp(reinterpret_cast<const int32_t*>(S.src_f[s]));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? src[d0 + i] : 0.0;
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? (double)src[d0 + i] : 0.0;
+      sectors += sec4;
+    } else {
+      gmem<double>* __restrict__ src = gp(S.src_f[s]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? src[d0 + i] : 0.0;
+      sectors += sec8;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (!((m >> i) & 1u)) continue;
@@ -307,6 +327,7 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
   const int64_t total = segpre[p.num_segs];
   const int64_t glo = (int64_t)blockIdx.x * total / p.num_wgs, ghi = (int64_t)(blockIdx.x + 1) * total / p.num_wgs;
   unsigned long long matched = 0, scanned = 0, read = 0;  // read: star-tree documents of the emitted ranges
+  unsigned long long sectors = 0;  // metric-array sectors holding a matched doc (bytes model)
   // first segment of the run: binary search over the LDS prefix
   int seg = 0;
   {
@@ -401,14 +422,15 @@ __global__ __launch_bounds__(StarBlock<MODE>::value) void startree_scan_kernel(c
         moff += (S.dim_card[d] + 31) >> 5;
       }
       matched += __popc(mask);
-      if (__any((mask & 0xFFFFu) != 0u)) star_aggregate_half<MODE, 0>(p, S, g, mask, cache, cached, tbl, G);
-      if (__any((mask >> 16) != 0u)) star_aggregate_half<MODE, 16>(p, S, g, mask, cache, cached, tbl, G);
+      if (__any((mask & 0xFFFFu) != 0u)) star_aggregate_half<MODE, 0>(p, S, g, mask, cache, cached, tbl, G, sectors);
+      if (__any((mask >> 16) != 0u)) star_aggregate_half<MODE, 16>(p, S, g, mask, cache, cached, tbl, G, sectors);
     }
   }
   {
-    const int idx[3] = {0, 1, 3};
-    unsigned long long v[3] = {(unsigned long long)matched, (unsigned long long)scanned, (unsigned long long)read};
-    block_stats_add<3, BLOCK>(p.stats, idx, v);
+    const int idx[4] = {0, 1, 3, 7};
+    unsigned long long v[4] = {(unsigned long long)matched, (unsigned long long)scanned, (unsigned long long)read,
+                               sectors};
+    block_stats_add<4, BLOCK>(p.stats, idx, v);
   }
   if (MODE == MODE_LDS) {
     __syncthreads();

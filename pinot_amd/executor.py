@@ -578,6 +578,13 @@ class Plan:
         L.check(self.lib.pgpu_plan_timing(self.handle, out))
         return out[0], out[1], out[2], out[3]
 
+    def star_metric_bytes(self):
+        """Bytes of the star-tree metric arrays the last execution read: 64-B sectors holding a matched document
+        (-1: not read back for this plan's table size)."""
+        out = ctypes.c_int64(0)
+        L.check(self.lib.pgpu_plan_star_metric_bytes(self.handle, ctypes.byref(out)))
+        return out.value
+
     def star_work(self):
         """(star-tree segments, their nodes, star-tree documents read) of the last finalized execution."""
         out = (ctypes.c_int64 * 3)()

@@ -581,8 +581,11 @@ class Plan:
     def star_metric_bytes(self):
         """Bytes of the star-tree metric arrays the last execution read: 64-B sectors holding a matched document
         (-1: not read back for this plan's table size)."""
+        fn = getattr(self.lib, "pgpu_plan_star_metric_bytes", None)  # (an older library of an A/B run: -1)
+        if fn is None:
+            return -1
         out = ctypes.c_int64(0)
-        L.check(self.lib.pgpu_plan_star_metric_bytes(self.handle, ctypes.byref(out)))
+        L.check(fn(self.handle, ctypes.byref(out)))
         return out.value
 
     def star_work(self):

@@ -94,11 +94,17 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
   // Metric arrays whose values are all integers of int32 range are pinned as int32 (the kernel widens them exactly):
   // C4's SUM__m and COUNT__* -- the star-tree documents' metric bytes halve.
   auto ints32_f = [](const double* v, int64_t n) {
+#ifdef PGPU_STAR_NO_NARROW  // (A/B build: 8-byte metric arrays)
+    return false;
+#endif
     for (int64_t i = 0; i < n; ++i)
       if (!(v[i] >= -2147483648.0 && v[i] <= 2147483647.0) || v[i] != (double)(int32_t)v[i]) return false;
     return true;
   };
   auto ints32_c = [](const int64_t* v, int64_t n) {
+#ifdef PGPU_STAR_NO_NARROW
+    return false;
+#endif
     for (int64_t i = 0; i < n; ++i)
       if (v[i] < INT32_MIN || v[i] > INT32_MAX) return false;
     return true;

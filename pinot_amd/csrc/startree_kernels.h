@@ -225,7 +225,9 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? src[d0 + i] : 1;
       }
+#ifndef PGPU_STAR_NO_SECTORS
       if (has) sectors += nar ? sec4 : sec8;
+#endif
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         if ((m >> i) & 1u) atomicAdd(reinterpret_cast<unsigned long long*>(row + key[i]), (unsigned long long)c[i]);
@@ -236,12 +238,16 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
       gmem<int32_t>* __restrict__ src = gp(reinterpret_cast<const int32_t*>(S.src_f[s]));
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? (double)src[d0 + i] : 0.0;
+#ifndef PGPU_STAR_NO_SECTORS
       sectors += sec4;
+#endif
     } else {
       gmem<double>* __restrict__ src = gp(S.src_f[s]);
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? src[d0 + i] : 0.0;
+#ifndef PGPU_STAR_NO_SECTORS
       sectors += sec8;
+#endif
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {

@@ -251,7 +251,6 @@ inline double key_double(int64_t k) {
 
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
 constexpr int64_t kExportBytes = 64 * 1024;  // LDS-table plans up to this size: the epilogue writes them to host memory
-constexpr int kStatsRing = 256;              // statistics entries zeroed per fill (Scratch::stats_ring)
 constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
 #ifndef PGPU_PART_LDS_KB
 #define PGPU_PART_LDS_KB 64
@@ -474,10 +473,6 @@ struct Scratch {
   // receives finalize's copies.  Separate buffers, because a finalize that had to grow the upload buffer would
   // free it while its uploads may still be queued behind other queries' work on a shared stream.
   HostPinned stage, readback, starstage, bitstage, maskstage;
-  // Statistics words: 64-byte entries of a ring zeroed kStatsRing executions at a time (exec_prologue); an entry
-  // stays the plan's until it executes again or releases the scratch
-  DevBuf stats_ring;
-  int ring_pos = 0;
   // small LDS-table plans: the epilogue's copy of table + statistics (pinned host) and its block counter
   HostPinned exported;
   DevBuf export_done;
@@ -495,7 +490,7 @@ struct Scratch {
     for (const DevBuf* b : {&docbits, &bittasks, &bitblocks, &rawtasks, &segrec, &sets, &slab, &table, &hash_keys,
                             &stats, &ckeys, &cslots, &counter, &bitmap, &tile_seg, &starrec, &starwork, &part_start,
                             &block_off, &rec_key, &rec_val, &rec_key32, &stage_keys, &coarse_fill, &fine_fill,
-                            &mid_key, &mid_val, &leap_maps, &mask_jobs, &leaf_masks, &hsort, &part_mm, &stats_ring,
+                            &mid_key, &mid_val, &leap_maps, &mask_jobs, &leaf_masks, &hsort, &part_mm,
                             &export_done})
       n += b->cap;
     return n;
@@ -517,7 +512,7 @@ struct Scratch {
     coarse_fill.release(); fine_fill.release(); mid_key.release(); mid_val.release();
     leap_maps.release(); mask_jobs.release(); leaf_masks.release(); maskstage.release();
     xcursor.release(); xstage.release(); xsend.release(); xrecv.release(); xshard.release(); hsort.release(); part_mm.release();
-    stats_ring.release(); ring_pos = 0; exported.release(); export_done.release();
+    exported.release(); export_done.release();
     for (auto& e : ev) if (e) { hipEventDestroy(e); e = nullptr; }
   }
 };

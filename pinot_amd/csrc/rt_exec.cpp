@@ -225,21 +225,20 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   TRY(sc->segrec.ensure(std::max<size_t>(rec_cap, 16)));
   TRY(sc->stage.ensure(std::max<size_t>(rec_cap + (size_t)std::max<int64_t>(P->set_words_bound,
                                                                              (int64_t)P->set_words.size()) * 4, 16)));
-  // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag): the next entry of the scratch's
-  // ring, whose entries are zeroed kStatsRing at a time -- one fill per kStatsRing executions instead of a fill
-  // launch (and its gap before the scan) per query
+  // Statistics words (docs matched, entries scanned, star-tree docs, timeout flag, star metric sectors): right after
+  // the group table when the table is internal, so finalize reads both with one copy.  (A ring of entries zeroed 256
+  // executions at a time, instead of this fill per query, was measured in r06 sessions i, j, m: no gain on C1 / C3,
+  // and C4's pipelined star-tree step lost 0.17 -> 0.21 ms with the second copy it needs; not kept.)
   constexpr size_t kStatsBytes = 64;
-  if (!d_table) TRY(sc->table.ensure(std::max<size_t>((size_t)X.words * 8, 8)));
-  if (sc->stats_ring.cap < kStatsBytes * kStatsRing) {
-    TRY(sc->stats_ring.ensure(kStatsBytes * kStatsRing));
-    sc->ring_pos = 0;
+  unsigned long long* stats;
+  if (!d_table) {
+    TRY(sc->table.ensure((size_t)X.words * 8 + kStatsBytes));
+    stats = reinterpret_cast<unsigned long long*>(sc->table.as<uint8_t>() + (size_t)X.words * 8);
+  } else {
+    TRY(sc->stats.ensure(kStatsBytes));
+    stats = sc->stats.as<unsigned long long>();
   }
-#ifdef PGPU_NO_STATS_RING  // (an A/B build of the library: one fill per execution)
-  sc->ring_pos = 0;
-#endif
-  if (sc->ring_pos == 0) HIP_TRY(hipMemsetAsync(sc->stats_ring.p, 0, kStatsBytes * kStatsRing, stream));
-  unsigned long long* stats = sc->stats_ring.as<unsigned long long>() + (size_t)sc->ring_pos * (kStatsBytes / 8);
-  sc->ring_pos = (sc->ring_pos + 1) % kStatsRing;
+  HIP_TRY(hipMemsetAsync(stats, 0, kStatsBytes, stream));
   P->d_stats = stats;
   P->exported = false;
   X.external = d_table != nullptr;

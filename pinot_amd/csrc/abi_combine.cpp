@@ -550,7 +550,8 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
   // so a rank that fails here still meets its peers there and every rank fails together.  The dense modes have no
   // host exchange (one would cost every query a round trip): a failed rank issues no collective, its peers' ones stay
   // pending on their streams, and their finalize waits end at the query deadline or the communicator's timeout,
-  // which aborts the communicator.
+  // which aborts the communicator -- for a query without a deadline at most kDenseCombineWaitMs (wait_plan), not the
+  // communicator's whole timeout.
   uint32_t conv = 0;
   int pre = 0;
   if (P->composite) pre = fail(PGPU_ERR_UNSUPPORTED, "numGroupsLimit plan: combine its finalized rows (ROWS)");
@@ -604,6 +605,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
     P->slot_kind.assign(kinds, kinds + ns);
   }
   P->comm_used = c->impl;
+  P->comm_dense = true;
   auto dtype = [&](int k) { return P->slot_kind[k] == SLOT_SUM_F64 ? pgpu::CDT_F64 : pgpu::CDT_I64; };
   auto op = [&](int k) {
     return P->slot_kind[k] == SLOT_MIN_KEY ? pgpu::COP_MIN : P->slot_kind[k] == SLOT_MAX_KEY ? pgpu::COP_MAX : pgpu::COP_SUM;

@@ -250,6 +250,10 @@ inline double key_double(int64_t k) {
 }
 
 constexpr int64_t kHostCompactBytes = 512 * 1024;  // dense tables up to this size are compacted on the host
+// A dense-mode combine has no status exchange: a peer that failed its own checks never joins the collectives.  The
+// finalize of a query without a deadline waits at most this long for them (then aborts the communicator), instead of
+// the communicator's whole timeout.
+constexpr int64_t kDenseCombineWaitMs = 30 * 1000;
 constexpr int64_t kExportBytes = 64 * 1024;  // LDS-table plans up to this size: the epilogue writes them to host memory
 constexpr int64_t kPartMinBytes = 32ll << 20;        // dense tables this large use the partitioned group-by
 #ifndef PGPU_PART_LDS_KB
@@ -565,6 +569,7 @@ struct pgpu_table_s {
   struct GlobalValues {
     uint64_t version = ~0ull;
     std::shared_ptr<DevMem> keys, vals;
+    int64_t n = 0;  // entries of the current arrays (device_bytes holds 16 n for them)
   };
   std::vector<GlobalValues> gvalues;
   hipStream_t stream = nullptr;
@@ -727,6 +732,7 @@ struct pgpu_plan_s {
   bool inflight_counted = false;  // counted in table->scans_inflight (inflight_begin / inflight_end)
   bool alone = false;             // no other execution of the table was in flight when this one launched
   bool exported = false;          // the last execution's epilogue copied table + statistics to scratch->exported
+  bool comm_dense = false;        // combined element-wise (ALL_REDUCE / REDUCE_SCATTER): no host exchange of status
   const void* d_table_used = nullptr;
   bool hash = false;
   // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local

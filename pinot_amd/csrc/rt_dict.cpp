@@ -182,8 +182,11 @@ int ensure_global_values(pgpu_table_s* t, int col, hipStream_t stream) {
   HIP_TRY(hipMemcpyAsync(k->p, key.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(v->p, val.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  if (!gv.keys) t->device_bytes += 16 * (int64_t)n;
-  gv.keys = std::move(k);  // the previous arrays live on in the plans that reference them
+  // the current arrays' bytes (a rebuild after the dictionary grew replaces the previous arrays in the account; those
+  // live on only in the plans that still reference them)
+  t->device_bytes += 16 * ((int64_t)n - gv.n);
+  gv.n = (int64_t)n;
+  gv.keys = std::move(k);
   gv.vals = std::move(v);
   gv.version = t->global_version[col];
   return 0;

@@ -104,7 +104,9 @@ int wait_plan(pgpu_plan_s* P, hipStream_t stream) {
   const auto t0 = std::chrono::steady_clock::now();
   // a combined plan's stream holds collectives that complete only when every peer joins them: the wait also ends at
   // the communicator's timeout, and an expired wait aborts the communicator (the collectives' kernels exit)
-  const int64_t comm_lim = P->comm_used ? P->comm_used->timeout_ms.load(std::memory_order_relaxed) : 0;
+  int64_t comm_lim = P->comm_used ? P->comm_used->timeout_ms.load(std::memory_order_relaxed) : 0;
+  if (P->comm_used && P->comm_dense && P->end_time_ms <= 0)
+    comm_lim = comm_lim > 0 ? std::min(comm_lim, kDenseCombineWaitMs) : kDenseCombineWaitMs;
   for (int spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(sc->busy);
     if (e == hipSuccess) {
@@ -205,6 +207,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   P->shard = nullptr;
   P->shard_begin = P->shard_count = 0;
   P->comm_used = nullptr;
+  P->comm_dense = false;
   P->merged_records = -1;
   Scratch* sc = P->scratch;
   X.nslots = (int)P->slot_kind.size();

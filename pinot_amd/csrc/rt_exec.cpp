@@ -333,7 +333,11 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   // and leaf registers are loaded once per run).  Plans with many matches (dense, and the sparse ones of estimated
   // selectivity >= 1/16) gather enough to want the former: C4's scan path 151 -> 141 us interleaved, where C3
   // (0.18 %) loses 7 % and the indexed C3 15 % (profiles/r05_ab_summary.txt, session za).
+#ifdef PGPU_CHUNK_ALL  // (an A/B build of the library: contiguous runs for the dense and wide plans too)
+  kp.tile_chunks = 1;
+#else
   kp.tile_chunks = P->dense || P->fast_wide ? 0 : 1;
+#endif
   kp.num_slots = nslots;
   for (int sl = 0; sl < nslots; ++sl) { kp.slot_kind[sl] = P->slot_kind[sl]; kp.slot_col[sl] = P->slot_col[sl]; }
   kp.pair_leaves = 1;

@@ -755,49 +755,6 @@ __device__ __forceinline__ void accumulate16_i(uint64_t* __restrict__ row, const
         for (int i = 0; i < 16; ++i)
           if ((m >> i) & 1u) atomicAdd(u + key[i], (unsigned long long)v[i] + addend);
         break;
-#ifndef PGPU_MINMAX_ALWAYS_ATOMIC
-      // MIN / MAX: the words are read first (4 docs at a time) and an atomic issued only where the value would change
-      // one (a read of an older word is never below the current minimum / above the current maximum, so no update is
-      // lost); over a dense tile's docs most groups' extremes are reached early, and an LDS read costs less than an
-      // atomic
-      case SLOT_MIN_KEY:
-      default: {
-        const bool mn = kind == SLOT_MIN_KEY;
-#pragma unroll
-        for (int i0 = 0; i0 < 16; i0 += 4) {
-          if (narrow) {
-            uint32_t cur[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cur[j] = w32[2 * key[i0 + j]];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int i = i0 + j;
-              const uint32_t x = (uint32_t)v[i];
-              const bool need = ((m >> i) & 1u) && (mn ? x < cur[j] : x > cur[j]);
-              if (__any(need) && need) {
-                if (mn) atomicMin(w32 + 2 * key[i], x);
-                else atomicMax(w32 + 2 * key[i], x);
-              }
-            }
-          } else {
-            long long cur[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cur[j] = l[key[i0 + j]];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int i = i0 + j;
-              const long long x = (long long)v[i];
-              const bool need = ((m >> i) & 1u) && (mn ? x < cur[j] : x > cur[j]);
-              if (__any(need) && need) {
-                if (mn) atomicMin(l + key[i], x);
-                else atomicMax(l + key[i], x);
-              }
-            }
-          }
-        }
-        break;
-      }
-#else
       case SLOT_MIN_KEY:
         if (narrow) {
 #pragma unroll
@@ -820,7 +777,6 @@ __device__ __forceinline__ void accumulate16_i(uint64_t* __restrict__ row, const
             if ((m >> i) & 1u) atomicMax(l + key[i], (long long)v[i]);
         }
         break;
-#endif
     }
   } else {
 #pragma unroll

@@ -286,6 +286,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
     X.sets = im.sets.as<uint32_t>();
     X.tile_seg = im.tile_seg.as<int32_t>();
   }
+  X.mark("image");
   if (P->docbit_words > 0) TRY(sc->docbits.ensure((size_t)P->docbit_words * 4));
   if (!P->bit_blocks.empty()) {  // BitmapBasedFilterOperator leaves: OR the matching dictIds' containers
     TRY(sc->bittasks.ensure(std::max<size_t>(P->bit_tasks.size(), 1) * sizeof(KBitTask)));
@@ -567,6 +568,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
     return fail(PGPU_ERR_DEVICE, "expand launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   if (check_launch_on()) TRY(check_launch_inputs(P, stream, X, C));
+  X.mark("chunk set up");
   if (c == 0) PGPU_TIMING_RECORD(P, sc->ev[1], stream);
   PGPU_TIMING_RECORD(P, sc->cev[2 * c], stream);
   if (C.num_tiles > 0 && P->partitioned) {
@@ -680,6 +682,7 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
                                          scan_variant(P),
                                          grid, P->lds_bytes, stream);
     if (rc) return fail(PGPU_ERR_DEVICE, "scan launch failed: %s", hipGetErrorString(hipGetLastError()));
+    X.mark("scan launched");
     if (wg_times) TRY(diag_wg_times_report(P->table, kp, grid, stream));
   }
   PGPU_TIMING_RECORD(P, sc->cev[2 * c + 1], stream);
@@ -824,6 +827,7 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
       P->exported = exp;
     }
     X.leap_nsegs = 0;
+    X.mark("epilogue launched");
   }
   if (P->mode == MODE_HASH && !P->part_hash && kp.pack_slot >= 0 &&
       launch_hash_unpack(X.table, kp.hash_keys, P->num_keys, kp.pack_slot, kp.pack_shift, stream))
@@ -837,7 +841,8 @@ int exec_epilogue(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X) {
   if (trace_on()) {
     const double end = now_us();
     fprintf(stderr, "[pgpu] execute: %.1f us host\n", end - X.t_start);
-    if (end - X.t_start > 1000.0) {
+    static const bool all_marks = diag("marks");  // PGPU_TRACE=1,marks: every execution's marks
+    if (end - X.t_start > 1000.0 || all_marks) {
       double prev = X.t_start;
       for (const auto& m : X.marks) {
         fprintf(stderr, "[pgpu]   %s +%.1f us\n", m.first, m.second - prev);

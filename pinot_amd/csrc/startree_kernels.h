@@ -60,55 +60,60 @@ __global__ __launch_bounds__(256) void startree_traverse_kernel(const KStarSeg* 
     __syncthreads();
     if (tid == 0) next_n = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
+    // one wave per frontier entry, its children over the wave's lanes (the root of a group-by dimension has as many
+    // children as the dimension has values -- C4's d1: 100 -- which one thread used to push one by one)
+    const int lane = tid & 63, nwaves = (int)blockDim.x >> 6;
+    for (int i = tid >> 6; i < n; i += nwaves) {
       const int node = fa[3 * i], rp = fa[3 * i + 1], rg = fa[3 * i + 2];
       const int* N = nodes + 7 * (int64_t)node;
       const int first = N[5], last = N[6];
       if (rp == 0 && rg == 0) {  // all predicates and group-by dims matched: the aggregated document
-        const int r = atomicAdd(&nr, 1);
-        S.ranges[2 * r] = N[4];
-        S.ranges[2 * r + 1] = N[4] + 1;
+        if (lane == 0) {
+          const int r = atomicAdd(&nr, 1);
+          S.ranges[2 * r] = N[4];
+          S.ranges[2 * r + 1] = N[4] + 1;
+        }
       } else if (first < 0) {  // leaf: its documents, with the remaining predicates as a residual filter
-        const int r = atomicAdd(&nr, 1);
-        S.ranges[2 * r] = N[2];
-        S.ranges[2 * r + 1] = N[3];
-        atomicOr(&rem, rp);
+        if (lane == 0) {
+          const int r = atomicAdd(&nr, 1);
+          S.ranges[2 * r] = N[2];
+          S.ranges[2 * r + 1] = N[3];
+          atomicOr(&rem, rp);
+        }
       } else {
         const int cd = nodes[7 * (int64_t)first];  // getChildDimensionId
         const int bit = 1 << cd;
-        if (rp & bit) {  // predicate on the next dimension: children whose dictId matches
-          const uint32_t* m = S.match[cd];
-          for (int c = first; c <= last; ++c) {
-            const int v = nodes[7 * (int64_t)c + 1];
-            if (v >= 0 && ((m[v >> 5] >> (v & 31)) & 1u)) {
-              const int k = atomicAdd(&next_n, 1);
-              fb[3 * k] = c;
-              fb[3 * k + 1] = rp & ~bit;
-              fb[3 * k + 2] = rg;
-            }
+        const bool pred = (rp & bit) != 0;
+        // neither predicate nor group-by: the star child when it exists, else every non-star child
+        if (!pred && !(rg & bit) && nodes[7 * (int64_t)first + 1] == -1) {
+          if (lane == 0) {
+            const int k = atomicAdd(&next_n, 1);
+            fb[3 * k] = first;
+            fb[3 * k + 1] = rp;
+            fb[3 * k + 2] = rg;
           }
         } else {
-          int nrg = rg;
-          bool expand = true;
-          if (!(rg & bit)) {  // neither predicate nor group-by: the star child when it exists
-            if (nodes[7 * (int64_t)first + 1] == -1) {
-              const int k = atomicAdd(&next_n, 1);
-              fb[3 * k] = first;
-              fb[3 * k + 1] = rp;
-              fb[3 * k + 2] = rg;
-              expand = false;
+          // predicate: the children whose dictId matches; group-by (or no star child): every non-star child
+          const int nrp = pred ? rp & ~bit : rp, nrg = pred ? rg : rg & ~bit;
+          const uint32_t* m = S.match[cd];
+          for (int c0 = first; c0 <= last; c0 += 64) {
+            const int c = c0 + lane;
+            bool take = false;
+            if (c <= last) {
+              const int v = nodes[7 * (int64_t)c + 1];
+              take = pred ? (v >= 0 && ((m[v >> 5] >> (v & 31)) & 1u)) : v != -1;
             }
-          } else {
-            nrg = rg & ~bit;
-          }
-          if (expand)
-            for (int c = first; c <= last; ++c) {
-              if (nodes[7 * (int64_t)c + 1] == -1) continue;
-              const int k = atomicAdd(&next_n, 1);
+            const uint64_t bal = __ballot(take);
+            int base = 0;
+            if (lane == 0 && bal) base = atomicAdd(&next_n, __popcll(bal));
+            base = __shfl(base, 0);
+            if (take) {
+              const int k = base + __popcll(bal & ((1ull << lane) - 1ull));
               fb[3 * k] = c;
-              fb[3 * k + 1] = rp;
+              fb[3 * k + 1] = nrp;
               fb[3 * k + 2] = nrg;
             }
+          }
         }
       }
     }

@@ -82,6 +82,16 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
   // tile loop changes the sparse instance's register allocation (108 -> 134 VGPRs, one wave less per SIMD; an
   // in-loop check cost 18% on C3, measured).  A scan already running is abandoned by the host (wait_plan).
   if (p.deadline && p.stats[5]) return;
+#ifdef PGPU_SLOT_PRIO
+  // (A/B build) the later-dispatched workgroups' waves get the higher issue priority: the SIMDs otherwise issue the
+  // oldest wave first and equal shares end in dispatch-slot order
+  {
+    const int pr = (int)((blockIdx.x * 4u) / gridDim.x);
+    if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+  }
+#endif
 #ifdef PGPU_DIAG_WG_TIMES
   const unsigned long long diag_t0 = wall_clock64();
   unsigned long long diag_t1 = 0;

@@ -239,7 +239,7 @@ class GpuTable:
     def set_config(self, **fields):
         """pgpu_table_set_config: the named fields changed, the others kept (plan_cache, partitioned_group_by,
         hash_partitions, hash_partition_bits, hash_partition_lds_kb, lds_table_kb, plan_chunk_segments, stream_chunks,
-        compact_results, star_tree_workgroups, dense_selectivity -- include/pinotgpu.h).  Plans made afterwards use
+        compact_results, star_tree_workgroups, dense_selectivity, slot_weight_step -- include/pinotgpu.h).  Plans made afterwards use
         them (the compiled-plan cache is cleared)."""
         cur = self.config()
         bad = set(fields) - set(cur)

@@ -141,6 +141,7 @@ int pgpu_plan_exchange_merge(pgpu_plan P, void* stream, const int32_t* kinds, co
   PGPU_ABI_GUARD;
   TRY(exchangeable(P));
   P->exported = false;
+  P->k8d_counts = false;
   if (n < 0 || (n > 0 && !d_records) || n > (INT64_C(1) << 40))  // the table below holds >= 2n slots
     return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   uint32_t conv = 0;
@@ -532,6 +533,7 @@ int pgpu_plan_combine(pgpu_plan P, pgpu_comm c, void* stream, void* d_table, int
   PGPU_ABI_GUARD;
   if (!P || !c) return fail(PGPU_ERR_INVALID_ARGUMENT, "bad arguments");
   P->exported = false;  // the table changes: finalize reads it from the device
+  P->k8d_counts = false;
   if (mode == PGPU_COMBINE_LOCAL) {
     if (key_begin) *key_begin = 0;
     if (key_count) *key_count = P->num_keys;

@@ -291,6 +291,12 @@ struct KPartParams {
   // [num_parts][2][num_slots]: each partition's range of every slot's words (order-preserving u64, min then max) --
   // the compact result form's widths without a pass over the records (launch_hash_minmax_parts folds them)
   unsigned long long* out_mm;
+  // K8d with cs_pack and 2^pshift == kCompactChunk keys per partition (C5): partition b is the ordered compaction's
+  // chunk b, and K8d writes what compact_count_kernel would -- the chunk's present keys (chunk_cnt[b]) and the
+  // [min COUNT, min SUM, max COUNT, max SUM] row of its present keys (chunk_mm + 4 b) -- so finalize skips that
+  // pass over the 10 M-key table (null: not written)
+  uint32_t* chunk_cnt;
+  long long* chunk_mm;
 };
 // K8h: value streams a record carries in registers (plans with more use the global hash table).
 constexpr int kHashPartStreams = 4;
@@ -403,8 +409,12 @@ int launch_merge_records(const uint64_t* rec, int64_t n, int32_t num_slots, cons
 // words of the present groups in key order at compact_slot_width bytes, slot s from out_slots + s * cap * 8.
 // chunk_scratch bytes launch_compact_dense_count needs (chunk counts, then per-chunk slot ranges).
 size_t compact_scratch_bytes(int64_t num_keys, int32_t num_slots);
+// counted: chunk_scratch already holds the chunk counts and ranges (K8d's KPartParams.chunk_cnt / chunk_mm), only the
+// ranges' fold and the scan run.
 int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t num_keys, uint32_t* chunk_scratch,
-                               unsigned long long* total, long long* minmax, void* stream);
+                               unsigned long long* total, long long* minmax, void* stream, bool counted = false);
+// Keys per chunk of the ordered compaction (kernels.hip kCompactChunk).
+constexpr int kCompactChunkKeys = 4096;
 int launch_compact_dense_scatter(const uint64_t* table, int32_t num_slots, int64_t num_keys, const int32_t* slot_kind,
                                  const uint32_t* chunk_scratch, const long long* minmax, uint64_t* bitmap,
                                  void* out_slots, int64_t cap, void* stream);

@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void compact_kernel(const uint64_t* __restrict
 // Ordered compaction of a dense table (AggregationGroupByResult iteration in ascending key order, deterministic):
 // count per chunk -> one-workgroup exclusive scan -> scatter in key order.  Columnar output: keys[cap] then
 // slot s at out + (1 + s) * cap.
-constexpr int kCompactChunk = 4096;  // keys per workgroup (16 rounds of 256)
+constexpr int kCompactChunk = kCompactChunkKeys;  // keys per workgroup (16 rounds of 256)
 
 // minmax (optional, [2][num_slots] int64, pre-set to 0x7F.. / 0x80.. bytes): the range of every slot's words over
 // the present groups, from which the dense-bitmap scatter picks each slot's byte width.
@@ -993,13 +993,14 @@ int launch_compact_ordered(const uint64_t* table, int32_t num_slots, int64_t num
 }
 
 int launch_compact_dense_count(const uint64_t* table, int32_t num_slots, int64_t num_keys, uint32_t* chunk_scratch,
-                               unsigned long long* total, long long* minmax, void* stream) {
+                               unsigned long long* total, long long* minmax, void* stream, bool counted) {
   const int64_t nch = compact_ordered_chunks(num_keys);
   if (nch < 1 || nch > INT32_MAX || num_slots > kMaxSlots) return -1;
   // per-chunk ranges after the counts in chunk_scratch (compact_scratch_bytes), reduced into minmax
   long long* rows = reinterpret_cast<long long*>(reinterpret_cast<uint8_t*>(chunk_scratch) + ((nch * 4 + 7) & ~int64_t(7)));
-  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys, chunk_scratch,
-                     num_slots, minmax ? rows : nullptr);
+  if (!counted)
+    hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nch), dim3(256), 0, S(stream), table, num_keys,
+                       chunk_scratch, num_slots, minmax ? rows : nullptr);
   if (minmax)
     hipLaunchKernelGGL(compact_minmax_kernel, dim3(1), dim3(256), 0, S(stream), rows, nch, num_slots, minmax);
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, S(stream), chunk_scratch, (int32_t)nch, total);

@@ -671,16 +671,59 @@ __global__ __launch_bounds__(kBlock) void part_aggregate_kernel(const KPartParam
             atomicAdd(w64 + (wr[b] & low), (1ull << 40) | (unsigned long long)(wr[b] >> pp.pshift));
       }
       __syncthreads();
+      const bool last = c1 >= r1;
+      uint32_t present = 0;
+      long long mn[2] = {INT64_MAX, INT64_MAX}, mx[2] = {INT64_MIN, INT64_MIN};
       for (int i = tid; i < n; i += kBlock) {
         const uint64_t w = lds[i];
-        const uint64_t cnt = w >> 40;
-        const uint64_t sum = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)cnt * pp.pack_min);
+        uint64_t cnt = w >> 40;
+        uint64_t sum = (uint64_t)((int64_t)(w & ((1ull << 40) - 1)) + (int64_t)cnt * pp.pack_min);
         if (c0 == r0) {
           p.table[k0 + i] = cnt;      // COUNT (slot 0)
           p.table[G + k0 + i] = sum;  // SUM
         } else {
-          p.table[k0 + i] += cnt;
-          p.table[G + k0 + i] += sum;
+          cnt += p.table[k0 + i];
+          sum += p.table[G + k0 + i];
+          p.table[k0 + i] = cnt;
+          p.table[G + k0 + i] = sum;
+        }
+        if (last && pp.chunk_cnt && cnt) {  // the compaction's count pass, from the words in hand
+          ++present;
+          mn[0] = min(mn[0], (long long)cnt);
+          mx[0] = max(mx[0], (long long)cnt);
+          mn[1] = min(mn[1], (long long)sum);
+          mx[1] = max(mx[1], (long long)sum);
+        }
+      }
+      if (last && pp.chunk_cnt) {  // workgroup-uniform
+        __shared__ unsigned long long red_cnt[kBlock / 64];
+        __shared__ long long red_mm[kBlock / 64][4];
+        const int lane = tid & 63, wv = tid >> 6;
+        unsigned long long c = present;
+        for (int off = 32; off > 0; off >>= 1) {
+          c += __shfl_xor(c, off);
+          for (int s = 0; s < 2; ++s) {
+            mn[s] = min(mn[s], (long long)__shfl_xor(mn[s], off));
+            mx[s] = max(mx[s], (long long)__shfl_xor(mx[s], off));
+          }
+        }
+        if (lane == 0) {
+          red_cnt[wv] = c;
+          red_mm[wv][0] = mn[0];
+          red_mm[wv][1] = mn[1];
+          red_mm[wv][2] = mx[0];
+          red_mm[wv][3] = mx[1];
+        }
+        __syncthreads();
+        if (tid < 4) {
+          long long v = tid < 2 ? INT64_MAX : INT64_MIN;
+          for (int w = 0; w < kBlock / 64; ++w) v = tid < 2 ? min(v, red_mm[w][tid]) : max(v, red_mm[w][tid]);
+          pp.chunk_mm[4 * (int64_t)blockIdx.x + tid] = v;
+        }
+        if (tid == 0) {
+          unsigned long long t = 0;
+          for (int w = 0; w < kBlock / 64; ++w) t += red_cnt[w];
+          pp.chunk_cnt[blockIdx.x] = (uint32_t)t;
         }
       }
       __syncthreads();  // the words are read before the next chunk clears them

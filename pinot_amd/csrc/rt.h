@@ -733,6 +733,7 @@ struct pgpu_plan_s {
   bool alone = false;             // no other execution of the table was in flight when this one launched
   bool exported = false;          // the last execution's epilogue copied table + statistics to scratch->exported
   bool comm_dense = false;        // combined element-wise (ALL_REDUCE / REDUCE_SCATTER): no host exchange of status
+  bool k8d_counts = false;        // K8d wrote the compaction's chunk counts / ranges (KPartParams.chunk_cnt)
   const void* d_table_used = nullptr;
   bool hash = false;
   // numGroupsLimit (InstancePlanMakerImplV2.java:70): a segment whose group-key space (product of its local

@@ -208,6 +208,7 @@ int exec_prologue(pgpu_plan_s* P, hipStream_t stream, void* d_table, int max_chu
   P->shard_begin = P->shard_count = 0;
   P->comm_used = nullptr;
   P->comm_dense = false;
+  P->k8d_counts = false;
   P->merged_records = -1;
   Scratch* sc = P->scratch;
   X.nslots = (int)P->slot_kind.size();
@@ -671,6 +672,18 @@ int exec_launch_chunk(pgpu_plan_s* P, hipStream_t stream, ExecCtx& X, const Laun
 #endif
     TRY(sc->block_off.ensure((size_t)grid * pp.num_coarse * 4));
     pp.block_off = sc->block_off.as<uint32_t>();
+    // K8d's partitions are the ordered compaction's chunks (C5): K8d writes their counts and ranges, and finalize
+    // skips compact_count_kernel's pass over the table (P->k8d_counts)
+    {
+      const int64_t G = P->num_keys, nch = compact_ordered_chunks(G);
+      if (pp.cs_pack && !P->hash && ((int64_t)1 << pp.pshift) == kCompactChunkKeys && nch == P->num_parts &&
+          (int64_t)nslots * G * 8 > kHostCompactBytes) {
+        TRY(sc->cslots.ensure(compact_scratch_bytes(G, nslots)));
+        pp.chunk_cnt = sc->cslots.as<uint32_t>();
+        pp.chunk_mm = reinterpret_cast<long long*>(sc->cslots.as<uint8_t>() + ((nch * 4 + 7) & ~int64_t(7)));
+        P->k8d_counts = true;
+      }
+    }
     if (launch_partitioned(pp, grid, P->part_lds, stream))
       return fail(PGPU_ERR_DEVICE, "partitioned group-by launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else if (C.num_tiles > 0) {
@@ -949,8 +962,10 @@ int plan_finalize_impl(pgpu_plan_s* P, hipStream_t stream, const void* d_table, 
     TRY(sc->counter.ensure(64 + (size_t)nslots * 16));
     TRY(sc->cslots.ensure(compact_scratch_bytes(G, nslots)));
     long long* d_minmax = reinterpret_cast<long long*>(sc->counter.as<uint8_t>() + 64);
+    // K8d already counted this execution's table by chunk (unchanged since: no combine, the whole key range)
+    const bool counted = P->k8d_counts && table == P->d_table_used && key_begin == 0 && G == P->num_keys;
     if (launch_compact_dense_count(table, nslots, G, sc->cslots.as<uint32_t>(), sc->counter.as<unsigned long long>(),
-                                   d_minmax, stream))
+                                   d_minmax, stream, counted))
       return fail(PGPU_ERR_DEVICE, "compact count launch failed: %s", hipGetErrorString(hipGetLastError()));
     TRY(sc->readback.ensure(64 + (size_t)nslots * 16));
     uint64_t* st = reinterpret_cast<uint64_t*>(sc->readback.p);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06 session z: K8d writes the ordered compaction's chunk counts and ranges (C5: partitions == compaction chunks), so
+# r06 session z (and zb: the compact scatter with every round's words loaded up front): K8d writes the ordered compaction's chunk counts and ranges (C5: partitions == compaction chunks), so
 # finalize skips compact_count_kernel: partitioned / workload GPU tests, then C5 at 100 and 13 segments against the
 # previous library.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

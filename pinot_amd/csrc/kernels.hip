@@ -336,20 +336,9 @@ __global__ __launch_bounds__(256) void compact_dense_scatter_kernel(const uint64
   int width[kMaxSlots];
   for (int s = 0; s < num_slots; ++s) width[s] = slot_width(minmax[s], minmax[num_slots + s], kinds.k[s]);
   uint32_t pos = chunk_off[blockIdx.x];
-  // every round's COUNT word (and slot 1's) loaded up front: 16 loads in flight per lane instead of one dependent
-  // load per round between the rounds' barriers
-  constexpr int R = kCompactChunk / 256;
-  uint64_t c0[R], c1[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
+  for (int r = 0; r < kCompactChunk / 256; ++r) {
     const int64_t k = base + r * 256 + threadIdx.x;
-    c0[r] = k < num_keys ? table[k] : 0ull;
-    c1[r] = k < num_keys && num_slots > 1 ? table[num_keys + k] : 0ull;
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t k = base + r * 256 + threadIdx.x;
-    const bool f = c0[r] != 0;
+    const bool f = k < num_keys && table[k] != 0;
     const unsigned long long bal = __ballot(f);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
     if (lane == 0) {
@@ -365,7 +354,7 @@ __global__ __launch_bounds__(256) void compact_dense_scatter_kernel(const uint64
       const int64_t j = (int64_t)pos + before + rank;
       if (j < cap) {
         for (int s = 0; s < num_slots; ++s) {
-          const uint64_t v = s == 0 ? c0[r] : s == 1 ? c1[r] : table[(int64_t)s * num_keys + k];
+          const uint64_t v = table[(int64_t)s * num_keys + k];
           put_compact(out_slots + (int64_t)s * cap * 8, j, width[s], v);
         }
       }

@@ -212,7 +212,11 @@ __global__ __launch_bounds__(kBlock, DENSE ? (SIMPLE ? PGPU_SIMPLE_MIN_WAVES : P
       const int64_t gclamp = group < ngroups ? group : ngroups - 1;
       if (fast) {
         // STATS_LEAP2 (two scans in leap-frog): both masks are needed for the entry count, no early exit
+#ifdef PGPU_DIAG_NO_LEAP  // diagnostics build only (wrong numEntriesScannedInFilter): the leap-frog statistics' cost
+        const bool leap = false;
+#else
         const bool leap = (stats & 3) == KSTATS_LEAP2;
+#endif
         const uint32_t v = mask;
         const int la = (stats >> 8) & 3, lb = (stats >> 10) & 3;
         uint32_t ma = 0, mb = 0;

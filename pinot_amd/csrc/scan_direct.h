@@ -20,12 +20,11 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
   a &= v;
   b &= v;
   const uint32_t e = a | b;
-  uint32_t fill = a & ~b, seen = e;  // scanner after doc i: B (1) / A (0), where some doc <= i matches
-#pragma unroll
-  for (int k = 1; k < 32; k <<= 1) {
-    fill |= (fill << k) & ~seen;
-    seen |= seen << k;
-  }
+  // scanner after doc i: B (1) where the last matching doc <= i matched A only, A (0) otherwise -- the A-only docs'
+  // ones carried up through the docs B does not match, by one addition (a set bit p of y inside a run of ~b ones
+  // flips the run from p up, so (~b + y) ^ ~b marks it; y's own bits are put back for runs holding several)
+  const uint32_t y = a & ~b, nb = ~b;
+  const uint32_t fill = (nb & ((nb + y) ^ nb)) | y;
   const uint32_t before = fill << 1;  // scanner before each doc, entering in A
   uint32_t c = __popc(v) + __popc((a & ~before) | (b & before));
   const int f = e ? __builtin_ctz(e) : 0;

@@ -31,13 +31,12 @@ __device__ __forceinline__ uint32_t leap2_entries(uint8_t* __restrict__ maps, in
   const int d = e ? (int)((b >> f) & 1u) - (int)((a >> f) & 1u) : 0;  // entering in B instead, at the first match
   // wave-wide state from ballots only (scalar masks, no lane shuffles, no divergent branch)
   const uint64_t evm = __ballot(e != 0u), exm = __ballot(e != 0u && (fill >> 31));
-  const uint64_t bfm = __ballot((b >> f) & 1u), afm = __ballot((a >> f) & 1u);
   const uint64_t below = evm & ((1ull << lane) - 1ull);
   if (below && ((exm >> (63 - __builtin_clzll(below))) & 1ull)) c += d;
   uint32_t m = 0;
   if (evm) {
     const int first = __builtin_ctzll(evm), last = 63 - __builtin_clzll(evm);
-    const int df = (int)((bfm >> first) & 1ull) - (int)((afm >> first) & 1ull);
+    const int df = __builtin_amdgcn_readlane(d, first);  // the first matching lane's difference
     m = 1u | (uint32_t)(((exm >> last) & 1ull) << 1) | ((uint32_t)(df + 1) << 2);
   }
   if (lane == 0) maps[slot] = (uint8_t)m;  // an LDS slot: global stores inside the tile loop cost the loop registers

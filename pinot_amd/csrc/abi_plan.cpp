@@ -121,9 +121,8 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
     st->metrics.push_back(a);
     st->mf_narrow.push_back(needs_f && ints32_f(d->metric_f64[m], d->num_docs));
     st->mc_narrow.push_back(needs_c && ints32_c(d->metric_i64[m], d->num_docs));
-    // each array 16-B aligned with 128 B past its last document: K6 loads a lane's 16 documents as one line
     bytes += (needs_f ? (int64_t)d->num_docs * (st->mf_narrow.back() ? 4 : 8) : 0) +
-             (needs_c ? (int64_t)d->num_docs * (st->mc_narrow.back() ? 4 : 8) : 0) + 2 * (128 + 32);
+             (needs_c ? (int64_t)d->num_docs * (st->mc_narrow.back() ? 4 : 8) : 0) + 32;
   }
   HIP_TRY(hipMalloc(&st->d_block, bytes));
   st->bytes = bytes;
@@ -150,7 +149,7 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
         memcpy(host.data() + off, d->metric_f64[m], (size_t)d->num_docs * 8);
       }
       pf = reinterpret_cast<const double*>((uint8_t*)st->d_block + off);
-      off = (off + (int64_t)d->num_docs * (st->mf_narrow[m] ? 4 : 8) + 128 + 15) & ~int64_t(15);
+      off += (int64_t)d->num_docs * (st->mf_narrow[m] ? 4 : 8) + 16;
     }
     if (a.fn == PGPU_AGG_COUNT || a.fn == PGPU_AGG_AVG) {
       if (st->mc_narrow[m]) {
@@ -160,7 +159,7 @@ int pgpu_attach_startree(pgpu_table t, int64_t h, const pgpu_startree_desc* d) t
         memcpy(host.data() + off, d->metric_i64[m], (size_t)d->num_docs * 8);
       }
       pc = reinterpret_cast<const int64_t*>((uint8_t*)st->d_block + off);
-      off = (off + (int64_t)d->num_docs * (st->mc_narrow[m] ? 4 : 8) + 128 + 15) & ~int64_t(15);
+      off += (int64_t)d->num_docs * (st->mc_narrow[m] ? 4 : 8) + 16;
     }
     st->d_mf.push_back(pf);
     st->d_mc.push_back(pc);

@@ -226,26 +226,9 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? (int64_t)src[d0 + i] : 1;
       } else {
-#ifndef PGPU_STAR_SCALAR_LOADS
-        // the lane's 16 counts are one 128-B line (16-B aligned, padded past the last document at pin): 8 16-byte
-        // loads instead of 16 8-byte ones, when any of them matched
-        typedef long long ll2 __attribute__((ext_vector_type(2)));
-        const ll2* __restrict__ src2 = reinterpret_cast<const ll2*>(S.src_c[0] + d0);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = 1;
-        if (has && m) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const ll2 x = src2[j];
-            c[2 * j] = x.x;
-            c[2 * j + 1] = x.y;
-          }
-        }
-#else
         gmem<int64_t>* __restrict__ src = gp(S.src_c[0]);
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = has && ((m >> i) & 1u) ? src[d0 + i] : 1;
-#endif
       }
 #ifndef PGPU_STAR_NO_SECTORS
       if (has) sectors += nar ? sec4 : sec8;
@@ -264,24 +247,9 @@ __device__ __forceinline__ void star_aggregate_half(const KStarParams& p, const 
       sectors += sec4;
 #endif
     } else {
-#ifndef PGPU_STAR_SCALAR_LOADS
-      typedef double d2 __attribute__((ext_vector_type(2)));
-      const d2* __restrict__ src2 = reinterpret_cast<const d2*>(S.src_f[s] + d0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = 0.0;
-      if (m) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const d2 x = src2[j];
-          v[2 * j] = x.x;
-          v[2 * j + 1] = x.y;
-        }
-      }
-#else
       gmem<double>* __restrict__ src = gp(S.src_f[s]);
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((m >> i) & 1u) ? src[d0 + i] : 0.0;
-#endif
 #ifndef PGPU_STAR_NO_SECTORS
       sectors += sec8;
 #endif
